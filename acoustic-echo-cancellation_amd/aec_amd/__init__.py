@@ -1,0 +1,25 @@
+"""aec_amd — MI355X (gfx950) drop-in for the Stage-2 AEC inference path of
+SZU-Speech/Acoustic-Echo-Cancellation (Stage2_lhm/).
+
+Public surface (mirrors the reference):
+  * ``Little_net(conf, erb_bands)``                 scripts/network/ERB.py:203
+  * ``EquivalentRectangularBandwidth(...).filters`` scripts/network/ERB.py:10
+  * ``speech_conf`` / ``erb_conf``                  scripts/configs.py:1-27
+The compute runs in ``libaec_hip.so`` (C ABI: include/aec_hip.h).
+"""
+from .configs import speech_conf, erb_conf, train_conf          # noqa: F401
+from .erb import EquivalentRectangularBandwidth, erb_matrix     # noqa: F401
+from .little_net import Little_net                              # noqa: F401
+
+WIN_SIZE = 512
+HOP_SIZE = 256
+
+
+def num_frames(n: int) -> int:
+    """T = N//256 + 1 (attention_ccrn.py:48-49)."""
+    return n // HOP_SIZE + 1
+
+
+def out_len(n: int) -> int:
+    """256*(N//256) (attention_ccrn.py:92,99)."""
+    return HOP_SIZE * (n // HOP_SIZE)

@@ -1,0 +1,144 @@
+"""ctypes binding of libaec_hip.so (C ABI declared in include/aec_hip.h).
+
+The HIP library is the ONLY compute path: there is no CPU fallback.  If the
+library has not been built (``python -c "import __graft_entry__ as g; g.build()"``)
+every entry point raises ``RuntimeError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libaec_hip.so')
+
+# aec_status codes (include/aec_hip.h)
+AEC_OK = 0
+AEC_ERR_INVALID_ARG = 1
+AEC_ERR_OOM = 2
+AEC_ERR_HIP = 3
+AEC_ERR_UNSUPPORTED = 4
+_STATUS = {0: 'AEC_OK', 1: 'AEC_ERR_INVALID_ARG', 2: 'AEC_ERR_OOM', 3: 'AEC_ERR_HIP', 4: 'AEC_ERR_UNSUPPORTED'}
+
+# every symbol include/aec_hip.h declares
+EXPORTS = ('aec_weights_count', 'aec_create', 'aec_set_weights', 'aec_set_erb', 'aec_process',
+           'aec_set_debug', 'aec_debug_copy', 'aec_profile_enable', 'aec_profile_read',
+           'aec_num_frames', 'aec_out_len', 'aec_last_error', 'aec_destroy')
+
+
+class AecConfig(ctypes.Structure):
+    _fields_ = [('win_size', ctypes.c_int32), ('hop_size', ctypes.c_int32),
+                ('erb_bands', ctypes.c_int32), ('nlms_taps', ctypes.c_int32),
+                ('nlms_mu', ctypes.c_float), ('nlms_beta', ctypes.c_float),
+                ('nlms_delta', ctypes.c_float), ('reserved', ctypes.c_int32)]
+
+
+_lib = None
+
+
+def load():
+    """Load (once) and return the ctypes library; raise if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f'libaec_hip.so not found at {LIB_PATH}: build it first '
+                           '(python -c "import __graft_entry__ as g; g.build()"); '
+                           'there is no CPU fallback')
+    lib = ctypes.CDLL(LIB_PATH)
+    P = ctypes.c_void_p
+    lib.aec_weights_count.argtypes = [ctypes.c_int32]
+    lib.aec_weights_count.restype = ctypes.c_size_t
+    lib.aec_create.argtypes = [ctypes.POINTER(AecConfig), P, ctypes.c_size_t, P, ctypes.c_int32,
+                               ctypes.POINTER(P)]
+    lib.aec_create.restype = ctypes.c_int
+    lib.aec_set_weights.argtypes = [P, P, ctypes.c_size_t]
+    lib.aec_set_weights.restype = ctypes.c_int
+    lib.aec_set_erb.argtypes = [P, P]
+    lib.aec_set_erb.restype = ctypes.c_int
+    lib.aec_process.argtypes = [P, P, P, P, P, ctypes.c_int32, ctypes.c_int64, P, ctypes.c_int64, P, P]
+    lib.aec_process.restype = ctypes.c_int
+    lib.aec_set_debug.argtypes = [P, ctypes.c_int32]
+    lib.aec_set_debug.restype = ctypes.c_int
+    lib.aec_debug_copy.argtypes = [P, ctypes.c_int32, P, ctypes.c_size_t, P]
+    lib.aec_debug_copy.restype = ctypes.c_int
+    lib.aec_profile_enable.argtypes = [P, ctypes.c_int32]
+    lib.aec_profile_enable.restype = ctypes.c_int
+    lib.aec_profile_read.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
+    lib.aec_profile_read.restype = ctypes.c_int
+    lib.aec_num_frames.argtypes = [ctypes.c_int64]
+    lib.aec_num_frames.restype = ctypes.c_int64
+    lib.aec_out_len.argtypes = [ctypes.c_int64]
+    lib.aec_out_len.restype = ctypes.c_int64
+    lib.aec_last_error.argtypes = [P]
+    lib.aec_last_error.restype = ctypes.c_char_p
+    lib.aec_destroy.argtypes = [P]
+    lib.aec_destroy.restype = None
+    _lib = lib
+    return lib
+
+
+def check(status, handle=None, what=''):
+    if status == AEC_OK:
+        return
+    msg = ''
+    if handle is not None and _lib is not None:
+        m = _lib.aec_last_error(handle)
+        msg = m.decode() if m else ''
+    raise RuntimeError(f'{what} failed: {_STATUS.get(status, status)} {msg}'.strip())
+
+
+class Handle:
+    """Owns one aec_handle (one per device)."""
+
+    def __init__(self, device: int, nlms_taps=0, nlms_mu=0.5, nlms_beta=0.9, nlms_delta=1e-4):
+        self.lib = load()
+        cfg = AecConfig(512, 256, 32, int(nlms_taps), float(nlms_mu), float(nlms_beta), float(nlms_delta), 0)
+        h = ctypes.c_void_p()
+        st = self.lib.aec_create(ctypes.byref(cfg), None, 0, None, int(device), ctypes.byref(h))
+        check(st, None, 'aec_create')
+        self.h = h
+        self.device = device
+
+    def set_weights(self, blob):
+        import numpy as np
+        blob = np.ascontiguousarray(blob, dtype=np.float32)
+        check(self.lib.aec_set_weights(self.h, blob.ctypes.data, blob.size), self.h, 'aec_set_weights')
+
+    def set_erb(self, erb):
+        import numpy as np
+        erb = np.ascontiguousarray(erb, dtype=np.float32)
+        if erb.shape != (257, 32):
+            raise ValueError(f'erb must be [257, 32], got {tuple(erb.shape)}')
+        check(self.lib.aec_set_erb(self.h, erb.ctypes.data), self.h, 'aec_set_erb')
+
+    def set_debug(self, on: bool):
+        check(self.lib.aec_set_debug(self.h, int(bool(on))), self.h, 'aec_set_debug')
+
+    def process(self, mic_ptr, ref_ptr, near_ptr, lengths, B, ld, out_ptr, ld_out, loss_ptr, stream):
+        import numpy as np
+        lens = np.ascontiguousarray(lengths, dtype=np.int64)
+        st = self.lib.aec_process(self.h, mic_ptr, ref_ptr, near_ptr, lens.ctypes.data, int(B), int(ld),
+                                  out_ptr, int(ld_out), loss_ptr, stream)
+        check(st, self.h, 'aec_process')
+
+    def debug_copy(self, what, dst_ptr, n, stream):
+        check(self.lib.aec_debug_copy(self.h, int(what), dst_ptr, int(n), stream), self.h, 'aec_debug_copy')
+
+    def profile_enable(self, on: bool):
+        check(self.lib.aec_profile_enable(self.h, int(bool(on))), self.h, 'aec_profile_enable')
+
+    def profile_read(self):
+        """-> (ms per kernel [moments, analysis, gru, synthesis] summed, calls)"""
+        ms = (ctypes.c_double * 4)()
+        calls = ctypes.c_int64()
+        check(self.lib.aec_profile_read(self.h, ms, ctypes.byref(calls)), self.h, 'aec_profile_read')
+        return list(ms), int(calls.value)
+
+    def __del__(self):
+        try:
+            if getattr(self, 'h', None):
+                self.lib.aec_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass

@@ -1,0 +1,202 @@
+"""``Little_net`` — drop-in for the reference's Stage-2 post-filter module.
+
+Reference: ``Little_net`` in Stage2_lhm/scripts/network/ERB.py:203-334.
+
+Same constructor ``Little_net(conf, erb_bands)``, same submodule / parameter /
+buffer names (so the reference's ``state_dict`` loads with ``strict=True``,
+scripts/test.py:124), same parameter init (orthogonal GRU weights, Kaiming
+linears, ERB.py:226-250, in the same RNG order, so ``torch.manual_seed(s)``
+gives the reference's weights), and the same
+``forward(mic, ref, near, erb) -> (out_wav, loss)`` (ERB.py:252-334).
+
+The forward runs entirely on the GPU through ``libaec_hip.so``; there is no
+CPU fallback.  Per-stream semantics: every row of a [B, N] batch is processed
+as the reference processes a batch of one (its normaliser uses the row's own
+mean/std, ERB.py:254-256 at batch=1 — SURVEY.md §0.5).  ``loss`` is the sum of
+the per-row losses, which equals the reference's value at B = 1.
+
+Inference only: the reference trains through autograd (scripts/train1.py:207-218);
+this module raises if asked for gradients.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+WIN, HOP = 512, 256
+
+
+def _stft_bases():
+    """Closed forms of the reference's fixed STFT buffers (attention_ccrn.py:8-25):
+    forward rows [cos; -sin](2 pi k n / 512) * hann, inverse rows = irfft weights
+    (c_k / 512, c_0 = c_256 = 1 else 2) * hann, i.e. pinv(forward).T * hann."""
+    n = np.arange(WIN)
+    k = np.arange(WIN // 2 + 1)[:, None]
+    win = 0.5 - 0.5 * np.cos(2 * np.pi * n / WIN)
+    ang = 2 * np.pi * k * n[None, :] / WIN
+    fwd = np.concatenate([np.cos(ang), -np.sin(ang)], 0)
+    ck = np.full((WIN // 2 + 1, 1), 2.0)
+    ck[0] = ck[-1] = 1.0
+    inv = np.concatenate([np.cos(ang) * ck, -np.sin(ang) * ck], 0) / WIN
+    inv[WIN // 2 + 1] = 0.0          # imaginary DC row (pinv of an all-zero row)
+    inv[-1] = 0.0                    # imaginary Nyquist row
+    f32 = lambda a: torch.from_numpy((a * win).astype(np.float32))[:, None, :]
+    return f32(fwd), f32(inv), torch.from_numpy(win.astype(np.float32))[None, :, None]
+
+
+class _ConvSTFTBuffers(nn.Module):
+    """Holds ``cpx_stft.weight`` [514,1,512] (attention_ccrn.py:36-38)."""
+
+    def __init__(self, weight):
+        super().__init__()
+        self.register_buffer('weight', weight)
+
+
+class _ConviSTFTBuffers(nn.Module):
+    """Holds ``istft.weight`` / ``istft.window`` / ``istft.enframe`` (attention_ccrn.py:68-80)."""
+
+    def __init__(self, weight, window):
+        super().__init__()
+        self.register_buffer('weight', weight)
+        self.register_buffer('window', window)
+        self.register_buffer('enframe', torch.eye(WIN)[:, None, :])
+
+
+class Little_net(nn.Module):
+    def __init__(self, conf, erb_bands, nlms=None):
+        super().__init__()
+        self.config = conf
+        self.win_len = conf['win_size']
+        self.win_inc = conf['hop_size']
+        if self.win_len != WIN or self.win_inc != HOP or erb_bands != 32:
+            raise NotImplementedError('the gfx950 path implements win 512 / hop 256 / 32 ERB bands '
+                                      '(speech_conf, erb_conf of the reference)')
+        self.win_type = 'hann'
+        # same module creation order as ERB.py:213-217 (RNG order matters for the init)
+        self.gru1 = nn.GRU(2 * erb_bands, erb_bands, num_layers=1, batch_first=True, bias=True)
+        self.linear1 = nn.Linear(2 * erb_bands, erb_bands, bias=True)
+        self.linear2 = nn.Linear(erb_bands, erb_bands, bias=True)
+        self.relu = nn.ReLU()
+        self.sigmoid = nn.Sigmoid()
+        fwd, inv, win = _stft_bases()
+        self.cpx_stft = _ConvSTFTBuffers(fwd)
+        self.istft = _ConviSTFTBuffers(inv, win)
+        self.gru1.apply(self._orthogonal)
+        self.linear1.apply(lambda m: self._kaiming(m, 'relu'))
+        self.linear2.apply(lambda m: self._kaiming(m, 'sigmoid'))
+        self.nlms = dict(nlms) if nlms else None
+        self._handles = {}
+        self._w_key = {}
+        self._erb_key = {}
+
+    # --- init, as ERB.py:231-250 -------------------------------------------
+    @staticmethod
+    def _kaiming(module, nonlinearity):
+        if isinstance(module, nn.Linear):
+            nn.init.kaiming_uniform_(module.weight, mode='fan_in', nonlinearity=nonlinearity)
+            if module.bias is not None:
+                nn.init.zeros_(module.bias)
+
+    @staticmethod
+    def _orthogonal(module):
+        if isinstance(module, nn.GRU):
+            for name, param in module.named_parameters():
+                if 'weight' in name:
+                    nn.init.orthogonal_(param.data)
+
+    # --- device plumbing ------------------------------------------------------
+    def _params(self):
+        g = self.gru1
+        return [g.weight_ih_l0, g.weight_hh_l0, g.bias_ih_l0, g.bias_hh_l0,
+                self.linear1.weight, self.linear1.bias, self.linear2.weight, self.linear2.bias]
+
+    def weights_blob(self):
+        """The 12,544-float blob in state_dict order (include/aec_hip.h)."""
+        return torch.cat([p.detach().reshape(-1).float().cpu() for p in self._params()]).numpy()
+
+    def _handle(self, device):
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        h = self._handles.get(idx)
+        if h is None:
+            nl = self.nlms or {}
+            h = _lib.Handle(idx, nlms_taps=nl.get('taps', 0), nlms_mu=nl.get('mu', 0.5),
+                            nlms_beta=nl.get('beta', 0.9), nlms_delta=nl.get('delta', 1e-4))
+            self._handles[idx] = h
+        wkey = tuple((p.data_ptr(), p._version) for p in self._params())
+        if self._w_key.get(idx) != wkey:
+            h.set_weights(self.weights_blob())
+            self._w_key[idx] = wkey
+        return h, idx
+
+    def _sync_erb(self, h, idx, erb):
+        key = (erb.data_ptr(), erb._version, str(erb.device), tuple(erb.shape))
+        if self._erb_key.get(idx) != key:
+            h.set_erb(erb.detach().float().cpu().numpy())
+            self._erb_key[idx] = key
+
+    def set_debug(self, on=True, device=None):
+        device = torch.device(device or 'cuda')
+        h, _ = self._handle(device)
+        h.set_debug(on)
+
+    # --- forward --------------------------------------------------------------
+    def forward(self, mic, ref, near, erb):
+        """(ERB.py:252-334) mic/ref/near [B, N] (or [N]) float32 on a HIP device."""
+        if mic.dim() == 1:
+            mic, ref, near = mic[None], ref[None], near[None] if near is not None else None
+        B, N = mic.shape
+        out, loss = self.forward_ragged(mic, ref, near, erb, [N] * B)
+        return out, (loss.sum() if loss is not None else None)
+
+    def forward_ragged(self, mic, ref, near, erb, lengths):
+        """Batched call with per-row true lengths (rows zero-padded to a common
+        width).  Returns out [B, 256*(max(lengths)//256)] (row b valid up to
+        256*(lengths[b]//256), zero beyond) and per-row losses [B] (None when
+        ``near`` is None)."""
+        if torch.is_grad_enabled() and (mic.requires_grad or any(p.requires_grad for p in self._params())
+                                        and self.training):
+            raise NotImplementedError('Little_net (gfx950) is inference-only: call it under torch.no_grad() '
+                                      'and net.eval(), as scripts/test.py:134,156 does')
+        dev = mic.device
+        if dev.type != 'cuda':
+            raise RuntimeError(f'Little_net (gfx950) needs its inputs on a HIP device, got {dev}; '
+                               'there is no CPU path')
+        tens = [mic, ref] + ([near] if near is not None else [])
+        for t in tens:
+            if t.shape != mic.shape or t.device != dev:
+                raise ValueError('mic, ref and near must share shape and device')
+        if erb.shape != (257, 32):
+            raise ValueError(f'erb must be [257, 32], got {tuple(erb.shape)}')
+        mic = mic.contiguous().float()
+        ref = ref.contiguous().float()
+        near = near.contiguous().float() if near is not None else None
+        B, L = mic.shape
+        lengths = np.asarray(lengths, dtype=np.int64)
+        if lengths.shape != (B,) or (lengths < 1).any() or (lengths > L).any():
+            raise ValueError('lengths must be [B] with 1 <= length <= N')
+        h, idx = self._handle(dev)
+        self._sync_erb(h, idx, erb)
+        lout = HOP * (int(lengths.max()) // HOP)
+        out = torch.zeros(B, lout, device=dev, dtype=torch.float32) if (lengths != lengths.max()).any() \
+            else torch.empty(B, lout, device=dev, dtype=torch.float32)
+        loss = torch.empty(B, device=dev, dtype=torch.float32) if near is not None else None
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        if B > 0:
+            with torch.cuda.device(dev):
+                h.process(mic.data_ptr(), ref.data_ptr(), near.data_ptr() if near is not None else None,
+                          lengths, B, L, out.data_ptr(), max(lout, 1), loss.data_ptr() if loss is not None else None,
+                          stream)
+        return out, loss
+
+    def debug_intermediate(self, what, B, T, device=None):
+        """Copy an intermediate of the last forward: 'mic_erb', 'ref_erb',
+        'near_erb', 'gru_out', 'mask', 'est_erb' -> [B, T, 32]."""
+        codes = dict(mic_erb=0, ref_erb=1, near_erb=2, gru_out=3, mask=4, est_erb=5)
+        device = torch.device(device or 'cuda')
+        h, _ = self._handle(device)
+        dst = torch.empty(B, T, 32, device=device, dtype=torch.float32)
+        h.debug_copy(codes[what], dst.data_ptr(), dst.numel(), torch.cuda.current_stream(device).cuda_stream)
+        return dst

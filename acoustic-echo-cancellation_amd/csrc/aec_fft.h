@@ -1,0 +1,141 @@
+// aec_fft.h — gfx950 device building blocks for the 512-point STFT / iSTFT.
+//
+// The reference computes its STFT as conv1d with a 514x512 windowed-DFT basis
+// and its iSTFT as conv_transpose1d with the pinv basis
+// (Stage2_lhm/scripts/network/attention_ccrn.py:8-101).  Both are exactly a
+// windowed rFFT-512 / irFFT-512, so here a real 512-point
+// frame is packed into a 256-point complex sequence z[m] = x[2m] + i x[2m+1]
+// and transformed with a radix-16 x 16 FFT held in registers:
+//
+//   one 16-lane group per frame, lane b holds z[16a + b], a = 0..15
+//   DFT16 over a (registers) -> twiddle W256^(b k1) -> LDS transpose (row stride
+//   18 complex: conflict-free b64 writes / b128 reads) -> DFT16 over b
+//   -> lane k1 holds Z[k1 + 16 k2].
+//
+// A wave (64 lanes) therefore transforms 4 frames at once with one LDS round
+// trip; no block barrier is needed inside a transform (all lanes of a group
+// live in one wave and LDS ops of a wave execute in order).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace aec {
+
+constexpr int kWin = 512;
+constexpr int kHop = 256;
+constexpr int kBins = 257;
+constexpr int kBands = 32;
+constexpr int kGroupFloats = 576;   // per-frame LDS scratch: 16 rows x 36 floats
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 conjf2(float2 a) { return make_float2(a.x, -a.y); }
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+
+// a * (c + i*s)
+__device__ __forceinline__ float2 crot(float2 a, float c, float s) {
+    return make_float2(a.x * c - a.y * s, a.x * s + a.y * c);
+}
+
+// 4-point DFT in place.  Forward uses W4 = -i, inverse W4 = +i (unnormalised).
+template <bool INV>
+__device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
+    const float2 t0 = cadd(a0, a2), t1 = csub(a0, a2);
+    const float2 t2 = cadd(a1, a3), t3 = csub(a1, a3);
+    a0 = cadd(t0, t2);
+    a2 = csub(t0, t2);
+    if (!INV) {   // t1 - i t3 , t1 + i t3
+        a1 = make_float2(t1.x + t3.y, t1.y - t3.x);
+        a3 = make_float2(t1.x - t3.y, t1.y + t3.x);
+    } else {
+        a1 = make_float2(t1.x - t3.y, t1.y + t3.x);
+        a3 = make_float2(t1.x + t3.y, t1.y - t3.x);
+    }
+}
+
+// Position of output index k after dft16: C[k] lives in v[kP(k)].
+__host__ __device__ constexpr int kP(int k) { return 4 * (k & 3) + (k >> 2); }
+
+// 16-point DFT in registers (radix 4 x 4).  Input v[a] = c[a] (natural order);
+// output C[k] = sum_a c[a] W16^(+-a k) at v[kP(k)].
+template <bool INV>
+__device__ __forceinline__ void dft16(float2 (&v)[16]) {
+    constexpr float C1 = 0.92387953251128674f;   // cos(pi/8)
+    constexpr float S1 = 0.38268343236508978f;   // sin(pi/8)
+    constexpr float R2 = 0.70710678118654752f;
+    constexpr float sg = INV ? 1.f : -1.f;       // W16^m = cos(2pi m/16) + i*sg*sin(2pi m/16)
+#pragma unroll
+    for (int a0 = 0; a0 < 4; ++a0) dft4<INV>(v[a0], v[a0 + 4], v[a0 + 8], v[a0 + 12]);
+    // v[a0 + 4 k0] = D[a0][k0]; twiddle by W16^(a0 k0)
+    v[1 + 4] = crot(v[1 + 4], C1, sg * S1);     // W^1
+    v[1 + 8] = crot(v[1 + 8], R2, sg * R2);     // W^2
+    v[1 + 12] = crot(v[1 + 12], S1, sg * C1);   // W^3
+    v[2 + 4] = crot(v[2 + 4], R2, sg * R2);     // W^2
+    v[2 + 8] = INV ? make_float2(-v[2 + 8].y, v[2 + 8].x)          // * (+i)
+                   : make_float2(v[2 + 8].y, -v[2 + 8].x);         // * (-i)   W^4
+    v[2 + 12] = crot(v[2 + 12], -R2, sg * R2);  // W^6
+    v[3 + 4] = crot(v[3 + 4], S1, sg * C1);     // W^3
+    v[3 + 8] = crot(v[3 + 8], -R2, sg * R2);    // W^6
+    v[3 + 12] = crot(v[3 + 12], -C1, -sg * S1); // W^9 = cos(9pi/8) + i sg sin(9pi/8)
+#pragma unroll
+    for (int k0 = 0; k0 < 4; ++k0) dft4<INV>(v[4 * k0], v[4 * k0 + 1], v[4 * k0 + 2], v[4 * k0 + 3]);
+}
+
+__device__ __forceinline__ void wave_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// 256-point complex FFT for one 16-lane group.
+//   in : v[a] = z[16a + lb]
+//   out: v[kP(k2)] = Z[lb + 16 k2]   (unnormalised, sign per INV)
+// scr: this group's LDS scratch (>= 16*36 floats, 16-B aligned).
+// tw : LDS table W256^j = (cos 2pi j/256, -sin 2pi j/256), j = 0..255.
+template <bool INV>
+__device__ __forceinline__ void fft256(float2 (&v)[16], int lb, float* scr, const float2* tw) {
+    dft16<INV>(v);
+    float2* s2 = reinterpret_cast<float2*>(scr);
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1) {
+        float2 w = tw[(lb * k1) & 255];
+        if (INV) w.y = -w.y;
+        s2[k1 * 18 + lb] = cmul(v[kP(k1)], w);
+    }
+    wave_fence();
+    const float4* s4 = reinterpret_cast<const float4*>(scr) + lb * 9;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const float4 t = s4[q];
+        v[2 * q] = make_float2(t.x, t.y);
+        v[2 * q + 1] = make_float2(t.z, t.w);
+    }
+    wave_fence();
+    dft16<INV>(v);
+}
+
+// Forward real-FFT unpack for one pair (k, 256-k), 1 <= k <= 127:
+//   A = Z[k], Bz = Z[256-k], w = W512^k  ->  X[k], X[256-k]
+__device__ __forceinline__ void rfft_pair(float2 A, float2 Bz, float2 w, float2& Xk, float2& Xmk) {
+    const float2 Bc = conjf2(Bz);
+    const float2 Fe = cscale(cadd(A, Bc), 0.5f);
+    const float2 D = cscale(csub(A, Bc), 0.5f);
+    const float2 Fo = make_float2(D.y, -D.x);          // -i * D
+    const float2 t = cmul(w, Fo);
+    Xk = cadd(Fe, t);
+    Xmk = conjf2(csub(Fe, t));
+}
+
+// Inverse real-FFT pack for one pair (k, 256-k): S[k], S[256-k] -> 2*Z'[k],
+// 2*Z'[256-k] such that IDFT256(2 Z') = 512 * (x[2m] + i x[2m+1]).
+__device__ __forceinline__ void irfft_pair(float2 Sk, float2 Smk, float2 w, float2& Zk, float2& Zmk) {
+    const float2 Bc = conjf2(Smk);
+    const float2 Fe = cadd(Sk, Bc);
+    const float2 Fo = cmul(csub(Sk, Bc), conjf2(w));
+    Zk = make_float2(Fe.x - Fo.y, Fe.y + Fo.x);                       // Fe + i Fo
+    Zmk = make_float2(Fe.x + Fo.y, -Fe.y + Fo.x);                     // conj(Fe) + i conj(Fo)
+}
+
+}  // namespace aec

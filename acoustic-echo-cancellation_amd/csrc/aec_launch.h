@@ -1,0 +1,69 @@
+// aec_launch.h — kernel argument blocks and host launchers (internal).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "aec_fft.h"
+
+namespace aec {
+
+constexpr int kFPB = 16;            // frames per analysis / synthesis block (16 groups x 16 lanes)
+constexpr int kHopsOut = kFPB - 1;  // output hops per synthesis block
+constexpr int kCH = 16;             // frames per chunk in the GRU pipeline
+
+struct AnalysisArgs {
+    const float* sig[3];
+    int64_t ld;
+    const int64_t* lens;
+    const float* cvals;
+    const float* tables;     // DevTables
+    const int* erb_csr;      // ErbCSR blob
+    int nnz;
+    int nsig;
+    float* feats;            // [B][Tmax][96]
+    int64_t Tmax;
+};
+
+struct GruArgs {
+    const float* feats;      // [B][Tmax][96]
+    int64_t Tmax;
+    const int64_t* lens;
+    const float* w;          // weights blob (state_dict order)
+    float* est;              // [B][Tmax][32]
+    float* loss;             // [B] or null
+    int has_near;
+    float* dbg_h;            // [B][Tmax][32] or null
+    float* dbg_mask;         // [B][Tmax][32] or null
+};
+
+struct SynthArgs {
+    const float* mic;
+    int64_t ld;
+    const int64_t* lens;
+    const float* cvals;
+    const float* tables;
+    const int* erb_csr;
+    int nnz;
+    const float* est;        // [B][Tmax][32]
+    int64_t Tmax;
+    float* out;
+    int64_t ld_out;
+};
+
+// dynamic LDS bytes (must match the carve in the kernels)
+inline size_t analysis_smem_bytes(int nnz) {
+    const size_t fl = 256 * 2 + 258 * 2 + 512 + (size_t)kFPB * kGroupFloats;
+    return fl * 4 + (36 + (size_t)((nnz + 3) & ~3) + (size_t)nnz) * 4;
+}
+inline size_t synthesis_smem_bytes(int nnz) {
+    const size_t fl = 256 * 2 + 258 * 2 + 512 + 256 + kFPB * 32 + (size_t)kFPB * kGroupFloats;
+    return fl * 4 + (260 + (size_t)((nnz + 3) & ~3) + (size_t)nnz) * 4;
+}
+
+hipError_t launch_moments(const float* mic, const float* ref, const float* near, int64_t ld,
+                          const int64_t* lens, float* cvals, int B, int nsig, hipStream_t st);
+hipError_t launch_analysis(const AnalysisArgs& a, int B, hipStream_t st);
+hipError_t launch_gru(const GruArgs& a, int B, hipStream_t st);
+hipError_t launch_synthesis(const SynthArgs& a, int B, hipStream_t st);
+
+}  // namespace aec

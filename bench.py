@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""Benchmark of the Stage-2 AEC hot path on MI355X (one process per GPU).
+
+Metric (BASELINE.json): 16 kHz frames/s (one frame = one 256-sample hop), batched
+AEC, plus RTF at batch 1.  Workload at N=1 = BASELINE config C2's shape: 256
+concurrent 10 s streams (N = 160,000 samples, T = 626 frames each) through the
+whole per-frame loop STFT -> ERB-GRU post-filter -> iSTFT, synthetic seeded
+scenes (aec_amd.synth), seed-0 reference weights, inputs resident in HBM.
+N>1 (torchrun): every rank runs its own 256 streams (weak scaling, no data-path
+collective); timing = max over ranks.
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, 'acoustic-echo-cancellation_amd'))
+
+HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector (= f32 MFMA) peak
+KERNELS = ['moments', 'analysis', 'gru', 'synthesis']
+# Algorithmic work per frame: bytes that must cross HBM and
+# FLOPs of the FFT-based algorithm, for B streams with near (loss) enabled.
+ALG = {
+    'moments': dict(bytes=3 * 256 * 4, flops=3 * 256 * 4),
+    'analysis': dict(bytes=3 * 256 * 4 + 3 * 32 * 4, flops=3 * (11520 + 512 + 3 * 257 + 2 * 483)),
+    'gru': dict(bytes=3 * 32 * 4 + 32 * 4, flops=2 * 96 * 64 + 2 * 96 * 32 + 2 * (32 * 64 + 32 * 32) + 400),
+    'synthesis': dict(bytes=256 * 4 + 32 * 4 + 256 * 4, flops=2 * 11520 + 512 + 2 * 483 + 6 * 257 + 3 * 256),
+}
+PIPE = dict(bytes=4096, flops=82000)      # whole path, per frame
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--streams', type=int, default=256)
+    ap.add_argument('--seconds', type=float, default=10.0)
+    ap.add_argument('--cpu-seconds', type=float, default=12.0, help='bounded CPU-baseline sample (wall s)')
+    ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--sweep', action='store_true', help='also report a batch sweep')
+    return ap.parse_args()
+
+
+def roofline(kernel, ms_per_launch, frames_per_launch, pmc):
+    a = ALG[kernel]
+    t = ms_per_launch * 1e-3
+    gbs = a['bytes'] * frames_per_launch / t / 1e9
+    tfl = a['flops'] * frames_per_launch / t / 1e12
+    t_hbm = a['bytes'] / (HBM_PEAK_GBS * 1e9)
+    t_fl = a['flops'] / (FP32_PEAK_TFLOPS * 1e12)
+    traffic = None
+    if pmc and kernel in pmc.get('kernels', {}):
+        traffic = pmc['kernels'][kernel].get('hbm_bytes_per_launch')
+    if t_hbm >= t_fl:
+        return dict(bound='hbm', achieved=round(gbs, 1), peak=HBM_PEAK_GBS, unit='GB/s',
+                    frac=round(gbs / HBM_PEAK_GBS, 4), traffic=traffic, kernel=kernel,
+                    alg_bytes_per_frame=a['bytes'], frames_per_launch=frames_per_launch)
+    return dict(bound='valu_fp32', achieved=round(tfl, 3), peak=FP32_PEAK_TFLOPS, unit='TFLOP/s',
+                frac=round(tfl / FP32_PEAK_TFLOPS, 4), traffic=traffic, kernel=kernel,
+                alg_flops_per_frame=a['flops'], frames_per_launch=frames_per_launch)
+
+
+def cpu_baseline(seconds, B=16, n=160000):
+    """The reference op mix on host cores (oracle/torch_port.py), bounded sample."""
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.join(REPO, 'oracle'))
+    from torch_port import TorchPort
+    from aec_amd import synth, erb_matrix
+    w = dict(np.load(os.path.join(REPO, 'tests', 'golden', 'weights.npz')))
+    port = TorchPort(w, erb_matrix())
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    mic, ref, near = (torch.from_numpy(a) for a in synth.batch(B, n, seed0=5000))
+    port(mic[:2], ref[:2], near[:2])               # warm-up
+    frames = 0
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        port(mic, ref, near)
+        reps += 1
+        frames += B * (n // 256 + 1)
+        el = time.perf_counter() - t0
+        if el >= seconds and reps >= 2:
+            break
+    return dict(value=round(frames / el, 1), unit='frames/s', cores=threads, kind='port',
+                sample=f'{reps} x [{B} streams x {n} samples] through oracle/torch_port.py '
+                       f'(reference op mix: conv1d DFT, nn.GRU, conv_transpose1d), {el:.1f} s wall')
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    import aec_amd
+    from aec_amd import synth
+
+    B = args.streams
+    n = int(round(args.seconds * 16000))
+    T = n // 256 + 1
+    w = dict(np.load(os.path.join(REPO, 'tests', 'golden', 'weights.npz')))
+    net = aec_amd.Little_net(aec_amd.speech_conf, 32).eval()
+    sd = net.state_dict()
+    for k in ['gru1.weight_ih_l0', 'gru1.weight_hh_l0', 'gru1.bias_ih_l0', 'gru1.bias_hh_l0',
+              'linear1.weight', 'linear1.bias', 'linear2.weight', 'linear2.bias']:
+        sd[k] = torch.from_numpy(w[k])
+    net.load_state_dict(sd)
+    net = net.to(dev)
+    erb = torch.tensor(aec_amd.erb_matrix(), dtype=torch.float32, device=dev)
+    mic, ref, near = (torch.from_numpy(a).to(dev) for a in synth.batch(B, n, seed0=1000 * rank))
+    lens = [n] * B
+
+    def step():
+        return net.forward_ragged(mic, ref, near, erb, lens)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        h, _ = net._handle(dev)
+        h.profile_enable(True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        kms, calls = h.profile_read()
+        h.profile_enable(False)
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t)
+        # RTF at batch 1: one 10 s utterance, synchronous latency (median of 7)
+        lat = []
+        for _ in range(7):
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            net.forward_ragged(mic[:1], ref[:1], near[:1], erb, [n])
+            torch.cuda.synchronize(dev)
+            lat.append(time.perf_counter() - t1)
+        rtf1 = float(np.median(lat)) / args.seconds
+        sweep = None
+        if args.sweep and rank == 0:
+            sweep = {}
+            for bb in [1, 16, 64, 256, 1024, 4096]:
+                if bb > B:
+                    mm, rr, nn_ = (x.repeat((bb + B - 1) // B, 1)[:bb] for x in (mic, ref, near))
+                else:
+                    mm, rr, nn_ = mic[:bb], ref[:bb], near[:bb]
+                net.forward_ragged(mm, rr, nn_, erb, [n] * bb)
+                torch.cuda.synchronize(dev)
+                t1 = time.perf_counter()
+                for _ in range(3):
+                    net.forward_ragged(mm, rr, nn_, erb, [n] * bb)
+                torch.cuda.synchronize(dev)
+                sweep[bb] = round(bb * T * 3 / (time.perf_counter() - t1), 1)
+
+    frames_total = world * B * T * args.steps
+    value = frames_total / el
+    ms_step = el / args.steps * 1e3
+    per_kernel_ms = {k: kms[i] / max(calls, 1) for i, k in enumerate(KERNELS)}
+    dom = max(per_kernel_ms, key=per_kernel_ms.get)
+    pmc = None
+    pmc_path = os.path.join(REPO, 'profiles', 'pmc_latest.json')
+    if os.path.exists(pmc_path):
+        pmc = json.load(open(pmc_path))
+    roof = roofline(dom, per_kernel_ms[dom], B * T, pmc)
+    pipe_t = ms_step * 1e-3 / world
+    pipe_gbs = PIPE['bytes'] * B * T / pipe_t / 1e9
+    pipe_tfl = PIPE['flops'] * B * T / pipe_t / 1e12
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        line = {
+            'metric': '16kHz frames/sec/GPU (batched AEC) + RTF@batch=1; ERLE delta vs reference',
+            'value': round(value, 1), 'unit': 'frames/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(ms_step, 4), 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
+            'config': {'workload': 'C2 shape: 256 concurrent 10 s 16 kHz streams per GPU, '
+                                   'STFT -> ERB-GRU post-filter -> iSTFT (Little_net path, FD-NLMS bypass)',
+                       'streams_per_gpu': B, 'samples_per_stream': n, 'frames_per_stream': T,
+                       'frame': '256-sample hop', 'parallelism': f'streams sharded, {world} rank(s)'},
+            'xRT': round(value * 256 / 16000, 1),
+            'rtf_batch1': rtf1,
+            'kernel_ms_per_step': {k: round(v, 4) for k, v in per_kernel_ms.items()},
+            'roofline': roof,
+            'pipeline_roofline': {'alg_bytes_per_frame': PIPE['bytes'], 'alg_flops_per_frame': PIPE['flops'],
+                                  'hbm_frac': round(pipe_gbs / HBM_PEAK_GBS, 4),
+                                  'fp32_frac': round(pipe_tfl / FP32_PEAK_TFLOPS, 4)},
+            'cpu_baseline': cpu,
+        }
+        if sweep:
+            line['batch_sweep_frames_per_s'] = sweep
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

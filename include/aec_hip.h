@@ -1,0 +1,117 @@
+/*
+ * aec_hip.h — C ABI of libaec_hip.so, the MI355X (gfx950) Stage-2 AEC hot path.
+ *
+ * Drop-in boundary for the reference's Stage-2 inference path
+ * (SZU-Speech/Acoustic-Echo-Cancellation, Stage2_lhm/):
+ *
+ *   aec_create / aec_set_weights / aec_set_erb
+ *        replace  Little_net.__init__ + net.load_state_dict(...)
+ *                 (scripts/network/ERB.py:204-229, scripts/test.py:102-124)
+ *                 and the ERB matrix upload (scripts/test.py:108-111).
+ *   aec_process
+ *        replaces Little_net.forward(mic, ref, near, erb) -> (out_wav, loss)
+ *                 (scripts/network/ERB.py:252-334) as called at
+ *                 scripts/test.py:157, with batch=1 semantics per stream
+ *                 (per-stream normaliser over its true length).
+ *   aec_debug_copy
+ *        exposes the intermediates the reference computes inside forward
+ *        (ERB.py:282-307) for parity tests.
+ *
+ * Conventions: plain pointers and sizes only.  Signal / output / loss
+ * pointers are DEVICE pointers (e.g. torch tensor data_ptr()); weights, ERB
+ * matrix and lengths are HOST pointers.  `stream` is a hipStream_t passed as
+ * void* (NULL = the null stream).  Calls are asynchronous on `stream`.
+ * Errors are integer status codes; no exceptions cross the ABI;
+ * aec_last_error() describes the last failure on a handle.
+ * One handle per device; calls on one handle must be serialised by the caller.
+ */
+#ifndef AEC_HIP_H
+#define AEC_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    AEC_OK = 0,
+    AEC_ERR_INVALID_ARG = 1,
+    AEC_ERR_OOM = 2,
+    AEC_ERR_HIP = 3,
+    AEC_ERR_UNSUPPORTED = 4
+} aec_status;
+
+typedef struct aec_handle aec_handle;
+
+/* Mirrors speech_conf/erb_conf (scripts/configs.py:1-8,21-27) + the
+ * build-defined FD-NLMS stage (no reference counterpart; nlms_taps = 0 is the
+ * reference-parity bypass). */
+typedef struct {
+    int32_t win_size;    /* 512  (speech_conf['win_size'])  — only 512 supported  */
+    int32_t hop_size;    /* 256  (speech_conf['hop_size'])  — only 256 supported  */
+    int32_t erb_bands;   /* 32   (erb_conf['total_erb_bands']); GRU hidden = bands */
+    int32_t nlms_taps;   /* 0 = bypass; 1..8 taps per bin                          */
+    float   nlms_mu;     /* step size                                               */
+    float   nlms_beta;   /* far-end power smoothing                                 */
+    float   nlms_delta;  /* regulariser                                             */
+    int32_t reserved;
+} aec_config;
+
+/* Number of floats in the weights blob: the reference state_dict parameters
+ * concatenated in state_dict order (gru1.weight_ih_l0 [96,64],
+ * gru1.weight_hh_l0 [96,32], gru1.bias_ih_l0 [96], gru1.bias_hh_l0 [96],
+ * linear1.weight [32,64], linear1.bias [32], linear2.weight [32,32],
+ * linear2.bias [32]) = 12,544 for 32 bands. */
+size_t aec_weights_count(int32_t erb_bands);
+
+/* Create a handle on `device`.  weights: host blob (see above, may be NULL =
+ * zeros, set later); erb_257x32: host [257, bands] float32 row-major (may be
+ * NULL = set later). */
+aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weights,
+                      const float* erb_257xbands, int32_t device, aec_handle** out);
+
+aec_status aec_set_weights(aec_handle* h, const float* weights, size_t n_weights);
+aec_status aec_set_erb(aec_handle* h, const float* erb_257xbands);
+
+/* Run the whole hot path for B streams.
+ *   mic, ref : device [B, ld]   float32 (row b holds lengths[b] valid samples)
+ *   near     : device [B, ld]   float32 or NULL (then no loss is computed)
+ *   lengths  : host   [B]       int64, each in [1, ld]
+ *   out      : device [B, ld_out] float32; row b receives 256*(lengths[b]/256)
+ *              samples (the reference's output length), the rest is untouched
+ *   loss     : device [B] float32 or NULL; loss[b] = sum_{t,j}
+ *              (near_erb^0.5 - est_erb^0.5)^2 / (T_b * bands)   (ERB.py:318-323)
+ */
+aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const float* near,
+                       const int64_t* lengths, int32_t B, int64_t ld,
+                       float* out, int64_t ld_out, float* loss, void* stream);
+
+/* Debug / parity: copy an intermediate of the LAST aec_process call into the
+ * device buffer dst ([B, T_max, 32] float32, frames beyond a stream's T left
+ * unspecified).  Requires aec_set_debug(h, 1) before that call.
+ * what: 0 = mic_erb, 1 = ref_erb, 2 = near_erb, 3 = gru_out (h_t),
+ *       4 = mask, 5 = est_erb. */
+aec_status aec_set_debug(aec_handle* h, int32_t enable);
+aec_status aec_debug_copy(aec_handle* h, int32_t what, float* dst, size_t n_floats, void* stream);
+
+/* Kernel timing: when enabled, aec_process records a HIP event before and
+ * after each of its kernels on `stream`.  aec_profile_read waits for those
+ * events, returns the summed milliseconds per kernel (ms[0..3] = moments,
+ * analysis, gru, synthesis) over all calls since the previous read and the
+ * number of calls, and clears the record. */
+aec_status aec_profile_enable(aec_handle* h, int32_t enable);
+aec_status aec_profile_read(aec_handle* h, double* ms4, int64_t* calls);
+
+/* Frame / output-length integers (bit-exact framing contract). */
+int64_t aec_num_frames(int64_t n_samples);   /* n//256 + 1 */
+int64_t aec_out_len(int64_t n_samples);      /* 256*(n//256) */
+
+const char* aec_last_error(const aec_handle* h);
+void aec_destroy(aec_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AEC_HIP_H */
