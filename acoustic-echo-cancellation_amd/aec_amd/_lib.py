@@ -23,7 +23,7 @@ _STATUS = {0: 'AEC_OK', 1: 'AEC_ERR_INVALID_ARG', 2: 'AEC_ERR_OOM', 3: 'AEC_ERR_
 # every symbol include/aec_hip.h declares
 EXPORTS = ('aec_weights_count', 'aec_create', 'aec_set_weights', 'aec_set_erb', 'aec_process',
            'aec_set_debug', 'aec_debug_copy', 'aec_profile_enable', 'aec_profile_read',
-           'aec_num_frames', 'aec_out_len', 'aec_last_error', 'aec_destroy')
+           'aec_erb_tables_check', 'aec_num_frames', 'aec_out_len', 'aec_last_error', 'aec_destroy')
 
 
 class AecConfig(ctypes.Structure):
@@ -66,6 +66,8 @@ def load():
     lib.aec_profile_enable.restype = ctypes.c_int
     lib.aec_profile_read.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
     lib.aec_profile_read.restype = ctypes.c_int
+    lib.aec_erb_tables_check.argtypes = [P, P, P, P, P, ctypes.POINTER(ctypes.c_int32)]
+    lib.aec_erb_tables_check.restype = ctypes.c_int
     lib.aec_num_frames.argtypes = [ctypes.c_int64]
     lib.aec_num_frames.restype = ctypes.c_int64
     lib.aec_out_len.argtypes = [ctypes.c_int64]
@@ -86,6 +88,21 @@ def check(status, handle=None, what=''):
         m = _lib.aec_last_error(handle)
         msg = m.decode() if m else ''
     raise RuntimeError(f'{what} failed: {_STATUS.get(status, status)} {msg}'.strip())
+
+
+def erb_tables_check(erb, mags, est):
+    """Host-side application of the device ERB tables (include/aec_hip.h)."""
+    import numpy as np
+    lib = load()
+    erb = np.ascontiguousarray(erb, np.float32)
+    mags = np.ascontiguousarray(mags, np.float32)
+    est = np.ascontiguousarray(est, np.float32)
+    bands = np.zeros(32, np.float32)
+    gains = np.zeros(257, np.float32)
+    L = ctypes.c_int32()
+    check(lib.aec_erb_tables_check(erb.ctypes.data, mags.ctypes.data, est.ctypes.data, bands.ctypes.data,
+                                   gains.ctypes.data, ctypes.byref(L)), None, 'aec_erb_tables_check')
+    return bands, gains, int(L.value)
 
 
 class Handle:

@@ -187,7 +187,7 @@ class Little_net(nn.Module):
         if B > 0:
             with torch.cuda.device(dev):
                 h.process(mic.data_ptr(), ref.data_ptr(), near.data_ptr() if near is not None else None,
-                          lengths, B, L, out.data_ptr(), max(lout, 1), loss.data_ptr() if loss is not None else None,
+                          lengths, B, L, out.data_ptr() if lout > 0 else None, max(lout, 1), loss.data_ptr() if loss is not None else None,
                           stream)
         return out, loss
 

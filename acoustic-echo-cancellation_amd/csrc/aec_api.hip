@@ -8,6 +8,8 @@
 
 #include <cmath>
 #include <cstdio>
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -17,6 +19,105 @@
 #include "aec_launch.h"
 #include "aec_tables.h"
 
+
+// ---------------------------------------------------------------------------
+// ERB tables (see aec_tables.h): balanced forward schedule + transpose table
+// ---------------------------------------------------------------------------
+namespace aec {
+ErbTables build_erb_tables(const float* erb) {
+    const int NB = 32, NF = 257, LANES = 16, SLOTS = 3;
+    ErbTables t;
+    std::vector<std::vector<int>> bins(NB);
+    int maxw = 0, nnz = 0;
+    for (int j = 0; j < NB; ++j) {
+        for (int k = 0; k < NF; ++k)
+            if (erb[k * NB + j] != 0.f) bins[j].push_back(k);
+        maxw = std::max(maxw, (int)bins[j].size());
+        nnz += (int)bins[j].size();
+    }
+    // transpose table: <= 2 bands per bin
+    t.bintab.assign(NF * 4, 0.f);
+    for (int k = 0; k < NF; ++k) {
+        int cnt = 0;
+        for (int j = 0; j < NB; ++j) {
+            const float v = erb[k * NB + j];
+            if (v == 0.f) continue;
+            if (cnt == 2) { t.why = "a bin lies in more than 2 bands"; return t; }
+            int ib = j;
+            std::memcpy(&t.bintab[k * 4 + 2 * cnt], &ib, 4);
+            t.bintab[k * 4 + 2 * cnt + 1] = v;
+            ++cnt;
+        }
+        if (cnt == 1) { int ib; std::memcpy(&ib, &t.bintab[k * 4], 4); std::memcpy(&t.bintab[k * 4 + 2], &ib, 4); }
+    }
+    // forward schedule: split bands wider than `split` in two, pack pieces
+    struct Piece { int band, first, count; };
+    for (int split = std::max(26, (maxw + 1) / 2); split <= NF; split += 2) {
+        std::vector<Piece> pieces;
+        for (int j = 0; j < NB; ++j) {
+            const int w = (int)bins[j].size();
+            if (w == 0) continue;
+            if (w > split) {
+                pieces.push_back({j, 0, (w + 1) / 2});
+                pieces.push_back({j, (w + 1) / 2, w - (w + 1) / 2});
+            } else {
+                pieces.push_back({j, 0, w});
+            }
+        }
+        std::stable_sort(pieces.begin(), pieces.end(), [](const Piece& a, const Piece& b) { return a.count > b.count; });
+        std::vector<std::vector<int>> lane(LANES);
+        std::vector<int> load(LANES, 0);
+        bool fits = true;
+        for (int p = 0; p < (int)pieces.size() && fits; ++p) {
+            int best = -1;
+            for (int l = 0; l < LANES; ++l)
+                if ((int)lane[l].size() < SLOTS && (best < 0 || load[l] < load[best])) best = l;
+            if (best < 0) fits = false;
+            else { lane[best].push_back(p); load[best] += pieces[p].count; }
+        }
+        if (!fits) continue;
+        int L = 0;
+        for (int l = 0; l < LANES; ++l) L = std::max(L, load[l]);
+        L = (L + 3) & ~3;
+        if (L > 48) { t.why = "ERB schedule longer than 48 entries per lane"; return t; }
+        t.sched_len = L;
+        t.sched.assign((size_t)L * LANES * 4 + 64, 0.f);
+        std::vector<int> comb(2 * NB, -1);
+        for (int l = 0; l < LANES; ++l) {
+            int e = 0;
+            for (int s = 0; s < (int)lane[l].size(); ++s) {
+                const Piece& pc = pieces[lane[l][s]];
+                for (int i = 0; i < pc.count; ++i, ++e) {
+                    const int k = bins[pc.band][pc.first + i];
+                    float* en = &t.sched[((size_t)e * LANES + l) * 4];
+                    std::memcpy(&en[0], &k, 4);
+                    en[1 + s] = erb[k * NB + pc.band];
+                }
+                const int slot = 3 * l + s;
+                if (comb[2 * pc.band] < 0) comb[2 * pc.band] = slot;
+                else comb[2 * pc.band + 1] = slot;
+            }
+            // padding entries: bin 0, all weights 0 (already zero-filled)
+        }
+        // bands with no non-zeros read a zero slot: point both at a lane with < 3 pieces, else -1 pair
+        for (int j = 0; j < NB; ++j) {
+            if (comb[2 * j] < 0) {
+                int z = -1;
+                for (int l = 0; l < LANES && z < 0; ++l)
+                    if ((int)lane[l].size() < SLOTS) z = 3 * l + (int)lane[l].size();
+                if (z < 0) { t.why = "no zero slot for an empty band"; return t; }
+                comb[2 * j] = z;
+            }
+        }
+        std::memcpy(&t.sched[(size_t)L * LANES * 4], comb.data(), 64 * 4);
+        t.ok = true;
+        return t;
+    }
+    t.why = "could not balance the ERB schedule";
+    return t;
+}
+}  // namespace aec
+
 using namespace aec;
 
 struct aec_handle {
@@ -25,18 +126,20 @@ struct aec_handle {
     std::string err;
     float* d_w = nullptr;        // weights blob
     DevTables* d_tab = nullptr;
-    int* d_erb = nullptr;        // ErbCSR blob
-    int nnz = 0;
+    float* d_sched = nullptr;    // ERB forward schedule (ErbTables::sched)
+    float* d_bintab = nullptr;   // ERB transpose table (ErbTables::bintab)
+    int sched_len = 0;
     bool have_w = false, have_erb = false;
     // workspace (grow-only)
     int64_t ws_B = 0, ws_T = 0;
-    float* d_c = nullptr;        // [B][3]
+    double2* d_mom = nullptr;    // [B][3][kMomChunks]
     int64_t* d_len = nullptr;    // [B]
     float* d_feats = nullptr;    // [B][T][96]
     float* d_est = nullptr;      // [B][T][32]
     float* d_dbg = nullptr;      // [2][B][T][32]  (h, mask)
     std::vector<int64_t> last_lens;
     int debug = 0;
+    int gru_mode = 0;            // AEC_GRU_MODE (timing experiments; results invalid unless 0)
     int64_t last_B = 0, last_T = 0;
     // kernel timing (aec_profile_*)
     int profile = 0;
@@ -90,7 +193,7 @@ static void build_tables(DevTables& t) {
     for (int r = 0; r < 256; ++r) {
         const float a = t.hann[r], b = t.hann[r + 256];
         const float c = a * a + b * b;      // f32, as conv_transpose1d(window^2, eye) does
-        t.coffp[r] = c + 1e-8f;
+        t.inv_coff[r] = (float)(1.0 / (double)(c + 1e-8f));
     }
 }
 
@@ -106,39 +209,17 @@ aec_status aec_set_weights(aec_handle* h, const float* w, size_t n) {
 aec_status aec_set_erb(aec_handle* h, const float* erb) {
     if (!h) return AEC_ERR_INVALID_ARG;
     if (!erb) return fail(h, AEC_ERR_INVALID_ARG, "erb matrix is null");
-    const int NB = 32, NF = 257;
-    std::vector<int> band_ptr(NB + 1, 0), bin_ptr(NF + 1, 0), band_bin, bin_band;
-    std::vector<float> band_w, bin_w;
-    for (int j = 0; j < NB; ++j) {
-        band_ptr[j] = (int)band_bin.size();
-        for (int k = 0; k < NF; ++k) {
-            const float v = erb[k * NB + j];
-            if (v != 0.f) { band_bin.push_back(k); band_w.push_back(v); }
-        }
-    }
-    band_ptr[NB] = (int)band_bin.size();
-    for (int k = 0; k < NF; ++k) {
-        bin_ptr[k] = (int)bin_band.size();
-        for (int j = 0; j < NB; ++j) {
-            const float v = erb[k * NB + j];
-            if (v != 0.f) { bin_band.push_back(j); bin_w.push_back(v); }
-        }
-    }
-    bin_ptr[NF] = (int)bin_band.size();
-    const int nnz = (int)band_bin.size();
-    if (nnz > 2048) return fail(h, AEC_ERR_UNSUPPORTED, "erb matrix has > 2048 non-zeros (banded filterbanks only)");
-    std::vector<int> blob(erb_blob_words(nnz), 0);
-    std::memcpy(blob.data(), band_ptr.data(), 33 * 4);
-    std::memcpy(blob.data() + 33, bin_ptr.data(), 258 * 4);
-    std::memcpy(blob.data() + 33 + 258, band_bin.data(), nnz * 4);
-    std::memcpy(blob.data() + 33 + 258 + nnz, band_w.data(), nnz * 4);
-    std::memcpy(blob.data() + 33 + 258 + 2 * nnz, bin_band.data(), nnz * 4);
-    std::memcpy(blob.data() + 33 + 258 + 3 * nnz, bin_w.data(), nnz * 4);
+    const ErbTables t = build_erb_tables(erb);
+    if (!t.ok) return fail(h, AEC_ERR_UNSUPPORTED, std::string("erb matrix: ") + t.why);
     HIP_TRY(h, hipSetDevice(h->device));
-    if (h->d_erb) { HIP_TRY(h, hipFree(h->d_erb)); h->d_erb = nullptr; }
-    HIP_TRY(h, hipMalloc(&h->d_erb, blob.size() * 4));
-    HIP_TRY(h, hipMemcpy(h->d_erb, blob.data(), blob.size() * 4, hipMemcpyHostToDevice));
-    h->nnz = nnz;
+    HIP_TRY(h, hipDeviceSynchronize());   // the previous tables may still be in use
+    if (h->d_sched) { HIP_TRY(h, hipFree(h->d_sched)); h->d_sched = nullptr; }
+    if (h->d_bintab) { HIP_TRY(h, hipFree(h->d_bintab)); h->d_bintab = nullptr; }
+    HIP_TRY(h, hipMalloc(&h->d_sched, t.sched.size() * 4));
+    HIP_TRY(h, hipMemcpy(h->d_sched, t.sched.data(), t.sched.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(h, hipMalloc(&h->d_bintab, t.bintab.size() * 4));
+    HIP_TRY(h, hipMemcpy(h->d_bintab, t.bintab.data(), t.bintab.size() * 4, hipMemcpyHostToDevice));
+    h->sched_len = t.sched_len;
     h->have_erb = true;
     return AEC_OK;
 }
@@ -154,6 +235,7 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
     if (!h) return AEC_ERR_OOM;
     h->cfg = *cfg;
     h->device = device;
+    if (const char* m = std::getenv("AEC_GRU_MODE")) h->gru_mode = std::atoi(m);
     auto bail = [&](aec_status s) { aec_destroy(h); return s; };
     if (hipSetDevice(device) != hipSuccess) return bail(AEC_ERR_HIP);
     if (hipMalloc(&h->d_w, kWeights32 * sizeof(float)) != hipSuccess) return bail(AEC_ERR_OOM);
@@ -176,11 +258,11 @@ static aec_status ensure_ws(aec_handle* h, int64_t B, int64_t T) {
     const int64_t nB = B > h->ws_B ? B : h->ws_B;
     const int64_t nT = T > h->ws_T ? T : h->ws_T;
     HIP_TRY(h, hipDeviceSynchronize());
-    (void)hipFree(h->d_c); (void)hipFree(h->d_len); (void)hipFree(h->d_feats); (void)hipFree(h->d_est); (void)hipFree(h->d_dbg);
-    h->d_c = nullptr; h->d_len = nullptr; h->d_feats = h->d_est = h->d_dbg = nullptr;
+    (void)hipFree(h->d_mom); (void)hipFree(h->d_len); (void)hipFree(h->d_feats); (void)hipFree(h->d_est); (void)hipFree(h->d_dbg);
+    h->d_mom = nullptr; h->d_len = nullptr; h->d_feats = h->d_est = h->d_dbg = nullptr;
     h->ws_B = h->ws_T = 0;
     h->last_lens.clear();
-    HIP_TRY(h, hipMalloc(&h->d_c, nB * 3 * sizeof(float)));
+    HIP_TRY(h, hipMalloc(&h->d_mom, nB * 3 * kMomChunks * sizeof(double2)));
     HIP_TRY(h, hipMalloc(&h->d_len, nB * sizeof(int64_t)));
     HIP_TRY(h, hipMalloc(&h->d_feats, nB * nT * 96 * sizeof(float)));
     HIP_TRY(h, hipMalloc(&h->d_est, nB * nT * 32 * sizeof(float)));
@@ -203,7 +285,7 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
     if (!h->have_w || !h->have_erb) return fail(h, AEC_ERR_INVALID_ARG, "weights / erb not set");
     if (B < 0 || !lengths) return fail(h, AEC_ERR_INVALID_ARG, "bad batch / lengths");
     if (B == 0) return AEC_OK;
-    if (!mic || !ref || !out) return fail(h, AEC_ERR_INVALID_ARG, "null mic / ref / out");
+    if (!mic || !ref) return fail(h, AEC_ERR_INVALID_ARG, "null mic / ref");
     if (loss && !near) return fail(h, AEC_ERR_INVALID_ARG, "loss requires near");
     int64_t nmax = 0;
     for (int b = 0; b < B; ++b) {
@@ -211,6 +293,7 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
         if (aec_out_len(lengths[b]) > ld_out) return fail(h, AEC_ERR_INVALID_ARG, "ld_out too small");
         nmax = lengths[b] > nmax ? lengths[b] : nmax;
     }
+    if (!out && aec_out_len(nmax) > 0) return fail(h, AEC_ERR_INVALID_ARG, "null out");
     const int64_t Tmax = aec_num_frames(nmax);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     HIP_TRY(h, hipSetDevice(h->device));
@@ -223,13 +306,13 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
     }
     const int nsig = near ? 3 : 2;
     mark(h, st);
-    HIP_TRY(h, launch_moments(mic, ref, near, ld, h->d_len, h->d_c, B, nsig, st));
+    HIP_TRY(h, launch_moments(mic, ref, near, ld, h->d_len, h->d_mom, B, nsig, st));
 
     AnalysisArgs a{};
     a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
-    a.ld = ld; a.lens = h->d_len; a.cvals = h->d_c;
+    a.ld = ld; a.lens = h->d_len; a.mom = h->d_mom;
     a.tables = reinterpret_cast<const float*>(h->d_tab);
-    a.erb_csr = h->d_erb; a.nnz = h->nnz; a.nsig = nsig;
+    a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
     a.feats = h->d_feats; a.Tmax = Tmax;
     mark(h, st);
     HIP_TRY(h, launch_analysis(a, B, st));
@@ -240,13 +323,14 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
     g.est = h->d_est; g.loss = loss; g.has_near = near != nullptr;
     g.dbg_h = h->debug ? h->d_dbg : nullptr;
     g.dbg_mask = h->debug ? h->d_dbg + B * Tmax * 32 : nullptr;
+    g.mode = h->gru_mode;
     HIP_TRY(h, launch_gru(g, B, st));
     mark(h, st);
 
     SynthArgs y{};
-    y.mic = mic; y.ld = ld; y.lens = h->d_len; y.cvals = h->d_c;
+    y.mic = mic; y.ld = ld; y.lens = h->d_len; y.mom = h->d_mom;
     y.tables = reinterpret_cast<const float*>(h->d_tab);
-    y.erb_csr = h->d_erb; y.nnz = h->nnz; y.est = h->d_est; y.Tmax = Tmax;
+    y.bintab = h->d_bintab; y.est = h->d_est; y.Tmax = Tmax;
     y.out = out; y.ld_out = ld_out;
     HIP_TRY(h, launch_synthesis(y, B, st));
     mark(h, st);
@@ -303,12 +387,43 @@ aec_status aec_profile_read(aec_handle* h, double* ms4, int64_t* calls) {
     return AEC_OK;
 }
 
+aec_status aec_erb_tables_check(const float* erb, const float* mags, const float* est, float* bands,
+                                float* gains, int32_t* sched_len) {
+    if (!erb || !mags || !est || !bands || !gains) return AEC_ERR_INVALID_ARG;
+    const ErbTables t = build_erb_tables(erb);
+    if (!t.ok) return AEC_ERR_UNSUPPORTED;
+    const int L = t.sched_len;
+    float part[48];
+    for (int l = 0; l < 16; ++l) {
+        float a[3] = {0.f, 0.f, 0.f};
+        for (int e = 0; e < L; ++e) {
+            const float* en = &t.sched[((size_t)e * 16 + l) * 4];
+            int k;
+            std::memcpy(&k, en, 4);
+            for (int s = 0; s < 3; ++s) a[s] = std::fma(en[1 + s], mags[k], a[s]);
+        }
+        for (int s = 0; s < 3; ++s) part[3 * l + s] = a[s];
+    }
+    int comb[64];
+    std::memcpy(comb, &t.sched[(size_t)L * 16 * 4], sizeof(comb));
+    for (int j = 0; j < 32; ++j) bands[j] = part[comb[2 * j]] + (comb[2 * j + 1] >= 0 ? part[comb[2 * j + 1]] : 0.f);
+    for (int k = 0; k < 257; ++k) {
+        const float* e = &t.bintab[k * 4];
+        int ja, jb;
+        std::memcpy(&ja, &e[0], 4);
+        std::memcpy(&jb, &e[2], 4);
+        gains[k] = e[1] * est[ja] + e[3] * est[jb];
+    }
+    if (sched_len) *sched_len = L;
+    return AEC_OK;
+}
+
 void aec_destroy(aec_handle* h) {
     if (!h) return;
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     (void)hipSetDevice(h->device);
-    (void)hipFree(h->d_w); (void)hipFree(h->d_tab); (void)hipFree(h->d_erb);
-    (void)hipFree(h->d_c); (void)hipFree(h->d_len); (void)hipFree(h->d_feats); (void)hipFree(h->d_est); (void)hipFree(h->d_dbg);
+    (void)hipFree(h->d_w); (void)hipFree(h->d_tab); (void)hipFree(h->d_sched); (void)hipFree(h->d_bintab);
+    (void)hipFree(h->d_mom); (void)hipFree(h->d_len); (void)hipFree(h->d_feats); (void)hipFree(h->d_est); (void)hipFree(h->d_dbg);
     delete h;
 }
 

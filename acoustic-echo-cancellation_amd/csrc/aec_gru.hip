@@ -1,0 +1,231 @@
+// aec_gru.hip — the recurrent part of the Stage-2 post-filter on gfx950.
+//
+// Reference: nn.GRU(64, 32) + linear1/relu + linear2/sigmoid + mask
+// (Stage2_lhm/scripts/network/ERB.py:213-217, 287-304) and the loss (:318-323).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "aec_fft.h"
+#include "aec_launch.h"
+
+namespace aec {
+
+// --------------------------------------------------------------------------
+// K3: GRU recurrence + head.  grid = B, block = 256:
+//   wave 0      : the recurrence (h_t depends on h_{t-1}); one step per frame
+//   waves 1..3  : helpers, software-pipelined one chunk (16 frames) ahead and
+//                 behind the recurrence: x-load (c+2), gi = W_ih x + b (c+1),
+//                 head / mask / est_erb / loss (c-1)
+// --------------------------------------------------------------------------
+
+__device__ __forceinline__ float sigmoidf_(float x) {
+    return __builtin_amdgcn_rcpf(1.f + __expf(-x));
+}
+__device__ __forceinline__ float tanhf_(float x) {
+    return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x));
+}
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+
+__global__ __launch_bounds__(256) void gru_kernel(GruArgs p) {
+    __shared__ __attribute__((aligned(16))) float sX[2][kCH][64];
+    __shared__ __attribute__((aligned(16))) float sGi[2][kCH][96];
+    __shared__ __attribute__((aligned(16))) float sH[2][kCH][32];
+    __shared__ __attribute__((aligned(16))) float sMic[4][kCH][32];
+    __shared__ __attribute__((aligned(16))) float sO[6][32];
+    __shared__ float sLoss[4];
+
+    const int b = blockIdx.x;
+    const int64_t n = p.lens[b];
+    const int T = (int)(n / kHop + 1);
+    const int nch = (T + kCH - 1) / kCH;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const float* W_ih = p.w;                  // [96][64]
+    const float* W_hh = p.w + 96 * 64;        // [96][32]
+    const float* b_ih = W_hh + 96 * 32;       // [96]
+    const float* b_hh = b_ih + 96;            // [96]
+    const float* W1 = b_hh + 96;              // [32][64]
+    const float* b1 = W1 + 32 * 64;           // [32]
+    const float* W2 = b1 + 32;                // [32][32]
+    const float* b2 = W2 + 32 * 32;           // [32]
+    const float* fb = p.feats + (int64_t)b * p.Tmax * 96;
+
+    if (wave == 0) {
+        // ---------------- recurrence wave ----------------
+        const bool run = p.mode != 2;
+        // lane l: j = l & 31, half = l >> 5.  Row pair per lane: (r_j, n_j) in
+        // half 0, (z_j, n_j) in half 1, full 32-long dot products with h held
+        // wave-uniform in SGPRs (v_readlane), so no LDS round trip sits on the
+        // h_{t-1} -> h_t chain; h_j is computed identically in both halves.
+        const int j = lane & 31, half = lane >> 5;
+        f2v w[32];
+        {
+            const float* rA = W_hh + (half ? (32 + j) : j) * 32;
+            const float* rN = W_hh + (64 + j) * 32;
+#pragma unroll
+            for (int k = 0; k < 32; ++k) w[k] = f2v{rA[k], rN[k]};
+        }
+        const float bhn = b_hh[64 + j];
+        float hj = 0.f;                                   // h_{-1} = 0
+        for (int c = -2; c <= nch; ++c) {
+            if (run && c >= 0 && c < nch) {
+                const int f_end = min(kCH, T - c * kCH);
+                const float* gi = &sGi[c & 1][0][0];
+                float gr = gi[j], gz = gi[32 + j], gn = gi[64 + j];
+                for (int f = 0; f < f_end; ++f) {
+                    // prefetch next step's input projections (independent of h)
+                    const int fn = f + 1 < f_end ? f + 1 : f;
+                    const float ngr = gi[fn * 96 + j], ngz = gi[fn * 96 + 32 + j], ngn = gi[fn * 96 + 64 + j];
+                    float hk[32];
+#pragma unroll
+                    for (int k = 0; k < 32; ++k) hk[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hj), k));
+                    __builtin_amdgcn_sched_barrier(0);
+                    f2v acc[4] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}};
+#pragma unroll
+                    for (int k = 0; k < 32; ++k) acc[k & 3] = __builtin_elementwise_fma(w[k], f2v{hk[k], hk[k]}, acc[k & 3]);
+                    const f2v acc2 = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+                    const float sA = acc2.x;           // r-dot (half 0) or z-dot (half 1)
+                    const float sN = acc2.y;           // n-dot (both halves)
+                    // v_permlane32_swap: lanes 32..63 of vdst <-> lanes 0..31 of vsrc, so the
+                    // other half's value is res[1] in lanes 0..31 and res[0] in lanes 32..63
+                    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(sA), __float_as_uint(sA), false, false);
+                    const float other = __uint_as_float(half ? sw[0] : sw[1]);
+                    const float rdot = half ? other : sA;
+                    const float zdot = half ? sA : other;
+                    const float r = sigmoidf_(gr + rdot);
+                    const float z = sigmoidf_(gz + zdot);
+                    const float nn = tanhf_(gn + r * (sN + bhn));
+                    hj = (1.f - z) * nn + z * hj;
+                    if (half == 0) sH[c & 1][f][j] = hj;  // for the head (off the chain)
+                    gr = ngr; gz = ngz; gn = ngn;
+                }
+            }
+            __syncthreads();
+        }
+    } else {
+        // ---------------- helper waves ----------------
+        const int hl = tid - 64;                       // 0..191
+        // gi role: row = hl % 96, frames f = fpar, fpar+2, ...
+        const int grow = hl % 96, gpar = hl / 96;
+        float wih[64];
+#pragma unroll
+        for (int k = 0; k < 64; ++k) wih[k] = W_ih[grow * 64 + k];
+        const float gbias = b_ih[grow] + (grow < 64 ? b_hh[grow] : 0.f);
+        // head role: j = hl & 31, frames f = fg, fg+6, fg+12
+        const int hj_ = hl & 31, fg = hl >> 5;
+        float w1[64], w2[32];
+#pragma unroll
+        for (int k = 0; k < 64; ++k) w1[k] = W1[hj_ * 64 + k];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) w2[k] = W2[hj_ * 32 + k];
+        const float b1j = b1[hj_], b2j = b2[hj_];
+        float lacc = 0.f;
+
+        const bool run = p.mode != 1;
+        for (int c = -2; c <= nch; ++c) {
+            // (a) x-load for chunk c+2 -> sX[(c+2)&1], mic_erb -> sMic[(c+2)&3]
+            {
+                const int cc = c + 2;
+                if (run && cc < nch) {
+                    for (int e = hl; e < kCH * 32; e += 192) {
+                        const int f = e >> 5, jj = e & 31;
+                        const int t = cc * kCH + f;
+                        float me = 0.f, re = 0.f;
+                        if (t < T) {
+                            me = fb[(int64_t)t * 96 + jj];
+                            re = fb[(int64_t)t * 96 + 32 + jj];
+                        }
+                        sX[cc & 1][f][jj] = me;
+                        sX[cc & 1][f][32 + jj] = fabsf(me - re);
+                        sMic[cc & 3][f][jj] = me;
+                    }
+                }
+            }
+            // (b) gi for chunk c+1
+            {
+                const int cc = c + 1;
+                if (run && cc >= 0 && cc < nch) {
+                    for (int f = gpar; f < kCH; f += 2) {
+                        const float4* x4 = reinterpret_cast<const float4*>(&sX[cc & 1][f][0]);
+                        f2v a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
+#pragma unroll
+                        for (int q = 0; q < 16; ++q) {
+                            const float4 xv = x4[q];
+                            a0 = __builtin_elementwise_fma(f2v{wih[4 * q], wih[4 * q + 1]}, f2v{xv.x, xv.y}, a0);
+                            a1 = __builtin_elementwise_fma(f2v{wih[4 * q + 2], wih[4 * q + 3]}, f2v{xv.z, xv.w}, a1);
+                        }
+                        const f2v s2 = a0 + a1;
+                        sGi[cc & 1][f][grow] = gbias + (s2.x + s2.y);
+                    }
+                }
+            }
+            // (c) head for chunk c-1
+            {
+                const int cc = c - 1;
+                if (run && cc >= 0 && cc < nch) {
+                    for (int f = fg; f < kCH; f += 6) {
+                        const int t = cc * kCH + f;
+                        if (t >= T) break;               // uniform within the 32-lane group
+                        const float4* h4 = reinterpret_cast<const float4*>(&sH[cc & 1][f][0]);
+                        const float4* m4 = reinterpret_cast<const float4*>(&sMic[cc & 3][f][0]);
+                        f2v a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) {
+                            const float4 hv = h4[q];
+                            const float4 mv = m4[q];
+                            a0 = __builtin_elementwise_fma(f2v{w1[4 * q], w1[4 * q + 1]}, f2v{hv.x, hv.y}, a0);
+                            a1 = __builtin_elementwise_fma(f2v{w1[4 * q + 2], w1[4 * q + 3]}, f2v{hv.z, hv.w}, a1);
+                            a0 = __builtin_elementwise_fma(f2v{w1[32 + 4 * q], w1[32 + 4 * q + 1]}, f2v{mv.x, mv.y}, a0);
+                            a1 = __builtin_elementwise_fma(f2v{w1[32 + 4 * q + 2], w1[32 + 4 * q + 3]}, f2v{mv.z, mv.w}, a1);
+                        }
+                        const f2v s1 = a0 + a1;
+                        const float o = fmaxf(b1j + (s1.x + s1.y), 0.f);
+                        sO[fg][hj_] = o;
+                        wave_fence();
+                        const float4* o4 = reinterpret_cast<const float4*>(&sO[fg][0]);
+                        f2v c0 = {0.f, 0.f}, c1 = {0.f, 0.f};
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) {
+                            const float4 ov = o4[q];
+                            c0 = __builtin_elementwise_fma(f2v{w2[4 * q], w2[4 * q + 1]}, f2v{ov.x, ov.y}, c0);
+                            c1 = __builtin_elementwise_fma(f2v{w2[4 * q + 2], w2[4 * q + 3]}, f2v{ov.z, ov.w}, c1);
+                        }
+                        wave_fence();
+                        const f2v s2 = c0 + c1;
+                        const float mask = sigmoidf_(b2j + (s2.x + s2.y));
+                        const float me = sMic[cc & 3][f][hj_];
+                        const float est = mask * me;
+                        const int64_t o_idx = ((int64_t)b * p.Tmax + t) * 32 + hj_;
+                        p.est[o_idx] = est;
+                        if (p.dbg_h) p.dbg_h[o_idx] = sH[cc & 1][f][hj_];
+                        if (p.dbg_mask) p.dbg_mask[o_idx] = mask;
+                        if (p.has_near) {
+                            const float ne = fb[(int64_t)t * 96 + 64 + hj_];
+                            const float d = sqrtf(ne) - sqrtf(est);
+                            lacc += d * d;
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        if (p.loss) {
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) lacc += __shfl_xor(lacc, o);
+            if (lane == 0) sLoss[wave] = lacc;
+        }
+    }
+    if (p.loss) {
+        __syncthreads();
+        if (tid == 0) p.loss[b] = ((sLoss[1] + sLoss[2]) + sLoss[3]) / (float)(T * 32);
+    }
+}
+
+hipError_t launch_gru(const GruArgs& a, int B, hipStream_t st) {
+    hipLaunchKernelGGL(gru_kernel, dim3(B), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace aec

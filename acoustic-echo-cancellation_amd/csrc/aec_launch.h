@@ -10,15 +10,16 @@ namespace aec {
 constexpr int kFPB = 16;            // frames per analysis / synthesis block (16 groups x 16 lanes)
 constexpr int kHopsOut = kFPB - 1;  // output hops per synthesis block
 constexpr int kCH = 16;             // frames per chunk in the GRU pipeline
+constexpr int kMomChunks = 8;       // moment partials per (stream, signal)
 
 struct AnalysisArgs {
     const float* sig[3];
     int64_t ld;
     const int64_t* lens;
-    const float* cvals;
+    const double2* mom;      // [B][3][kMomChunks]
     const float* tables;     // DevTables
-    const int* erb_csr;      // ErbCSR blob
-    int nnz;
+    const float* sched;      // ERB schedule: float4[L][16] then int2[32] (aec_tables.h)
+    int sched_len;           // L (multiple of 4)
     int nsig;
     float* feats;            // [B][Tmax][96]
     int64_t Tmax;
@@ -34,16 +35,16 @@ struct GruArgs {
     int has_near;
     float* dbg_h;            // [B][Tmax][32] or null
     float* dbg_mask;         // [B][Tmax][32] or null
+    int mode;                // timing experiments only: 0 full, 1 recurrence only, 2 helpers only
 };
 
 struct SynthArgs {
     const float* mic;
     int64_t ld;
     const int64_t* lens;
-    const float* cvals;
+    const double2* mom;
     const float* tables;
-    const int* erb_csr;
-    int nnz;
+    const float* bintab;     // float4[257]: (band_a, w_a, band_b, w_b) per bin
     const float* est;        // [B][Tmax][32]
     int64_t Tmax;
     float* out;
@@ -51,17 +52,17 @@ struct SynthArgs {
 };
 
 // dynamic LDS bytes (must match the carve in the kernels)
-inline size_t analysis_smem_bytes(int nnz) {
+inline size_t analysis_smem_bytes(int sched_len) {
     const size_t fl = 256 * 2 + 258 * 2 + 512 + (size_t)kFPB * kGroupFloats;
-    return fl * 4 + (36 + (size_t)((nnz + 3) & ~3) + (size_t)nnz) * 4;
+    return fl * 4 + (size_t)sched_len * 16 * 16 + 32 * 8;
 }
-inline size_t synthesis_smem_bytes(int nnz) {
+inline size_t synthesis_smem_bytes() {
     const size_t fl = 256 * 2 + 258 * 2 + 512 + 256 + kFPB * 32 + (size_t)kFPB * kGroupFloats;
-    return fl * 4 + (260 + (size_t)((nnz + 3) & ~3) + (size_t)nnz) * 4;
+    return fl * 4 + 260 * 16;
 }
 
 hipError_t launch_moments(const float* mic, const float* ref, const float* near, int64_t ld,
-                          const int64_t* lens, float* cvals, int B, int nsig, hipStream_t st);
+                          const int64_t* lens, double2* mom, int B, int nsig, hipStream_t st);
 hipError_t launch_analysis(const AnalysisArgs& a, int B, hipStream_t st);
 hipError_t launch_gru(const GruArgs& a, int B, hipStream_t st);
 hipError_t launch_synthesis(const SynthArgs& a, int B, hipStream_t st);

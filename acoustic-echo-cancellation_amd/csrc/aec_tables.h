@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 namespace aec {
 
 // Built by the host at aec_create (float64 math, rounded to float32).
@@ -9,33 +11,33 @@ struct DevTables {
     float2 tw256[256];   // W256^j = (cos 2pi j/256, -sin 2pi j/256)
     float2 tw512[258];   // W512^k, k = 0..256 (+1 pad)
     float hann[512];     // periodic Hann = scipy get_window('hann', 512) (attention_ccrn.py:12)
-    float coffp[256];    // f32(hann[r]^2 + hann[r+256]^2) + 1e-8  (attention_ccrn.py:94-96)
+    float inv_coff[256]; // 1 / (f32(hann[r]^2 + hann[r+256]^2) + 1e-8)  (attention_ccrn.py:94-96)
 };
 
-// ERB matrix in two sparse views (the reference multiplies the dense [257,32]
-// matrix, ERB.py:282-284 and :306-307; only its 483 non-zeros matter).
-// Blob layout (int32 words; weights stored as float bit patterns):
-//   band_ptr[33] | bin_ptr[258] | band_bin[nnz] | band_w[nnz] | bin_band[nnz] | bin_w[nnz]
-struct ErbCSRView {
-    const int* band_ptr;
-    const int* bin_ptr;
-    const int* band_bin;
-    const float* band_w;
-    const int* bin_band;
-    const float* bin_w;
+// ERB matrix views.  The reference multiplies the dense [257,32] float32
+// matrix (ERB.py:282-284 forward, :306-307 transpose); only its non-zeros
+// (483 for erb_conf) matter, and every bin lies in at most 2 bands.
+//
+// Forward (bins -> bands), analysis kernel: a per-lane schedule for the 16
+// lanes of a frame group.  Bands wider than `split` bins are cut into two
+// pieces; the pieces are packed (first-fit decreasing, <= 3 pieces per lane)
+// so every lane runs the same L entries.  Entry = float4(bin as int bits,
+// w0, w1, w2): exactly one of w0..w2 is the matrix value (the piece's slot
+// in that lane), the others are 0, so the lane does 3 FMAs and no selects.
+// comb[j] = (slot index of piece 0, slot index of piece 1 or -1), slot index
+// = 3*lane + slot.  Blob = float4[L][16] followed by int2[32].
+//
+// Transpose (bands -> bins), synthesis kernel: float4[257] =
+// (band_a as int bits, w_a, band_b as int bits, w_b); w_b = 0 when the bin is
+// in one band, both 0 when in none (DC / Nyquist).
+struct ErbTables {
+    int sched_len = 0;
+    std::vector<float> sched;    // 16 * 4 * L floats + 64 ints (as floats)
+    std::vector<float> bintab;   // 257 * 4
+    bool ok = false;
+    const char* why = "";
 };
 
-__host__ __device__ inline ErbCSRView erb_view(const int* blob, int nnz) {
-    ErbCSRView v;
-    v.band_ptr = blob;
-    v.bin_ptr = blob + 33;
-    v.band_bin = blob + 33 + 258;
-    v.band_w = reinterpret_cast<const float*>(v.band_bin + nnz);
-    v.bin_band = reinterpret_cast<const int*>(v.band_w + nnz);
-    v.bin_w = reinterpret_cast<const float*>(v.bin_band + nnz);
-    return v;
-}
-
-inline size_t erb_blob_words(int nnz) { return 33 + 258 + 4 * (size_t)nnz; }
+ErbTables build_erb_tables(const float* erb /* [257][32] */);
 
 }  // namespace aec

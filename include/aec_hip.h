@@ -80,7 +80,8 @@ aec_status aec_set_erb(aec_handle* h, const float* erb_257xbands);
  *   near     : device [B, ld]   float32 or NULL (then no loss is computed)
  *   lengths  : host   [B]       int64, each in [1, ld]
  *   out      : device [B, ld_out] float32; row b receives 256*(lengths[b]/256)
- *              samples (the reference's output length), the rest is untouched
+ *              samples (the reference's output length), the rest is untouched;
+ *              may be NULL when every length is < 256 (empty outputs)
  *   loss     : device [B] float32 or NULL; loss[b] = sum_{t,j}
  *              (near_erb^0.5 - est_erb^0.5)^2 / (T_b * bands)   (ERB.py:318-323)
  */
@@ -103,6 +104,15 @@ aec_status aec_debug_copy(aec_handle* h, int32_t what, float* dst, size_t n_floa
  * number of calls, and clears the record. */
 aec_status aec_profile_enable(aec_handle* h, int32_t enable);
 aec_status aec_profile_read(aec_handle* h, double* ms4, int64_t* calls);
+
+/* Host-side check of the ERB tables the device uses (no GPU needed): builds
+ * the forward schedule / transpose table for erb_257xbands exactly as
+ * aec_set_erb does and applies them on the CPU:
+ *   bands[32]  = schedule applied to mags[257]   (== mags @ erb, ERB.py:282)
+ *   gains[257] = transpose table applied to est[32] (== est @ erb^T, ERB.py:306)
+ * Returns the schedule length per lane in *sched_len. */
+aec_status aec_erb_tables_check(const float* erb_257xbands, const float* mags, const float* est,
+                                float* bands, float* gains, int32_t* sched_len);
 
 /* Frame / output-length integers (bit-exact framing contract). */
 int64_t aec_num_frames(int64_t n_samples);   /* n//256 + 1 */

@@ -26,6 +26,14 @@ def _run(net, erb, mic, ref, near, dev='cuda:0'):
     return out[0].cpu().numpy(), (float(loss) if loss is not None else None)
 
 
+def _loss_ok(got, exp, tol=1e-4):
+    """Loss parity; an all-zero near signal makes the reference's normaliser
+    0/0 = NaN (ERB.py:256) and the loss NaN — both paths must then agree on NaN."""
+    if np.isnan(exp):
+        return bool(np.isnan(got))
+    return abs(got - exp) <= tol * max(1.0, abs(exp))
+
+
 def _rms(a, b):
     return float(np.sqrt(np.mean((np.asarray(a, np.float64) - b) ** 2))) if np.size(a) else 0.0
 
@@ -122,7 +130,7 @@ def test_vs_oracle_random_lengths(gpu_net, golden_weights, golden_erb, n):
     o, l = O.little_net_forward(mic, ref, near, golden_erb.astype(np.float32), golden_weights)
     assert out.shape == o.shape
     assert _rms(out, o) <= WAVE_RMS_TOL
-    assert abs(loss - l) <= 1e-4 * max(1.0, abs(l))
+    assert _loss_ok(loss, l)
 
 
 def test_near_none_and_unaligned_rows(gpu_net, golden_weights, golden_erb):
@@ -144,7 +152,7 @@ def test_near_none_and_unaligned_rows(gpu_net, golden_weights, golden_erb):
     for b in range(B):
         o, l = O.little_net_forward(mic[b], ref[b], near[b], golden_erb.astype(np.float32), golden_weights)
         assert _rms(o_b[b].cpu().numpy(), o) <= WAVE_RMS_TOL
-        assert abs(float(l_b[b]) - l) <= 1e-4 * max(1.0, abs(l))
+        assert _loss_ok(float(l_b[b]), l)
 
 
 def test_erle_delta_vs_oracle(gpu_net, golden_weights, golden_erb):

@@ -91,3 +91,26 @@ def test_cpu_tensors_fail_loudly(golden_erb):
     x = torch.zeros(1, 1000)
     with torch.no_grad(), pytest.raises(RuntimeError, match='HIP device'):
         net(x, x, x, torch.tensor(golden_erb, dtype=torch.float32))
+
+
+def test_erb_device_tables_match_dense(golden_erb):
+    """The balanced ERB schedule and the transpose table the kernels use
+    reproduce the reference's dense products mags @ erb and est @ erb^T."""
+    from aec_amd import _lib
+    rng = np.random.default_rng(0)
+    erb32 = golden_erb.astype(np.float32)
+    for _ in range(5):
+        mags = rng.uniform(0, 3, 257).astype(np.float32)
+        est = rng.uniform(0, 2, 32).astype(np.float32)
+        bands, gains, L = _lib.erb_tables_check(erb32, mags, est)
+        assert L == 32                                   # 483 nnz over 16 lanes, <= 32 entries each
+        ref_b = mags.astype(np.float64) @ erb32.astype(np.float64)
+        ref_g = est.astype(np.float64) @ erb32.T.astype(np.float64)
+        assert np.abs(bands - ref_b).max() <= 1e-5 * np.abs(ref_b).max()
+        assert np.abs(gains - ref_g).max() <= 1e-5 * np.abs(ref_g).max()
+    # a filterbank with a bin in 3 bands is refused (UNSUPPORTED), not silently wrong
+    bad = erb32.copy()
+    bad[100, :3] = 1.0
+    import pytest
+    with pytest.raises(RuntimeError, match='UNSUPPORTED'):
+        _lib.erb_tables_check(bad, mags, est)
