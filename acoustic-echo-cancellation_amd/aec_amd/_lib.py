@@ -66,7 +66,8 @@ def load():
     lib.aec_profile_enable.restype = ctypes.c_int
     lib.aec_profile_read.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
     lib.aec_profile_read.restype = ctypes.c_int
-    lib.aec_erb_tables_check.argtypes = [P, P, P, P, P, ctypes.POINTER(ctypes.c_int32)]
+    lib.aec_erb_tables_check.argtypes = [P, P, P, P, P, ctypes.POINTER(ctypes.c_int32),
+                                         ctypes.POINTER(ctypes.c_int32)]
     lib.aec_erb_tables_check.restype = ctypes.c_int
     lib.aec_num_frames.argtypes = [ctypes.c_int64]
     lib.aec_num_frames.restype = ctypes.c_int64
@@ -100,9 +101,11 @@ def erb_tables_check(erb, mags, est):
     bands = np.zeros(32, np.float32)
     gains = np.zeros(257, np.float32)
     L = ctypes.c_int32()
+    nc = ctypes.c_int32()
     check(lib.aec_erb_tables_check(erb.ctypes.data, mags.ctypes.data, est.ctypes.data, bands.ctypes.data,
-                                   gains.ctypes.data, ctypes.byref(L)), None, 'aec_erb_tables_check')
-    return bands, gains, int(L.value)
+                                   gains.ctypes.data, ctypes.byref(L), ctypes.byref(nc)), None,
+          'aec_erb_tables_check')
+    return bands, gains, int(L.value), int(nc.value)
 
 
 class Handle:

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <algorithm>
+#include <functional>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -83,21 +84,71 @@ ErbTables build_erb_tables(const float* erb) {
         t.sched_len = L;
         t.sched.assign((size_t)L * LANES * 4 + 64, 0.f);
         std::vector<int> comb(2 * NB, -1);
-        for (int l = 0; l < LANES; ++l) {
-            int e = 0;
+        // Order every lane's entries so that at each step the 16 lanes read
+        // bins with distinct residues mod 16: with the per-frame XOR swizzle the
+        // 32 lanes of a ds_read_b32 then hit 32 distinct banks.  One bipartite
+        // matching (lanes x residues, Kuhn) per step; lanes with no slack left
+        // must take a real entry, the others may take a zero-weight padding
+        // entry on a free residue (bin = residue).
+        struct Item { int k, s; float w; };
+        std::vector<std::vector<Item>> items(LANES);
+        for (int l = 0; l < LANES; ++l)
             for (int s = 0; s < (int)lane[l].size(); ++s) {
                 const Piece& pc = pieces[lane[l][s]];
-                for (int i = 0; i < pc.count; ++i, ++e) {
+                for (int i = 0; i < pc.count; ++i) {
                     const int k = bins[pc.band][pc.first + i];
-                    float* en = &t.sched[((size_t)e * LANES + l) * 4];
-                    std::memcpy(&en[0], &k, 4);
-                    en[1 + s] = erb[k * NB + pc.band];
+                    items[l].push_back({k, s, erb[k * NB + pc.band]});
                 }
                 const int slot = 3 * l + s;
                 if (comb[2 * pc.band] < 0) comb[2 * pc.band] = slot;
                 else comb[2 * pc.band + 1] = slot;
             }
-            // padding entries: bin 0, all weights 0 (already zero-filled)
+        t.conflicts = 0;
+        for (int e = 0; e < L; ++e) {
+            const int left = L - e;
+            std::vector<int> owner(16, -1), match(LANES, -1);
+            std::vector<int> order(LANES);
+            for (int l = 0; l < LANES; ++l) order[l] = l;
+            std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+                return left - (int)items[a].size() < left - (int)items[b].size(); });
+            std::function<bool(int, std::vector<char>&)> aug = [&](int l, std::vector<char>& seen) -> bool {
+                for (const Item& it : items[l]) {
+                    const int r = it.k & 15;
+                    if (seen[r]) continue;
+                    seen[r] = 1;
+                    if (owner[r] < 0 || aug(owner[r], seen)) { owner[r] = l; match[l] = r; return true; }
+                }
+                return false;
+            };
+            for (int l : order) {
+                if (items[l].empty()) continue;
+                std::vector<char> seen(16, 0);
+                aug(l, seen);
+            }
+            for (int l = 0; l < LANES; ++l) {
+                float* en = &t.sched[((size_t)e * LANES + l) * 4];
+                if (match[l] >= 0) {
+                    for (size_t i = 0; i < items[l].size(); ++i)
+                        if ((items[l][i].k & 15) == match[l]) {
+                            const Item it = items[l][i];
+                            std::memcpy(&en[0], &it.k, 4);
+                            en[1 + it.s] = it.w;
+                            items[l].erase(items[l].begin() + i);
+                            break;
+                        }
+                } else if ((int)items[l].size() >= left) {       // no slack: take one anyway
+                    const Item it = items[l].front();
+                    std::memcpy(&en[0], &it.k, 4);
+                    en[1 + it.s] = it.w;
+                    items[l].erase(items[l].begin());
+                    ++t.conflicts;
+                } else {                                          // zero-weight padding on a free residue
+                    int r = 0;
+                    while (owner[r] >= 0) ++r;
+                    owner[r] = l;
+                    std::memcpy(&en[0], &r, 4);
+                }
+            }
         }
         // bands with no non-zeros read a zero slot: point both at a lane with < 3 pieces, else -1 pair
         for (int j = 0; j < NB; ++j) {
@@ -133,6 +184,10 @@ struct aec_handle {
     // workspace (grow-only)
     int64_t ws_B = 0, ws_T = 0;
     double2* d_mom = nullptr;    // [B][3][kMomChunks]
+    float* d_cvals = nullptr;    // [B][3]
+    WorkItem* d_items = nullptr; // analysis work list (rebuilt when the lengths change)
+    int64_t items_cap = 0, nitems = 0;
+    int num_cus = 256;
     int64_t* d_len = nullptr;    // [B]
     float* d_feats = nullptr;    // [B][T][96]
     float* d_est = nullptr;      // [B][T][32]
@@ -187,7 +242,11 @@ const char* aec_last_error(const aec_handle* h) { return h ? h->err.c_str() : "n
 
 static void build_tables(DevTables& t) {
     const double PI = 3.14159265358979323846;
-    for (int j = 0; j < 256; ++j) t.tw256[j] = make_float2((float)std::cos(2 * PI * j / 256), (float)-std::sin(2 * PI * j / 256));
+    for (int k1 = 0; k1 < 16; ++k1)
+        for (int lb = 0; lb < 16; ++lb) {
+            const int j = (lb * k1) & 255;
+            t.twT[k1 * 16 + lb] = make_float2((float)std::cos(2 * PI * j / 256), (float)-std::sin(2 * PI * j / 256));
+        }
     for (int k = 0; k < 258; ++k) t.tw512[k] = make_float2((float)std::cos(2 * PI * k / 512), (float)-std::sin(2 * PI * k / 512));
     for (int n = 0; n < 512; ++n) t.hann[n] = (float)(0.5 - 0.5 * std::cos(2 * PI * n / 512));
     for (int r = 0; r < 256; ++r) {
@@ -236,6 +295,11 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
     h->cfg = *cfg;
     h->device = device;
     if (const char* m = std::getenv("AEC_GRU_MODE")) h->gru_mode = std::atoi(m);
+    {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+            h->num_cus = cus;
+    }
     auto bail = [&](aec_status s) { aec_destroy(h); return s; };
     if (hipSetDevice(device) != hipSuccess) return bail(AEC_ERR_HIP);
     if (hipMalloc(&h->d_w, kWeights32 * sizeof(float)) != hipSuccess) return bail(AEC_ERR_OOM);
@@ -258,11 +322,13 @@ static aec_status ensure_ws(aec_handle* h, int64_t B, int64_t T) {
     const int64_t nB = B > h->ws_B ? B : h->ws_B;
     const int64_t nT = T > h->ws_T ? T : h->ws_T;
     HIP_TRY(h, hipDeviceSynchronize());
-    (void)hipFree(h->d_mom); (void)hipFree(h->d_len); (void)hipFree(h->d_feats); (void)hipFree(h->d_est); (void)hipFree(h->d_dbg);
-    h->d_mom = nullptr; h->d_len = nullptr; h->d_feats = h->d_est = h->d_dbg = nullptr;
+    (void)hipFree(h->d_mom); (void)hipFree(h->d_cvals); (void)hipFree(h->d_len); (void)hipFree(h->d_feats);
+    (void)hipFree(h->d_est); (void)hipFree(h->d_dbg);
+    h->d_mom = nullptr; h->d_cvals = nullptr; h->d_len = nullptr; h->d_feats = h->d_est = h->d_dbg = nullptr;
     h->ws_B = h->ws_T = 0;
     h->last_lens.clear();
     HIP_TRY(h, hipMalloc(&h->d_mom, nB * 3 * kMomChunks * sizeof(double2)));
+    HIP_TRY(h, hipMalloc(&h->d_cvals, nB * 3 * sizeof(float)));
     HIP_TRY(h, hipMalloc(&h->d_len, nB * sizeof(int64_t)));
     HIP_TRY(h, hipMalloc(&h->d_feats, nB * nT * 96 * sizeof(float)));
     HIP_TRY(h, hipMalloc(&h->d_est, nB * nT * 32 * sizeof(float)));
@@ -290,6 +356,7 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
     int64_t nmax = 0;
     for (int b = 0; b < B; ++b) {
         if (lengths[b] < 1 || lengths[b] > ld) return fail(h, AEC_ERR_INVALID_ARG, "length out of [1, ld]");
+        if (lengths[b] > INT32_MAX - 4096) return fail(h, AEC_ERR_UNSUPPORTED, "stream longer than 2^31 - 4096 samples");
         if (aec_out_len(lengths[b]) > ld_out) return fail(h, AEC_ERR_INVALID_ARG, "ld_out too small");
         nmax = lengths[b] > nmax ? lengths[b] : nmax;
     }
@@ -301,21 +368,37 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
     if (s != AEC_OK) return s;
     if (h->last_lens.size() != (size_t)B || std::memcmp(h->last_lens.data(), lengths, B * sizeof(int64_t)) != 0) {
         h->last_lens.assign(lengths, lengths + B);
-        // pageable source: staged synchronously by the runtime, safe to reuse on return
+        // analysis work list: 4-frame items of every stream, valid frames only
+        std::vector<WorkItem> items;
+        for (int b = 0; b < B; ++b) {
+            const int64_t T = aec_num_frames(lengths[b]);
+            for (int64_t wt = 0; wt < T; wt += 4) items.push_back({b, (int32_t)wt, lengths[b]});
+        }
+        if ((int64_t)items.size() > h->items_cap) {
+            HIP_TRY(h, hipStreamSynchronize(st));
+            if (h->d_items) HIP_TRY(h, hipFree(h->d_items));
+            h->d_items = nullptr;
+            HIP_TRY(h, hipMalloc(&h->d_items, items.size() * sizeof(WorkItem)));
+            h->items_cap = (int64_t)items.size();
+        }
+        h->nitems = (int64_t)items.size();
+        // pageable sources: staged synchronously by the runtime, safe to reuse on return
         HIP_TRY(h, hipMemcpyAsync(h->d_len, h->last_lens.data(), B * sizeof(int64_t), hipMemcpyHostToDevice, st));
+        HIP_TRY(h, hipMemcpyAsync(h->d_items, items.data(), items.size() * sizeof(WorkItem), hipMemcpyHostToDevice, st));
     }
     const int nsig = near ? 3 : 2;
     mark(h, st);
     HIP_TRY(h, launch_moments(mic, ref, near, ld, h->d_len, h->d_mom, B, nsig, st));
+    HIP_TRY(h, launch_norm_finalize(h->d_mom, h->d_len, h->d_cvals, B, nsig, st));
 
     AnalysisArgs a{};
     a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
-    a.ld = ld; a.lens = h->d_len; a.mom = h->d_mom;
+    a.ld = ld; a.items = h->d_items; a.nitems = h->nitems; a.num_cus = h->num_cus; a.cvals = h->d_cvals;
     a.tables = reinterpret_cast<const float*>(h->d_tab);
     a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
     a.feats = h->d_feats; a.Tmax = Tmax;
     mark(h, st);
-    HIP_TRY(h, launch_analysis(a, B, st));
+    HIP_TRY(h, launch_analysis(a, st));
     mark(h, st);
 
     GruArgs g{};
@@ -328,7 +411,7 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
     mark(h, st);
 
     SynthArgs y{};
-    y.mic = mic; y.ld = ld; y.lens = h->d_len; y.mom = h->d_mom;
+    y.mic = mic; y.ld = ld; y.lens = h->d_len; y.cvals = h->d_cvals;
     y.tables = reinterpret_cast<const float*>(h->d_tab);
     y.bintab = h->d_bintab; y.est = h->d_est; y.Tmax = Tmax;
     y.out = out; y.ld_out = ld_out;
@@ -388,7 +471,7 @@ aec_status aec_profile_read(aec_handle* h, double* ms4, int64_t* calls) {
 }
 
 aec_status aec_erb_tables_check(const float* erb, const float* mags, const float* est, float* bands,
-                                float* gains, int32_t* sched_len) {
+                                float* gains, int32_t* sched_len, int32_t* conflicts) {
     if (!erb || !mags || !est || !bands || !gains) return AEC_ERR_INVALID_ARG;
     const ErbTables t = build_erb_tables(erb);
     if (!t.ok) return AEC_ERR_UNSUPPORTED;
@@ -415,6 +498,7 @@ aec_status aec_erb_tables_check(const float* erb, const float* mags, const float
         gains[k] = e[1] * est[ja] + e[3] * est[jb];
     }
     if (sched_len) *sched_len = L;
+    if (conflicts) *conflicts = t.conflicts;
     return AEC_OK;
 }
 
@@ -423,7 +507,8 @@ void aec_destroy(aec_handle* h) {
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     (void)hipSetDevice(h->device);
     (void)hipFree(h->d_w); (void)hipFree(h->d_tab); (void)hipFree(h->d_sched); (void)hipFree(h->d_bintab);
-    (void)hipFree(h->d_mom); (void)hipFree(h->d_len); (void)hipFree(h->d_feats); (void)hipFree(h->d_est); (void)hipFree(h->d_dbg);
+    (void)hipFree(h->d_mom); (void)hipFree(h->d_cvals); (void)hipFree(h->d_items); (void)hipFree(h->d_len);
+    (void)hipFree(h->d_feats); (void)hipFree(h->d_est); (void)hipFree(h->d_dbg);
     delete h;
 }
 

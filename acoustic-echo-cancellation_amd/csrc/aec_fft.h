@@ -18,6 +18,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 namespace aec {
 
 constexpr int kWin = 512;
@@ -26,12 +28,29 @@ constexpr int kBins = 257;
 constexpr int kBands = 32;
 constexpr int kGroupFloats = 576;   // per-frame LDS scratch: 16 rows x 36 floats
 
+// Compile-time loop: f(std::integral_constant<int, I>) for I in [B, E).  Used
+// where a register-array index must stay static (a loop holding convergent
+// DPP intrinsics is not always fully unrolled, which would demote the array
+// to scratch memory).
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
     return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 __device__ __forceinline__ float2 conjf2(float2 a) { return make_float2(a.x, -a.y); }
+// Per-component select (a float2 struct select can be lowered to a
+// stack-indexed load).
+__device__ __forceinline__ float2 csel(bool c, float2 a, float2 b) {
+    return make_float2(c ? a.x : b.x, c ? a.y : b.y);
+}
 __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
 
 // a * (c + i*s)
@@ -93,14 +112,17 @@ __device__ __forceinline__ void wave_fence() {
 //   in : v[a] = z[16a + lb]
 //   out: v[kP(k2)] = Z[lb + 16 k2]   (unnormalised, sign per INV)
 // scr: this group's LDS scratch (>= 16*36 floats, 16-B aligned).
-// tw : LDS table W256^j = (cos 2pi j/256, -sin 2pi j/256), j = 0..255.
+// twT: LDS table twT[k1*16 + lb] = W256^(lb k1) (lane-major: the 16 lanes of a
+//      group read 16 consecutive entries, conflict-free; a gather
+//      tw[(lb*k1) & 255] would be 2-4-way conflicted for k1 = 4, 8, 12).
 template <bool INV>
-__device__ __forceinline__ void fft256(float2 (&v)[16], int lb, float* scr, const float2* tw) {
+__device__ __forceinline__ void fft256(float2 (&v)[16], int lb, float* scr, const float2* twT) {
     dft16<INV>(v);
     float2* s2 = reinterpret_cast<float2*>(scr);
+    s2[lb] = v[kP(0)];
 #pragma unroll
-    for (int k1 = 0; k1 < 16; ++k1) {
-        float2 w = tw[(lb * k1) & 255];
+    for (int k1 = 1; k1 < 16; ++k1) {
+        float2 w = twT[k1 * 16 + lb];
         if (INV) w.y = -w.y;
         s2[k1 * 18 + lb] = cmul(v[kP(k1)], w);
     }
@@ -115,6 +137,15 @@ __device__ __forceinline__ void fft256(float2 (&v)[16], int lb, float* scr, cons
     wave_fence();
     dft16<INV>(v);
 }
+
+// Cross-lane partner within each 16-lane row: out[lb] = x[(16 - lb) & 15]
+// (row_mirror then row_ror:1, two DPP moves, no LDS).  Lane 0 receives its
+// own value; callers patch lane 0.
+__device__ __forceinline__ float mirror16(float x) {
+    const int y = __builtin_amdgcn_mov_dpp(__float_as_int(x), 0x140, 0xF, 0xF, false);   // row_mirror
+    return __int_as_float(__builtin_amdgcn_mov_dpp(y, 0x121, 0xF, 0xF, false));          // row_ror:1
+}
+__device__ __forceinline__ float2 mirror16(float2 x) { return make_float2(mirror16(x.x), mirror16(x.y)); }
 
 // Forward real-FFT unpack for one pair (k, 256-k), 1 <= k <= 127:
 //   A = Z[k], Bz = Z[256-k], w = W512^k  ->  X[k], X[256-k]

@@ -108,76 +108,20 @@ __device__ __forceinline__ float norm_scalar(const double2* __restrict__ mom, in
     return (float)(mean / sd);
 }
 
+// c for every (stream, signal): cvals[b*3 + s]
+__global__ __launch_bounds__(256) void norm_finalize_kernel(const double2* __restrict__ mom,
+                                                            const int64_t* __restrict__ lens,
+                                                            float* __restrict__ cvals, int B, int nsig) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= B * 3) return;
+    const int b = i / 3, s = i % 3;
+    cvals[i] = s < nsig ? norm_scalar(mom, b, s, lens[b]) : 0.f;
+}
+
 // --------------------------------------------------------------------------
 // shared helpers for K2 / K4
 // --------------------------------------------------------------------------
-constexpr int kHopsPB = kFPB + 1;        // sample hops staged per block
 constexpr int kHopStride = 288;          // floats per staged hop (256 + 32: frames g, g+1 on disjoint banks)
-
-// Stage hops [t0-1, t0+16) of one normalised signal row into LDS.  Samples
-// outside [0, n) are the reference's zero padding (F.pad after the
-// normaliser, attention_ccrn.py:48) and stay 0.
-__device__ __forceinline__ void stage_hops(float* samp, const float* __restrict__ row, int64_t n,
-                                           int64_t t0, float c, bool aligned) {
-    const int64_t base = (t0 - 1) * kHop;
-    for (int q = threadIdx.x; q < kHopsPB * (kHop / 4); q += blockDim.x) {
-        const int64_t i = base + 4 * q;
-        float4 v;
-        if (aligned && i >= 0 && i + 3 < n) {
-            v = *reinterpret_cast<const float4*>(row + i);
-            v.x -= c; v.y -= c; v.z -= c; v.w -= c;
-        } else {
-            v.x = (i + 0 >= 0 && i + 0 < n) ? row[i + 0] - c : 0.f;
-            v.y = (i + 1 >= 0 && i + 1 < n) ? row[i + 1] - c : 0.f;
-            v.z = (i + 2 >= 0 && i + 2 < n) ? row[i + 2] - c : 0.f;
-            v.w = (i + 3 >= 0 && i + 3 < n) ? row[i + 3] - c : 0.f;
-        }
-        *reinterpret_cast<float4*>(samp + (q >> 6) * kHopStride + (q & 63) * 4) = v;
-    }
-}
-
-// Register-staged variant of stage_hops: prefetch_hops issues the global
-// loads of the raw samples (0 outside [0, n)), commit_hops normalises and
-// writes them to LDS.  Thread t owns float4 slots q = t + 256 u, u < kPf.
-constexpr int kPf = (kHopsPB * (kHop / 4) + 255) / 256;     // 5
-__device__ __forceinline__ void prefetch_hops(float4 (&pf)[kPf], const float* __restrict__ row, int64_t n,
-                                              int64_t t0, bool aligned) {
-    const int64_t base = (t0 - 1) * kHop;
-#pragma unroll
-    for (int u = 0; u < kPf; ++u) {
-        const int q = threadIdx.x + 256 * u;
-        const int64_t i = base + 4 * q;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (q < kHopsPB * (kHop / 4)) {
-            if (aligned && i >= 0 && i + 3 < n) {
-                v = *reinterpret_cast<const float4*>(row + i);
-            } else {
-                if (i + 0 >= 0 && i + 0 < n) v.x = row[i + 0];
-                if (i + 1 >= 0 && i + 1 < n) v.y = row[i + 1];
-                if (i + 2 >= 0 && i + 2 < n) v.z = row[i + 2];
-                if (i + 3 >= 0 && i + 3 < n) v.w = row[i + 3];
-            }
-        }
-        pf[u] = v;
-    }
-}
-// Normalise (x - c) inside [0, n) only — the zero padding stays 0 — and stage.
-__device__ __forceinline__ void commit_hops(float* samp, const float4 (&pf)[kPf], float c, int64_t n, int64_t t0) {
-    const int64_t base = (t0 - 1) * kHop;
-#pragma unroll
-    for (int u = 0; u < kPf; ++u) {
-        const int q = threadIdx.x + 256 * u;
-        if (q < kHopsPB * (kHop / 4)) {
-            const int64_t i = base + 4 * q;
-            float4 v = pf[u];
-            v.x = (i + 0 >= 0 && i + 0 < n) ? v.x - c : 0.f;
-            v.y = (i + 1 >= 0 && i + 1 < n) ? v.y - c : 0.f;
-            v.z = (i + 2 >= 0 && i + 2 < n) ? v.z - c : 0.f;
-            v.w = (i + 3 >= 0 && i + 3 < n) ? v.w - c : 0.f;
-            *reinterpret_cast<float4*>(samp + (q >> 6) * kHopStride + (q & 63) * 4) = v;
-        }
-    }
-}
 
 // Windowed packed input of frame g: v[a] = (x[32a+2lb], x[32a+2lb+1]) * hann
 __device__ __forceinline__ void load_frame(float2 (&v)[16], const float* samp, const float* hann, int g, int lb) {
@@ -193,34 +137,25 @@ __device__ __forceinline__ void load_frame(float2 (&v)[16], const float* samp, c
 
 // After a forward fft256 (v[kP(k2)] = Z[lb + 16 k2]) unpack the real spectrum.
 // Lane lb returns X[k] and X[256-k] for k = lb + 16 m, m = 0..7 in xa[m] / xb[m];
-// lane 0, m = 0 returns X[0] in xa[0] and X[256] in xb[0]; every lane returns
-// X[128] in x128 (only lane 0 uses it).  sw = 16*(g&1) XOR-swizzles the LDS
-// image so adjacent frames' b64 accesses fall on disjoint banks.
-__device__ __forceinline__ void rfft_unpack(const float2 (&v)[16], int lb, int sw, float* scr, const float2* tw512,
+// lane 0, m = 0 returns X[0] in xa[0] and X[256] in xb[0]; lane 0 also returns
+// X[128] in x128.  The partner Z[256-k] lives in lane (16-lb)&15 at k2 = 15-m
+// (lane 0: its own k2 = (16-m)&15) and is fetched with DPP (mirror16).
+__device__ __forceinline__ void rfft_unpack(const float2 (&v)[16], int lb, const float2* tw512,
                                             float2 (&xa)[8], float2 (&xb)[8], float2& x128) {
-    float2* s2 = reinterpret_cast<float2*>(scr);
-#pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) s2[(lb + 16 * k2) ^ sw] = v[kP(k2)];
-    wave_fence();
-    float2 A[8], Bz[8];
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-        A[m] = s2[(lb + 16 * m) ^ sw];
-        Bz[m] = s2[((256 - lb - 16 * m) & 255) ^ sw];
-    }
-    const float2 z128 = s2[128 ^ sw];
-    wave_fence();
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
+    static_for<0, 8>([&](auto mi) {
+        constexpr int m = decltype(mi)::value;
+        const float2 A = v[kP(m)];
+        const float2 mir = mirror16(v[kP(15 - m)]);
+        const float2 Bz = csel(lb == 0, v[kP((16 - m) & 15)], mir);
         const int k = lb + 16 * m;
         if (k == 0) {
-            xa[m] = make_float2(A[m].x + A[m].y, 0.f);
-            xb[m] = make_float2(A[m].x - A[m].y, 0.f);
+            xa[m] = make_float2(A.x + A.y, 0.f);
+            xb[m] = make_float2(A.x - A.y, 0.f);
         } else {
-            rfft_pair(A[m], Bz[m], tw512[k], xa[m], xb[m]);
+            rfft_pair(A, Bz, tw512[k], xa[m], xb[m]);
         }
-    }
-    x128 = conjf2(z128);
+    });
+    x128 = conjf2(v[kP(8)]);
 }
 
 // |X| = sqrt(re^2 + im^2 + 1e-9) (ERB.py:277-279).  The argument is >= 1e-9,
@@ -229,113 +164,186 @@ __device__ __forceinline__ float mag(float2 x) {
     return __builtin_amdgcn_sqrtf(fmaf(x.x, x.x, fmaf(x.y, x.y, 1e-9f)));
 }
 
-__device__ __forceinline__ void stage_common_tables(const DevTables* tb, float2* sTw256, float2* sTw512,
-                                                    float* sHann) {
-    const int tid = threadIdx.x;
-    sTw256[tid] = tb->tw256[tid];
-    sTw512[tid] = tb->tw512[tid];
-    if (tid == 0) sTw512[256] = tb->tw512[256];
-    sHann[tid] = tb->hann[tid];
-    sHann[tid + 256] = tb->hann[tid + 256];
+// --------------------------------------------------------------------------
+// K2: analysis.  grid = (ceil(Tmax/16), B), block = 256.  Each wave owns 4
+// consecutive frames (16 lanes per frame) and its own LDS region, stages its
+// own 5 hops per signal and runs the whole per-frame chain with wave-level
+// ordering only — the block barrier is used once, for the shared tables.
+// ERB projection: every lane runs the same number (L) of scheduled entries
+// (bin, w0, w1, w2) -> three partial accumulators; bands wider than the
+// schedule's split width are summed from two partials (ErbTables, aec_tables.h).
+// The schedule is ordered so the 32 lanes of each mag gather hit 32 banks.
+// --------------------------------------------------------------------------
+constexpr int kWaveFrames = 4;
+constexpr int kWaveHops = kWaveFrames + 1;
+constexpr int kWaveFloats = kWaveFrames * kGroupFloats;     // >= kWaveHops * kHopStride
+constexpr int kWavePf = kWaveHops;                          // float4 per lane per signal
+
+// Wave-local staging: the 5 hops [t-1, t+4) of frames t .. t+3; lane owns
+// float4 slot `lane` of every hop.  Raw buffer loads through a per-row
+// descriptor (wave-uniform base, n*4 bytes): 32-bit offsets, and the
+// hardware range check returns 0 outside the row (negative offsets wrap to
+// out-of-range), so the reference's zero padding needs no branches;
+// wave_commit re-applies the exact [0, n) mask.  Rows that are not 16-B
+// aligned take dword loads (wave-uniform branch).
+__device__ __forceinline__ void wave_prefetch(float4 (&pf)[kWavePf], const float* __restrict__ row, int n,
+                                              int t, int lane, bool aligned) {
+    // the row / length are wave-uniform (one item per wave); make that provable so
+    // hipcc keeps the descriptor in SGPRs (no waterfall loop per load)
+    const uint64_t ra = reinterpret_cast<uint64_t>(row);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)ra);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(ra >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane(n * 4);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, nb, 0x00020000);
+    const int base = ((t - 1) * kHop + 4 * lane) * 4;
+    if (__builtin_expect(aligned, 1)) {
+#pragma unroll
+        for (int u = 0; u < kWavePf; ++u) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, base + u * kHop * 4, 0, 0);
+            pf[u] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                                __uint_as_float(v[3]));
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < kWavePf; ++u) {
+            const int o = base + u * kHop * 4;
+            pf[u] = make_float4(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + 0, 0, 0)),
+                                __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + 4, 0, 0)),
+                                __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + 8, 0, 0)),
+                                __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + 12, 0, 0)));
+        }
+    }
+}
+// Normalise (x - c) inside [0, n) only — the zero padding stays 0 — and stage.
+__device__ __forceinline__ void wave_commit(float* wr, const float4 (&pf)[kWavePf], float c, int n,
+                                            int t, int lane) {
+    const int base = (t - 1) * kHop + 4 * lane;
+#pragma unroll
+    for (int u = 0; u < kWavePf; ++u) {
+        const int i = base + u * kHop;
+        float4 v = pf[u];
+        v.x = (i + 0 >= 0 && i + 0 < n) ? v.x - c : 0.f;
+        v.y = (i + 1 >= 0 && i + 1 < n) ? v.y - c : 0.f;
+        v.z = (i + 2 >= 0 && i + 2 < n) ? v.z - c : 0.f;
+        v.w = (i + 3 >= 0 && i + 3 < n) ? v.w - c : 0.f;
+        *reinterpret_cast<float4*>(wr + u * kHopStride + 4 * lane) = v;
+    }
 }
 
-// --------------------------------------------------------------------------
-// K2: analysis.  grid = (ceil(Tmax/16), B), block = 256 (16 frames x 16 lanes)
-// ERB projection: every lane runs the same number (Lmax) of scheduled entries
-// (bin, w0, w1, w2) -> three partial accumulators; bands wider than the
-// schedule's split width are summed from two partials (ErbSched, aec_tables.h).
-// --------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void analysis_kernel(AnalysisArgs p) {
+__global__ __launch_bounds__(256, 3) void analysis_kernel(AnalysisArgs p) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int b = blockIdx.y;
-    const int64_t n = p.lens[b];
-    const int64_t T = n / kHop + 1;
-    const int64_t t0 = (int64_t)blockIdx.x * kFPB;
-    if (t0 >= T) return;
     const int tid = threadIdx.x;
     const int L = p.sched_len;                                        // multiple of 4
 
-    float2* sTw256 = reinterpret_cast<float2*>(smem);                 // 256 float2
-    float2* sTw512 = sTw256 + 256;                                    // 258 float2
-    float* sHann = reinterpret_cast<float*>(sTw512 + 258);            // 512
-    float* sWork = sHann + 512;                                       // 16 * 576
-    float4* sSched = reinterpret_cast<float4*>(sWork + kFPB * kGroupFloats);   // L * 16
+    float4* sSched = reinterpret_cast<float4*>(smem);                 // L * 16
     int2* sComb = reinterpret_cast<int2*>(sSched + L * 16);           // 32
+    float2* sTw512 = reinterpret_cast<float2*>(sComb + 32);           // 258
+    float2* sTwT = sTw512 + 258;                                      // 256
+    float* sHann = reinterpret_cast<float*>(sTwT + 256);              // 512
+    float* sWave = sHann + 512;                                       // 4 * kWaveFloats
 
-    stage_common_tables(reinterpret_cast<const DevTables*>(p.tables), sTw256, sTw512, sHann);
+    const DevTables* tb = reinterpret_cast<const DevTables*>(p.tables);
     {
+        sTwT[tid] = tb->twT[tid];
         const float4* sch = reinterpret_cast<const float4*>(p.sched);
         for (int i = tid; i < L * 16; i += 256) sSched[i] = sch[i];
         if (tid < 32) sComb[tid] = reinterpret_cast<const int2*>(p.sched + 4 * 16 * L)[tid];
+        sTw512[tid] = tb->tw512[tid];
+        if (tid < 2) sTw512[256 + tid] = tb->tw512[256 + tid];
+        sHann[tid] = tb->hann[tid];
+        sHann[tid + 256] = tb->hann[tid + 256];
     }
-    const int g = tid >> 4, lb = tid & 15, sw = 16 * (g & 1);
-    const int64_t t = t0 + g;
-    float* scr = sWork + g * kGroupFloats;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int gg = lane >> 4, lb = lane & 15, sw = 16 * (gg & 1);
+    float* wr = sWave + wave * kWaveFloats;
+    float* scr = wr + gg * kGroupFloats;
+    // float4 fast path needs every row 16-B aligned (bit s of `al`)
     const bool aligned_ld = ((p.ld & 3) == 0);
+    int al = 0;
+    for (int s = 0; s < p.nsig; ++s)
+        al |= (aligned_ld && ((reinterpret_cast<uintptr_t>(p.sig[s]) & 15) == 0)) << s;
+    __syncthreads();                                                  // tables staged; no block barrier below
 
-    float cs[3];
-    for (int s = 0; s < p.nsig; ++s) cs[s] = norm_scalar(p.mom, b, s, n);
-    // register prefetch of one signal's 17 hops (5 float4 per thread): the
-    // loads of signal s+1 are in flight while signal s is transformed
-    float4 pf[kPf];
-    prefetch_hops(pf, p.sig[0] + (int64_t)b * p.ld, n, t0, aligned_ld && ((reinterpret_cast<uintptr_t>(p.sig[0]) & 15) == 0));
-
-    for (int s = 0; s < p.nsig; ++s) {
-        __syncthreads();                           // previous use of sWork finished
-        commit_hops(sWork, pf, cs[s], n, t0);
-        if (s + 1 < p.nsig)
-            prefetch_hops(pf, p.sig[s + 1] + (int64_t)b * p.ld, n, t0,
-                          aligned_ld && ((reinterpret_cast<uintptr_t>(p.sig[s + 1]) & 15) == 0));
-        __syncthreads();
-        float2 v[16];
-        load_frame(v, sWork, sHann, g, lb);
-        __syncthreads();                           // all frames read before scratch reuse
-        fft256<false>(v, lb, scr, sTw256);
-        float2 xa[8], xb[8], x128;
-        rfft_unpack(v, lb, sw, scr, sTw512, xa, xb, x128);
-        // magnitudes (ERB.py:277-279) -> scr[k ^ sw], k = 0..256
+    // Persistent wave: items gw, gw + NW, ... of the host-built work list
+    // (one item = 4 consecutive frames of one stream).  The samples of the
+    // next (item, signal) task are prefetched into registers while the
+    // current one is transformed; the next item's descriptor one item ahead.
+    const int NW = gridDim.x * 4;
+    int64_t k = (int64_t)blockIdx.x * 4 + wave;
+    if (k >= p.nitems) return;
+    WorkItem it = p.items[k];
+    float4 pf[kWavePf];
+    wave_prefetch(pf, p.sig[0] + (int64_t)it.b * p.ld, (int)it.n, it.wt, lane, al & 1);
+    for (;;) {
+        const int64_t k2 = k + NW;
+        const WorkItem it2 = k2 < p.nitems ? p.items[k2] : it;
+        const int64_t T = it.n / kHop + 1;
+        const int64_t t = it.wt + gg;                                 // this group's frame
+        for (int s = 0; s < p.nsig; ++s) {
+            // keep the LDS table reads inside the loop (hoisting the loop-invariant
+            // schedule / twiddle / window reads would pin ~100 VGPRs)
+            asm volatile("" ::: "memory");
+            wave_commit(wr, pf, p.cvals[it.b * 3 + s], (int)it.n, it.wt, lane);
+            if (s + 1 < p.nsig)
+                wave_prefetch(pf, p.sig[s + 1] + (int64_t)it.b * p.ld, (int)it.n, it.wt, lane, (al >> (s + 1)) & 1);
+            else if (k2 < p.nitems)
+                wave_prefetch(pf, p.sig[0] + (int64_t)it2.b * p.ld, (int)it2.n, it2.wt, lane, al & 1);
+            wave_fence();
+            float2 v[16];
+            load_frame(v, wr, sHann, gg, lb);
+            wave_fence();                                             // samples read before scratch reuse
+            fft256<false>(v, lb, scr, sTwT);
+            float2 xa[8], xb[8], x128;
+            rfft_unpack(v, lb, sTw512, xa, xb, x128);
+            // magnitudes (ERB.py:277-279) -> scr[k ^ sw], k = 0..256
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            const int k = lb + 16 * m;
-            scr[k ^ sw] = mag(xa[m]);
-            scr[(k == 0 ? 256 : 256 - k) ^ sw] = mag(xb[m]);
-        }
-        if (lb == 0) scr[128 ^ sw] = mag(x128);
-        wave_fence();
-        // balanced ERB schedule: L entries per lane, 3 partial sums
-        float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-        for (int e = 0; e < L; e += 4) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const float4 en = sSched[(e + u) * 16 + lb];
-                const float mg = scr[__float_as_int(en.x) ^ sw];
-                a0 = fmaf(en.y, mg, a0);
-                a1 = fmaf(en.z, mg, a1);
-                a2 = fmaf(en.w, mg, a2);
+            for (int m = 0; m < 8; ++m) {
+                const int kk = lb + 16 * m;
+                scr[kk ^ sw] = mag(xa[m]);
+                scr[(kk == 0 ? 256 : 256 - kk) ^ sw] = mag(xb[m]);
             }
-        }
-        float* part = scr + 512;
-        part[3 * lb + 0] = a0;
-        part[3 * lb + 1] = a1;
-        part[3 * lb + 2] = a2;
-        wave_fence();
-        if (t < T) {
-            float* fo = p.feats + ((int64_t)b * p.Tmax + t) * 96 + 32 * s;
+            if (lb == 0) scr[128 ^ sw] = mag(x128);
+            wave_fence();
+            // balanced ERB schedule: L entries per lane, 3 partial sums
+            float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+            for (int e = 0; e < L; e += 4) {
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int band = lb + 16 * h;
-                const int2 cb = sComb[band];
-                fo[band] = part[cb.x] + (cb.y >= 0 ? part[cb.y] : 0.f);
+                for (int u = 0; u < 4; ++u) {
+                    const float4 en = sSched[(e + u) * 16 + lb];
+                    const float mg = scr[__float_as_int(en.x) ^ sw];
+                    a0 = fmaf(en.y, mg, a0);
+                    a1 = fmaf(en.z, mg, a1);
+                    a2 = fmaf(en.w, mg, a2);
+                }
             }
+            float* part = scr + 512;
+            part[3 * lb + 0] = a0;
+            part[3 * lb + 1] = a1;
+            part[3 * lb + 2] = a2;
+            wave_fence();
+            if (t < T) {
+                float* fo = p.feats + ((int64_t)it.b * p.Tmax + t) * 96 + 32 * s;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int band = lb + 16 * h;
+                    const int2 cb = sComb[band];
+                    fo[band] = part[cb.x] + (cb.y >= 0 ? part[cb.y] : 0.f);
+                }
+            }
+            wave_fence();
         }
-        wave_fence();
+        if (k2 >= p.nitems) break;
+        k = k2;
+        it = it2;
     }
 }
 
 // --------------------------------------------------------------------------
 // K4: synthesis.  grid = (ceil(nhop_max/15), B), block = 256.  A block
-// re-derives the mic spectra of 16 consecutive frames, applies the ERB gains,
-// inverse-transforms them and overlap-adds 15 output hops.
+// re-derives the mic spectra of 16 consecutive frames (each wave stages and
+// transforms 4 of them), applies the ERB gains, inverse-transforms and, after
+// one block barrier, overlap-adds 15 output hops.
 // --------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void synthesis_kernel(SynthArgs p) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -347,37 +355,50 @@ __global__ __launch_bounds__(256) void synthesis_kernel(SynthArgs p) {
     if (h0 >= nhop) return;
     const int tid = threadIdx.x;
 
-    float2* sTw256 = reinterpret_cast<float2*>(smem);
-    float2* sTw512 = sTw256 + 256;
-    float* sHann = reinterpret_cast<float*>(sTw512 + 258);
-    float* sCoff = sHann + 512;                                  // 256: 1/(window^2 OLA + 1e-8)
-    float* sEst = sCoff + 256;                                   // 16 * 32
-    float* sWork = sEst + kFPB * 32;                             // 16 * 576
-    float4* sBin = reinterpret_cast<float4*>(sWork + kFPB * kGroupFloats);   // 257 (+3 pad)
+    float4* sBin = reinterpret_cast<float4*>(smem);                   // 257 (+3 pad)
+    float2* sTw512 = reinterpret_cast<float2*>(sBin + 260);           // 258
+    float2* sTwT = sTw512 + 258;                                      // 256
+    float* sHann = reinterpret_cast<float*>(sTwT + 256);              // 512
+    float* sCoff = sHann + 512;                                       // 256: 1/(window^2 OLA + 1e-8)
+    float* sEst = sCoff + 256;                                        // 16 * 32
+    float* sWave = sEst + kFPB * 32;                                  // 4 * kWaveFloats
 
-    stage_common_tables(reinterpret_cast<const DevTables*>(p.tables), sTw256, sTw512, sHann);
-    sCoff[tid] = reinterpret_cast<const DevTables*>(p.tables)->inv_coff[tid];
+    const DevTables* tb = reinterpret_cast<const DevTables*>(p.tables);
     {
         const float4* bt = reinterpret_cast<const float4*>(p.bintab);
         sBin[tid] = bt[tid];
         if (tid == 0) sBin[256] = bt[256];
+        sTwT[tid] = tb->twT[tid];
+        sTw512[tid] = tb->tw512[tid];
+        if (tid < 2) sTw512[256 + tid] = tb->tw512[256 + tid];
+        sHann[tid] = tb->hann[tid];
+        sHann[tid + 256] = tb->hann[tid + 256];
+        sCoff[tid] = tb->inv_coff[tid];
         for (int i = tid; i < kFPB * 32; i += 256) {
             const int64_t t = h0 + (i >> 5);
             sEst[i] = (t < T) ? p.est[((int64_t)b * p.Tmax + t) * 32 + (i & 31)] : 0.f;
         }
     }
-    const float* row = p.mic + (int64_t)b * p.ld;
-    const bool aligned = ((p.ld & 3) == 0) && ((reinterpret_cast<uintptr_t>(p.mic) & 15) == 0);
-    stage_hops(sWork, row, n, h0, norm_scalar(p.mom, b, 0, n), aligned);
-    __syncthreads();
-    const int g = tid >> 4, lb = tid & 15, sw = 16 * (g & 1);
-    float* scr = sWork + g * kGroupFloats;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int gg = lane >> 4, lb = lane & 15;
+    const int g = tid >> 4;                                           // frame h0 + g
+    const int64_t wt = h0 + kWaveFrames * wave;
+    float* wr = sWave + wave * kWaveFloats;
+    float* scr = wr + gg * kGroupFloats;
+    {
+        float4 pf[kWavePf];
+        const bool aligned = ((p.ld & 3) == 0) && ((reinterpret_cast<uintptr_t>(p.mic) & 15) == 0);
+        wave_prefetch(pf, p.mic + (int64_t)b * p.ld, (int)n, (int)wt, lane, aligned);
+        wave_commit(wr, pf, p.cvals[b * 3 + 0], (int)n, (int)wt, lane);
+    }
+    __syncthreads();                                                  // tables + est staged
+    wave_fence();
     float2 v[16];
-    load_frame(v, sWork, sHann, g, lb);
-    __syncthreads();
-    fft256<false>(v, lb, scr, sTw256);
+    load_frame(v, wr, sHann, gg, lb);
+    wave_fence();
+    fft256<false>(v, lb, scr, sTwT);
     float2 xa[8], xb[8], x128;
-    rfft_unpack(v, lb, sw, scr, sTw512, xa, xb, x128);
+    rfft_unpack(v, lb, sTw512, xa, xb, x128);
 
     // ERB gain per bin: g[k] = sum_j est_erb[j] erb[k][j] over the <= 2 bands
     // covering bin k (ERB.py:306-307), applied to the mic spectrum (:309-310)
@@ -386,31 +407,37 @@ __global__ __launch_bounds__(256) void synthesis_kernel(SynthArgs p) {
         const float4 e = sBin[k];
         return e.y * est[__float_as_int(e.x)] + e.w * est[__float_as_int(e.z)];
     };
-    float2* s2 = reinterpret_cast<float2*>(scr);
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
+    // inverse pack: lane lb forms 2Z'[k] and 2Z'[256-k] for k = lb + 16 m; the
+    // inverse FFT wants v[a] = 2Z'[16a + lb]: a <= 7 is this lane's own Zk[a],
+    // a >= 8 is Zmk[15-a] of lane (16-lb)&15 (DPP), lane 0 patched.
+    float2 Zk[8], Zmk[8];
+    static_for<0, 8>([&](auto mi) {
+        constexpr int m = decltype(mi)::value;
         const int k = lb + 16 * m;
-        if (k == 0) {
-            // DC / Nyquist: irfft ignores the imaginary parts
-            const float s0 = gain(0) * xa[m].x, s256 = gain(256) * xb[m].x;
-            s2[0 ^ sw] = make_float2(s0 + s256, s0 - s256);
-        } else {
-            float2 Zk, Zmk;
-            irfft_pair(cscale(xa[m], gain(k)), cscale(xb[m], gain(256 - k)), sTw512[k], Zk, Zmk);
-            s2[k ^ sw] = Zk;
-            s2[(256 - k) ^ sw] = Zmk;
-        }
-    }
+        // k == 0 (lane 0, m = 0): DC / Nyquist, irfft ignores their imaginary parts;
+        // gain(256 - 0) indexes bin 256 = Nyquist, as required
+        const float ga = gain(k), gb = gain(256 - k);
+        float2 zk, zmk;
+        irfft_pair(cscale(xa[m], ga), cscale(xb[m], gb), sTw512[k], zk, zmk);
+        const float s0 = ga * xa[m].x, s256 = gb * xb[m].x;
+        Zk[m] = csel(k == 0, make_float2(s0 + s256, s0 - s256), zk);
+        Zmk[m] = csel(k == 0, Zk[m], zmk);
+    });
+    float2 z128 = make_float2(0.f, 0.f);
     if (lb == 0) {
         const float2 S = cscale(x128, gain(128));
-        s2[128 ^ sw] = make_float2(2.f * S.x, -2.f * S.y);   // 2*conj(S[128])
+        z128 = make_float2(2.f * S.x, -2.f * S.y);   // 2*conj(S[128])
     }
-    wave_fence();
 #pragma unroll
-    for (int a = 0; a < 16; ++a) v[a] = s2[(16 * a + lb) ^ sw];
-    wave_fence();
-    fft256<true>(v, lb, scr, sTw256);
+    for (int a = 0; a < 8; ++a) v[a] = Zk[a];
+    static_for<8, 16>([&](auto ai) {
+        constexpr int a = decltype(ai)::value;
+        const float2 mir = mirror16(Zmk[15 - a]);
+        v[a] = csel(lb != 0, mir, a == 8 ? z128 : Zmk[(16 - a) & 7]);
+    });
+    fft256<true>(v, lb, scr, sTwT);
     // v[kP(m2)] = 512 * (x[2m] + i x[2m+1]), m = lb + 16 m2 ; window + 1/512
+    float2* s2 = reinterpret_cast<float2*>(scr);
 #pragma unroll
     for (int m2 = 0; m2 < 16; ++m2) {
         const int nn = 2 * (lb + 16 * m2);
@@ -425,8 +452,8 @@ __global__ __launch_bounds__(256) void synthesis_kernel(SynthArgs p) {
     if (oal) {
         for (int e = tid; e < nh * (kHop / 4); e += 256) {
             const int i = e >> 6, r = (e & 63) * 4;
-            const float4 a = *reinterpret_cast<const float4*>(sWork + i * kGroupFloats + 256 + r);
-            const float4 c = *reinterpret_cast<const float4*>(sWork + (i + 1) * kGroupFloats + r);
+            const float4 a = *reinterpret_cast<const float4*>(sWave + i * kGroupFloats + 256 + r);
+            const float4 c = *reinterpret_cast<const float4*>(sWave + (i + 1) * kGroupFloats + r);
             const float4 cf = *reinterpret_cast<const float4*>(sCoff + r);
             float4 o;
             o.x = (a.x + c.x) * cf.x + 1e-9f;
@@ -438,8 +465,8 @@ __global__ __launch_bounds__(256) void synthesis_kernel(SynthArgs p) {
     } else {
         for (int e = tid; e < nh * kHop; e += 256) {
             const int i = e >> 8, r = e & 255;
-            const float a = sWork[i * kGroupFloats + 256 + r];
-            const float c = sWork[(i + 1) * kGroupFloats + r];
+            const float a = sWave[i * kGroupFloats + 256 + r];
+            const float c = sWave[(i + 1) * kGroupFloats + r];
             orow[(h0 + i) * kHop + r] = (a + c) * sCoff[r] + 1e-9f;
         }
     }
@@ -454,9 +481,19 @@ hipError_t launch_moments(const float* mic, const float* ref, const float* near,
     return hipGetLastError();
 }
 
-hipError_t launch_analysis(const AnalysisArgs& a, int B, hipStream_t st) {
-    const dim3 grid((unsigned)((a.Tmax + kFPB - 1) / kFPB), B);
-    hipLaunchKernelGGL(analysis_kernel, grid, dim3(256), analysis_smem_bytes(a.sched_len), st, a);
+hipError_t launch_norm_finalize(const double2* mom, const int64_t* lens, float* cvals, int B, int nsig,
+                                hipStream_t st) {
+    hipLaunchKernelGGL(norm_finalize_kernel, dim3((B * 3 + 255) / 256), dim3(256), 0, st, mom, lens, cvals, B, nsig);
+    return hipGetLastError();
+}
+
+hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t st) {
+    if (a.nitems <= 0) return hipSuccess;
+    // persistent: at most kAnalysisBlocksPerCU blocks per CU, 4 waves (items) each
+    const int64_t want = (a.nitems + 3) / 4;
+    const int64_t cap = (int64_t)a.num_cus * kAnalysisBlocksPerCU;
+    const unsigned grid = (unsigned)(want < cap ? want : cap);
+    hipLaunchKernelGGL(analysis_kernel, dim3(grid), dim3(256), analysis_smem_bytes(a.sched_len), st, a);
     return hipGetLastError();
 }
 

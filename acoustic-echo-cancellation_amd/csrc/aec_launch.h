@@ -12,11 +12,22 @@ constexpr int kHopsOut = kFPB - 1;  // output hops per synthesis block
 constexpr int kCH = 16;             // frames per chunk in the GRU pipeline
 constexpr int kMomChunks = 8;       // moment partials per (stream, signal)
 
+constexpr int kAnalysisBlocksPerCU = 3;
+
+// One analysis work item: 4 consecutive frames [wt, wt+4) of stream b (length n).
+struct WorkItem {
+    int32_t b;
+    int32_t wt;
+    int64_t n;
+};
+
 struct AnalysisArgs {
     const float* sig[3];
     int64_t ld;
-    const int64_t* lens;
-    const double2* mom;      // [B][3][kMomChunks]
+    const WorkItem* items;   // host-built list (valid items only)
+    int64_t nitems;
+    int num_cus;
+    const float* cvals;      // [B][3] normaliser scalars
     const float* tables;     // DevTables
     const float* sched;      // ERB schedule: float4[L][16] then int2[32] (aec_tables.h)
     int sched_len;           // L (multiple of 4)
@@ -42,7 +53,7 @@ struct SynthArgs {
     const float* mic;
     int64_t ld;
     const int64_t* lens;
-    const double2* mom;
+    const float* cvals;
     const float* tables;
     const float* bintab;     // float4[257]: (band_a, w_a, band_b, w_b) per bin
     const float* est;        // [B][Tmax][32]
@@ -53,17 +64,17 @@ struct SynthArgs {
 
 // dynamic LDS bytes (must match the carve in the kernels)
 inline size_t analysis_smem_bytes(int sched_len) {
-    const size_t fl = 256 * 2 + 258 * 2 + 512 + (size_t)kFPB * kGroupFloats;
-    return fl * 4 + (size_t)sched_len * 16 * 16 + 32 * 8;
+    return (size_t)sched_len * 16 * 16 + 32 * 8 + (258 * 2 + 256 * 2 + 512 + (size_t)kFPB * kGroupFloats) * 4;
 }
 inline size_t synthesis_smem_bytes() {
-    const size_t fl = 256 * 2 + 258 * 2 + 512 + 256 + kFPB * 32 + (size_t)kFPB * kGroupFloats;
-    return fl * 4 + 260 * 16;
+    return 260 * 16 + (258 * 2 + 256 * 2 + 512 + 256 + kFPB * 32 + (size_t)kFPB * kGroupFloats) * 4;
 }
 
 hipError_t launch_moments(const float* mic, const float* ref, const float* near, int64_t ld,
                           const int64_t* lens, double2* mom, int B, int nsig, hipStream_t st);
-hipError_t launch_analysis(const AnalysisArgs& a, int B, hipStream_t st);
+hipError_t launch_norm_finalize(const double2* mom, const int64_t* lens, float* cvals, int B, int nsig,
+                                hipStream_t st);
+hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t st);
 hipError_t launch_gru(const GruArgs& a, int B, hipStream_t st);
 hipError_t launch_synthesis(const SynthArgs& a, int B, hipStream_t st);
 

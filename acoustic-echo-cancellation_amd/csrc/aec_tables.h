@@ -8,7 +8,7 @@ namespace aec {
 
 // Built by the host at aec_create (float64 math, rounded to float32).
 struct DevTables {
-    float2 tw256[256];   // W256^j = (cos 2pi j/256, -sin 2pi j/256)
+    float2 twT[256];     // twT[k1*16 + lb] = W256^(lb*k1), W256^j = (cos 2pi j/256, -sin 2pi j/256)
     float2 tw512[258];   // W512^k, k = 0..256 (+1 pad)
     float hann[512];     // periodic Hann = scipy get_window('hann', 512) (attention_ccrn.py:12)
     float inv_coff[256]; // 1 / (f32(hann[r]^2 + hann[r+256]^2) + 1e-8)  (attention_ccrn.py:94-96)
@@ -32,6 +32,7 @@ struct DevTables {
 // in one band, both 0 when in none (DC / Nyquist).
 struct ErbTables {
     int sched_len = 0;
+    int conflicts = 0;           // (step, lane) entries that could not get a distinct residue
     std::vector<float> sched;    // 16 * 4 * L floats + 64 ints (as floats)
     std::vector<float> bintab;   // 257 * 4
     bool ok = false;

@@ -110,9 +110,11 @@ aec_status aec_profile_read(aec_handle* h, double* ms4, int64_t* calls);
  * aec_set_erb does and applies them on the CPU:
  *   bands[32]  = schedule applied to mags[257]   (== mags @ erb, ERB.py:282)
  *   gains[257] = transpose table applied to est[32] (== est @ erb^T, ERB.py:306)
- * Returns the schedule length per lane in *sched_len. */
+ * Returns the schedule length per lane in *sched_len and the number of
+ * schedule entries whose LDS read could not be placed on a distinct bank
+ * residue in *conflicts. */
 aec_status aec_erb_tables_check(const float* erb_257xbands, const float* mags, const float* est,
-                                float* bands, float* gains, int32_t* sched_len);
+                                float* bands, float* gains, int32_t* sched_len, int32_t* conflicts);
 
 /* Frame / output-length integers (bit-exact framing contract). */
 int64_t aec_num_frames(int64_t n_samples);   /* n//256 + 1 */
