@@ -187,6 +187,8 @@ struct aec_handle {
     float* d_cvals = nullptr;    // [B][3]
     WorkItem* d_items = nullptr; // analysis work list (rebuilt when the lengths change)
     int64_t items_cap = 0, nitems = 0;
+    WorkItem* d_sitems = nullptr; // synthesis block-item list
+    int64_t sitems_cap = 0, nsitems = 0;
     int num_cus = 256;
     int64_t* d_len = nullptr;    // [B]
     float* d_feats = nullptr;    // [B][T][96]
@@ -374,14 +376,27 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
             const int64_t T = aec_num_frames(lengths[b]);
             for (int64_t wt = 0; wt < T; wt += 4) items.push_back({b, (int32_t)wt, lengths[b]});
         }
-        if ((int64_t)items.size() > h->items_cap) {
+        // synthesis work list: 15 output hops per block item
+        std::vector<WorkItem> sitems;
+        for (int b = 0; b < B; ++b) {
+            const int64_t nhop = lengths[b] / 256;
+            for (int64_t h0 = 0; h0 < nhop; h0 += kHopsOut) sitems.push_back({b, (int32_t)h0, lengths[b]});
+        }
+        if ((int64_t)items.size() > h->items_cap || (int64_t)sitems.size() > h->sitems_cap) {
             HIP_TRY(h, hipStreamSynchronize(st));
             if (h->d_items) HIP_TRY(h, hipFree(h->d_items));
-            h->d_items = nullptr;
-            HIP_TRY(h, hipMalloc(&h->d_items, items.size() * sizeof(WorkItem)));
+            if (h->d_sitems) HIP_TRY(h, hipFree(h->d_sitems));
+            h->d_items = h->d_sitems = nullptr;
+            HIP_TRY(h, hipMalloc(&h->d_items, std::max<size_t>(1, items.size()) * sizeof(WorkItem)));
+            HIP_TRY(h, hipMalloc(&h->d_sitems, std::max<size_t>(1, sitems.size()) * sizeof(WorkItem)));
             h->items_cap = (int64_t)items.size();
+            h->sitems_cap = (int64_t)sitems.size();
         }
         h->nitems = (int64_t)items.size();
+        h->nsitems = (int64_t)sitems.size();
+        if (!sitems.empty())
+            HIP_TRY(h, hipMemcpyAsync(h->d_sitems, sitems.data(), sitems.size() * sizeof(WorkItem),
+                                      hipMemcpyHostToDevice, st));
         // pageable sources: staged synchronously by the runtime, safe to reuse on return
         HIP_TRY(h, hipMemcpyAsync(h->d_len, h->last_lens.data(), B * sizeof(int64_t), hipMemcpyHostToDevice, st));
         HIP_TRY(h, hipMemcpyAsync(h->d_items, items.data(), items.size() * sizeof(WorkItem), hipMemcpyHostToDevice, st));
@@ -411,11 +426,12 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
     mark(h, st);
 
     SynthArgs y{};
-    y.mic = mic; y.ld = ld; y.lens = h->d_len; y.cvals = h->d_cvals;
+    y.mic = mic; y.ld = ld; y.items = h->d_sitems; y.nitems = h->nsitems; y.num_cus = h->num_cus;
+    y.cvals = h->d_cvals;
     y.tables = reinterpret_cast<const float*>(h->d_tab);
     y.bintab = h->d_bintab; y.est = h->d_est; y.Tmax = Tmax;
     y.out = out; y.ld_out = ld_out;
-    HIP_TRY(h, launch_synthesis(y, B, st));
+    HIP_TRY(h, launch_synthesis(y, st));
     mark(h, st);
     h->last_B = B;
     h->last_T = Tmax;
@@ -507,7 +523,7 @@ void aec_destroy(aec_handle* h) {
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     (void)hipSetDevice(h->device);
     (void)hipFree(h->d_w); (void)hipFree(h->d_tab); (void)hipFree(h->d_sched); (void)hipFree(h->d_bintab);
-    (void)hipFree(h->d_mom); (void)hipFree(h->d_cvals); (void)hipFree(h->d_items); (void)hipFree(h->d_len);
+    (void)hipFree(h->d_mom); (void)hipFree(h->d_cvals); (void)hipFree(h->d_items); (void)hipFree(h->d_sitems); (void)hipFree(h->d_len);
     (void)hipFree(h->d_feats); (void)hipFree(h->d_est); (void)hipFree(h->d_dbg);
     delete h;
 }

@@ -2,6 +2,15 @@
 //
 // Reference: nn.GRU(64, 32) + linear1/relu + linear2/sigmoid + mask
 // (Stage2_lhm/scripts/network/ERB.py:213-217, 287-304) and the loss (:318-323).
+//
+// One block per stream, 7 waves:
+//   wave 0      the recurrence h_{t-1} -> h_t (the only sequential dependency
+//               of the whole path), one step per frame, raised issue priority;
+//   waves 1..6  helpers, software-pipelined around it in ticks of kCH frames:
+//               at tick c they stage chunk c+2's features (loaded from HBM at
+//               tick c-1, so no load latency is exposed), issue the loads of
+//               chunk c+3, compute gi = W_ih x + b for chunk c+1 and run the
+//               head (linear1/relu/linear2/sigmoid, est_erb, loss) for chunk c-1.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -9,14 +18,6 @@
 #include "aec_launch.h"
 
 namespace aec {
-
-// --------------------------------------------------------------------------
-// K3: GRU recurrence + head.  grid = B, block = 256:
-//   wave 0      : the recurrence (h_t depends on h_{t-1}); one step per frame
-//   waves 1..3  : helpers, software-pipelined one chunk (16 frames) ahead and
-//                 behind the recurrence: x-load (c+2), gi = W_ih x + b (c+1),
-//                 head / mask / est_erb / loss (c-1)
-// --------------------------------------------------------------------------
 
 __device__ __forceinline__ float sigmoidf_(float x) {
     return __builtin_amdgcn_rcpf(1.f + __expf(-x));
@@ -27,14 +28,19 @@ __device__ __forceinline__ float tanhf_(float x) {
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
+constexpr int kGruHelpers = 6;
+constexpr int kGruThreads = 64 * (1 + kGruHelpers);
+constexpr int kHL = 64 * kGruHelpers;                 // helper lanes (384)
+constexpr int kHeadGroups = kHL / 32;                 // 12 (j, frame-group) groups of 32 lanes
 
-__global__ __launch_bounds__(256) void gru_kernel(GruArgs p) {
+__global__ __launch_bounds__(kGruThreads) void gru_kernel(GruArgs p) {
     __shared__ __attribute__((aligned(16))) float sX[2][kCH][64];
     __shared__ __attribute__((aligned(16))) float sGi[2][kCH][96];
     __shared__ __attribute__((aligned(16))) float sH[2][kCH][32];
     __shared__ __attribute__((aligned(16))) float sMic[4][kCH][32];
-    __shared__ __attribute__((aligned(16))) float sO[6][32];
-    __shared__ float sLoss[4];
+    __shared__ __attribute__((aligned(16))) float sNear[4][kCH][32];
+    __shared__ __attribute__((aligned(16))) float sO[kHeadGroups][32];
+    __shared__ float sLoss[1 + kGruHelpers];
 
     const int b = blockIdx.x;
     const int64_t n = p.lens[b];
@@ -54,11 +60,12 @@ __global__ __launch_bounds__(256) void gru_kernel(GruArgs p) {
 
     if (wave == 0) {
         // ---------------- recurrence wave ----------------
-        const bool run = p.mode != 2;
         // lane l: j = l & 31, half = l >> 5.  Row pair per lane: (r_j, n_j) in
         // half 0, (z_j, n_j) in half 1, full 32-long dot products with h held
         // wave-uniform in SGPRs (v_readlane), so no LDS round trip sits on the
         // h_{t-1} -> h_t chain; h_j is computed identically in both halves.
+        __builtin_amdgcn_s_setprio(3);
+        const bool run = p.mode != 2;
         const int j = lane & 31, half = lane >> 5;
         f2v w[32];
         {
@@ -69,7 +76,7 @@ __global__ __launch_bounds__(256) void gru_kernel(GruArgs p) {
         }
         const float bhn = b_hh[64 + j];
         float hj = 0.f;                                   // h_{-1} = 0
-        for (int c = -2; c <= nch; ++c) {
+        for (int c = -3; c <= nch; ++c) {
             if (run && c >= 0 && c < nch) {
                 const int f_end = min(kCH, T - c * kCH);
                 const float* gi = &sGi[c & 1][0][0];
@@ -106,14 +113,15 @@ __global__ __launch_bounds__(256) void gru_kernel(GruArgs p) {
         }
     } else {
         // ---------------- helper waves ----------------
-        const int hl = tid - 64;                       // 0..191
-        // gi role: row = hl % 96, frames f = fpar, fpar+2, ...
-        const int grow = hl % 96, gpar = hl / 96;
+        const bool run = p.mode != 1;
+        const int hl = tid - 64;                       // 0..383
+        // gi role: row = hl % 96, frames f = fq, fq+4, fq+8, fq+12
+        const int grow = hl % 96, fq = hl / 96;
         float wih[64];
 #pragma unroll
         for (int k = 0; k < 64; ++k) wih[k] = W_ih[grow * 64 + k];
         const float gbias = b_ih[grow] + (grow < 64 ? b_hh[grow] : 0.f);
-        // head role: j = hl & 31, frames f = fg, fg+6, fg+12
+        // head role: j = hl & 31, frames f = fg, fg + 12
         const int hj_ = hl & 31, fg = hl >> 5;
         float w1[64], w2[32];
 #pragma unroll
@@ -122,33 +130,47 @@ __global__ __launch_bounds__(256) void gru_kernel(GruArgs p) {
         for (int k = 0; k < 32; ++k) w2[k] = W2[hj_ * 32 + k];
         const float b1j = b1[hj_], b2j = b2[hj_];
         float lacc = 0.f;
+        // feature prefetch registers: elements e = hl and hl + kHL of a chunk's
+        // [16 frames][32 bands] tile (mic, ref, near)
+        float pm[2] = {0.f, 0.f}, pr[2] = {0.f, 0.f}, pn[2] = {0.f, 0.f};
+        auto load_chunk = [&](int cc) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int e = hl + u * kHL;
+                const int t = cc * kCH + (e >> 5);
+                const bool ok = e < kCH * 32 && t < T;
+                const float* f = fb + (int64_t)t * 96 + (e & 31);
+                pm[u] = ok ? f[0] : 0.f;
+                pr[u] = ok ? f[32] : 0.f;
+                pn[u] = ok && p.has_near ? f[64] : 0.f;
+            }
+        };
 
-        const bool run = p.mode != 1;
-        for (int c = -2; c <= nch; ++c) {
-            // (a) x-load for chunk c+2 -> sX[(c+2)&1], mic_erb -> sMic[(c+2)&3]
-            {
-                const int cc = c + 2;
-                if (run && cc < nch) {
-                    for (int e = hl; e < kCH * 32; e += 192) {
-                        const int f = e >> 5, jj = e & 31;
-                        const int t = cc * kCH + f;
-                        float me = 0.f, re = 0.f;
-                        if (t < T) {
-                            me = fb[(int64_t)t * 96 + jj];
-                            re = fb[(int64_t)t * 96 + 32 + jj];
+        for (int c = -3; c <= nch; ++c) {
+            if (run) {
+                // (a) stage chunk c+2 (loaded at tick c-1) and load chunk c+3
+                const int cs = c + 2;
+                if (cs >= 0 && cs < nch) {
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const int e = hl + u * kHL;
+                        if (e < kCH * 32) {
+                            const int f = e >> 5, jj = e & 31;
+                            sX[cs & 1][f][jj] = pm[u];
+                            sX[cs & 1][f][32 + jj] = fabsf(pm[u] - pr[u]);
+                            sMic[cs & 3][f][jj] = pm[u];
+                            sNear[cs & 3][f][jj] = pn[u];
                         }
-                        sX[cc & 1][f][jj] = me;
-                        sX[cc & 1][f][32 + jj] = fabsf(me - re);
-                        sMic[cc & 3][f][jj] = me;
                     }
                 }
-            }
-            // (b) gi for chunk c+1
-            {
-                const int cc = c + 1;
-                if (run && cc >= 0 && cc < nch) {
-                    for (int f = gpar; f < kCH; f += 2) {
-                        const float4* x4 = reinterpret_cast<const float4*>(&sX[cc & 1][f][0]);
+                if (c + 3 < nch) load_chunk(c + 3);
+                // (b) gi for chunk c+1
+                const int cg = c + 1;
+                if (cg >= 0 && cg < nch) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int f = fq + 4 * i;
+                        const float4* x4 = reinterpret_cast<const float4*>(&sX[cg & 1][f][0]);
                         f2v a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
 #pragma unroll
                         for (int q = 0; q < 16; ++q) {
@@ -157,19 +179,17 @@ __global__ __launch_bounds__(256) void gru_kernel(GruArgs p) {
                             a1 = __builtin_elementwise_fma(f2v{wih[4 * q + 2], wih[4 * q + 3]}, f2v{xv.z, xv.w}, a1);
                         }
                         const f2v s2 = a0 + a1;
-                        sGi[cc & 1][f][grow] = gbias + (s2.x + s2.y);
+                        sGi[cg & 1][f][grow] = gbias + (s2.x + s2.y);
                     }
                 }
-            }
-            // (c) head for chunk c-1
-            {
-                const int cc = c - 1;
-                if (run && cc >= 0 && cc < nch) {
-                    for (int f = fg; f < kCH; f += 6) {
-                        const int t = cc * kCH + f;
+                // (c) head for chunk c-1
+                const int ch = c - 1;
+                if (ch >= 0 && ch < nch) {
+                    for (int f = fg; f < kCH; f += kHeadGroups) {
+                        const int t = ch * kCH + f;
                         if (t >= T) break;               // uniform within the 32-lane group
-                        const float4* h4 = reinterpret_cast<const float4*>(&sH[cc & 1][f][0]);
-                        const float4* m4 = reinterpret_cast<const float4*>(&sMic[cc & 3][f][0]);
+                        const float4* h4 = reinterpret_cast<const float4*>(&sH[ch & 1][f][0]);
+                        const float4* m4 = reinterpret_cast<const float4*>(&sMic[ch & 3][f][0]);
                         f2v a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
 #pragma unroll
                         for (int q = 0; q < 8; ++q) {
@@ -195,15 +215,14 @@ __global__ __launch_bounds__(256) void gru_kernel(GruArgs p) {
                         wave_fence();
                         const f2v s2 = c0 + c1;
                         const float mask = sigmoidf_(b2j + (s2.x + s2.y));
-                        const float me = sMic[cc & 3][f][hj_];
+                        const float me = sMic[ch & 3][f][hj_];
                         const float est = mask * me;
                         const int64_t o_idx = ((int64_t)b * p.Tmax + t) * 32 + hj_;
                         p.est[o_idx] = est;
-                        if (p.dbg_h) p.dbg_h[o_idx] = sH[cc & 1][f][hj_];
+                        if (p.dbg_h) p.dbg_h[o_idx] = sH[ch & 1][f][hj_];
                         if (p.dbg_mask) p.dbg_mask[o_idx] = mask;
                         if (p.has_near) {
-                            const float ne = fb[(int64_t)t * 96 + 64 + hj_];
-                            const float d = sqrtf(ne) - sqrtf(est);
+                            const float d = sqrtf(sNear[ch & 3][f][hj_]) - sqrtf(est);
                             lacc += d * d;
                         }
                     }
@@ -219,12 +238,16 @@ __global__ __launch_bounds__(256) void gru_kernel(GruArgs p) {
     }
     if (p.loss) {
         __syncthreads();
-        if (tid == 0) p.loss[b] = ((sLoss[1] + sLoss[2]) + sLoss[3]) / (float)(T * 32);
+        if (tid == 0) {
+            float s = 0.f;
+            for (int w = 1; w <= kGruHelpers; ++w) s += sLoss[w];
+            p.loss[b] = s / (float)(T * 32);
+        }
     }
 }
 
 hipError_t launch_gru(const GruArgs& a, int B, hipStream_t st) {
-    hipLaunchKernelGGL(gru_kernel, dim3(B), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(gru_kernel, dim3(B), dim3(kGruThreads), 0, st, a);
     return hipGetLastError();
 }
 

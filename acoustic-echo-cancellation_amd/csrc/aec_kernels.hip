@@ -340,19 +340,19 @@ __global__ __launch_bounds__(256, 3) void analysis_kernel(AnalysisArgs p) {
 }
 
 // --------------------------------------------------------------------------
-// K4: synthesis.  grid = (ceil(nhop_max/15), B), block = 256.  A block
-// re-derives the mic spectra of 16 consecutive frames (each wave stages and
-// transforms 4 of them), applies the ERB gains, inverse-transforms and, after
-// one block barrier, overlap-adds 15 output hops.
+// K4: synthesis.  One block of 256 threads per item of a host-built list
+// (stream b, first output hop h0).  The block re-derives the mic spectra of
+// the 16 frames h0 .. h0+15 (each wave stages and transforms 4 of them),
+// applies the ERB gains, inverse-transforms and, after a block barrier,
+// overlap-adds the 15 output hops h0 .. h0+14.  (A persistent variant that
+// prefetches the next item was measured slower: the prefetch registers live
+// across both transforms and cost a wave per SIMD.)  est_erb rows are padded
+// to 33 floats (two frames' gathers of the same band hit different banks).
 // --------------------------------------------------------------------------
+constexpr int kEstStride = 33;
+
 __global__ __launch_bounds__(256) void synthesis_kernel(SynthArgs p) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int b = blockIdx.y;
-    const int64_t n = p.lens[b];
-    const int64_t T = n / kHop + 1;
-    const int64_t nhop = T - 1;
-    const int64_t h0 = (int64_t)blockIdx.x * kHopsOut;
-    if (h0 >= nhop) return;
     const int tid = threadIdx.x;
 
     float4* sBin = reinterpret_cast<float4*>(smem);                   // 257 (+3 pad)
@@ -360,8 +360,8 @@ __global__ __launch_bounds__(256) void synthesis_kernel(SynthArgs p) {
     float2* sTwT = sTw512 + 258;                                      // 256
     float* sHann = reinterpret_cast<float*>(sTwT + 256);              // 512
     float* sCoff = sHann + 512;                                       // 256: 1/(window^2 OLA + 1e-8)
-    float* sEst = sCoff + 256;                                        // 16 * 32
-    float* sWave = sEst + kFPB * 32;                                  // 4 * kWaveFloats
+    float* sEst = sCoff + 256;                                        // 16 * 33 (+4 pad)
+    float* sWave = sEst + kFPB * kEstStride + 4;                      // 4 * kWaveFloats
 
     const DevTables* tb = reinterpret_cast<const DevTables*>(p.tables);
     {
@@ -374,100 +374,110 @@ __global__ __launch_bounds__(256) void synthesis_kernel(SynthArgs p) {
         sHann[tid] = tb->hann[tid];
         sHann[tid + 256] = tb->hann[tid + 256];
         sCoff[tid] = tb->inv_coff[tid];
-        for (int i = tid; i < kFPB * 32; i += 256) {
-            const int64_t t = h0 + (i >> 5);
-            sEst[i] = (t < T) ? p.est[((int64_t)b * p.Tmax + t) * 32 + (i & 31)] : 0.f;
-        }
     }
     const int wave = tid >> 6, lane = tid & 63;
     const int gg = lane >> 4, lb = lane & 15;
     const int g = tid >> 4;                                           // frame h0 + g
-    const int64_t wt = h0 + kWaveFrames * wave;
     float* wr = sWave + wave * kWaveFloats;
     float* scr = wr + gg * kGroupFloats;
+    const bool aligned = ((p.ld & 3) == 0) && ((reinterpret_cast<uintptr_t>(p.mic) & 15) == 0);
+    const bool oal = ((p.ld_out & 3) == 0) && ((reinterpret_cast<uintptr_t>(p.out) & 15) == 0);
+
+    const WorkItem it = p.items[blockIdx.x];
     {
+        const int b = it.b;
+        const int64_t n = it.n;
+        const int64_t T = n / kHop + 1;
+        const int64_t h0 = it.wt;
         float4 pf[kWavePf];
-        const bool aligned = ((p.ld & 3) == 0) && ((reinterpret_cast<uintptr_t>(p.mic) & 15) == 0);
-        wave_prefetch(pf, p.mic + (int64_t)b * p.ld, (int)n, (int)wt, lane, aligned);
-        wave_commit(wr, pf, p.cvals[b * 3 + 0], (int)n, (int)wt, lane);
+        wave_prefetch(pf, p.mic + (int64_t)b * p.ld, (int)n, (int)(h0 + kWaveFrames * wave), lane, aligned);
+        for (int i = tid; i < kFPB * 32; i += 256) {
+            const int64_t t = h0 + (i >> 5);
+            sEst[(i >> 5) * kEstStride + (i & 31)] = (t < T) ? p.est[((int64_t)b * p.Tmax + t) * 32 + (i & 31)] : 0.f;
+        }
+        wave_commit(wr, pf, p.cvals[b * 3 + 0], (int)n, (int)(h0 + kWaveFrames * wave), lane);
     }
     __syncthreads();                                                  // tables + est staged
-    wave_fence();
-    float2 v[16];
-    load_frame(v, wr, sHann, gg, lb);
-    wave_fence();
-    fft256<false>(v, lb, scr, sTwT);
-    float2 xa[8], xb[8], x128;
-    rfft_unpack(v, lb, sTw512, xa, xb, x128);
+    {
+        const int b = it.b;
+        const int64_t nhop = it.n / kHop;                             // T - 1
+        const int64_t h0 = it.wt;
+        float2 v[16];
+        load_frame(v, wr, sHann, gg, lb);
+        wave_fence();
+        fft256<false>(v, lb, scr, sTwT);
+        float2 xa[8], xb[8], x128;
+        rfft_unpack(v, lb, sTw512, xa, xb, x128);
 
-    // ERB gain per bin: g[k] = sum_j est_erb[j] erb[k][j] over the <= 2 bands
-    // covering bin k (ERB.py:306-307), applied to the mic spectrum (:309-310)
-    const float* est = sEst + g * 32;
-    auto gain = [&](int k) {
-        const float4 e = sBin[k];
-        return e.y * est[__float_as_int(e.x)] + e.w * est[__float_as_int(e.z)];
-    };
-    // inverse pack: lane lb forms 2Z'[k] and 2Z'[256-k] for k = lb + 16 m; the
-    // inverse FFT wants v[a] = 2Z'[16a + lb]: a <= 7 is this lane's own Zk[a],
-    // a >= 8 is Zmk[15-a] of lane (16-lb)&15 (DPP), lane 0 patched.
-    float2 Zk[8], Zmk[8];
-    static_for<0, 8>([&](auto mi) {
-        constexpr int m = decltype(mi)::value;
-        const int k = lb + 16 * m;
-        // k == 0 (lane 0, m = 0): DC / Nyquist, irfft ignores their imaginary parts;
-        // gain(256 - 0) indexes bin 256 = Nyquist, as required
-        const float ga = gain(k), gb = gain(256 - k);
-        float2 zk, zmk;
-        irfft_pair(cscale(xa[m], ga), cscale(xb[m], gb), sTw512[k], zk, zmk);
-        const float s0 = ga * xa[m].x, s256 = gb * xb[m].x;
-        Zk[m] = csel(k == 0, make_float2(s0 + s256, s0 - s256), zk);
-        Zmk[m] = csel(k == 0, Zk[m], zmk);
-    });
-    float2 z128 = make_float2(0.f, 0.f);
-    if (lb == 0) {
-        const float2 S = cscale(x128, gain(128));
-        z128 = make_float2(2.f * S.x, -2.f * S.y);   // 2*conj(S[128])
-    }
-#pragma unroll
-    for (int a = 0; a < 8; ++a) v[a] = Zk[a];
-    static_for<8, 16>([&](auto ai) {
-        constexpr int a = decltype(ai)::value;
-        const float2 mir = mirror16(Zmk[15 - a]);
-        v[a] = csel(lb != 0, mir, a == 8 ? z128 : Zmk[(16 - a) & 7]);
-    });
-    fft256<true>(v, lb, scr, sTwT);
-    // v[kP(m2)] = 512 * (x[2m] + i x[2m+1]), m = lb + 16 m2 ; window + 1/512
-    float2* s2 = reinterpret_cast<float2*>(scr);
-#pragma unroll
-    for (int m2 = 0; m2 < 16; ++m2) {
-        const int nn = 2 * (lb + 16 * m2);
-        const float2 z = v[kP(m2)];
-        s2[lb + 16 * m2] = make_float2(z.x * (sHann[nn] * (1.f / 512.f)), z.y * (sHann[nn + 1] * (1.f / 512.f)));
-    }
-    __syncthreads();
-    // overlap-add + WOLA normalisation + trim (attention_ccrn.py:92-99) + 1e-9 (ERB.py:316)
-    float* orow = p.out + (int64_t)b * p.ld_out;
-    const int nh = (int)min((int64_t)kHopsOut, nhop - h0);
-    const bool oal = ((p.ld_out & 3) == 0) && ((reinterpret_cast<uintptr_t>(p.out) & 15) == 0);
-    if (oal) {
-        for (int e = tid; e < nh * (kHop / 4); e += 256) {
-            const int i = e >> 6, r = (e & 63) * 4;
-            const float4 a = *reinterpret_cast<const float4*>(sWave + i * kGroupFloats + 256 + r);
-            const float4 c = *reinterpret_cast<const float4*>(sWave + (i + 1) * kGroupFloats + r);
-            const float4 cf = *reinterpret_cast<const float4*>(sCoff + r);
-            float4 o;
-            o.x = (a.x + c.x) * cf.x + 1e-9f;
-            o.y = (a.y + c.y) * cf.y + 1e-9f;
-            o.z = (a.z + c.z) * cf.z + 1e-9f;
-            o.w = (a.w + c.w) * cf.w + 1e-9f;
-            *reinterpret_cast<float4*>(orow + (h0 + i) * kHop + r) = o;
+        // ERB gain per bin: g[k] = sum_j est_erb[j] erb[k][j] over the <= 2 bands
+        // covering bin k (ERB.py:306-307), applied to the mic spectrum (:309-310)
+        const float* est = sEst + g * kEstStride;
+        auto gain = [&](int kk) {
+            const float4 e = sBin[kk];
+            return e.y * est[__float_as_int(e.x)] + e.w * est[__float_as_int(e.z)];
+        };
+        // inverse pack: lane lb forms 2Z'[k] and 2Z'[256-k] for k = lb + 16 m; the
+        // inverse FFT wants v[a] = 2Z'[16a + lb]: a <= 7 is this lane's own Zk[a],
+        // a >= 8 is Zmk[15-a] of lane (16-lb)&15 (DPP), lane 0 patched.
+        float2 Zk[8], Zmk[8];
+        static_for<0, 8>([&](auto mi) {
+            constexpr int m = decltype(mi)::value;
+            const int kk = lb + 16 * m;
+            // kk == 0 (lane 0, m = 0): DC / Nyquist, irfft ignores their imaginary parts;
+            // gain(256 - 0) indexes bin 256 = Nyquist, as required
+            const float ga = gain(kk), gb = gain(256 - kk);
+            float2 zk, zmk;
+            irfft_pair(cscale(xa[m], ga), cscale(xb[m], gb), sTw512[kk], zk, zmk);
+            const float s0 = ga * xa[m].x, s256 = gb * xb[m].x;
+            Zk[m] = csel(kk == 0, make_float2(s0 + s256, s0 - s256), zk);
+            Zmk[m] = csel(kk == 0, Zk[m], zmk);
+        });
+        float2 z128 = make_float2(0.f, 0.f);
+        if (lb == 0) {
+            const float2 S = cscale(x128, gain(128));
+            z128 = make_float2(2.f * S.x, -2.f * S.y);   // 2*conj(S[128])
         }
-    } else {
-        for (int e = tid; e < nh * kHop; e += 256) {
-            const int i = e >> 8, r = e & 255;
-            const float a = sWave[i * kGroupFloats + 256 + r];
-            const float c = sWave[(i + 1) * kGroupFloats + r];
-            orow[(h0 + i) * kHop + r] = (a + c) * sCoff[r] + 1e-9f;
+#pragma unroll
+        for (int a = 0; a < 8; ++a) v[a] = Zk[a];
+        static_for<8, 16>([&](auto ai) {
+            constexpr int a = decltype(ai)::value;
+            const float2 mir = mirror16(Zmk[15 - a]);
+            v[a] = csel(lb != 0, mir, a == 8 ? z128 : Zmk[(16 - a) & 7]);
+        });
+        fft256<true>(v, lb, scr, sTwT);
+        // v[kP(m2)] = 512 * (x[2m] + i x[2m+1]), m = lb + 16 m2 ; window + 1/512
+        float2* s2 = reinterpret_cast<float2*>(scr);
+        const float2* h2 = reinterpret_cast<const float2*>(sHann);
+#pragma unroll
+        for (int m2 = 0; m2 < 16; ++m2) {
+            const float2 z = v[kP(m2)];
+            const float2 w = h2[lb + 16 * m2];
+            s2[lb + 16 * m2] = make_float2(z.x * (w.x * (1.f / 512.f)), z.y * (w.y * (1.f / 512.f)));
+        }
+        __syncthreads();
+        // overlap-add + WOLA normalisation + trim (attention_ccrn.py:92-99) + 1e-9 (ERB.py:316)
+        float* orow = p.out + (int64_t)b * p.ld_out;
+        const int nh = (int)min((int64_t)kHopsOut, nhop - h0);
+        if (oal) {
+            for (int e = tid; e < nh * (kHop / 4); e += 256) {
+                const int i = e >> 6, r = (e & 63) * 4;
+                const float4 a = *reinterpret_cast<const float4*>(sWave + i * kGroupFloats + 256 + r);
+                const float4 c = *reinterpret_cast<const float4*>(sWave + (i + 1) * kGroupFloats + r);
+                const float4 cf = *reinterpret_cast<const float4*>(sCoff + r);
+                float4 o;
+                o.x = (a.x + c.x) * cf.x + 1e-9f;
+                o.y = (a.y + c.y) * cf.y + 1e-9f;
+                o.z = (a.z + c.z) * cf.z + 1e-9f;
+                o.w = (a.w + c.w) * cf.w + 1e-9f;
+                *reinterpret_cast<float4*>(orow + (h0 + i) * kHop + r) = o;
+            }
+        } else {
+            for (int e = tid; e < nh * kHop; e += 256) {
+                const int i = e >> 8, r = e & 255;
+                const float a = sWave[i * kGroupFloats + 256 + r];
+                const float c = sWave[(i + 1) * kGroupFloats + r];
+                orow[(h0 + i) * kHop + r] = (a + c) * sCoff[r] + 1e-9f;
+            }
         }
     }
 }
@@ -497,11 +507,9 @@ hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_synthesis(const SynthArgs& a, int B, hipStream_t st) {
-    const int64_t nhop = a.Tmax - 1;
-    if (nhop <= 0) return hipSuccess;
-    const dim3 grid((unsigned)((nhop + kHopsOut - 1) / kHopsOut), B);
-    hipLaunchKernelGGL(synthesis_kernel, grid, dim3(256), synthesis_smem_bytes(), st, a);
+hipError_t launch_synthesis(const SynthArgs& a, hipStream_t st) {
+    if (a.nitems <= 0) return hipSuccess;
+    hipLaunchKernelGGL(synthesis_kernel, dim3((unsigned)a.nitems), dim3(256), synthesis_smem_bytes(), st, a);
     return hipGetLastError();
 }
 

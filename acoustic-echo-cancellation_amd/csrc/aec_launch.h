@@ -52,7 +52,9 @@ struct GruArgs {
 struct SynthArgs {
     const float* mic;
     int64_t ld;
-    const int64_t* lens;
+    const WorkItem* items;   // host-built list: (b, first output hop h0, n), h0 += 15
+    int64_t nitems;
+    int num_cus;
     const float* cvals;
     const float* tables;
     const float* bintab;     // float4[257]: (band_a, w_a, band_b, w_b) per bin
@@ -67,7 +69,7 @@ inline size_t analysis_smem_bytes(int sched_len) {
     return (size_t)sched_len * 16 * 16 + 32 * 8 + (258 * 2 + 256 * 2 + 512 + (size_t)kFPB * kGroupFloats) * 4;
 }
 inline size_t synthesis_smem_bytes() {
-    return 260 * 16 + (258 * 2 + 256 * 2 + 512 + 256 + kFPB * 32 + (size_t)kFPB * kGroupFloats) * 4;
+    return 260 * 16 + (258 * 2 + 256 * 2 + 512 + 256 + kFPB * 33 + 4 + (size_t)kFPB * kGroupFloats) * 4;
 }
 
 hipError_t launch_moments(const float* mic, const float* ref, const float* near, int64_t ld,
@@ -76,6 +78,6 @@ hipError_t launch_norm_finalize(const double2* mom, const int64_t* lens, float* 
                                 hipStream_t st);
 hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t st);
 hipError_t launch_gru(const GruArgs& a, int B, hipStream_t st);
-hipError_t launch_synthesis(const SynthArgs& a, int B, hipStream_t st);
+hipError_t launch_synthesis(const SynthArgs& a, hipStream_t st);
 
 }  // namespace aec
