@@ -190,6 +190,18 @@ struct aec_handle {
     WorkItem* d_sitems = nullptr; // synthesis block-item list
     int64_t sitems_cap = 0, nsitems = 0;
     int num_cus = 256;
+    std::vector<int64_t> item_off, sitem_off;   // first analysis / synthesis item of stream b (B+1 entries)
+    // sub-batch pipelining (AEC_SUBBATCH=S, default 1 = off): streams
+    // [b_k, b_k+1) run their chain on internal stream k; chain k+1 starts its
+    // moments/analysis once chain k's analysis is done, meant to overlap its
+    // FFT work with chain k's latency-bound recurrence.  Measured slower on
+    // MI355X (S=2: 0.80 ms vs 0.69 ms per 256-stream step): the persistent
+    // analysis grid fills every CU's LDS and the GRU's 244-VGPR waves cannot
+    // co-reside, so the sub-batch GRUs serialise.  Kept for co-residency work.
+    static constexpr int kMaxSub = 4;
+    int sub_max = 1;
+    hipStream_t sst[kMaxSub] = {};
+    hipEvent_t ev_start = nullptr, ev_ana[kMaxSub] = {}, ev_done[kMaxSub] = {};
     int64_t* d_len = nullptr;    // [B]
     float* d_feats = nullptr;    // [B][T][96]
     float* d_est = nullptr;      // [B][T][32]
@@ -297,6 +309,7 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
     h->cfg = *cfg;
     h->device = device;
     if (const char* m = std::getenv("AEC_GRU_MODE")) h->gru_mode = std::atoi(m);
+    if (const char* m = std::getenv("AEC_SUBBATCH")) h->sub_max = std::max(1, std::min(aec_handle::kMaxSub, std::atoi(m)));
     {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
@@ -304,6 +317,13 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
     }
     auto bail = [&](aec_status s) { aec_destroy(h); return s; };
     if (hipSetDevice(device) != hipSuccess) return bail(AEC_ERR_HIP);
+    for (int k = 0; k < aec_handle::kMaxSub; ++k) {
+        if (hipStreamCreateWithFlags(&h->sst[k], hipStreamNonBlocking) != hipSuccess) return bail(AEC_ERR_HIP);
+        if (hipEventCreateWithFlags(&h->ev_ana[k], hipEventDisableTiming) != hipSuccess) return bail(AEC_ERR_HIP);
+        if (hipEventCreateWithFlags(&h->ev_done[k], hipEventDisableTiming) != hipSuccess) return bail(AEC_ERR_HIP);
+    }
+    if (hipEventCreateWithFlags(&h->ev_start, hipEventDisableTiming) != hipSuccess) return bail(AEC_ERR_HIP);
+
     if (hipMalloc(&h->d_w, kWeights32 * sizeof(float)) != hipSuccess) return bail(AEC_ERR_OOM);
     if (hipMemset(h->d_w, 0, kWeights32 * sizeof(float)) != hipSuccess) return bail(AEC_ERR_HIP);
     if (hipMalloc(&h->d_tab, sizeof(DevTables)) != hipSuccess) return bail(AEC_ERR_OOM);
@@ -372,16 +392,22 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
         h->last_lens.assign(lengths, lengths + B);
         // analysis work list: 4-frame items of every stream, valid frames only
         std::vector<WorkItem> items;
+        h->item_off.assign(B + 1, 0);
         for (int b = 0; b < B; ++b) {
+            h->item_off[b] = (int64_t)items.size();
             const int64_t T = aec_num_frames(lengths[b]);
             for (int64_t wt = 0; wt < T; wt += 4) items.push_back({b, (int32_t)wt, lengths[b]});
         }
+        h->item_off[B] = (int64_t)items.size();
         // synthesis work list: 15 output hops per block item
         std::vector<WorkItem> sitems;
+        h->sitem_off.assign(B + 1, 0);
         for (int b = 0; b < B; ++b) {
+            h->sitem_off[b] = (int64_t)sitems.size();
             const int64_t nhop = lengths[b] / 256;
             for (int64_t h0 = 0; h0 < nhop; h0 += kHopsOut) sitems.push_back({b, (int32_t)h0, lengths[b]});
         }
+        h->sitem_off[B] = (int64_t)sitems.size();
         if ((int64_t)items.size() > h->items_cap || (int64_t)sitems.size() > h->sitems_cap) {
             HIP_TRY(h, hipStreamSynchronize(st));
             if (h->d_items) HIP_TRY(h, hipFree(h->d_items));
@@ -402,37 +428,54 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
         HIP_TRY(h, hipMemcpyAsync(h->d_items, items.data(), items.size() * sizeof(WorkItem), hipMemcpyHostToDevice, st));
     }
     const int nsig = near ? 3 : 2;
-    mark(h, st);
-    HIP_TRY(h, launch_moments(mic, ref, near, ld, h->d_len, h->d_mom, B, nsig, st));
-    HIP_TRY(h, launch_norm_finalize(h->d_mom, h->d_len, h->d_cvals, B, nsig, st));
+    const int S = std::max(1, std::min(h->sub_max, B / 32));
+    if (S > 1) HIP_TRY(h, hipEventRecord(h->ev_start, st));
+    for (int k = 0; k < S; ++k) {
+        const int b0 = (int)((int64_t)B * k / S), b1 = (int)((int64_t)B * (k + 1) / S);
+        hipStream_t ks = S > 1 ? h->sst[k] : st;
+        if (S > 1) {
+            HIP_TRY(h, hipStreamWaitEvent(ks, h->ev_start, 0));
+            if (k > 0) HIP_TRY(h, hipStreamWaitEvent(ks, h->ev_ana[k - 1], 0));
+        }
+        mark(h, ks);
+        HIP_TRY(h, launch_moments(mic, ref, near, ld, h->d_len, h->d_mom, b0, b1 - b0, nsig, ks));
+        HIP_TRY(h, launch_norm_finalize(h->d_mom, h->d_len, h->d_cvals, b0, b1, nsig, ks));
 
-    AnalysisArgs a{};
-    a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
-    a.ld = ld; a.items = h->d_items; a.nitems = h->nitems; a.num_cus = h->num_cus; a.cvals = h->d_cvals;
-    a.tables = reinterpret_cast<const float*>(h->d_tab);
-    a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
-    a.feats = h->d_feats; a.Tmax = Tmax;
-    mark(h, st);
-    HIP_TRY(h, launch_analysis(a, st));
-    mark(h, st);
+        AnalysisArgs a{};
+        a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
+        a.ld = ld; a.items = h->d_items + h->item_off[b0]; a.nitems = h->item_off[b1] - h->item_off[b0];
+        a.num_cus = h->num_cus; a.cvals = h->d_cvals;
+        a.tables = reinterpret_cast<const float*>(h->d_tab);
+        a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
+        a.feats = h->d_feats; a.Tmax = Tmax;
+        mark(h, ks);
+        HIP_TRY(h, launch_analysis(a, ks));
+        mark(h, ks);
+        if (S > 1) HIP_TRY(h, hipEventRecord(h->ev_ana[k], ks));
 
-    GruArgs g{};
-    g.feats = h->d_feats; g.Tmax = Tmax; g.lens = h->d_len; g.w = h->d_w;
-    g.est = h->d_est; g.loss = loss; g.has_near = near != nullptr;
-    g.dbg_h = h->debug ? h->d_dbg : nullptr;
-    g.dbg_mask = h->debug ? h->d_dbg + B * Tmax * 32 : nullptr;
-    g.mode = h->gru_mode;
-    HIP_TRY(h, launch_gru(g, B, st));
-    mark(h, st);
+        GruArgs g{};
+        g.feats = h->d_feats; g.Tmax = Tmax; g.lens = h->d_len; g.w = h->d_w;
+        g.est = h->d_est; g.loss = loss; g.has_near = near != nullptr;
+        g.dbg_h = h->debug ? h->d_dbg : nullptr;
+        g.dbg_mask = h->debug ? h->d_dbg + B * Tmax * 32 : nullptr;
+        g.mode = h->gru_mode;
+        g.b0 = b0;
+        HIP_TRY(h, launch_gru(g, b1 - b0, ks));
+        mark(h, ks);
 
-    SynthArgs y{};
-    y.mic = mic; y.ld = ld; y.items = h->d_sitems; y.nitems = h->nsitems; y.num_cus = h->num_cus;
-    y.cvals = h->d_cvals;
-    y.tables = reinterpret_cast<const float*>(h->d_tab);
-    y.bintab = h->d_bintab; y.est = h->d_est; y.Tmax = Tmax;
-    y.out = out; y.ld_out = ld_out;
-    HIP_TRY(h, launch_synthesis(y, st));
-    mark(h, st);
+        SynthArgs y{};
+        y.mic = mic; y.ld = ld; y.items = h->d_sitems + h->sitem_off[b0];
+        y.nitems = h->sitem_off[b1] - h->sitem_off[b0]; y.num_cus = h->num_cus;
+        y.cvals = h->d_cvals;
+        y.tables = reinterpret_cast<const float*>(h->d_tab);
+        y.bintab = h->d_bintab; y.est = h->d_est; y.Tmax = Tmax;
+        y.out = out; y.ld_out = ld_out;
+        HIP_TRY(h, launch_synthesis(y, ks));
+        mark(h, ks);
+        if (S > 1) HIP_TRY(h, hipEventRecord(h->ev_done[k], ks));
+    }
+    if (S > 1)
+        for (int k = 0; k < S; ++k) HIP_TRY(h, hipStreamWaitEvent(st, h->ev_done[k], 0));
     h->last_B = B;
     h->last_T = Tmax;
     return AEC_OK;
@@ -521,6 +564,12 @@ aec_status aec_erb_tables_check(const float* erb, const float* mags, const float
 void aec_destroy(aec_handle* h) {
     if (!h) return;
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+    for (int k = 0; k < aec_handle::kMaxSub; ++k) {
+        if (h->sst[k]) (void)hipStreamDestroy(h->sst[k]);
+        if (h->ev_ana[k]) (void)hipEventDestroy(h->ev_ana[k]);
+        if (h->ev_done[k]) (void)hipEventDestroy(h->ev_done[k]);
+    }
+    if (h->ev_start) (void)hipEventDestroy(h->ev_start);
     (void)hipSetDevice(h->device);
     (void)hipFree(h->d_w); (void)hipFree(h->d_tab); (void)hipFree(h->d_sched); (void)hipFree(h->d_bintab);
     (void)hipFree(h->d_mom); (void)hipFree(h->d_cvals); (void)hipFree(h->d_items); (void)hipFree(h->d_sitems); (void)hipFree(h->d_len);

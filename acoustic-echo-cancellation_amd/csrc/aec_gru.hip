@@ -42,7 +42,7 @@ __global__ __launch_bounds__(kGruThreads) void gru_kernel(GruArgs p) {
     __shared__ __attribute__((aligned(16))) float sO[kHeadGroups][32];
     __shared__ float sLoss[1 + kGruHelpers];
 
-    const int b = blockIdx.x;
+    const int b = p.b0 + blockIdx.x;
     const int64_t n = p.lens[b];
     const int T = (int)(n / kHop + 1);
     const int nch = (T + kCH - 1) / kCH;

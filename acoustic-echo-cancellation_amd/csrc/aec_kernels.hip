@@ -35,8 +35,8 @@ __global__ __launch_bounds__(256) void moments_kernel(const float* __restrict__ 
                                                       const float* __restrict__ ref,
                                                       const float* __restrict__ near, int64_t ld,
                                                       const int64_t* __restrict__ lens,
-                                                      double2* __restrict__ mom) {
-    const int ch = blockIdx.x, s = blockIdx.y, b = blockIdx.z;
+                                                      double2* __restrict__ mom, int b0) {
+    const int ch = blockIdx.x, s = blockIdx.y, b = b0 + blockIdx.z;
     const float* base = (s == 0 ? mic : (s == 1 ? ref : near));
     const float* x = base + (int64_t)b * ld;
     const int64_t n = lens[b];
@@ -111,9 +111,9 @@ __device__ __forceinline__ float norm_scalar(const double2* __restrict__ mom, in
 // c for every (stream, signal): cvals[b*3 + s]
 __global__ __launch_bounds__(256) void norm_finalize_kernel(const double2* __restrict__ mom,
                                                             const int64_t* __restrict__ lens,
-                                                            float* __restrict__ cvals, int B, int nsig) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= B * 3) return;
+                                                            float* __restrict__ cvals, int b0, int b1, int nsig) {
+    const int i = b0 * 3 + blockIdx.x * 256 + threadIdx.x;
+    if (i >= b1 * 3) return;
     const int b = i / 3, s = i % 3;
     cvals[i] = s < nsig ? norm_scalar(mom, b, s, lens[b]) : 0.f;
 }
@@ -486,14 +486,17 @@ __global__ __launch_bounds__(256) void synthesis_kernel(SynthArgs p) {
 // host-side launchers (called by aec_api.hip)
 // --------------------------------------------------------------------------
 hipError_t launch_moments(const float* mic, const float* ref, const float* near, int64_t ld,
-                          const int64_t* lens, double2* mom, int B, int nsig, hipStream_t st) {
-    hipLaunchKernelGGL(moments_kernel, dim3(kMomChunks, nsig, B), dim3(256), 0, st, mic, ref, near, ld, lens, mom);
+                          const int64_t* lens, double2* mom, int b0, int nb, int nsig, hipStream_t st) {
+    if (nb <= 0) return hipSuccess;
+    hipLaunchKernelGGL(moments_kernel, dim3(kMomChunks, nsig, nb), dim3(256), 0, st, mic, ref, near, ld, lens, mom, b0);
     return hipGetLastError();
 }
 
-hipError_t launch_norm_finalize(const double2* mom, const int64_t* lens, float* cvals, int B, int nsig,
+hipError_t launch_norm_finalize(const double2* mom, const int64_t* lens, float* cvals, int b0, int b1, int nsig,
                                 hipStream_t st) {
-    hipLaunchKernelGGL(norm_finalize_kernel, dim3((B * 3 + 255) / 256), dim3(256), 0, st, mom, lens, cvals, B, nsig);
+    if (b1 <= b0) return hipSuccess;
+    hipLaunchKernelGGL(norm_finalize_kernel, dim3(((b1 - b0) * 3 + 255) / 256), dim3(256), 0, st, mom, lens, cvals,
+                       b0, b1, nsig);
     return hipGetLastError();
 }
 

@@ -47,6 +47,7 @@ struct GruArgs {
     float* dbg_h;            // [B][Tmax][32] or null
     float* dbg_mask;         // [B][Tmax][32] or null
     int mode;                // timing experiments only: 0 full, 1 recurrence only, 2 helpers only
+    int b0;                  // first stream of this launch (block i runs stream b0 + i)
 };
 
 struct SynthArgs {
@@ -73,8 +74,8 @@ inline size_t synthesis_smem_bytes() {
 }
 
 hipError_t launch_moments(const float* mic, const float* ref, const float* near, int64_t ld,
-                          const int64_t* lens, double2* mom, int B, int nsig, hipStream_t st);
-hipError_t launch_norm_finalize(const double2* mom, const int64_t* lens, float* cvals, int B, int nsig,
+                          const int64_t* lens, double2* mom, int b0, int nb, int nsig, hipStream_t st);
+hipError_t launch_norm_finalize(const double2* mom, const int64_t* lens, float* cvals, int b0, int b1, int nsig,
                                 hipStream_t st);
 hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t st);
 hipError_t launch_gru(const GruArgs& a, int B, hipStream_t st);

@@ -179,13 +179,17 @@ def main():
     frames_total = world * B * T * args.steps
     value = frames_total / el
     ms_step = el / args.steps * 1e3
-    per_kernel_ms = {k: kms[i] / max(calls, 1) for i, k in enumerate(KERNELS)}
+    # `calls` counts kernel launches (aec_process splits a batch into sub-batches,
+    # one launch of each kernel per sub-batch); per-step = per-call sum
+    launches_per_step = max(calls, 1) / args.steps
+    per_kernel_ms = {k: kms[i] / args.steps for i, k in enumerate(KERNELS)}
+    per_launch_ms = {k: kms[i] / max(calls, 1) for i, k in enumerate(KERNELS)}
     dom = max(per_kernel_ms, key=per_kernel_ms.get)
     pmc = None
     pmc_path = os.path.join(REPO, 'profiles', 'pmc_latest.json')
     if os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path))
-    roof = roofline(dom, per_kernel_ms[dom], B * T, pmc)
+    roof = roofline(dom, per_launch_ms[dom], int(round(B * T / launches_per_step)), pmc)
     pipe_t = ms_step * 1e-3 / world
     pipe_gbs = PIPE['bytes'] * B * T / pipe_t / 1e9
     pipe_tfl = PIPE['flops'] * B * T / pipe_t / 1e12
@@ -205,6 +209,7 @@ def main():
             'xRT': round(value * 256 / 16000, 1),
             'rtf_batch1': rtf1,
             'kernel_ms_per_step': {k: round(v, 4) for k, v in per_kernel_ms.items()},
+            'launches_per_step': launches_per_step,
             'roofline': roof,
             'pipeline_roofline': {'alg_bytes_per_frame': PIPE['bytes'], 'alg_flops_per_frame': PIPE['flops'],
                                   'hbm_frac': round(pipe_gbs / HBM_PEAK_GBS, 4),
