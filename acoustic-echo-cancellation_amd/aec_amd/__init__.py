@@ -2,12 +2,12 @@
 SZU-Speech/Acoustic-Echo-Cancellation (Stage2_lhm/).
 
 Public surface (mirrors the reference):
-  * ``Little_net(conf, erb_bands)``                 scripts/network/ERB.py:203
+  * ``Little_net(conf, erb_bands, nlms=None)``      scripts/network/ERB.py:203 (+ build-defined FD-NLMS)
   * ``EquivalentRectangularBandwidth(...).filters`` scripts/network/ERB.py:10
   * ``speech_conf`` / ``erb_conf``                  scripts/configs.py:1-27
 The compute runs in ``libaec_hip.so`` (C ABI: include/aec_hip.h).
 """
-from .configs import speech_conf, erb_conf, train_conf          # noqa: F401
+from .configs import speech_conf, erb_conf, train_conf, nlms_conf  # noqa: F401
 from .erb import EquivalentRectangularBandwidth, erb_matrix     # noqa: F401
 from .little_net import Little_net                              # noqa: F401
 

@@ -206,6 +206,7 @@ struct aec_handle {
     float* d_feats = nullptr;    // [B][T][96]
     float* d_est = nullptr;      // [B][T][32]
     float* d_dbg = nullptr;      // [2][B][T][32]  (h, mask)
+    float2* d_spec = nullptr;    // [B][T][256] NLMS error spectrum (nlms_taps > 0 only)
     std::vector<int64_t> last_lens;
     int debug = 0;
     int gru_mode = 0;            // AEC_GRU_MODE (timing experiments; results invalid unless 0)
@@ -303,7 +304,10 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
     *out = nullptr;
     if (!cfg) return AEC_ERR_INVALID_ARG;
     if (cfg->win_size != 512 || cfg->hop_size != 256 || cfg->erb_bands != 32) return AEC_ERR_UNSUPPORTED;
-    if (cfg->nlms_taps != 0) return AEC_ERR_UNSUPPORTED;   // FD-NLMS: not in this build yet
+    if (cfg->nlms_taps < 0 || cfg->nlms_taps > 8) return AEC_ERR_UNSUPPORTED;
+    if (cfg->nlms_taps > 0 && !(cfg->nlms_mu >= 0.f && cfg->nlms_mu < 2.f && cfg->nlms_beta >= 0.f &&
+                                cfg->nlms_beta < 1.f && cfg->nlms_delta > 0.f && std::isfinite(cfg->nlms_delta)))
+        return AEC_ERR_INVALID_ARG;
     aec_handle* h = new (std::nothrow) aec_handle();
     if (!h) return AEC_ERR_OOM;
     h->cfg = *cfg;
@@ -345,8 +349,9 @@ static aec_status ensure_ws(aec_handle* h, int64_t B, int64_t T) {
     const int64_t nT = T > h->ws_T ? T : h->ws_T;
     HIP_TRY(h, hipDeviceSynchronize());
     (void)hipFree(h->d_mom); (void)hipFree(h->d_cvals); (void)hipFree(h->d_len); (void)hipFree(h->d_feats);
-    (void)hipFree(h->d_est); (void)hipFree(h->d_dbg);
+    (void)hipFree(h->d_est); (void)hipFree(h->d_dbg); (void)hipFree(h->d_spec);
     h->d_mom = nullptr; h->d_cvals = nullptr; h->d_len = nullptr; h->d_feats = h->d_est = h->d_dbg = nullptr;
+    h->d_spec = nullptr;
     h->ws_B = h->ws_T = 0;
     h->last_lens.clear();
     HIP_TRY(h, hipMalloc(&h->d_mom, nB * 3 * kMomChunks * sizeof(double2)));
@@ -355,6 +360,7 @@ static aec_status ensure_ws(aec_handle* h, int64_t B, int64_t T) {
     HIP_TRY(h, hipMalloc(&h->d_feats, nB * nT * 96 * sizeof(float)));
     HIP_TRY(h, hipMalloc(&h->d_est, nB * nT * 32 * sizeof(float)));
     HIP_TRY(h, hipMalloc(&h->d_dbg, 2 * nB * nT * 32 * sizeof(float)));
+    if (h->cfg.nlms_taps > 0) HIP_TRY(h, hipMalloc(&h->d_spec, nB * nT * 256 * sizeof(float2)));
     h->ws_B = nB;
     h->ws_T = nT;
     return AEC_OK;
@@ -441,15 +447,29 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
         HIP_TRY(h, launch_moments(mic, ref, near, ld, h->d_len, h->d_mom, b0, b1 - b0, nsig, ks));
         HIP_TRY(h, launch_norm_finalize(h->d_mom, h->d_len, h->d_cvals, b0, b1, nsig, ks));
 
-        AnalysisArgs a{};
-        a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
-        a.ld = ld; a.items = h->d_items + h->item_off[b0]; a.nitems = h->item_off[b1] - h->item_off[b0];
-        a.num_cus = h->num_cus; a.cvals = h->d_cvals;
-        a.tables = reinterpret_cast<const float*>(h->d_tab);
-        a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
-        a.feats = h->d_feats; a.Tmax = Tmax;
-        mark(h, ks);
-        HIP_TRY(h, launch_analysis(a, ks));
+        if (h->cfg.nlms_taps > 0) {
+            if (nlms_smem_bytes(h->sched_len, h->cfg.nlms_taps) > 160 * 1024)
+                return fail(h, AEC_ERR_UNSUPPORTED, "erb schedule too long for the NLMS kernel's LDS budget");
+            NlmsArgs a{};
+            a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
+            a.ld = ld; a.lens = h->d_len; a.b0 = b0; a.cvals = h->d_cvals;
+            a.tables = reinterpret_cast<const float*>(h->d_tab);
+            a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
+            a.feats = h->d_feats; a.Tmax = Tmax; a.spec = h->d_spec;
+            a.taps = h->cfg.nlms_taps; a.mu = h->cfg.nlms_mu; a.beta = h->cfg.nlms_beta; a.delta = h->cfg.nlms_delta;
+            mark(h, ks);
+            HIP_TRY(h, launch_nlms_analysis(a, b1 - b0, ks));
+        } else {
+            AnalysisArgs a{};
+            a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
+            a.ld = ld; a.items = h->d_items + h->item_off[b0]; a.nitems = h->item_off[b1] - h->item_off[b0];
+            a.num_cus = h->num_cus; a.cvals = h->d_cvals;
+            a.tables = reinterpret_cast<const float*>(h->d_tab);
+            a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
+            a.feats = h->d_feats; a.Tmax = Tmax;
+            mark(h, ks);
+            HIP_TRY(h, launch_analysis(a, ks));
+        }
         mark(h, ks);
         if (S > 1) HIP_TRY(h, hipEventRecord(h->ev_ana[k], ks));
 
@@ -470,6 +490,7 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
         y.tables = reinterpret_cast<const float*>(h->d_tab);
         y.bintab = h->d_bintab; y.est = h->d_est; y.Tmax = Tmax;
         y.out = out; y.ld_out = ld_out;
+        y.spec = h->cfg.nlms_taps > 0 ? h->d_spec : nullptr;
         HIP_TRY(h, launch_synthesis(y, ks));
         mark(h, ks);
         if (S > 1) HIP_TRY(h, hipEventRecord(h->ev_done[k], ks));

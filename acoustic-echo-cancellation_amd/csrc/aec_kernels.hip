@@ -164,6 +164,40 @@ __device__ __forceinline__ float mag(float2 x) {
     return __builtin_amdgcn_sqrtf(fmaf(x.x, x.x, fmaf(x.y, x.y, 1e-9f)));
 }
 
+// Balanced ERB projection of one frame's magnitudes (scr[k ^ sw], k = 0..256)
+// onto the 32 bands (ERB.py:282-284): L scheduled entries per lane, three
+// partial sums, pieces of split bands combined through comb.  fo = the
+// frame's 32-float feature row, or null (frame beyond the stream: compute
+// nothing visible).  Leaves the wave fenced.
+__device__ __forceinline__ void erb_project(float* scr, const float4* sSched, const int2* sComb, int L, int lb,
+                                            int sw, float* fo) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    for (int e = 0; e < L; e += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float4 en = sSched[(e + u) * 16 + lb];
+            const float mg = scr[__float_as_int(en.x) ^ sw];
+            a0 = fmaf(en.y, mg, a0);
+            a1 = fmaf(en.z, mg, a1);
+            a2 = fmaf(en.w, mg, a2);
+        }
+    }
+    float* part = scr + 512;
+    part[3 * lb + 0] = a0;
+    part[3 * lb + 1] = a1;
+    part[3 * lb + 2] = a2;
+    wave_fence();
+    if (fo) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int band = lb + 16 * h;
+            const int2 cb = sComb[band];
+            fo[band] = part[cb.x] + (cb.y >= 0 ? part[cb.y] : 0.f);
+        }
+    }
+    wave_fence();
+}
+
 // --------------------------------------------------------------------------
 // K2: analysis.  grid = (ceil(Tmax/16), B), block = 256.  Each wave owns 4
 // consecutive frames (16 lanes per frame) and its own LDS region, stages its
@@ -305,37 +339,275 @@ __global__ __launch_bounds__(256, 3) void analysis_kernel(AnalysisArgs p) {
             }
             if (lb == 0) scr[128 ^ sw] = mag(x128);
             wave_fence();
-            // balanced ERB schedule: L entries per lane, 3 partial sums
-            float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-            for (int e = 0; e < L; e += 4) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const float4 en = sSched[(e + u) * 16 + lb];
-                    const float mg = scr[__float_as_int(en.x) ^ sw];
-                    a0 = fmaf(en.y, mg, a0);
-                    a1 = fmaf(en.z, mg, a1);
-                    a2 = fmaf(en.w, mg, a2);
-                }
-            }
-            float* part = scr + 512;
-            part[3 * lb + 0] = a0;
-            part[3 * lb + 1] = a1;
-            part[3 * lb + 2] = a2;
-            wave_fence();
-            if (t < T) {
-                float* fo = p.feats + ((int64_t)it.b * p.Tmax + t) * 96 + 32 * s;
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int band = lb + 16 * h;
-                    const int2 cb = sComb[band];
-                    fo[band] = part[cb.x] + (cb.y >= 0 ? part[cb.y] : 0.f);
-                }
-            }
-            wave_fence();
+            erb_project(scr, sSched, sComb, L, lb, sw,
+                        t < T ? p.feats + ((int64_t)it.b * p.Tmax + t) * 96 + 32 * s : nullptr);
         }
         if (k2 >= p.nitems) break;
         k = k2;
         it = it2;
+    }
+}
+
+// --------------------------------------------------------------------------
+// K2n: analysis with the frequency-domain NLMS linear echo canceller
+// (SURVEY.md §8 a13 — absent from the reference, which feeds the raw mic
+// spectrum to the post-filter; parity is held by the tests against the
+// float64 restatement of this recursion, tests/test_gpu_nlms.py).
+//
+// The NLMS is sequential over frames and independent over (stream, bin), so
+// one block owns one stream and walks it in chunks of 16 frames.  The block
+// has 12 waves in three roles, one of each per SIMD (wave w -> role w / 4,
+// frames 4 (w % 4) .. +3 of the chunk):
+//   mic  waves: transform mic -> spectrum row M[f] in the group's own LDS
+//               scratch; after the NLMS, project |E[f]| onto the ERB bands
+//               -> mic_erb;
+//   ref  waves: transform ref -> |R| -> ref_erb, then spectrum row R[f];
+//   near waves: run the NLMS of the chunk (thread k = bin k, thread 0 also
+//               bin 256; taps, power and far-end history live in LDS between
+//               chunks), writing E over M and to the spectrum buffer for K4;
+//               then transform near -> near_erb.
+// Two block barriers per chunk: rows complete -> NLMS -> rows consumed.
+// Row layout: 256 float2, slot 0 packs the real pair (X[0], X[256]).
+// Per bin and frame:
+//   E = D - sum_l W[l] R[t-l];  P = beta P + (1-beta) sum_l |R[t-l]|^2;
+//   W[l] += mu E conj(R[t-l]) / (P + delta)
+// HBM traffic beyond K2: the E spectrum, 2 KiB per frame.
+// --------------------------------------------------------------------------
+constexpr int kSpecRow = 256;          // float2 per spectrum row
+constexpr int kNlmsWaves = 12;
+
+// One bin's NLMS state, stored structure-of-arrays in LDS: slot i of bin k
+// at st[i * 257 + k] (consecutive threads, consecutive banks).
+template <int TAPS>
+struct NlmsBin {
+    static constexpr int kSlots = 4 * TAPS - 1;          // w (2 TAPS), h (2 (TAPS-1)), p
+    float2 w[TAPS];
+    float2 h[TAPS > 1 ? TAPS - 1 : 1];   // R[t-1] .. R[t-TAPS+1]
+    float p;
+    __device__ __forceinline__ void load(const float* st, int k) {
+#pragma unroll
+        for (int l = 0; l < TAPS; ++l) w[l] = make_float2(st[(2 * l) * 257 + k], st[(2 * l + 1) * 257 + k]);
+#pragma unroll
+        for (int l = 0; l < TAPS - 1; ++l)
+            h[l] = make_float2(st[(2 * TAPS + 2 * l) * 257 + k], st[(2 * TAPS + 2 * l + 1) * 257 + k]);
+        p = st[(kSlots - 1) * 257 + k];
+    }
+    __device__ __forceinline__ void store(float* st, int k) const {
+#pragma unroll
+        for (int l = 0; l < TAPS; ++l) {
+            st[(2 * l) * 257 + k] = w[l].x;
+            st[(2 * l + 1) * 257 + k] = w[l].y;
+        }
+#pragma unroll
+        for (int l = 0; l < TAPS - 1; ++l) {
+            st[(2 * TAPS + 2 * l) * 257 + k] = h[l].x;
+            st[(2 * TAPS + 2 * l + 1) * 257 + k] = h[l].y;
+        }
+        st[(kSlots - 1) * 257 + k] = p;
+    }
+    __device__ __forceinline__ float2 step(float2 d, float2 r, float mu, float beta, float delta) {
+        float2 y = cmul(w[0], r);
+        float pw = fmaf(r.x, r.x, r.y * r.y);
+#pragma unroll
+        for (int l = 1; l < TAPS; ++l) {
+            y = cadd(y, cmul(w[l], h[l - 1]));
+            pw = fmaf(h[l - 1].x, h[l - 1].x, fmaf(h[l - 1].y, h[l - 1].y, pw));
+        }
+        const float2 e = csub(d, y);
+        p = fmaf(beta, p, (1.f - beta) * pw);
+        const float2 ge = cscale(e, mu * __builtin_amdgcn_rcpf(p + delta));
+        w[0] = cadd(w[0], cmul(ge, conjf2(r)));
+#pragma unroll
+        for (int l = 1; l < TAPS; ++l) w[l] = cadd(w[l], cmul(ge, conjf2(h[l - 1])));
+#pragma unroll
+        for (int l = TAPS - 2; l >= 1; --l) h[l] = h[l - 1];
+        if (TAPS > 1) h[0] = r;
+        return e;
+    }
+};
+
+template <int TAPS>
+__global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsArgs p) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x;
+    const int L = p.sched_len;
+    constexpr int kSlots = NlmsBin<TAPS>::kSlots;
+
+    float4* sSched = reinterpret_cast<float4*>(smem);                 // L * 16
+    int2* sComb = reinterpret_cast<int2*>(sSched + L * 16);           // 32
+    float2* sTw512 = reinterpret_cast<float2*>(sComb + 32);           // 258
+    float2* sTwT = sTw512 + 258;                                      // 256
+    float* sHann = reinterpret_cast<float*>(sTwT + 256);              // 512
+    float* sWave = sHann + 512;                                       // kNlmsWaves * kWaveFloats
+    float* sState = sWave + kNlmsWaves * kWaveFloats;                 // kSlots * 257
+
+    const DevTables* tb = reinterpret_cast<const DevTables*>(p.tables);
+    if (tid < 256) {
+        sTwT[tid] = tb->twT[tid];
+        sTw512[tid] = tb->tw512[tid];
+        if (tid < 2) sTw512[256 + tid] = tb->tw512[256 + tid];
+        sHann[tid] = tb->hann[tid];
+        sHann[tid + 256] = tb->hann[tid + 256];
+        if (tid < 32) sComb[tid] = reinterpret_cast<const int2*>(p.sched + 4 * 16 * L)[tid];
+    }
+    {
+        const float4* sch = reinterpret_cast<const float4*>(p.sched);
+        for (int i = tid; i < L * 16; i += kNlmsWaves * 64) sSched[i] = sch[i];
+        for (int i = tid; i < kSlots * 257; i += kNlmsWaves * 64) sState[i] = 0.f;
+    }
+    const int wave = tid >> 6, lane = tid & 63;
+    const int role = wave >> 2, q = wave & 3;                        // 0 mic, 1 ref, 2 near
+    const int gg = lane >> 4, lb = lane & 15, sw = 16 * (gg & 1);
+    float* wr = sWave + wave * kWaveFloats;
+    float* scr = wr + gg * kGroupFloats;
+    const int b = p.b0 + blockIdx.x;
+    const int n = (int)p.lens[b];
+    const int64_t T = n / kHop + 1;
+    const bool act = role < p.nsig;                                   // near waves idle without near
+    const bool al = ((p.ld & 3) == 0) && act && ((reinterpret_cast<uintptr_t>(p.sig[role]) & 15) == 0);
+    const float* row_in = act ? p.sig[role] + (int64_t)b * p.ld : nullptr;
+    const float cval = act ? p.cvals[b * 3 + role] : 0.f;
+    float2* spec = p.spec + (int64_t)b * p.Tmax * kSpecRow;
+    const float mu = p.mu, beta = p.beta, delta = p.delta;
+    __syncthreads();
+
+    float4 pf[kWavePf];
+    if (act) wave_prefetch(pf, row_in, n, 4 * q, lane, al);
+    for (int64_t c0 = 0; c0 < T; c0 += kFPB) {
+        const int wt = (int)c0 + 4 * q;
+        const int64_t t = wt + gg;
+        // near waves: NLMS of this chunk's rows happens after barrier 1, so the
+        // near transform below runs after it (keeps the role waves balanced)
+        float2 xa[8], xb[8], x128;
+        if (act && role < 2) {
+            asm volatile("" ::: "memory");
+            wave_commit(wr, pf, cval, n, wt, lane);
+            if (c0 + kFPB < T) wave_prefetch(pf, row_in, n, wt + kFPB, lane, al);
+            wave_fence();
+            float2 v[16];
+            load_frame(v, wr, sHann, gg, lb);
+            wave_fence();
+            fft256<false>(v, lb, scr, sTwT);
+            rfft_unpack(v, lb, sTw512, xa, xb, x128);
+            if (role == 1) {
+#pragma unroll
+                for (int m = 0; m < 8; ++m) {
+                    const int kk = lb + 16 * m;
+                    scr[kk ^ sw] = mag(xa[m]);
+                    scr[(kk == 0 ? 256 : 256 - kk) ^ sw] = mag(xb[m]);
+                }
+                if (lb == 0) scr[128 ^ sw] = mag(x128);
+                wave_fence();
+                erb_project(scr, sSched, sComb, L, lb, sw,
+                            t < T ? p.feats + ((int64_t)b * p.Tmax + t) * 96 + 32 : nullptr);
+            }
+            float2* row = reinterpret_cast<float2*>(scr);
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const int kk = lb + 16 * m;
+                if (kk == 0) {
+                    row[0] = make_float2(xa[0].x, xb[0].x);           // (X[0], X[256]), both real
+                } else {
+                    row[kk] = xa[m];
+                    row[256 - kk] = xb[m];
+                }
+            }
+            if (lb == 0) row[128] = x128;
+        }
+        __syncthreads();                                              // M / R rows of the chunk complete
+        if (role == 2 || tid == 4 * 64) {
+            // NLMS over the chunk: bin k = tid - 512 for the near waves; bin 256
+            // on the first ref wave's lane 0 (idle here).  Bins 0 and 256 are
+            // real and share row slot 0 (.x / .y).
+            const int k = role == 2 ? tid - 2 * 4 * 64 : 256;
+            const int slot = k & 255;
+            const bool nyq = k == 256, dc = k == 0;
+            const int nf = (int)min((int64_t)kFPB, T - c0);
+            NlmsBin<TAPS> st;
+            st.load(sState, k);
+            // 4 frames at a time: their (D, R) are loaded before the steps so the
+            // recursion's dependency chain carries no LDS latency
+#pragma unroll
+            for (int i0 = 0; i0 < kFPB; i0 += 4) {
+                float2 dd[4], rr[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = i0 + u;
+                    const float2 d = reinterpret_cast<const float2*>(sWave + (i >> 2) * kWaveFloats +
+                                                                     (i & 3) * kGroupFloats)[slot];
+                    const float2 r = reinterpret_cast<const float2*>(sWave + (4 + (i >> 2)) * kWaveFloats +
+                                                                     (i & 3) * kGroupFloats)[slot];
+                    dd[u] = nyq ? make_float2(d.y, 0.f) : (dc ? make_float2(d.x, 0.f) : d);
+                    rr[u] = nyq ? make_float2(r.y, 0.f) : (dc ? make_float2(r.x, 0.f) : r);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = i0 + u;
+                    if (i < nf) {
+                        const float2 e = st.step(dd[u], rr[u], mu, beta, delta);
+                        float* mrow = sWave + (i >> 2) * kWaveFloats + (i & 3) * kGroupFloats;
+                        float* gsp = reinterpret_cast<float*>(spec + (c0 + i) * kSpecRow);
+                        if (dc || nyq) {
+                            mrow[nyq ? 1 : 0] = e.x;                  // packed (E[0], E[256])
+                            gsp[nyq ? 1 : 0] = e.x;
+                        } else {
+                            reinterpret_cast<float2*>(mrow)[k] = e;
+                            reinterpret_cast<float2*>(gsp)[k] = e;
+                        }
+                    }
+                }
+            }
+            st.store(sState, k);
+        }
+        __syncthreads();                                              // E rows complete, R rows consumed
+        if (role == 0) {
+            // mic_erb = ERB(|E|) of this group's frame; the row is read into
+            // registers before the magnitudes overwrite it
+            const float2* row = reinterpret_cast<const float2*>(scr);
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const int kk = lb + 16 * m;
+                xa[m] = row[kk];
+                xb[m] = row[(256 - kk) & 255];
+            }
+            x128 = row[128];
+            wave_fence();
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const int kk = lb + 16 * m;
+                if (kk == 0) {
+                    scr[0 ^ sw] = mag(make_float2(xa[0].x, 0.f));
+                    scr[256 ^ sw] = mag(make_float2(xa[0].y, 0.f));
+                } else {
+                    scr[kk ^ sw] = mag(xa[m]);
+                    scr[(256 - kk) ^ sw] = mag(xb[m]);
+                }
+            }
+            if (lb == 0) scr[128 ^ sw] = mag(x128);
+            wave_fence();
+            erb_project(scr, sSched, sComb, L, lb, sw, t < T ? p.feats + ((int64_t)b * p.Tmax + t) * 96 : nullptr);
+        } else if (role == 2 && act) {
+            asm volatile("" ::: "memory");
+            wave_commit(wr, pf, cval, n, wt, lane);
+            if (c0 + kFPB < T) wave_prefetch(pf, row_in, n, wt + kFPB, lane, al);
+            wave_fence();
+            float2 v[16];
+            load_frame(v, wr, sHann, gg, lb);
+            wave_fence();
+            fft256<false>(v, lb, scr, sTwT);
+            rfft_unpack(v, lb, sTw512, xa, xb, x128);
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const int kk = lb + 16 * m;
+                scr[kk ^ sw] = mag(xa[m]);
+                scr[(kk == 0 ? 256 : 256 - kk) ^ sw] = mag(xb[m]);
+            }
+            if (lb == 0) scr[128 ^ sw] = mag(x128);
+            wave_fence();
+            erb_project(scr, sSched, sComb, L, lb, sw, t < T ? p.feats + ((int64_t)b * p.Tmax + t) * 96 + 64 : nullptr);
+        }
+        // the next chunk's rows are written by the same waves after their own
+        // work above; the NLMS reads of this chunk ended at barrier 2
     }
 }
 
@@ -351,6 +623,7 @@ __global__ __launch_bounds__(256, 3) void analysis_kernel(AnalysisArgs p) {
 // --------------------------------------------------------------------------
 constexpr int kEstStride = 33;
 
+template <bool kSpec>
 __global__ __launch_bounds__(256) void synthesis_kernel(SynthArgs p) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x;
@@ -390,12 +663,13 @@ __global__ __launch_bounds__(256) void synthesis_kernel(SynthArgs p) {
         const int64_t T = n / kHop + 1;
         const int64_t h0 = it.wt;
         float4 pf[kWavePf];
-        wave_prefetch(pf, p.mic + (int64_t)b * p.ld, (int)n, (int)(h0 + kWaveFrames * wave), lane, aligned);
+        if (!kSpec)
+            wave_prefetch(pf, p.mic + (int64_t)b * p.ld, (int)n, (int)(h0 + kWaveFrames * wave), lane, aligned);
         for (int i = tid; i < kFPB * 32; i += 256) {
             const int64_t t = h0 + (i >> 5);
             sEst[(i >> 5) * kEstStride + (i & 31)] = (t < T) ? p.est[((int64_t)b * p.Tmax + t) * 32 + (i & 31)] : 0.f;
         }
-        wave_commit(wr, pf, p.cvals[b * 3 + 0], (int)n, (int)(h0 + kWaveFrames * wave), lane);
+        if (!kSpec) wave_commit(wr, pf, p.cvals[b * 3 + 0], (int)n, (int)(h0 + kWaveFrames * wave), lane);
     }
     __syncthreads();                                                  // tables + est staged
     {
@@ -403,11 +677,28 @@ __global__ __launch_bounds__(256) void synthesis_kernel(SynthArgs p) {
         const int64_t nhop = it.n / kHop;                             // T - 1
         const int64_t h0 = it.wt;
         float2 v[16];
-        load_frame(v, wr, sHann, gg, lb);
-        wave_fence();
-        fft256<false>(v, lb, scr, sTwT);
         float2 xa[8], xb[8], x128;
-        rfft_unpack(v, lb, sTw512, xa, xb, x128);
+        if (kSpec) {
+            // NLMS error spectrum of frame h0 + g (slot 0 = (E[0], E[256]))
+            const int64_t t = h0 + g;
+            const bool ok = t <= nhop;
+            const float2* row = p.spec + ((int64_t)b * p.Tmax + (ok ? t : 0)) * 256;
+            const float2 z = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const int kk = lb + 16 * m;
+                const float2 a = ok ? row[kk] : z;
+                const float2 c = ok ? row[(256 - kk) & 255] : z;
+                xa[m] = kk == 0 ? make_float2(a.x, 0.f) : a;
+                xb[m] = kk == 0 ? make_float2(a.y, 0.f) : c;
+            }
+            x128 = ok ? row[128] : z;
+        } else {
+            load_frame(v, wr, sHann, gg, lb);
+            wave_fence();
+            fft256<false>(v, lb, scr, sTwT);
+            rfft_unpack(v, lb, sTw512, xa, xb, x128);
+        }
 
         // ERB gain per bin: g[k] = sum_j est_erb[j] erb[k][j] over the <= 2 bands
         // covering bin k (ERB.py:306-307), applied to the mic spectrum (:309-310)
@@ -512,8 +803,37 @@ hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t st) {
 
 hipError_t launch_synthesis(const SynthArgs& a, hipStream_t st) {
     if (a.nitems <= 0) return hipSuccess;
-    hipLaunchKernelGGL(synthesis_kernel, dim3((unsigned)a.nitems), dim3(256), synthesis_smem_bytes(), st, a);
+    if (a.spec)
+        hipLaunchKernelGGL(synthesis_kernel<true>, dim3((unsigned)a.nitems), dim3(256), synthesis_smem_bytes(), st, a);
+    else
+        hipLaunchKernelGGL(synthesis_kernel<false>, dim3((unsigned)a.nitems), dim3(256), synthesis_smem_bytes(), st, a);
     return hipGetLastError();
+}
+
+template <int TAPS>
+static hipError_t launch_nlms_t(const NlmsArgs& a, int nb, hipStream_t st) {
+    // > 64 KiB of LDS: opt in once per instantiation
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(nlms_analysis_kernel<TAPS>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (attr != hipSuccess) return attr;
+    hipLaunchKernelGGL(nlms_analysis_kernel<TAPS>, dim3(nb), dim3(kNlmsWaves * 64), nlms_smem_bytes(a.sched_len, TAPS),
+                       st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_nlms_analysis(const NlmsArgs& a, int nb, hipStream_t st) {
+    if (nb <= 0) return hipSuccess;
+    switch (a.taps) {
+        case 1: return launch_nlms_t<1>(a, nb, st);
+        case 2: return launch_nlms_t<2>(a, nb, st);
+        case 3: return launch_nlms_t<3>(a, nb, st);
+        case 4: return launch_nlms_t<4>(a, nb, st);
+        case 5: return launch_nlms_t<5>(a, nb, st);
+        case 6: return launch_nlms_t<6>(a, nb, st);
+        case 7: return launch_nlms_t<7>(a, nb, st);
+        case 8: return launch_nlms_t<8>(a, nb, st);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 }  // namespace aec

@@ -36,6 +36,24 @@ struct AnalysisArgs {
     int64_t Tmax;
 };
 
+// K2n: per-stream analysis with the FD-NLMS canceller (one block per stream).
+struct NlmsArgs {
+    const float* sig[3];
+    int64_t ld;
+    const int64_t* lens;
+    int b0;                  // first stream of this launch (block i runs stream b0 + i)
+    const float* cvals;
+    const float* tables;
+    const float* sched;
+    int sched_len;
+    int nsig;
+    float* feats;            // [B][Tmax][96]
+    int64_t Tmax;
+    float2* spec;            // [B][Tmax][256] error spectrum E (slot 0 = (E[0], E[256]))
+    int taps;
+    float mu, beta, delta;
+};
+
 struct GruArgs {
     const float* feats;      // [B][Tmax][96]
     int64_t Tmax;
@@ -63,11 +81,17 @@ struct SynthArgs {
     int64_t Tmax;
     float* out;
     int64_t ld_out;
+    const float2* spec;      // NLMS error spectrum [B][Tmax][256], or null: re-derive the mic spectrum
 };
 
 // dynamic LDS bytes (must match the carve in the kernels)
 inline size_t analysis_smem_bytes(int sched_len) {
     return (size_t)sched_len * 16 * 16 + 32 * 8 + (258 * 2 + 256 * 2 + 512 + (size_t)kFPB * kGroupFloats) * 4;
+}
+// K2n: tables + 12 wave regions + NLMS state (4 TAPS - 1 slots x 257 bins)
+inline size_t nlms_smem_bytes(int sched_len, int taps) {
+    return (size_t)sched_len * 16 * 16 + 32 * 8 + (258 * 2 + 256 * 2 + 512 + (size_t)12 * 4 * kGroupFloats) * 4 +
+           (size_t)(4 * taps - 1) * 257 * 4;
 }
 inline size_t synthesis_smem_bytes() {
     return 260 * 16 + (258 * 2 + 256 * 2 + 512 + 256 + kFPB * 33 + 4 + (size_t)kFPB * kGroupFloats) * 4;
@@ -78,6 +102,7 @@ hipError_t launch_moments(const float* mic, const float* ref, const float* near,
 hipError_t launch_norm_finalize(const double2* mom, const int64_t* lens, float* cvals, int b0, int b1, int nsig,
                                 hipStream_t st);
 hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t st);
+hipError_t launch_nlms_analysis(const NlmsArgs& a, int nb, hipStream_t st);
 hipError_t launch_gru(const GruArgs& a, int B, hipStream_t st);
 hipError_t launch_synthesis(const SynthArgs& a, hipStream_t st);
 

@@ -25,13 +25,34 @@ sys.path.insert(0, os.path.join(REPO, 'acoustic-echo-cancellation_amd'))
 HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector (= f32 MFMA) peak
 KERNELS = ['moments', 'analysis', 'gru', 'synthesis']
-# Algorithmic work per frame (DESIGN.md §4): bytes that must cross HBM and
+# Algorithmic work per frame (DESIGN.md §5): bytes that must cross HBM and
 # FLOPs of the FFT-based algorithm, for B streams with near (loss) enabled.
+RFFT = 11520                   # 2.5 N log2 N, N = 512
+ANA_SIG = RFFT + 512 + 3 * 257 + 2 * 483          # window, rFFT, |X|, sparse ERB
+NLMS_FLOPS = 257 * (16 * 4 + 10)                  # SURVEY.md §8(d), 4 taps
+SYN_TAIL = RFFT + 512 + 2 * 483 + 6 * 257 + 3 * 256   # gains, irFFT, window, WOLA
+GRU = dict(bytes=3 * 32 * 4 + 32 * 4, flops=2 * 96 * 64 + 2 * 96 * 32 + 2 * (32 * 64 + 32 * 32) + 400)
 ALG = {
-    'moments': dict(bytes=3 * 256 * 4, flops=3 * 256 * 4),
-    'analysis': dict(bytes=3 * 256 * 4 + 3 * 32 * 4, flops=3 * (11520 + 512 + 3 * 257 + 2 * 483)),
-    'gru': dict(bytes=3 * 32 * 4 + 32 * 4, flops=2 * 96 * 64 + 2 * 96 * 32 + 2 * (32 * 64 + 32 * 32) + 400),
-    'synthesis': dict(bytes=256 * 4 + 32 * 4 + 256 * 4, flops=2 * 11520 + 512 + 2 * 483 + 6 * 257 + 3 * 256),
+    'postfilter': {
+        'moments': dict(bytes=3 * 256 * 4, flops=3 * 256 * 4),
+        'analysis': dict(bytes=3 * 256 * 4 + 3 * 32 * 4, flops=3 * ANA_SIG),
+        'gru': GRU,
+        'synthesis': dict(bytes=256 * 4 + 32 * 4 + 256 * 4, flops=RFFT + 512 + SYN_TAIL),
+    },
+    'full': {
+        'moments': dict(bytes=3 * 256 * 4, flops=3 * 256 * 4),
+        # + the error spectrum E written for K4 (2 KiB) and |E| -> ERB
+        'analysis': dict(bytes=3 * 256 * 4 + 3 * 32 * 4 + 256 * 8, flops=3 * ANA_SIG + NLMS_FLOPS + 3 * 257 + 2 * 483),
+        'gru': GRU,
+        # E (2 KiB) instead of the mic samples; no forward transform
+        'synthesis': dict(bytes=256 * 8 + 32 * 4 + 256 * 4, flops=SYN_TAIL),
+    },
+}
+WORKLOAD = {
+    'full': 'C2 (BASELINE configs[1]) shape: 256 concurrent 10 s 16 kHz streams per GPU through '
+            'STFT -> FD-NLMS (4 taps/bin) -> ERB-GRU post-filter -> iSTFT',
+    'postfilter': 'C2 shape: 256 concurrent 10 s 16 kHz streams per GPU, STFT -> ERB-GRU post-filter '
+                  '-> iSTFT (reference Little_net path, FD-NLMS bypass)',
 }
 PIPE = dict(bytes=4096, flops=82000)      # whole path, per frame
 
@@ -45,20 +66,25 @@ def parse():
     ap.add_argument('--seconds', type=float, default=10.0)
     ap.add_argument('--cpu-seconds', type=float, default=12.0, help='bounded CPU-baseline sample (wall s)')
     ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--pipeline', choices=['full', 'postfilter'], default='full',
+                    help='full = STFT -> FD-NLMS -> ERB-GRU post-filter -> iSTFT (north_star); '
+                         'postfilter = the reference Little_net path alone (NLMS bypass)')
+    ap.add_argument('--no-rtf', action='store_true', help='skip the batch-1 latency probe (profiling runs)')
     ap.add_argument('--sweep', action='store_true', help='also report a batch sweep')
     return ap.parse_args()
 
 
-def roofline(kernel, ms_per_launch, frames_per_launch, pmc):
-    a = ALG[kernel]
+def roofline(pipeline, kernel, ms_per_launch, frames_per_launch, pmc):
+    a = ALG[pipeline][kernel]
     t = ms_per_launch * 1e-3
     gbs = a['bytes'] * frames_per_launch / t / 1e9
     tfl = a['flops'] * frames_per_launch / t / 1e12
     t_hbm = a['bytes'] / (HBM_PEAK_GBS * 1e9)
     t_fl = a['flops'] / (FP32_PEAK_TFLOPS * 1e12)
     traffic = None
-    if pmc and kernel in pmc.get('kernels', {}):
-        traffic = pmc['kernels'][kernel].get('hbm_bytes_per_launch')
+    kname = 'nlms_analysis' if (pipeline == 'full' and kernel == 'analysis') else kernel
+    if pmc and pmc.get('pipeline') == pipeline and kname in pmc.get('kernels', {}):
+        traffic = pmc['kernels'][kname].get('hbm_bytes_per_launch')
     if t_hbm >= t_fl:
         return dict(bound='hbm', achieved=round(gbs, 1), peak=HBM_PEAK_GBS, unit='GB/s',
                     frac=round(gbs / HBM_PEAK_GBS, 4), traffic=traffic, kernel=kernel,
@@ -109,13 +135,14 @@ def main():
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     dev = torch.device('cuda', local)
     import aec_amd
-    from aec_amd import synth
+    from aec_amd import shard, synth
 
     B = args.streams
     n = int(round(args.seconds * 16000))
     T = n // 256 + 1
     w = dict(np.load(os.path.join(REPO, 'tests', 'golden', 'weights.npz')))
-    net = aec_amd.Little_net(aec_amd.speech_conf, 32).eval()
+    nlms = aec_amd.nlms_conf if args.pipeline == 'full' else None
+    net = aec_amd.Little_net(aec_amd.speech_conf, 32, nlms=nlms).eval()
     sd = net.state_dict()
     for k in ['gru1.weight_ih_l0', 'gru1.weight_hh_l0', 'gru1.bias_ih_l0', 'gru1.bias_hh_l0',
               'linear1.weight', 'linear1.bias', 'linear2.weight', 'linear2.bias']:
@@ -147,19 +174,16 @@ def main():
         el = time.perf_counter() - t0
         kms, calls = h.profile_read()
         h.profile_enable(False)
-        if world > 1:
-            t = torch.tensor([el], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t)
+        el = shard.max_over_ranks(el)              # all_reduce(MAX) of one scalar, outside the timed region
         # RTF at batch 1: one 10 s utterance, synchronous latency (median of 7)
         lat = []
-        for _ in range(7):
+        for _ in range(0 if args.no_rtf else 7):
             torch.cuda.synchronize(dev)
             t1 = time.perf_counter()
             net.forward_ragged(mic[:1], ref[:1], near[:1], erb, [n])
             torch.cuda.synchronize(dev)
             lat.append(time.perf_counter() - t1)
-        rtf1 = float(np.median(lat)) / args.seconds
+        rtf1 = float(np.median(lat)) / args.seconds if lat else None
         sweep = None
         if args.sweep and rank == 0:
             sweep = {}
@@ -186,10 +210,10 @@ def main():
     per_launch_ms = {k: kms[i] / max(calls, 1) for i, k in enumerate(KERNELS)}
     dom = max(per_kernel_ms, key=per_kernel_ms.get)
     pmc = None
-    pmc_path = os.path.join(REPO, 'profiles', 'pmc_latest.json')
+    pmc_path = os.path.join(REPO, 'profiles', f'pmc_latest_{args.pipeline}.json')
     if os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path))
-    roof = roofline(dom, per_launch_ms[dom], int(round(B * T / launches_per_step)), pmc)
+    roof = roofline(args.pipeline, dom, per_launch_ms[dom], int(round(B * T / launches_per_step)), pmc)
     pipe_t = ms_step * 1e-3 / world
     pipe_gbs = PIPE['bytes'] * B * T / pipe_t / 1e9
     pipe_tfl = PIPE['flops'] * B * T / pipe_t / 1e12
@@ -202,10 +226,10 @@ def main():
             'value': round(value, 1), 'unit': 'frames/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms_step, 4), 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
-            'config': {'workload': 'C2 shape: 256 concurrent 10 s 16 kHz streams per GPU, '
-                                   'STFT -> ERB-GRU post-filter -> iSTFT (Little_net path, FD-NLMS bypass)',
+            'config': {'workload': WORKLOAD[args.pipeline],
                        'streams_per_gpu': B, 'samples_per_stream': n, 'frames_per_stream': T,
-                       'frame': '256-sample hop', 'parallelism': f'streams sharded, {world} rank(s)'},
+                       'frame': '256-sample hop', 'pipeline': args.pipeline,
+                       'parallelism': f'streams sharded, {world} rank(s)'},
             'xRT': round(value * 256 / 16000, 1),
             'rtf_batch1': rtf1,
             'kernel_ms_per_step': {k: round(v, 4) for k, v in per_kernel_ms.items()},

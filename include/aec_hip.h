@@ -52,10 +52,10 @@ typedef struct {
     int32_t win_size;    /* 512  (speech_conf['win_size'])  — only 512 supported  */
     int32_t hop_size;    /* 256  (speech_conf['hop_size'])  — only 256 supported  */
     int32_t erb_bands;   /* 32   (erb_conf['total_erb_bands']); GRU hidden = bands */
-    int32_t nlms_taps;   /* 0 = bypass; 1..8 taps per bin                          */
-    float   nlms_mu;     /* step size                                               */
-    float   nlms_beta;   /* far-end power smoothing                                 */
-    float   nlms_delta;  /* regulariser                                             */
+    int32_t nlms_taps;   /* 0 = bypass; 1..8 taps per bin (frames of far-end history) */
+    float   nlms_mu;     /* step size, [0, 2); 0 leaves the mic spectrum unchanged    */
+    float   nlms_beta;   /* far-end power smoothing, [0, 1)                           */
+    float   nlms_delta;  /* regulariser, > 0                                          */
     int32_t reserved;
 } aec_config;
 
@@ -71,6 +71,12 @@ size_t aec_weights_count(int32_t erb_bands);
  * NULL = set later). */
 aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weights,
                       const float* erb_257xbands, int32_t device, aec_handle** out);
+/* With nlms_taps > 0 every frame's mic spectrum is first replaced by the
+ * a-priori error of a per-bin complex NLMS driven by the ref spectrum
+ *   E = D - sum_l W[l] R[t-l],  P = beta P + (1-beta) sum_l |R[t-l]|^2,
+ *   W[l] += mu E conj(R[t-l]) / (P + delta)      (W, P = 0 at each stream start)
+ * and the post-filter (features, gains, iSTFT) runs on E instead of the mic
+ * spectrum. */
 
 aec_status aec_set_weights(aec_handle* h, const float* weights, size_t n_weights);
 aec_status aec_set_erb(aec_handle* h, const float* erb_257xbands);

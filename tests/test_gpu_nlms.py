@@ -1,0 +1,153 @@
+"""GPU parity of the FD-NLMS stage.
+
+The reference has no linear echo canceller, so the float64 restatement
+oracle/aec_oracle.py:nlms / aec_forward is the only oracle ("parity unpinned"
+against the reference itself); its known answers are pinned in
+tests/test_oracle_golden.py.  Here the gfx950 path (C ABI via Little_net with
+``nlms=``) is held to the same bars as the bypass path: integer framing
+bit-exact, waveform <= 1e-4 RMS, features <= 1e-5 relative, ERLE delta <= 0.1 dB.
+"""
+import numpy as np
+import pytest
+import torch
+
+import aec_oracle as O
+from conftest import PARAM_KEYS
+
+pytestmark = pytest.mark.gpu
+
+WAVE_RMS_TOL = 1e-4
+NLMS = dict(taps=4, mu=0.3, beta=0.5, delta=1e-4)      # aec_amd.configs.nlms_conf
+
+
+def _net(golden_weights, nlms):
+    import aec_amd
+    net = aec_amd.Little_net(aec_amd.speech_conf, 32, nlms=nlms).eval()
+    sd = net.state_dict()
+    for k in PARAM_KEYS:
+        sd[k] = torch.from_numpy(golden_weights[k])
+    net.load_state_dict(sd, strict=True)
+    return net.to('cuda:0')
+
+
+@pytest.fixture(scope='module')
+def nlms_net(golden_weights):
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+    return _net(golden_weights, NLMS)
+
+
+def _rms(a, b):
+    return float(np.sqrt(np.mean((np.asarray(a, np.float64) - b) ** 2))) if np.size(a) else 0.0
+
+
+def _loss_ok(got, exp, tol=1e-4):
+    if np.isnan(exp):
+        return bool(np.isnan(got))
+    return abs(got - exp) <= tol * max(1.0, abs(exp))
+
+
+def _run(net, erb, mic, ref, near):
+    dev = 'cuda:0'
+    T = lambda a: torch.as_tensor(a, device=dev)[None] if a is not None else None
+    with torch.no_grad():
+        out, loss = net(T(mic), T(ref), T(near), torch.tensor(erb, dtype=torch.float32, device=dev))
+    torch.cuda.synchronize()
+    return out[0].cpu().numpy(), (float(loss) if loss is not None else None)
+
+
+@pytest.mark.parametrize('n', [255, 256, 513, 4097, 16123, 33333])
+def test_nlms_vs_oracle(nlms_net, golden_weights, golden_erb, n):
+    from aec_amd import synth
+    mic, ref, near = synth.scene(n, 2000 + n)
+    out, loss = _run(nlms_net, golden_erb, mic, ref, near)
+    o, l = O.aec_forward(mic, ref, near, golden_erb.astype(np.float32), golden_weights, nlms_cfg=NLMS)
+    assert out.shape == o.shape                               # bit-exact framing
+    assert _rms(out, o) <= WAVE_RMS_TOL
+    assert _loss_ok(loss, l)
+
+
+def test_nlms_features_vs_oracle(nlms_net, golden_erb):
+    """mic_erb = ERB(|E|) of the NLMS error, ref_erb / near_erb unchanged."""
+    from aec_amd import synth
+    n = 20000
+    mic, ref, near = synth.scene(n, 31)
+    erb = golden_erb.astype(np.float32).astype(np.float64)
+    nlms_net.set_debug(True)
+    try:
+        _run(nlms_net, golden_erb, mic, ref, near)
+        T = n // 256 + 1
+        got = {k: nlms_net.debug_intermediate(k, 1, T)[0].cpu().numpy() for k in ['mic_erb', 'ref_erb', 'near_erb']}
+    finally:
+        nlms_net.set_debug(False)
+    Sm, Sr, Sn = (O.stft(O.normalise(x)) for x in (mic, ref, near))
+    E = O.nlms(Sm, Sr, **NLMS)
+    exp = {'mic_erb': O.magnitude(E) @ erb, 'ref_erb': O.magnitude(Sr) @ erb, 'near_erb': O.magnitude(Sn) @ erb}
+    for k in exp:
+        scale = np.abs(exp[k]).max()
+        assert np.abs(got[k] - exp[k]).max() <= 1e-5 * scale, k
+
+
+@pytest.mark.parametrize('taps', [1, 2, 8])
+def test_nlms_tap_counts(golden_weights, golden_erb, taps):
+    from aec_amd import synth
+    cfg = dict(NLMS, taps=taps)
+    net = _net(golden_weights, cfg)
+    mic, ref, near = synth.scene(12345, 50 + taps)
+    out, loss = _run(net, golden_erb, mic, ref, near)
+    o, l = O.aec_forward(mic, ref, near, golden_erb.astype(np.float32), golden_weights, nlms_cfg=cfg)
+    assert _rms(out, o) <= WAVE_RMS_TOL
+    assert _loss_ok(loss, l)
+
+
+def test_nlms_mu0_equals_bypass(golden_weights, golden_erb, gpu_net):
+    """Known answer: mu = 0 keeps W = 0, so E = D exactly and the path equals
+    the reference-parity bypass.  The two paths run the same transform in
+    different kernels (the compiler may contract differently), so equality
+    is to float32 rounding: <= 1e-6 of the signal scale."""
+    from aec_amd import synth
+    net0 = _net(golden_weights, dict(NLMS, mu=0.0))
+    B, n = 4, 17000
+    mic, ref, near = synth.batch(B, n, seed0=90)
+    dev = 'cuda:0'
+    erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
+    M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
+    with torch.no_grad():
+        a, la = net0.forward_ragged(M, R, N, erb_t, [n] * B)
+        b, lb = gpu_net.forward_ragged(M, R, N, erb_t, [n] * B)
+    assert float((a - b).abs().max()) <= 1e-6 * float(b.abs().max())
+    # an all-zero near row gives the reference's NaN loss (0/0 normaliser) on both paths
+    torch.testing.assert_close(la, lb, rtol=1e-6, atol=0.0, equal_nan=True)
+
+
+def test_nlms_ragged_and_batch_invariance(nlms_net, golden_weights, golden_erb):
+    from aec_amd import synth
+    lens = [7000, 12801, 9472, 300]
+    L = max(lens)
+    rows = [synth.scene(n, 600 + i) for i, n in enumerate(lens)]
+    mic, ref, near = (np.zeros((len(lens), L), np.float32) for _ in range(3))
+    for i, (m, r, nn_) in enumerate(rows):
+        mic[i, :lens[i]], ref[i, :lens[i]], near[i, :lens[i]] = m, r, nn_
+    dev = 'cuda:0'
+    erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
+    M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
+    with torch.no_grad():
+        out, loss = nlms_net.forward_ragged(M, R, N, erb_t, lens)
+        out2, _ = nlms_net.forward_ragged(M[1:2], R[1:2], N[1:2], erb_t, lens[1:2])
+    out = out.cpu().numpy()
+    for i, n in enumerate(lens):
+        ol = 256 * (n // 256)
+        o, l = O.aec_forward(*rows[i], golden_erb.astype(np.float32), golden_weights, nlms_cfg=NLMS)
+        assert _rms(out[i, :ol], o) <= WAVE_RMS_TOL
+        assert not out[i, ol:].any()
+        assert _loss_ok(float(loss[i]), l)
+    assert np.array_equal(out[1:2, :out2.shape[1]], out2.cpu().numpy())
+
+
+def test_nlms_erle_delta_vs_oracle(nlms_net, golden_weights, golden_erb):
+    from aec_amd import synth
+    mic, ref, near = synth.scene(48000, 9, double_talk=False)
+    near = near + np.float32(1e-3) * np.random.default_rng(9).standard_normal(48000).astype(np.float32)
+    out, _ = _run(nlms_net, golden_erb, mic, ref, near)
+    o, _ = O.aec_forward(mic, ref, near, golden_erb.astype(np.float32), golden_weights, nlms_cfg=NLMS)
+    assert abs(O.erle_db(mic, out) - O.erle_db(mic, o)) <= 0.1

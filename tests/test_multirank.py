@@ -1,0 +1,80 @@
+"""N > 1 path on CPU: world-size-2 gloo process groups.
+
+The HIP path has no data-path collective: every rank runs its own streams.
+What must be right by construction is:
+- the shard table: every rank derives the same one, shards are disjoint and
+  complete, and the load is balanced;
+- the scalar reductions the bench and the run metrics use.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from aec_amd import shard
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, lengths, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        mine = shard.balanced_shards(lengths, world)[rank]
+        tables = [None] * world
+        dist.all_gather_object(tables, mine)
+        el = shard.max_over_ranks(1.0 + rank)
+        sums = shard.sum_over_ranks([sum(shard.frames_of(lengths[i]) for i in mine), 1.0])
+        q.put((rank, tables, el, sums))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_gloo_shards_and_reductions(world):
+    lengths = [160000, 64123, 191999, 100000, 75000, 160000, 255, 513, 120000, 99999, 64000]
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, lengths, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    tables = res[0][1]
+    assert all(r[1] == tables for r in res)                           # same table on every rank
+    flat = sorted(i for t in tables for i in t)
+    assert flat == list(range(len(lengths)))                          # disjoint and complete
+    for _, _, el, sums in res:
+        assert el == float(world)                                     # max over ranks of 1 + rank
+        assert sums[0] == sum(shard.frames_of(n) for n in lengths)
+        assert sums[1] == float(world)
+
+
+def test_balanced_shards_properties():
+    import random
+    rng = random.Random(0)
+    for world in [1, 2, 4, 8]:
+        lengths = [rng.randint(64000, 192000) for _ in range(257)]
+        sh = shard.balanced_shards(lengths, world)
+        assert sorted(i for s in sh for i in s) == list(range(len(lengths)))
+        loads = [sum(shard.frames_of(lengths[i]) for i in s) for s in sh]
+        ideal = sum(loads) / world
+        assert max(loads) <= ideal + max(shard.frames_of(n) for n in lengths)   # LPT bound
+    assert shard.balanced_shards([], 4) == [[], [], [], []]
+    assert shard.balanced_shards([5, 5, 5], 8)[3:] == [[]] * 5
+    with pytest.raises(ValueError):
+        shard.balanced_shards([1], 0)
