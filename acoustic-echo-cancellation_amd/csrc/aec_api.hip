@@ -210,6 +210,7 @@ struct aec_handle {
     std::vector<int64_t> last_lens;
     int debug = 0;
     int gru_mode = 0;            // AEC_GRU_MODE (timing experiments; results invalid unless 0)
+    int nlms_mode = 0;           // AEC_NLMS_MODE (timing experiments; results invalid unless 0)
     int64_t last_B = 0, last_T = 0;
     // kernel timing (aec_profile_*)
     int profile = 0;
@@ -313,6 +314,7 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
     h->cfg = *cfg;
     h->device = device;
     if (const char* m = std::getenv("AEC_GRU_MODE")) h->gru_mode = std::atoi(m);
+    if (const char* m = std::getenv("AEC_NLMS_MODE")) h->nlms_mode = std::atoi(m);
     if (const char* m = std::getenv("AEC_SUBBATCH")) h->sub_max = std::max(1, std::min(aec_handle::kMaxSub, std::atoi(m)));
     {
         int cus = 0;
@@ -457,6 +459,7 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
             a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
             a.feats = h->d_feats; a.Tmax = Tmax; a.spec = h->d_spec;
             a.taps = h->cfg.nlms_taps; a.mu = h->cfg.nlms_mu; a.beta = h->cfg.nlms_beta; a.delta = h->cfg.nlms_delta;
+            a.mode = h->nlms_mode;
             mark(h, ks);
             HIP_TRY(h, launch_nlms_analysis(a, b1 - b0, ks));
         } else {

@@ -378,18 +378,32 @@ constexpr int kNlmsWaves = 12;
 
 // One bin's NLMS state, stored structure-of-arrays in LDS: slot i of bin k
 // at st[i * 257 + k] (consecutive threads, consecutive banks).
+// Packed-FP32 complex helpers for the recursion: a complex value is a
+// float2 vector, so the products below map to v_pk_mul_f32 / v_pk_fma_f32
+// (two lanes of arithmetic per instruction slot).
+typedef float v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ v2f vfma(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ v2f vsplat(float a) { return v2f{a, a}; }
+__device__ __forceinline__ v2f vrot(v2f a) { return v2f{-a.y, a.x}; }       // i * a
+
 template <int TAPS>
 struct NlmsBin {
     static constexpr int kSlots = 4 * TAPS - 1;          // w (2 TAPS), h (2 (TAPS-1)), p
-    float2 w[TAPS];
-    float2 h[TAPS > 1 ? TAPS - 1 : 1];   // R[t-1] .. R[t-TAPS+1]
+    static constexpr int kH = TAPS > 1 ? TAPS - 1 : 1;
+    v2f w[TAPS];
+    v2f h[kH];        // R[t-1] .. R[t-TAPS+1]
+    v2f hr[kH];       // i * h (kept so each product is two packed FMAs)
+    float q[kH];      // |h|^2
     float p;
     __device__ __forceinline__ void load(const float* st, int k) {
 #pragma unroll
-        for (int l = 0; l < TAPS; ++l) w[l] = make_float2(st[(2 * l) * 257 + k], st[(2 * l + 1) * 257 + k]);
+        for (int l = 0; l < TAPS; ++l) w[l] = v2f{st[(2 * l) * 257 + k], st[(2 * l + 1) * 257 + k]};
 #pragma unroll
-        for (int l = 0; l < TAPS - 1; ++l)
-            h[l] = make_float2(st[(2 * TAPS + 2 * l) * 257 + k], st[(2 * TAPS + 2 * l + 1) * 257 + k]);
+        for (int l = 0; l < TAPS - 1; ++l) {
+            h[l] = v2f{st[(2 * TAPS + 2 * l) * 257 + k], st[(2 * TAPS + 2 * l + 1) * 257 + k]};
+            hr[l] = vrot(h[l]);
+            q[l] = fmaf(h[l].x, h[l].x, h[l].y * h[l].y);
+        }
         p = st[(kSlots - 1) * 257 + k];
     }
     __device__ __forceinline__ void store(float* st, int k) const {
@@ -405,24 +419,43 @@ struct NlmsBin {
         }
         st[(kSlots - 1) * 257 + k] = p;
     }
-    __device__ __forceinline__ float2 step(float2 d, float2 r, float mu, float beta, float delta) {
-        float2 y = cmul(w[0], r);
-        float pw = fmaf(r.x, r.x, r.y * r.y);
+    // One frame: returns E = D - sum_l W[l] R[t-l] and adapts W.
+    __device__ __forceinline__ float2 step(float2 d2, float2 r2, float mu, float beta, float delta) {
+        const v2f d{d2.x, d2.y}, r{r2.x, r2.y}, rr = vrot(r);
+        const float qr = fmaf(r.x, r.x, r.y * r.y);
+        // y = sum_l W[l] * h_l: (w.x + i w.y) h = w.x h + w.y (i h)
+        v2f y = vfma(vsplat(w[0].y), rr, vsplat(w[0].x) * r);
+        float pw = qr;
 #pragma unroll
         for (int l = 1; l < TAPS; ++l) {
-            y = cadd(y, cmul(w[l], h[l - 1]));
-            pw = fmaf(h[l - 1].x, h[l - 1].x, fmaf(h[l - 1].y, h[l - 1].y, pw));
+            y = vfma(vsplat(w[l].x), h[l - 1], y);
+            y = vfma(vsplat(w[l].y), hr[l - 1], y);
+            pw += q[l - 1];
         }
-        const float2 e = csub(d, y);
+        const v2f e = d - y;
         p = fmaf(beta, p, (1.f - beta) * pw);
-        const float2 ge = cscale(e, mu * __builtin_amdgcn_rcpf(p + delta));
-        w[0] = cadd(w[0], cmul(ge, conjf2(r)));
+        const v2f ge = e * vsplat(mu * __builtin_amdgcn_rcpf(p + delta));
+        // W[l] += ge * conj(h_l) = h.x * ge + h.y * (ge.y, -ge.x)
+        const v2f gs = -vrot(ge);
+        w[0] = vfma(vsplat(r.x), ge, w[0]);
+        w[0] = vfma(vsplat(r.y), gs, w[0]);
 #pragma unroll
-        for (int l = 1; l < TAPS; ++l) w[l] = cadd(w[l], cmul(ge, conjf2(h[l - 1])));
+        for (int l = 1; l < TAPS; ++l) {
+            w[l] = vfma(vsplat(h[l - 1].x), ge, w[l]);
+            w[l] = vfma(vsplat(h[l - 1].y), gs, w[l]);
+        }
 #pragma unroll
-        for (int l = TAPS - 2; l >= 1; --l) h[l] = h[l - 1];
-        if (TAPS > 1) h[0] = r;
-        return e;
+        for (int l = TAPS - 2; l >= 1; --l) {
+            h[l] = h[l - 1];
+            hr[l] = hr[l - 1];
+            q[l] = q[l - 1];
+        }
+        if (TAPS > 1) {
+            h[0] = r;
+            hr[0] = rr;
+            q[0] = qr;
+        }
+        return make_float2(e.x, e.y);
     }
 };
 
@@ -479,7 +512,7 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
         // near waves: NLMS of this chunk's rows happens after barrier 1, so the
         // near transform below runs after it (keeps the role waves balanced)
         float2 xa[8], xb[8], x128;
-        if (act && role < 2) {
+        if (act && role < 2 && !(p.mode & 8)) {
             asm volatile("" ::: "memory");
             wave_commit(wr, pf, cval, n, wt, lane);
             if (c0 + kFPB < T) wave_prefetch(pf, row_in, n, wt + kFPB, lane, al);
@@ -515,14 +548,15 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
             if (lb == 0) row[128] = x128;
         }
         __syncthreads();                                              // M / R rows of the chunk complete
-        if (role == 2 || tid == 4 * 64) {
+        if ((role == 2 || tid == 4 * 64) && !(p.mode & 1)) {
             // NLMS over the chunk: bin k = tid - 512 for the near waves; bin 256
             // on the first ref wave's lane 0 (idle here).  Bins 0 and 256 are
             // real and share row slot 0 (.x / .y).
             const int k = role == 2 ? tid - 2 * 4 * 64 : 256;
             const int slot = k & 255;
             const bool nyq = k == 256, dc = k == 0;
-            const int nf = (int)min((int64_t)kFPB, T - c0);
+            const int ia = nyq ? 1 : 2 * k;
+            const int ib = (dc || nyq) ? 2 * kSpecRow : 2 * k + 1;     // 2*256: first padding word
             NlmsBin<TAPS> st;
             st.load(sState, k);
             // 4 frames at a time: their (D, R) are loaded before the steps so the
@@ -542,25 +576,21 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
+                    // frames past the stream end only perturb state nobody reads
+                    // again; stepping them keeps the unrolled recursion branch-free
                     const int i = i0 + u;
-                    if (i < nf) {
-                        const float2 e = st.step(dd[u], rr[u], mu, beta, delta);
-                        float* mrow = sWave + (i >> 2) * kWaveFloats + (i & 3) * kGroupFloats;
-                        float* gsp = reinterpret_cast<float*>(spec + (c0 + i) * kSpecRow);
-                        if (dc || nyq) {
-                            mrow[nyq ? 1 : 0] = e.x;                  // packed (E[0], E[256])
-                            gsp[nyq ? 1 : 0] = e.x;
-                        } else {
-                            reinterpret_cast<float2*>(mrow)[k] = e;
-                            reinterpret_cast<float2*>(gsp)[k] = e;
-                        }
-                    }
+                    const float2 e = st.step(dd[u], rr[u], mu, beta, delta);
+                    float* mrow = sWave + (i >> 2) * kWaveFloats + (i & 3) * kGroupFloats;
+                    // E over M; the real DC / Nyquist pair shares slot 0 (.x / .y) and
+                    // their imaginary parts go to a dummy word of the row's padding
+                    mrow[ia] = e.x;
+                    mrow[ib] = e.y;
                 }
             }
             st.store(sState, k);
         }
         __syncthreads();                                              // E rows complete, R rows consumed
-        if (role == 0) {
+        if (role == 0 && !(p.mode & 4)) {
             // mic_erb = ERB(|E|) of this group's frame; the row is read into
             // registers before the magnitudes overwrite it
             const float2* row = reinterpret_cast<const float2*>(scr);
@@ -572,6 +602,15 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
             }
             x128 = row[128];
             wave_fence();
+            if (t < T) {                                              // E row -> spectrum buffer (K4)
+                float2* g = spec + t * kSpecRow;
+#pragma unroll
+                for (int m = 0; m < 8; ++m) g[lb + 16 * m] = xa[m];
+#pragma unroll
+                for (int m = 0; m < 8; ++m)
+                    if (lb + 16 * m != 0) g[256 - lb - 16 * m] = xb[m];
+                if (lb == 0) g[128] = x128;
+            }
 #pragma unroll
             for (int m = 0; m < 8; ++m) {
                 const int kk = lb + 16 * m;
@@ -586,7 +625,7 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
             if (lb == 0) scr[128 ^ sw] = mag(x128);
             wave_fence();
             erb_project(scr, sSched, sComb, L, lb, sw, t < T ? p.feats + ((int64_t)b * p.Tmax + t) * 96 : nullptr);
-        } else if (role == 2 && act) {
+        } else if (role == 2 && act && !(p.mode & 2)) {
             asm volatile("" ::: "memory");
             wave_commit(wr, pf, cval, n, wt, lane);
             if (c0 + kFPB < T) wave_prefetch(pf, row_in, n, wt + kFPB, lane, al);

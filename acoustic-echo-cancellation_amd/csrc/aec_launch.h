@@ -52,6 +52,8 @@ struct NlmsArgs {
     float2* spec;            // [B][Tmax][256] error spectrum E (slot 0 = (E[0], E[256]))
     int taps;
     float mu, beta, delta;
+    int mode;                // timing experiments only (AEC_NLMS_MODE): bit0 skip recursion,
+                             // bit1 skip near transform, bit2 skip mic ERB, bit3 skip mic/ref transforms
 };
 
 struct GruArgs {
