@@ -355,29 +355,30 @@ __global__ __launch_bounds__(256, 3) void analysis_kernel(AnalysisArgs p) {
 // float64 restatement of this recursion, tests/test_gpu_nlms.py).
 //
 // The NLMS is sequential over frames and independent over (stream, bin), so
-// one block owns one stream and walks it in chunks of 16 frames.  The block
-// has 12 waves in three roles, one of each per SIMD (wave w -> role w / 4,
-// frames 4 (w % 4) .. +3 of the chunk):
-//   mic  waves: transform mic -> spectrum row M[f] in the group's own LDS
-//               scratch; after the NLMS, project |E[f]| onto the ERB bands
-//               -> mic_erb;
-//   ref  waves: transform ref -> |R| -> ref_erb, then spectrum row R[f];
-//   near waves: run the NLMS of the chunk (thread k = bin k, thread 0 also
-//               bin 256; taps, power and far-end history live in LDS between
-//               chunks), writing E over M and to the spectrum buffer for K4;
-//               then transform near -> near_erb.
-// Two block barriers per chunk: rows complete -> NLMS -> rows consumed.
+// one block owns one stream and walks it in chunks of 16 frames ("ticks").
+// The block has 12 waves in three roles, one of each per SIMD (wave w ->
+// role w / 4; frames 4 (w % 4) .. +3 of a chunk):
+//   mic  waves, tick c: near transform -> near_erb; mic transform ->
+//        spectrum row M[f] (left in the group's LDS scratch);
+//   ref  waves, tick c: mic_erb of chunk c-2 from the error rows E (read back
+//        from the spectrum buffer); ref transform -> ref_erb -> row R[f];
+//   nlms waves, tick c: the 16 recursion steps of chunk c-1 for bin k = lane
+//        (+ bin 256 on lane 0), from registers, E rows -> spectrum buffer.
+// So the latency-bound recursion runs beside the transforms of the next
+// chunk.  Tick end: barrier; the nlms waves copy (M, R) of their bin for the
+// 16 frames into registers; barrier (rows consumed).  Taps, power and
+// far-end history stay in the nlms waves' registers for the whole stream.
 // Row layout: 256 float2, slot 0 packs the real pair (X[0], X[256]).
 // Per bin and frame:
 //   E = D - sum_l W[l] R[t-l];  P = beta P + (1-beta) sum_l |R[t-l]|^2;
 //   W[l] += mu E conj(R[t-l]) / (P + delta)
-// HBM traffic beyond K2: the E spectrum, 2 KiB per frame.
+// HBM traffic beyond K2: the E spectrum, 2 KiB per frame, written once and
+// read back once (L2-resident) for mic_erb.
 // --------------------------------------------------------------------------
 constexpr int kSpecRow = 256;          // float2 per spectrum row
 constexpr int kNlmsWaves = 12;
+constexpr int kERow = 512 + 48;        // floats per LDS error row: 256 float2, then ERB partials
 
-// One bin's NLMS state, stored structure-of-arrays in LDS: slot i of bin k
-// at st[i * 257 + k] (consecutive threads, consecutive banks).
 // Packed-FP32 complex helpers for the recursion: a complex value is a
 // float2 vector, so the products below map to v_pk_mul_f32 / v_pk_fma_f32
 // (two lanes of arithmetic per instruction slot).
@@ -386,93 +387,121 @@ __device__ __forceinline__ v2f vfma(v2f a, v2f b, v2f c) { return __builtin_elem
 __device__ __forceinline__ v2f vsplat(float a) { return v2f{a, a}; }
 __device__ __forceinline__ v2f vrot(v2f a) { return v2f{-a.y, a.x}; }       // i * a
 
+// One lane's NLMS.  A lane runs either one complex bin or, on the lane that
+// owns row slot 0, the two real bins 0 and 256 side by side (x, y halves).
+// Both cases are the same instruction stream over per-tap operands
+//   complex: A = h, B = i h              dual real: A = (h.x, 0), B = (0, h.y)
+//   y  = sum_l w.x A + w.y B             (complex W h  /  (w.x h.x, w.y h.y))
+//   W += ge.x conj(A) + ge.y (-B.x, B.y) (ge conj(h)   /  (ge.x h.x, ge.y h.y))
+//   pw = sum_l A*A + B*B                 (|h|^2 in both halves / (h.x^2, h.y^2))
+// with ge = e * mu / (P + delta) per half.
 template <int TAPS>
 struct NlmsBin {
-    static constexpr int kSlots = 4 * TAPS - 1;          // w (2 TAPS), h (2 (TAPS-1)), p
-    static constexpr int kH = TAPS > 1 ? TAPS - 1 : 1;
     v2f w[TAPS];
-    v2f h[kH];        // R[t-1] .. R[t-TAPS+1]
-    v2f hr[kH];       // i * h (kept so each product is two packed FMAs)
-    float q[kH];      // |h|^2
-    float p;
-    __device__ __forceinline__ void load(const float* st, int k) {
+    v2f a[TAPS], bq[TAPS], qq[TAPS];   // operands A, B and A*A + B*B of R[t], R[t-1], ...
+    v2f p;
+    v2f ma, mb, mc;                    // operand masks: complex (1,1), (-1,1), (0,0); dual (1,0), (0,0), (0,1)
+    __device__ __forceinline__ void reset(bool dual) {
 #pragma unroll
-        for (int l = 0; l < TAPS; ++l) w[l] = v2f{st[(2 * l) * 257 + k], st[(2 * l + 1) * 257 + k]};
-#pragma unroll
-        for (int l = 0; l < TAPS - 1; ++l) {
-            h[l] = v2f{st[(2 * TAPS + 2 * l) * 257 + k], st[(2 * TAPS + 2 * l + 1) * 257 + k]};
-            hr[l] = vrot(h[l]);
-            q[l] = fmaf(h[l].x, h[l].x, h[l].y * h[l].y);
-        }
-        p = st[(kSlots - 1) * 257 + k];
-    }
-    __device__ __forceinline__ void store(float* st, int k) const {
-#pragma unroll
-        for (int l = 0; l < TAPS; ++l) {
-            st[(2 * l) * 257 + k] = w[l].x;
-            st[(2 * l + 1) * 257 + k] = w[l].y;
-        }
-#pragma unroll
-        for (int l = 0; l < TAPS - 1; ++l) {
-            st[(2 * TAPS + 2 * l) * 257 + k] = h[l].x;
-            st[(2 * TAPS + 2 * l + 1) * 257 + k] = h[l].y;
-        }
-        st[(kSlots - 1) * 257 + k] = p;
+        for (int l = 0; l < TAPS; ++l) w[l] = a[l] = bq[l] = qq[l] = vsplat(0.f);
+        p = vsplat(0.f);
+        ma = dual ? v2f{1.f, 0.f} : v2f{1.f, 1.f};
+        mb = dual ? v2f{0.f, 0.f} : v2f{-1.f, 1.f};
+        mc = dual ? v2f{0.f, 1.f} : v2f{0.f, 0.f};
     }
     // One frame: returns E = D - sum_l W[l] R[t-l] and adapts W.
     __device__ __forceinline__ float2 step(float2 d2, float2 r2, float mu, float beta, float delta) {
-        const v2f d{d2.x, d2.y}, r{r2.x, r2.y}, rr = vrot(r);
-        const float qr = fmaf(r.x, r.x, r.y * r.y);
-        // y = sum_l W[l] * h_l: (w.x + i w.y) h = w.x h + w.y (i h)
-        v2f y = vfma(vsplat(w[0].y), rr, vsplat(w[0].x) * r);
-        float pw = qr;
+        const v2f d{d2.x, d2.y}, r{r2.x, r2.y};
 #pragma unroll
-        for (int l = 1; l < TAPS; ++l) {
-            y = vfma(vsplat(w[l].x), h[l - 1], y);
-            y = vfma(vsplat(w[l].y), hr[l - 1], y);
-            pw += q[l - 1];
+        for (int l = TAPS - 1; l >= 1; --l) {
+            a[l] = a[l - 1];
+            bq[l] = bq[l - 1];
+            qq[l] = qq[l - 1];
         }
-        const v2f e = d - y;
-        p = fmaf(beta, p, (1.f - beta) * pw);
-        const v2f ge = e * vsplat(mu * __builtin_amdgcn_rcpf(p + delta));
-        // W[l] += ge * conj(h_l) = h.x * ge + h.y * (ge.y, -ge.x)
-        const v2f gs = -vrot(ge);
-        w[0] = vfma(vsplat(r.x), ge, w[0]);
-        w[0] = vfma(vsplat(r.y), gs, w[0]);
+        a[0] = r * ma;
+        bq[0] = vfma(v2f{r.y, r.x}, mb, r * mc);
+        qq[0] = vfma(a[0], a[0], bq[0] * bq[0]);
+        // independent per-tap products summed as a tree (short dependency chain)
+        v2f pr[TAPS];
+        v2f pw = qq[0];
 #pragma unroll
-        for (int l = 1; l < TAPS; ++l) {
-            w[l] = vfma(vsplat(h[l - 1].x), ge, w[l]);
-            w[l] = vfma(vsplat(h[l - 1].y), gs, w[l]);
-        }
+        for (int l = 0; l < TAPS; ++l) pr[l] = vfma(vsplat(w[l].y), bq[l], vsplat(w[l].x) * a[l]);
 #pragma unroll
-        for (int l = TAPS - 2; l >= 1; --l) {
-            h[l] = h[l - 1];
-            hr[l] = hr[l - 1];
-            q[l] = q[l - 1];
-        }
-        if (TAPS > 1) {
-            h[0] = r;
-            hr[0] = rr;
-            q[0] = qr;
+        for (int l = 1; l < TAPS; ++l) pw = pw + qq[l];
+#pragma unroll
+        for (int s = 1; s < TAPS; s *= 2)
+#pragma unroll
+            for (int l = 0; l + s < TAPS; l += 2 * s) pr[l] = pr[l] + pr[l + s];
+        const v2f e = d - pr[0];
+        p = vfma(vsplat(beta), p, vsplat(1.f - beta) * pw);
+        const v2f g = v2f{__builtin_amdgcn_rcpf(p.x + delta), __builtin_amdgcn_rcpf(p.y + delta)} * vsplat(mu);
+        const v2f ge = e * g;
+#pragma unroll
+        for (int l = 0; l < TAPS; ++l) {
+            w[l] = vfma(vsplat(ge.x), v2f{a[l].x, -a[l].y}, w[l]);
+            w[l] = vfma(vsplat(ge.y), v2f{-bq[l].x, bq[l].y}, w[l]);
         }
         return make_float2(e.x, e.y);
     }
 };
+
+// One transform pass of a wave: commit the prefetched samples of (signal,
+// 4 frames at wt), prefetch the next task, window + rFFT -> xa / xb / x128.
+__device__ __forceinline__ void nlms_transform(float* wr, float* scr, float4 (&pf)[kWavePf], float cval, int n, int wt,
+                                               int lane, int gg, int lb, const float* sHann, const float2* sTwT,
+                                               const float2* sTw512, const float* next_row, int next_wt,
+                                               bool next_al, float2 (&xa)[8], float2 (&xb)[8], float2& x128) {
+    asm volatile("" ::: "memory");
+    wave_commit(wr, pf, cval, n, wt, lane);
+    if (next_row) wave_prefetch(pf, next_row, n, next_wt, lane, next_al);
+    wave_fence();
+    float2 v[16];
+    load_frame(v, wr, sHann, gg, lb);
+    wave_fence();
+    fft256<false>(v, lb, scr, sTwT);
+    rfft_unpack(v, lb, sTw512, xa, xb, x128);
+}
+
+__device__ __forceinline__ void mags_to_scr(float* scr, int lb, int sw, const float2 (&xa)[8], const float2 (&xb)[8],
+                                            float2 x128) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const int kk = lb + 16 * m;
+        scr[kk ^ sw] = mag(xa[m]);
+        scr[(kk == 0 ? 256 : 256 - kk) ^ sw] = mag(xb[m]);
+    }
+    if (lb == 0) scr[128 ^ sw] = mag(x128);
+}
+
+__device__ __forceinline__ void row_to_scr(float* scr, int lb, const float2 (&xa)[8], const float2 (&xb)[8],
+                                           float2 x128) {
+    float2* row = reinterpret_cast<float2*>(scr);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const int kk = lb + 16 * m;
+        if (kk == 0) {
+            row[0] = make_float2(xa[0].x, xb[0].x);                   // (X[0], X[256]), both real
+        } else {
+            row[kk] = xa[m];
+            row[256 - kk] = xb[m];
+        }
+    }
+    if (lb == 0) row[128] = x128;
+}
 
 template <int TAPS>
 __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsArgs p) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x;
     const int L = p.sched_len;
-    constexpr int kSlots = NlmsBin<TAPS>::kSlots;
 
     float4* sSched = reinterpret_cast<float4*>(smem);                 // L * 16
     int2* sComb = reinterpret_cast<int2*>(sSched + L * 16);           // 32
     float2* sTw512 = reinterpret_cast<float2*>(sComb + 32);           // 258
     float2* sTwT = sTw512 + 258;                                      // 256
     float* sHann = reinterpret_cast<float*>(sTwT + 256);              // 512
-    float* sWave = sHann + 512;                                       // kNlmsWaves * kWaveFloats
-    float* sState = sWave + kNlmsWaves * kWaveFloats;                 // kSlots * 257
+    float* sWave = sHann + 512;                                       // 8 * kWaveFloats (mic, ref waves)
+    float* sE = sWave + 8 * kWaveFloats;                              // 2 x kFPB error rows (kERow floats)
 
     const DevTables* tb = reinterpret_cast<const DevTables*>(p.tables);
     if (tid < 256) {
@@ -486,167 +515,129 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
     {
         const float4* sch = reinterpret_cast<const float4*>(p.sched);
         for (int i = tid; i < L * 16; i += kNlmsWaves * 64) sSched[i] = sch[i];
-        for (int i = tid; i < kSlots * 257; i += kNlmsWaves * 64) sState[i] = 0.f;
     }
     const int wave = tid >> 6, lane = tid & 63;
-    const int role = wave >> 2, q = wave & 3;                        // 0 mic, 1 ref, 2 near
+    const int role = wave >> 2, q = wave & 3;                        // 0 mic, 1 ref, 2 nlms
     const int gg = lane >> 4, lb = lane & 15, sw = 16 * (gg & 1);
-    float* wr = sWave + wave * kWaveFloats;
+    float* wr = sWave + (role < 2 ? wave : 0) * kWaveFloats;
     float* scr = wr + gg * kGroupFloats;
     const int b = p.b0 + blockIdx.x;
     const int n = (int)p.lens[b];
     const int64_t T = n / kHop + 1;
-    const bool act = role < p.nsig;                                   // near waves idle without near
-    const bool al = ((p.ld & 3) == 0) && act && ((reinterpret_cast<uintptr_t>(p.sig[role]) & 15) == 0);
-    const float* row_in = act ? p.sig[role] + (int64_t)b * p.ld : nullptr;
-    const float cval = act ? p.cvals[b * 3 + role] : 0.f;
+    const int nch = (int)((T + kFPB - 1) / kFPB);
+    const bool have_near = p.nsig == 3;
+    const int64_t ld = p.ld;
+    const float* row_mic = p.sig[0] + (int64_t)b * ld;
+    const float* row_ref = p.sig[1] + (int64_t)b * ld;
+    const float* row_near = have_near ? p.sig[2] + (int64_t)b * ld : nullptr;
+    const bool al_ld = (ld & 3) == 0;
+    const bool al_mic = al_ld && ((reinterpret_cast<uintptr_t>(p.sig[0]) & 15) == 0);
+    const bool al_ref = al_ld && ((reinterpret_cast<uintptr_t>(p.sig[1]) & 15) == 0);
+    const bool al_near = have_near && al_ld && ((reinterpret_cast<uintptr_t>(p.sig[2]) & 15) == 0);
     float2* spec = p.spec + (int64_t)b * p.Tmax * kSpecRow;
+    float* feats = p.feats + (int64_t)b * p.Tmax * 96;
     const float mu = p.mu, beta = p.beta, delta = p.delta;
     __syncthreads();
 
+    // The nlms waves and the transform waves run separate loops with the same
+    // two barriers per tick, so the register allocator sees the recursion's
+    // state and the transforms' working set in disjoint regions.
+    if (role == 2) {
+        const int k = lane + 64 * q;                                  // bin k; k = 0 also bin 256
+        NlmsBin<TAPS> st;
+        st.reset(k == 0);
+        float2 dd[kFPB], rr[kFPB];
+        for (int c = 0; c < nch + 2; ++c) {
+            const int c1 = c - 1;
+            if (c1 >= 0 && c1 < nch && !(p.mode & 1)) {
+                // recursion of chunk c-1 -> E rows (LDS buffer c-1 & 1, spectrum
+                // buffer); frames past the stream end only perturb state nobody
+                // reads again (the unrolled loop stays branch-free)
+                const int64_t t0 = (int64_t)c1 * kFPB;
+                float* eb = sE + (c1 & 1) * kFPB * kERow;
+#pragma unroll
+                for (int i = 0; i < kFPB; ++i) {
+                    const float2 e = st.step(dd[i], rr[i], mu, beta, delta);
+                    reinterpret_cast<float2*>(eb + i * kERow)[k] = e;
+                    if (t0 + i < T) spec[(t0 + i) * kSpecRow + k] = e;
+                }
+            }
+            __syncthreads();                                          // rows of chunk c complete
+            if (c < nch) {
+#pragma unroll
+                for (int i = 0; i < kFPB; ++i) {
+                    const float* base = sWave + (i >> 2) * kWaveFloats + (i & 3) * kGroupFloats;
+                    dd[i] = reinterpret_cast<const float2*>(base)[k];
+                    rr[i] = reinterpret_cast<const float2*>(base + 4 * kWaveFloats)[k];
+                }
+            }
+            __syncthreads();                                          // rows consumed
+        }
+        return;
+    }
+
+    // mic waves walk near(c), mic(c), near(c+1), ...; ref waves ref(c), ref(c+1), ...
     float4 pf[kWavePf];
-    if (act) wave_prefetch(pf, row_in, n, 4 * q, lane, al);
-    for (int64_t c0 = 0; c0 < T; c0 += kFPB) {
-        const int wt = (int)c0 + 4 * q;
+    if (role == 0) {
+        if (have_near) wave_prefetch(pf, row_near, n, 4 * q, lane, al_near);
+        else wave_prefetch(pf, row_mic, n, 4 * q, lane, al_mic);
+    } else {
+        wave_prefetch(pf, row_ref, n, 4 * q, lane, al_ref);
+    }
+    for (int c = 0; c < nch + 2; ++c) {
+        const int wt = c * kFPB + 4 * q;
         const int64_t t = wt + gg;
-        // near waves: NLMS of this chunk's rows happens after barrier 1, so the
-        // near transform below runs after it (keeps the role waves balanced)
         float2 xa[8], xb[8], x128;
-        if (act && role < 2 && !(p.mode & 8)) {
-            asm volatile("" ::: "memory");
-            wave_commit(wr, pf, cval, n, wt, lane);
-            if (c0 + kFPB < T) wave_prefetch(pf, row_in, n, wt + kFPB, lane, al);
-            wave_fence();
-            float2 v[16];
-            load_frame(v, wr, sHann, gg, lb);
-            wave_fence();
-            fft256<false>(v, lb, scr, sTwT);
-            rfft_unpack(v, lb, sTw512, xa, xb, x128);
-            if (role == 1) {
+        if (role == 0) {
+            if (c < nch && !(p.mode & 8)) {
+                if (have_near) {
+                    nlms_transform(wr, scr, pf, p.cvals[b * 3 + 2], n, wt, lane, gg, lb, sHann, sTwT, sTw512,
+                                   row_mic, wt, al_mic, xa, xb, x128);
+                    if (!(p.mode & 2)) {
+                        mags_to_scr(scr, lb, sw, xa, xb, x128);
+                        wave_fence();
+                        erb_project(scr, sSched, sComb, L, lb, sw, t < T ? feats + t * 96 + 64 : nullptr);
+                    }
+                }
+                const bool more = c + 1 < nch;
+                nlms_transform(wr, scr, pf, p.cvals[b * 3 + 0], n, wt, lane, gg, lb, sHann, sTwT, sTw512,
+                               more ? (have_near ? row_near : row_mic) : nullptr, wt + kFPB,
+                               have_near ? al_near : al_mic, xa, xb, x128);
+                row_to_scr(scr, lb, xa, xb, x128);
+            }
+        } else {
+            const int c2 = c - 2;
+            if (c2 >= 0 && !(p.mode & 4)) {
+                // mic_erb of chunk c-2 from its error rows (complete since the
+                // barriers of tick c-1); this group's frame 4 q + gg
+                const int64_t t2 = (int64_t)c2 * kFPB + 4 * q + gg;
+                float* er = sE + (c2 & 1) * kFPB * kERow + (4 * q + gg) * kERow;
+                const float2* row = reinterpret_cast<const float2*>(er);
 #pragma unroll
                 for (int m = 0; m < 8; ++m) {
                     const int kk = lb + 16 * m;
-                    scr[kk ^ sw] = mag(xa[m]);
-                    scr[(kk == 0 ? 256 : 256 - kk) ^ sw] = mag(xb[m]);
+                    xa[m] = row[kk];
+                    xb[m] = row[(256 - kk) & 255];
                 }
-                if (lb == 0) scr[128 ^ sw] = mag(x128);
+                x128 = row[128];
+                xa[0] = lb == 0 ? make_float2(xa[0].x, 0.f) : xa[0];
+                xb[0] = lb == 0 ? make_float2(xb[0].y, 0.f) : xb[0];     // slot 0 = (E[0], E[256])
                 wave_fence();
-                erb_project(scr, sSched, sComb, L, lb, sw,
-                            t < T ? p.feats + ((int64_t)b * p.Tmax + t) * 96 + 32 : nullptr);
+                mags_to_scr(er, lb, sw, xa, xb, x128);
+                wave_fence();
+                erb_project(er, sSched, sComb, L, lb, sw, t2 < T ? feats + t2 * 96 : nullptr);
             }
-            float2* row = reinterpret_cast<float2*>(scr);
-#pragma unroll
-            for (int m = 0; m < 8; ++m) {
-                const int kk = lb + 16 * m;
-                if (kk == 0) {
-                    row[0] = make_float2(xa[0].x, xb[0].x);           // (X[0], X[256]), both real
-                } else {
-                    row[kk] = xa[m];
-                    row[256 - kk] = xb[m];
-                }
+            if (c < nch && !(p.mode & 8)) {
+                nlms_transform(wr, scr, pf, p.cvals[b * 3 + 1], n, wt, lane, gg, lb, sHann, sTwT, sTw512,
+                               c + 1 < nch ? row_ref : nullptr, wt + kFPB, al_ref, xa, xb, x128);
+                mags_to_scr(scr, lb, sw, xa, xb, x128);
+                wave_fence();
+                erb_project(scr, sSched, sComb, L, lb, sw, t < T ? feats + t * 96 + 32 : nullptr);
+                row_to_scr(scr, lb, xa, xb, x128);
             }
-            if (lb == 0) row[128] = x128;
         }
-        __syncthreads();                                              // M / R rows of the chunk complete
-        if ((role == 2 || tid == 4 * 64) && !(p.mode & 1)) {
-            // NLMS over the chunk: bin k = tid - 512 for the near waves; bin 256
-            // on the first ref wave's lane 0 (idle here).  Bins 0 and 256 are
-            // real and share row slot 0 (.x / .y).
-            const int k = role == 2 ? tid - 2 * 4 * 64 : 256;
-            const int slot = k & 255;
-            const bool nyq = k == 256, dc = k == 0;
-            const int ia = nyq ? 1 : 2 * k;
-            const int ib = (dc || nyq) ? 2 * kSpecRow : 2 * k + 1;     // 2*256: first padding word
-            NlmsBin<TAPS> st;
-            st.load(sState, k);
-            // 4 frames at a time: their (D, R) are loaded before the steps so the
-            // recursion's dependency chain carries no LDS latency
-#pragma unroll
-            for (int i0 = 0; i0 < kFPB; i0 += 4) {
-                float2 dd[4], rr[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int i = i0 + u;
-                    const float2 d = reinterpret_cast<const float2*>(sWave + (i >> 2) * kWaveFloats +
-                                                                     (i & 3) * kGroupFloats)[slot];
-                    const float2 r = reinterpret_cast<const float2*>(sWave + (4 + (i >> 2)) * kWaveFloats +
-                                                                     (i & 3) * kGroupFloats)[slot];
-                    dd[u] = nyq ? make_float2(d.y, 0.f) : (dc ? make_float2(d.x, 0.f) : d);
-                    rr[u] = nyq ? make_float2(r.y, 0.f) : (dc ? make_float2(r.x, 0.f) : r);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    // frames past the stream end only perturb state nobody reads
-                    // again; stepping them keeps the unrolled recursion branch-free
-                    const int i = i0 + u;
-                    const float2 e = st.step(dd[u], rr[u], mu, beta, delta);
-                    float* mrow = sWave + (i >> 2) * kWaveFloats + (i & 3) * kGroupFloats;
-                    // E over M; the real DC / Nyquist pair shares slot 0 (.x / .y) and
-                    // their imaginary parts go to a dummy word of the row's padding
-                    mrow[ia] = e.x;
-                    mrow[ib] = e.y;
-                }
-            }
-            st.store(sState, k);
-        }
-        __syncthreads();                                              // E rows complete, R rows consumed
-        if (role == 0 && !(p.mode & 4)) {
-            // mic_erb = ERB(|E|) of this group's frame; the row is read into
-            // registers before the magnitudes overwrite it
-            const float2* row = reinterpret_cast<const float2*>(scr);
-#pragma unroll
-            for (int m = 0; m < 8; ++m) {
-                const int kk = lb + 16 * m;
-                xa[m] = row[kk];
-                xb[m] = row[(256 - kk) & 255];
-            }
-            x128 = row[128];
-            wave_fence();
-            if (t < T) {                                              // E row -> spectrum buffer (K4)
-                float2* g = spec + t * kSpecRow;
-#pragma unroll
-                for (int m = 0; m < 8; ++m) g[lb + 16 * m] = xa[m];
-#pragma unroll
-                for (int m = 0; m < 8; ++m)
-                    if (lb + 16 * m != 0) g[256 - lb - 16 * m] = xb[m];
-                if (lb == 0) g[128] = x128;
-            }
-#pragma unroll
-            for (int m = 0; m < 8; ++m) {
-                const int kk = lb + 16 * m;
-                if (kk == 0) {
-                    scr[0 ^ sw] = mag(make_float2(xa[0].x, 0.f));
-                    scr[256 ^ sw] = mag(make_float2(xa[0].y, 0.f));
-                } else {
-                    scr[kk ^ sw] = mag(xa[m]);
-                    scr[(256 - kk) ^ sw] = mag(xb[m]);
-                }
-            }
-            if (lb == 0) scr[128 ^ sw] = mag(x128);
-            wave_fence();
-            erb_project(scr, sSched, sComb, L, lb, sw, t < T ? p.feats + ((int64_t)b * p.Tmax + t) * 96 : nullptr);
-        } else if (role == 2 && act && !(p.mode & 2)) {
-            asm volatile("" ::: "memory");
-            wave_commit(wr, pf, cval, n, wt, lane);
-            if (c0 + kFPB < T) wave_prefetch(pf, row_in, n, wt + kFPB, lane, al);
-            wave_fence();
-            float2 v[16];
-            load_frame(v, wr, sHann, gg, lb);
-            wave_fence();
-            fft256<false>(v, lb, scr, sTwT);
-            rfft_unpack(v, lb, sTw512, xa, xb, x128);
-#pragma unroll
-            for (int m = 0; m < 8; ++m) {
-                const int kk = lb + 16 * m;
-                scr[kk ^ sw] = mag(xa[m]);
-                scr[(kk == 0 ? 256 : 256 - kk) ^ sw] = mag(xb[m]);
-            }
-            if (lb == 0) scr[128 ^ sw] = mag(x128);
-            wave_fence();
-            erb_project(scr, sSched, sComb, L, lb, sw, t < T ? p.feats + ((int64_t)b * p.Tmax + t) * 96 + 64 : nullptr);
-        }
-        // the next chunk's rows are written by the same waves after their own
-        // work above; the NLMS reads of this chunk ended at barrier 2
+        __syncthreads();                                              // rows of chunk c complete
+        __syncthreads();                                              // rows consumed
     }
 }
 

@@ -90,10 +90,11 @@ struct SynthArgs {
 inline size_t analysis_smem_bytes(int sched_len) {
     return (size_t)sched_len * 16 * 16 + 32 * 8 + (258 * 2 + 256 * 2 + 512 + (size_t)kFPB * kGroupFloats) * 4;
 }
-// K2n: tables + 12 wave regions + NLMS state (4 TAPS - 1 slots x 257 bins)
-inline size_t nlms_smem_bytes(int sched_len, int taps) {
-    return (size_t)sched_len * 16 * 16 + 32 * 8 + (258 * 2 + 256 * 2 + 512 + (size_t)12 * 4 * kGroupFloats) * 4 +
-           (size_t)(4 * taps - 1) * 257 * 4;
+// K2n: tables + 8 wave regions (mic, ref waves; the nlms waves keep their
+// state in registers) + 2 x 16 error rows of 560 floats
+inline size_t nlms_smem_bytes(int sched_len, int /*taps*/) {
+    return (size_t)sched_len * 16 * 16 + 32 * 8 +
+           (258 * 2 + 256 * 2 + 512 + (size_t)8 * 4 * kGroupFloats + (size_t)2 * kFPB * 560) * 4;
 }
 inline size_t synthesis_smem_bytes() {
     return 260 * 16 + (258 * 2 + 256 * 2 + 512 + 256 + kFPB * 33 + 4 + (size_t)kFPB * kGroupFloats) * 4;
