@@ -25,7 +25,7 @@ import sys
 
 
 def short(name):
-    return name.split('(')[0].split('<')[0].replace('aec::', '').replace('_kernel', '')
+    return name.split('(')[0].split('<')[0].replace('void ', '').replace('aec::', '').replace('_kernel', '')
 
 
 def main():
