@@ -5,7 +5,8 @@
 //
 // One block per stream, 7 waves:
 //   wave 0      the recurrence h_{t-1} -> h_t (the only sequential dependency
-//               of the whole path), one step per frame, raised issue priority;
+//               of the whole path), one step per frame, raised issue priority,
+//               k-split over the two wave halves (24 packed FMAs per lane);
 //   waves 1..6  helpers, software-pipelined around it in ticks of kCH frames:
 //               at tick c they stage chunk c+2's features (loaded from HBM at
 //               tick c-1, so no load latency is exposed), issue the loads of
@@ -41,6 +42,7 @@ __global__ __launch_bounds__(kGruThreads) void gru_kernel(GruArgs p) {
     __shared__ __attribute__((aligned(16))) float sNear[4][kCH][32];
     __shared__ __attribute__((aligned(16))) float sO[kHeadGroups][32];
     __shared__ float sLoss[1 + kGruHelpers];
+    __shared__ __attribute__((aligned(16))) float sHb[32];   // h_{t-1} broadcast slot (recurrence wave)
 
     const int b = p.b0 + blockIdx.x;
     const int64_t n = p.lens[b];
@@ -60,22 +62,30 @@ __global__ __launch_bounds__(kGruThreads) void gru_kernel(GruArgs p) {
 
     if (wave == 0) {
         // ---------------- recurrence wave ----------------
-        // lane l: j = l & 31, half = l >> 5.  Row pair per lane: (r_j, n_j) in
-        // half 0, (z_j, n_j) in half 1, full 32-long dot products with h held
-        // wave-uniform in SGPRs (v_readlane), so no LDS round trip sits on the
-        // h_{t-1} -> h_t chain; h_j is computed identically in both halves.
+        // lane l: j = l & 31, kh = l >> 5.  Each lane holds rows r_j, z_j, n_j of
+        // W_hh restricted to its k-half [16 kh, 16 kh + 16): 24 packed FMAs per
+        // step instead of 32 full-length (r|z, n) dots, and no row computed
+        // twice.  h_{t-1} is broadcast through a 32-float LDS slot (one write,
+        // four b128 reads of the lane's half) and the two halves' partial dots
+        // are combined with v_permlane32_swap; h_j ends up identical in both
+        // halves.
         __builtin_amdgcn_s_setprio(3);
         const bool run = p.mode != 2;
-        const int j = lane & 31, half = lane >> 5;
-        f2v w[32];
+        const int j = lane & 31, kh = lane >> 5;
+        f2v wrz[16], wn[8];
         {
-            const float* rA = W_hh + (half ? (32 + j) : j) * 32;
-            const float* rN = W_hh + (64 + j) * 32;
+            const float* rR = W_hh + j * 32 + 16 * kh;
+            const float* rZ = W_hh + (32 + j) * 32 + 16 * kh;
+            const float* rN = W_hh + (64 + j) * 32 + 16 * kh;
 #pragma unroll
-            for (int k = 0; k < 32; ++k) w[k] = f2v{rA[k], rN[k]};
+            for (int k = 0; k < 16; ++k) wrz[k] = f2v{rR[k], rZ[k]};
+#pragma unroll
+            for (int i = 0; i < 8; ++i) wn[i] = f2v{rN[2 * i], rN[2 * i + 1]};
         }
         const float bhn = b_hh[64 + j];
         float hj = 0.f;                                   // h_{-1} = 0
+        float* hb = sHb;
+        if (lane < 32) hb[lane] = 0.f;
         for (int c = -3; c <= nch; ++c) {
             if (run && c >= 0 && c < nch) {
                 const int f_end = min(kCH, T - c * kCH);
@@ -85,27 +95,40 @@ __global__ __launch_bounds__(kGruThreads) void gru_kernel(GruArgs p) {
                     // prefetch next step's input projections (independent of h)
                     const int fn = f + 1 < f_end ? f + 1 : f;
                     const float ngr = gi[fn * 96 + j], ngz = gi[fn * 96 + 32 + j], ngn = gi[fn * 96 + 64 + j];
-                    float hk[32];
+                    // h_{t-1}[16 kh .. 16 kh + 15] (LDS ops of one wave execute in order;
+                    // measured faster than a permlane16_swap + 16 DPP row_newbcast
+                    // broadcast: 0.177 vs 0.197 ms recurrence-only)
+                    const float4* h4 = reinterpret_cast<const float4*>(hb + 16 * kh);
+                    const float4 q0 = h4[0], q1 = h4[1], q2 = h4[2], q3 = h4[3];
+                    const float hk[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                                          q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+                    f2v arz[4] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}};
+                    f2v an[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
 #pragma unroll
-                    for (int k = 0; k < 32; ++k) hk[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hj), k));
-                    __builtin_amdgcn_sched_barrier(0);
-                    f2v acc[4] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}};
+                    for (int k = 0; k < 16; ++k)
+                        arz[k & 3] = __builtin_elementwise_fma(wrz[k], f2v{hk[k], hk[k]}, arz[k & 3]);
 #pragma unroll
-                    for (int k = 0; k < 32; ++k) acc[k & 3] = __builtin_elementwise_fma(w[k], f2v{hk[k], hk[k]}, acc[k & 3]);
-                    const f2v acc2 = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-                    const float sA = acc2.x;           // r-dot (half 0) or z-dot (half 1)
-                    const float sN = acc2.y;           // n-dot (both halves)
+                    for (int i = 0; i < 8; ++i)
+                        an[i & 1] = __builtin_elementwise_fma(wn[i], f2v{hk[2 * i], hk[2 * i + 1]}, an[i & 1]);
+                    const f2v rz = (arz[0] + arz[1]) + (arz[2] + arz[3]);
+                    const f2v n2 = an[0] + an[1];
+                    const float pr = rz.x, pz = rz.y, pn = n2.x + n2.y;
                     // v_permlane32_swap: lanes 32..63 of vdst <-> lanes 0..31 of vsrc, so the
                     // other half's value is res[1] in lanes 0..31 and res[0] in lanes 32..63
-                    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(sA), __float_as_uint(sA), false, false);
-                    const float other = __uint_as_float(half ? sw[0] : sw[1]);
-                    const float rdot = half ? other : sA;
-                    const float zdot = half ? sA : other;
+                    const auto sr = __builtin_amdgcn_permlane32_swap(__float_as_uint(pr), __float_as_uint(pr), false, false);
+                    const auto sz = __builtin_amdgcn_permlane32_swap(__float_as_uint(pz), __float_as_uint(pz), false, false);
+                    const auto sn = __builtin_amdgcn_permlane32_swap(__float_as_uint(pn), __float_as_uint(pn), false, false);
+                    const float rdot = pr + __uint_as_float(kh ? sr[0] : sr[1]);
+                    const float zdot = pz + __uint_as_float(kh ? sz[0] : sz[1]);
+                    const float ndot = pn + __uint_as_float(kh ? sn[0] : sn[1]);
                     const float r = sigmoidf_(gr + rdot);
                     const float z = sigmoidf_(gz + zdot);
-                    const float nn = tanhf_(gn + r * (sN + bhn));
+                    const float nn = tanhf_(gn + r * (ndot + bhn));
                     hj = (1.f - z) * nn + z * hj;
-                    if (half == 0) sH[c & 1][f][j] = hj;  // for the head (off the chain)
+                    if (kh == 0) {
+                        hb[j] = hj;                            // broadcast slot for the next step
+                        sH[c & 1][f][j] = hj;                  // for the head (off the chain)
+                    }
                     gr = ngr; gz = ngz; gn = ngn;
                 }
             }
