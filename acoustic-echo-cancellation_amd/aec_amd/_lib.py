@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libaec_hip.so')
+# AEC_HIP_LIB: alternative build of the same library (A/B timing experiments)
+LIB_PATH = os.environ.get('AEC_HIP_LIB') or os.path.join(_HERE, 'libaec_hip.so')
 
 # aec_status codes (include/aec_hip.h)
 AEC_OK = 0

@@ -119,13 +119,23 @@ template <bool INV>
 __device__ __forceinline__ void fft256(float2 (&v)[16], int lb, float* scr, const float2* twT) {
     dft16<INV>(v);
     float2* s2 = reinterpret_cast<float2*>(scr);
+    // all 15 twiddle reads first: interleaved with the transpose writes (which
+    // may alias as far as the compiler knows) each read would wait for the
+    // previous write, exposing the LDS latency 15 times.  (A packed-FP32
+    // variant of these helpers was measured slower: 0.285 vs 0.245 ms for
+    // the analysis kernel — more v_mov for operand pairs and a stack temp.)
+    float2 w[15];
+    static_for<0, 15>([&](auto ii) {
+        constexpr int i = decltype(ii)::value;
+        w[i] = twT[(i + 1) * 16 + lb];
+    });
     s2[lb] = v[kP(0)];
-#pragma unroll
-    for (int k1 = 1; k1 < 16; ++k1) {
-        float2 w = twT[k1 * 16 + lb];
-        if (INV) w.y = -w.y;
-        s2[k1 * 18 + lb] = cmul(v[kP(k1)], w);
-    }
+    static_for<0, 15>([&](auto ii) {
+        constexpr int i = decltype(ii)::value;
+        float2 t = w[i];
+        if (INV) t.y = -t.y;
+        s2[(i + 1) * 18 + lb] = cmul(v[kP(i + 1)], t);
+    });
     wave_fence();
     const float4* s4 = reinterpret_cast<const float4*>(scr) + lb * 9;
 #pragma unroll
