@@ -1,0 +1,56 @@
+"""CPU: the DCCRN oracle (oracle/crn_oracle.py) against the golden vectors the
+reference itself produced (tests/golden/make_crn_golden.py).
+
+Pins the float64 restatement of dccrn.py / dccrn2.py
+before the GPU parity tests trust it.  Tolerance: relative RMS <= 1e-5 on
+every stored tensor (observed ~6e-7: float64 restatement vs the reference's
+float32 CPU path); framing integers exact.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import crn_oracle as C
+
+GOLD = os.path.join(os.path.dirname(__file__), 'golden')
+META = json.load(open(os.path.join(GOLD, 'crn_meta.json')))
+
+
+def rel(a, b):
+    b = np.asarray(b, np.float64)
+    if b.size == 0:
+        return 0.0
+    return float(np.sqrt(np.mean((np.asarray(a, np.float64) - b) ** 2)) / max(np.sqrt(np.mean(b ** 2)), 1e-30))
+
+
+@pytest.mark.parametrize('name', sorted(META))
+def test_oracle_matches_reference(name):
+    m = META[name]
+    d = np.load(os.path.join(GOLD, f'crn_{name}.npz'))
+    conf = dict(C.NET_CONF)
+    conf.update(m['overrides'])
+    w = C.make_weights(conf, m['version'], m['weight_seed'])
+    cap = {}
+    r = C.forward(w, conf, m['version'], d['mic'], d['far'], d['near'], d['echo'], capture=cap)
+    assert r['out_wav'].shape == d['out_wav'].shape == (256 * (m['n'] // 256),)
+    assert r['out_spec'].shape == d['out_spec'].shape == (514, m['n'] // 256 + 1)
+    assert rel(r['out_wav'], d['out_wav']) <= 1e-5
+    assert rel(r['out_spec'], d['out_spec']) <= 1e-5
+    assert rel(r['mask'], d['mask']) <= 1e-5
+    assert rel(r['near_spec'], d['near_spec']) <= 1e-5
+    if 'enc0' in d:
+        assert rel(cap['enc'][0], d['enc0']) <= 1e-5
+    if 'loss' in d:
+        assert abs(r['loss'] - float(d['loss'])) <= 1e-5 * abs(float(d['loss']))
+
+
+def test_param_shapes_cover_reference_names():
+    # the fixture weights name exactly the parameters / eval buffers the
+    # reference state_dict holds for these configs (make_crn_golden asserts the
+    # load was complete); spot-check the published sizes
+    n2 = sum(int(np.prod(s)) for k, s in C.param_shapes(C.NET_CONF, 2) if not k.split('.')[-1].startswith(('RM', 'RV')))
+    n1 = sum(int(np.prod(s)) for k, s in C.param_shapes(C.NET_CONF, 1) if not k.split('.')[-1].startswith('running'))
+    assert n2 == 34902237
+    assert n1 == 34885105
