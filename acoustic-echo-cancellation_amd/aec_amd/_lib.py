@@ -27,6 +27,19 @@ EXPORTS = ('aec_weights_count', 'aec_create', 'aec_set_weights', 'aec_set_erb', 
            'aec_erb_tables_check', 'aec_num_frames', 'aec_out_len', 'aec_last_error', 'aec_destroy')
 
 
+# every symbol include/aec_crn.h declares
+CRN_EXPORTS = ('aec_crn_param_count', 'aec_crn_create', 'aec_crn_set_params', 'aec_crn_process', 'aec_crn_stft',
+               'aec_crn_profile_enable', 'aec_crn_profile_read', 'aec_crn_last_error', 'aec_crn_destroy')
+
+
+class CrnConfig(ctypes.Structure):
+    """aec_crn_config (include/aec_crn.h)."""
+    _fields_ = [('version', ctypes.c_int32), ('n_layers', ctypes.c_int32),
+                ('conv_channels', ctypes.c_int32 * 9), ('hidden_dim', ctypes.c_int32),
+                ('rnn_layers', ctypes.c_int32), ('use_cbn', ctypes.c_int32),
+                ('masking_mode', ctypes.c_int32), ('dtype', ctypes.c_int32)]
+
+
 class AecConfig(ctypes.Structure):
     _fields_ = [('win_size', ctypes.c_int32), ('hop_size', ctypes.c_int32),
                 ('erb_bands', ctypes.c_int32), ('nlms_taps', ctypes.c_int32),
@@ -78,16 +91,35 @@ def load():
     lib.aec_last_error.restype = ctypes.c_char_p
     lib.aec_destroy.argtypes = [P]
     lib.aec_destroy.restype = None
+    # DCCRN (include/aec_crn.h)
+    lib.aec_crn_param_count.argtypes = [ctypes.POINTER(CrnConfig)]
+    lib.aec_crn_param_count.restype = ctypes.c_size_t
+    lib.aec_crn_create.argtypes = [ctypes.POINTER(CrnConfig), P, ctypes.c_size_t, ctypes.c_int32, ctypes.POINTER(P)]
+    lib.aec_crn_create.restype = ctypes.c_int
+    lib.aec_crn_set_params.argtypes = [P, P, ctypes.c_size_t]
+    lib.aec_crn_set_params.restype = ctypes.c_int
+    lib.aec_crn_process.argtypes = [P, P, P, P, ctypes.c_int32, ctypes.c_int64, P, ctypes.c_int64, P, P, P]
+    lib.aec_crn_process.restype = ctypes.c_int
+    lib.aec_crn_stft.argtypes = [P, P, P, ctypes.c_int32, ctypes.c_int64, P, P]
+    lib.aec_crn_stft.restype = ctypes.c_int
+    lib.aec_crn_profile_enable.argtypes = [P, ctypes.c_int32]
+    lib.aec_crn_profile_enable.restype = ctypes.c_int
+    lib.aec_crn_profile_read.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
+    lib.aec_crn_profile_read.restype = ctypes.c_int
+    lib.aec_crn_last_error.argtypes = [P]
+    lib.aec_crn_last_error.restype = ctypes.c_char_p
+    lib.aec_crn_destroy.argtypes = [P]
+    lib.aec_crn_destroy.restype = None
     _lib = lib
     return lib
 
 
-def check(status, handle=None, what=''):
+def check(status, handle=None, what='', crn=False):
     if status == AEC_OK:
         return
     msg = ''
     if handle is not None and _lib is not None:
-        m = _lib.aec_last_error(handle)
+        m = (_lib.aec_crn_last_error if crn else _lib.aec_last_error)(handle)
         msg = m.decode() if m else ''
     raise RuntimeError(f'{what} failed: {_STATUS.get(status, status)} {msg}'.strip())
 
@@ -160,6 +192,77 @@ class Handle:
         try:
             if getattr(self, 'h', None):
                 self.lib.aec_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+def crn_config(version, conf, dtype):
+    """aec_crn_config from a reference config dict (configs.net_conf, configs.py:29-46)."""
+    ch = list(conf['conv_channels'])
+    if len(ch) > 9:
+        raise NotImplementedError('at most 8 encoder layers')
+    c = CrnConfig()
+    c.version = int(version)
+    c.n_layers = len(ch) - 1
+    for i, v in enumerate(ch):
+        c.conv_channels[i] = int(v)
+    c.hidden_dim = int(conf.get('hidden_dim', 4))
+    c.rnn_layers = int(conf.get('rnn_layers', 1))
+    c.use_cbn = int(bool(conf.get('use_cbn', False)))
+    c.masking_mode = ord(conf.get('masking_mode', 'C')[0]) if version == 2 else ord('C')
+    c.dtype = {'f32': 0, 'float32': 0, 'bf16': 1, 'bfloat16': 1}[dtype]
+    return c
+
+
+def crn_param_count(version, conf, dtype='f32'):
+    cfg = crn_config(version, conf, dtype)
+    return int(load().aec_crn_param_count(ctypes.byref(cfg)))
+
+
+class CrnHandle:
+    """Owns one aec_crn_handle (include/aec_crn.h), one per device."""
+
+    def __init__(self, version, conf, dtype, device: int):
+        self.lib = load()
+        self.cfg = crn_config(version, conf, dtype)
+        h = ctypes.c_void_p()
+        check(self.lib.aec_crn_create(ctypes.byref(self.cfg), None, 0, int(device), ctypes.byref(h)), None,
+              'aec_crn_create (unsupported config?)')
+        self.h = h
+        self.device = device
+
+    def set_params(self, blob):
+        import numpy as np
+        blob = np.ascontiguousarray(blob, dtype=np.float32)
+        check(self.lib.aec_crn_set_params(self.h, blob.ctypes.data, blob.size), self.h, 'aec_crn_set_params', True)
+
+    def process(self, mic_ptr, far_ptr, lengths, B, ld, out_ptr, ld_out, spec_ptr, mask_ptr, stream):
+        import numpy as np
+        lens = np.ascontiguousarray(lengths, dtype=np.int64)
+        check(self.lib.aec_crn_process(self.h, mic_ptr, far_ptr, lens.ctypes.data, int(B), int(ld), out_ptr,
+                                       int(ld_out), spec_ptr, mask_ptr, stream), self.h, 'aec_crn_process', True)
+
+    def stft(self, x_ptr, lengths, B, ld, spec_ptr, stream):
+        import numpy as np
+        lens = np.ascontiguousarray(lengths, dtype=np.int64)
+        check(self.lib.aec_crn_stft(self.h, x_ptr, lens.ctypes.data, int(B), int(ld), spec_ptr, stream), self.h,
+              'aec_crn_stft', True)
+
+    def profile_enable(self, on: bool):
+        check(self.lib.aec_crn_profile_enable(self.h, int(bool(on))), self.h, 'aec_crn_profile_enable', True)
+
+    def profile_read(self):
+        """-> (ms [front, encoder, lstm, decoder, back] summed, calls)"""
+        ms = (ctypes.c_double * 5)()
+        calls = ctypes.c_int64()
+        check(self.lib.aec_crn_profile_read(self.h, ms, ctypes.byref(calls)), self.h, 'aec_crn_profile_read', True)
+        return list(ms), int(calls.value)
+
+    def __del__(self):
+        try:
+            if getattr(self, 'h', None):
+                self.lib.aec_crn_destroy(self.h)
                 self.h = None
         except Exception:
             pass

@@ -248,15 +248,9 @@ static aec_status fail(aec_handle* h, aec_status s, const std::string& m) {
     return s;
 }
 
-extern "C" {
-
-size_t aec_weights_count(int32_t erb_bands) { return erb_bands == 32 ? kWeights32 : 0; }
-int64_t aec_num_frames(int64_t n) { return n / 256 + 1; }
-int64_t aec_out_len(int64_t n) { return 256 * (n / 256); }
-
-const char* aec_last_error(const aec_handle* h) { return h ? h->err.c_str() : "null handle"; }
-
-static void build_tables(DevTables& t) {
+namespace aec {
+// STFT constant tables, float64 math rounded to float32 (aec_tables.h)
+void build_dev_tables(DevTables& t) {
     const double PI = 3.14159265358979323846;
     for (int k1 = 0; k1 < 16; ++k1)
         for (int lb = 0; lb < 16; ++lb) {
@@ -271,6 +265,16 @@ static void build_tables(DevTables& t) {
         t.inv_coff[r] = (float)(1.0 / (double)(c + 1e-8f));
     }
 }
+}  // namespace aec
+
+extern "C" {
+
+size_t aec_weights_count(int32_t erb_bands) { return erb_bands == 32 ? kWeights32 : 0; }
+int64_t aec_num_frames(int64_t n) { return n / 256 + 1; }
+int64_t aec_out_len(int64_t n) { return 256 * (n / 256); }
+
+const char* aec_last_error(const aec_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
 
 aec_status aec_set_weights(aec_handle* h, const float* w, size_t n) {
     if (!h) return AEC_ERR_INVALID_ARG;
@@ -334,7 +338,7 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
     if (hipMemset(h->d_w, 0, kWeights32 * sizeof(float)) != hipSuccess) return bail(AEC_ERR_HIP);
     if (hipMalloc(&h->d_tab, sizeof(DevTables)) != hipSuccess) return bail(AEC_ERR_OOM);
     DevTables tab;
-    build_tables(tab);
+    build_dev_tables(tab);
     if (hipMemcpy(h->d_tab, &tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess) return bail(AEC_ERR_HIP);
     if (weights && aec_set_weights(h, weights, n_weights) != AEC_OK) return bail(AEC_ERR_INVALID_ARG);
     if (erb) {

@@ -40,5 +40,6 @@ struct ErbTables {
 };
 
 ErbTables build_erb_tables(const float* erb /* [257][32] */);
+void build_dev_tables(DevTables& t);
 
 }  // namespace aec

@@ -1,0 +1,733 @@
+// crn_api.hip — the DCCRN C ABI (include/aec_crn.h) over crn_kernels.hip.
+//
+// Host side of the reference's DCCRN eval forward (Stage2_lhm/scripts/
+// network/dccrn.py:453-594, dccrn2.py:10-218): parses the state_dict-ordered
+// parameter blob, folds every eval-mode BatchNorm2d / ComplexBatchNorm into
+// its complex conv (float64), permutes weights into the kernels' layouts
+// (channels-last maps, decoder skip order, LSTM unit order and gate packing),
+// owns a grow-only workspace and sequences the launches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/aec_crn.h"
+#include "aec_tables.h"
+#include "crn_launch.h"
+
+using crn::bf16_t;
+
+namespace {
+
+int ilog2(int64_t v) {
+    int r = 0;
+    while ((1ll << r) < v) ++r;
+    return (1ll << r) == v ? r : -1;
+}
+
+uint16_t host_f2bf(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    if ((u & 0x7F800000u) == 0x7F800000u) return (uint16_t)(u >> 16) | ((u & 0xFFFF) ? 0x40 : 0);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+struct Cursor {
+    const float* p;
+    size_t n, off = 0;
+    bool ok = true;
+    const float* take(size_t k) {
+        if (off + k > n) {
+            ok = false;
+            return nullptr;
+        }
+        const float* r = p + off;
+        off += k;
+        return r;
+    }
+};
+
+// A packed GEMM weight operand (device) + bias
+struct Packed {
+    void* w = nullptr;          // [npad][kpad] elements of the compute type
+    float* bias = nullptr;      // [npad]
+    int npad = 0, kpad = 0, N = 0, K = 0;
+    float alpha = 0.f;
+    int act = 0;
+};
+
+}  // namespace
+
+struct aec_crn_handle {
+    aec_crn_config cfg{};
+    int device = 0;
+    std::string err;
+    int L = 6, D = 4, H = 0, S = 1, CELLS = 1, Q = 0, nrnn = 1;
+    size_t es = 4;                                 // element size
+    aec::DevTables* d_tab = nullptr;
+    std::vector<Packed> enc, dec;                  // dec: 2 per level (even, odd)
+    std::vector<Packed> lih, lhh;                  // per LSTM layer
+    bool have_params = false;
+    // workspace
+    int64_t ws_B = 0, ws_T = 0;
+    void* x0 = nullptr;
+    std::vector<void*> cat;                        // index 1..L
+    void* gx = nullptr;
+    void* y = nullptr;
+    void* xn = nullptr;
+    float* cst = nullptr;
+    float* mask = nullptr;
+    int64_t* d_len = nullptr;
+    std::vector<int64_t> last_lens;                // host copy of what d_len holds
+    std::vector<void*> allocs;
+    // profiling
+    int profile = 0;
+    std::vector<hipEvent_t> ev;
+    size_t ev_used = 0;
+    double ms[5] = {0, 0, 0, 0, 0};
+    int64_t calls = 0;
+};
+
+#define CRN_TRY(h, expr)                                                                 \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess) {                                                          \
+            (h)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                \
+            return e_ == hipErrorOutOfMemory ? AEC_ERR_OOM : AEC_ERR_HIP;                \
+        }                                                                                \
+    } while (0)
+
+static aec_status crn_fail(aec_crn_handle* h, aec_status s, const std::string& m) {
+    if (h) h->err = m;
+    return s;
+}
+
+// --------------------------------------------------------------------------
+// config validation + parameter layout
+// --------------------------------------------------------------------------
+static std::string check_cfg(const aec_crn_config& c) {
+    if (c.version != 1 && c.version != 2) return "version must be 1 (dccrn.py) or 2 (dccrn2.py)";
+    if (c.n_layers < 1 || c.n_layers > 8) return "n_layers out of range";
+    if (256 >> c.n_layers != 4) return "the LSTM width needs 256 >> n_layers == 4 (dccrn.py:514)";
+    if (c.conv_channels[0] != 4) return "conv_channels[0] must be 4 (mic/far real/imag)";
+    for (int i = 1; i <= c.n_layers; ++i)
+        if (c.conv_channels[i] < 8 || ilog2(c.conv_channels[i]) < 0) return "conv_channels must be powers of two >= 8";
+    if (c.dtype != 0 && c.dtype != 1) return "dtype must be 0 (f32) or 1 (bf16)";
+    if (c.version == 2) {
+        if (c.hidden_dim != 4) return "hidden_dim must equal the encoder output width (4)";
+        if (c.rnn_layers < 1 || c.rnn_layers > 8) return "rnn_layers out of range";
+        if (c.masking_mode != 'E' && c.masking_mode != 'C' && c.masking_mode != 'R') return "masking_mode must be E, C or R";
+    }
+    return "";
+}
+
+static size_t norm_count(const aec_crn_config& c, int ch) {
+    return (c.version == 2 && c.use_cbn) ? 10 * (size_t)(ch / 2) : 4 * (size_t)ch;
+}
+
+static size_t param_count(const aec_crn_config& c) {
+    if (!check_cfg(c).empty()) return 0;
+    const int* ch = c.conv_channels;
+    const int L = c.n_layers;
+    size_t n = 0;
+    for (int i = 0; i < L; ++i) {
+        const size_t co = ch[i + 1] / 2, ci = ch[i] / 2;
+        n += 2 * (co * ci * 5 + co) + norm_count(c, ch[i + 1]) + 1;
+    }
+    for (int cl = L; cl >= 1; --cl) {
+        const size_t ci = ch[cl], co = (cl != 1 ? ch[cl - 1] : 2) / 2;
+        n += 2 * (ci * co * 5 + co);
+        if (cl != 1)
+            n += norm_count(c, ch[cl - 1]) + 1;
+        else if (c.version == 1)
+            n += 4 * 2;
+    }
+    if (c.version == 1) {
+        const size_t H = (size_t)ch[L] * 4;
+        n += 2 * 4 * H * H + 2 * 4 * H;
+    } else {
+        const size_t H = (size_t)c.hidden_dim * ch[L] / 2;
+        n += (size_t)c.rnn_layers * 2 * (2 * 4 * H * H + 2 * 4 * H);
+    }
+    return n;
+}
+
+// --------------------------------------------------------------------------
+// folding: complex conv -> real [Co][Ci][5] (out x in, reference channel
+// order) + bias; then the eval norm as an affine map on the output channels
+// --------------------------------------------------------------------------
+struct RealConv {
+    int Co = 0, Ci = 0;
+    std::vector<double> w;   // [Co][Ci][5]
+    std::vector<double> b;   // [Co]
+    double& at(int o, int i, int k) { return w[((size_t)o * Ci + i) * 5 + k]; }
+};
+
+// ComplexConv2d (dccrn.py:140-153): weights [co'][ci'][5][1];
+// ComplexConvTranspose2d (dccrn.py:194-207): weights [ci'][co'][5][1].
+static RealConv complex_conv(Cursor& cur, int Ci, int Co, bool transposed) {
+    const int ci = Ci / 2, co = Co / 2;
+    const size_t nw = (size_t)ci * co * 5;
+    const float* wr = cur.take(nw);
+    const float* br = cur.take(co);
+    const float* wi = cur.take(nw);
+    const float* bi = cur.take(co);
+    RealConv r;
+    r.Co = Co;
+    r.Ci = Ci;
+    r.w.assign((size_t)Co * Ci * 5, 0.0);
+    r.b.assign(Co, 0.0);
+    if (!cur.ok) return r;
+    for (int o = 0; o < co; ++o)
+        for (int i = 0; i < ci; ++i)
+            for (int k = 0; k < 5; ++k) {
+                const size_t idx = transposed ? ((size_t)i * co + o) * 5 + k : ((size_t)o * ci + i) * 5 + k;
+                const double a = wr[idx], c = wi[idx];
+                r.at(o, i, k) = a;            // real <- real_conv(x_r)
+                r.at(o, ci + i, k) = -c;      //       - imag_conv(x_i)
+                r.at(co + o, i, k) = c;       // imag <- imag_conv(x_r)
+                r.at(co + o, ci + i, k) = a;  //       + real_conv(x_i)
+            }
+    for (int o = 0; o < co; ++o) {
+        r.b[o] = (double)br[o] - (double)bi[o];
+        r.b[co + o] = (double)bi[o] + (double)br[o];
+    }
+    return r;
+}
+
+// y = A z + c0 per output channel (pairs (o, co+o) for ComplexBatchNorm)
+static void fold_norm(Cursor& cur, RealConv& r, bool cbn) {
+    const int Co = r.Co;
+    const double eps = 1e-5;
+    std::vector<double> A((size_t)Co * Co, 0.0), c0(Co, 0.0);
+    if (cbn) {   // ComplexBatchNorm eval (dccrn.py:300-383)
+        const int c = Co / 2;
+        const float *Wrr = cur.take(c), *Wri = cur.take(c), *Wii = cur.take(c), *Br = cur.take(c), *Bi = cur.take(c);
+        const float *RMr = cur.take(c), *RMi = cur.take(c), *RVrr = cur.take(c), *RVri = cur.take(c),
+                    *RVii = cur.take(c);
+        if (!cur.ok) return;
+        for (int o = 0; o < c; ++o) {
+            const double Vrr = (double)RVrr[o] + eps, Vri = RVri[o], Vii = (double)RVii[o] + eps;
+            const double tau = Vrr + Vii;
+            const double s = std::sqrt(Vrr * Vii - Vri * Vri);
+            const double t = std::sqrt(tau + 2 * s);
+            const double rst = 1.0 / (s * t);
+            const double Urr = (s + Vii) * rst, Uii = (s + Vrr) * rst, Uri = -Vri * rst;
+            const double Zrr = Wrr[o] * Urr + Wri[o] * Uri;
+            const double Zri = Wrr[o] * Uri + Wri[o] * Uii;
+            const double Zir = Wri[o] * Urr + Wii[o] * Uri;
+            const double Zii = Wri[o] * Uri + Wii[o] * Uii;
+            A[(size_t)o * Co + o] = Zrr;
+            A[(size_t)o * Co + c + o] = Zri;
+            A[(size_t)(c + o) * Co + o] = Zir;
+            A[(size_t)(c + o) * Co + c + o] = Zii;
+            c0[o] = Br[o] - Zrr * RMr[o] - Zri * RMi[o];
+            c0[c + o] = Bi[o] - Zir * RMr[o] - Zii * RMi[o];
+        }
+    } else {     // BatchNorm2d eval
+        const float *w = cur.take(Co), *b = cur.take(Co), *rm = cur.take(Co), *rv = cur.take(Co);
+        if (!cur.ok) return;
+        for (int o = 0; o < Co; ++o) {
+            const double s = (double)w[o] / std::sqrt((double)rv[o] + eps);
+            A[(size_t)o * Co + o] = s;
+            c0[o] = (double)b[o] - s * rm[o];
+        }
+    }
+    RealConv f = r;
+    for (int o = 0; o < Co; ++o) {
+        for (size_t q = 0; q < (size_t)r.Ci * 5; ++q) {
+            double acc = 0;
+            for (int o2 = 0; o2 < Co; ++o2) {
+                const double a = A[(size_t)o * Co + o2];
+                if (a != 0.0) acc += a * r.w[(size_t)o2 * r.Ci * 5 + q];
+            }
+            f.w[(size_t)o * r.Ci * 5 + q] = acc;
+        }
+        double acc = c0[o];
+        for (int o2 = 0; o2 < Co; ++o2) acc += A[(size_t)o * Co + o2] * r.b[o2];
+        f.b[o] = acc;
+    }
+    r = f;
+}
+
+static aec_status upload_packed(aec_crn_handle* h, Packed& pk, const std::vector<double>& w,
+                                const std::vector<double>& b) {
+    const size_t n = (size_t)pk.npad * pk.kpad;
+    if (!pk.w) {
+        CRN_TRY(h, hipMalloc(&pk.w, n * h->es));
+        CRN_TRY(h, hipMalloc(&pk.bias, (size_t)pk.npad * sizeof(float)));
+    }
+    if (h->es == 4) {
+        std::vector<float> hw(n);
+        for (size_t i = 0; i < n; ++i) hw[i] = (float)w[i];
+        CRN_TRY(h, hipMemcpy(pk.w, hw.data(), n * 4, hipMemcpyHostToDevice));
+    } else {
+        std::vector<uint16_t> hw(n);
+        for (size_t i = 0; i < n; ++i) hw[i] = host_f2bf((float)w[i]);
+        CRN_TRY(h, hipMemcpy(pk.w, hw.data(), n * 2, hipMemcpyHostToDevice));
+    }
+    std::vector<float> hb(pk.npad, 0.f);
+    for (int i = 0; i < pk.N; ++i) hb[i] = (float)b[i];
+    CRN_TRY(h, hipMemcpy(pk.bias, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
+    return AEC_OK;
+}
+
+static int kpad_for(int K, size_t es) {
+    const int per = (int)(crn::kStageBytes / es);
+    return (K + per - 1) / per * per;
+}
+
+// encoder layer: Bt[co][tap*Cin_buf + q] = W[co][q][tap]  (q < real input channels)
+static aec_status pack_encoder(aec_crn_handle* h, Packed& pk, const RealConv& r, int cin_buf, float alpha) {
+    pk.N = r.Co;
+    pk.K = 5 * cin_buf;
+    pk.npad = (r.Co + crn::gemm_bn(r.Co) - 1) / crn::gemm_bn(r.Co) * crn::gemm_bn(r.Co);
+    pk.kpad = kpad_for(pk.K, h->es);
+    pk.alpha = alpha;
+    pk.act = 1;
+    std::vector<double> w((size_t)pk.npad * pk.kpad, 0.0);
+    for (int o = 0; o < r.Co; ++o)
+        for (int k = 0; k < 5; ++k)
+            for (int q = 0; q < std::min(cin_buf, r.Ci); ++q)
+                w[(size_t)o * pk.kpad + k * cin_buf + q] = r.w[((size_t)o * r.Ci + q) * 5 + k];
+    return upload_packed(h, pk, w, r.b);
+}
+
+// decoder level: input buffer channels [dec_r, dec_i, enc_r, enc_i] (C each
+// half-pair) vs the reference complex_cat order [dec_r, enc_r, dec_i, enc_i]
+// (dccrn.py:386-395); parity 0: taps (4, 2, 0) at bins (m-1, m, m+1),
+// parity 1: taps (3, 1) at (m, m+1).
+static aec_status pack_decoder(aec_crn_handle* h, Packed& pk, const RealConv& r, int parity, int act, float alpha) {
+    const int Cin = r.Ci, C = Cin / 2;
+    const int ntap = parity == 0 ? 3 : 2;
+    pk.N = r.Co;
+    pk.K = ntap * Cin;
+    const int bn = crn::gemm_bn(r.Co);
+    pk.npad = (r.Co + bn - 1) / bn * bn;
+    pk.kpad = kpad_for(pk.K, h->es);
+    pk.alpha = alpha;
+    pk.act = act;
+    auto ref = [&](int q) {
+        if (q < C / 2) return q;
+        if (q < C) return C + (q - C / 2);
+        if (q < 3 * C / 2) return C / 2 + (q - C);
+        return q;
+    };
+    std::vector<double> w((size_t)pk.npad * pk.kpad, 0.0);
+    for (int o = 0; o < r.Co; ++o)
+        for (int j = 0; j < ntap; ++j) {
+            const int tap = parity == 0 ? 4 - 2 * j : 3 - 2 * j;
+            for (int q = 0; q < Cin; ++q)
+                w[(size_t)o * pk.kpad + j * Cin + q] = r.w[((size_t)o * Cin + ref(q)) * 5 + tap];
+        }
+    return upload_packed(h, pk, w, r.b);
+}
+
+// LSTM cell(s): unit order u' = d*Q + c <-> reference u = c*D + d; gate
+// column p(q, u') = ((u'/16)*4 + q)*16 + u'%16 (i|f|g|o per 16 units)
+static aec_status pack_lstm(aec_crn_handle* h, Cursor& cur, Packed& ih, Packed& hh) {
+    const int H = h->H, D = h->D, Q = h->Q, C = h->CELLS;
+    const size_t G = (size_t)4 * H;
+    std::vector<double> wih((size_t)C * G * H), whh((size_t)C * G * H), bias((size_t)C * G);
+    auto perm = [&](int up) { return (up % Q) * D + up / Q; };
+    for (int cell = 0; cell < C; ++cell) {
+        const float* Wih = cur.take(G * H);
+        const float* Whh = cur.take(G * H);
+        const float* bih = cur.take(G);
+        const float* bhh = cur.take(G);
+        if (!cur.ok) return crn_fail(h, AEC_ERR_INVALID_ARG, "parameter blob too short");
+        for (int up = 0; up < H; ++up)
+            for (int q = 0; q < 4; ++q) {
+                const size_t p = (size_t)cell * G + ((size_t)(up / 16) * 4 + q) * 16 + up % 16;
+                const size_t src = (size_t)q * H + perm(up);
+                for (int kp = 0; kp < H; ++kp) {
+                    wih[p * H + kp] = Wih[src * H + perm(kp)];
+                    whh[p * H + kp] = Whh[src * H + perm(kp)];
+                }
+                bias[p] = (double)bih[src] + (double)bhh[src];
+            }
+    }
+    ih.N = hh.N = (int)(C * G);
+    ih.K = hh.K = H;
+    ih.npad = hh.npad = (int)(C * G);
+    ih.kpad = hh.kpad = H;
+    ih.act = 0;
+    aec_status s = upload_packed(h, ih, wih, bias);
+    if (s != AEC_OK) return s;
+    return upload_packed(h, hh, whh, bias);
+}
+
+static aec_status load_params(aec_crn_handle* h, const float* params, size_t n) {
+    const aec_crn_config& c = h->cfg;
+    if (n != param_count(c)) return crn_fail(h, AEC_ERR_INVALID_ARG, "parameter count mismatch");
+    Cursor cur{params, n};
+    const int* ch = c.conv_channels;
+    const int L = h->L;
+    const bool cbn = c.version == 2 && c.use_cbn;
+    for (int i = 0; i < L; ++i) {
+        RealConv r = complex_conv(cur, ch[i], ch[i + 1], false);
+        fold_norm(cur, r, cbn);
+        const float* a = cur.take(1);
+        if (!cur.ok) return crn_fail(h, AEC_ERR_INVALID_ARG, "parameter blob too short");
+        aec_status s = pack_encoder(h, h->enc[i], r, i == 0 ? 8 : ch[i], a[0]);
+        if (s != AEC_OK) return s;
+    }
+    for (int d = 0; d < L; ++d) {
+        const int cl = L - d;
+        const int co = cl != 1 ? ch[cl - 1] : 2;
+        RealConv r = complex_conv(cur, 2 * ch[cl], co, true);
+        int act = 0;
+        float alpha = 0.f;
+        if (cl != 1) {
+            fold_norm(cur, r, cbn);
+            const float* a = cur.take(1);
+            if (!cur.ok) return crn_fail(h, AEC_ERR_INVALID_ARG, "parameter blob too short");
+            act = 1;
+            alpha = a[0];
+        } else if (c.version == 1) {   // BatchNorm2d(2) + Tanh (dccrn.py:494-506)
+            fold_norm(cur, r, false);
+            act = 2;
+        }
+        if (!cur.ok) return crn_fail(h, AEC_ERR_INVALID_ARG, "parameter blob too short");
+        for (int par = 0; par < 2; ++par) {
+            aec_status s = pack_decoder(h, h->dec[2 * d + par], r, par, act, alpha);
+            if (s != AEC_OK) return s;
+        }
+    }
+    for (int l = 0; l < h->nrnn; ++l) {
+        aec_status s = pack_lstm(h, cur, h->lih[l], h->lhh[l]);
+        if (s != AEC_OK) return s;
+    }
+    if (!cur.ok || cur.off != n) return crn_fail(h, AEC_ERR_INVALID_ARG, "parameter blob layout mismatch");
+    h->have_params = true;
+    return AEC_OK;
+}
+
+static aec_status ensure_ws(aec_crn_handle* h, int64_t B, int64_t T) {
+    if (B <= h->ws_B && T <= h->ws_T) return AEC_OK;
+    for (void* p : h->allocs) (void)hipFree(p);
+    h->allocs.clear();
+    h->last_lens.clear();                          // d_len is reallocated below
+    const int64_t nB = std::max<int64_t>(B, h->ws_B), nT = std::max<int64_t>(T, h->ws_T);
+    const int64_t BT = nB * nT;
+    const size_t es = h->es;
+    auto alloc = [&](void** p, size_t bytes) {
+        hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 16));
+        if (e == hipSuccess) h->allocs.push_back(*p);
+        return e;
+    };
+    const int* ch = h->cfg.conv_channels;
+    CRN_TRY(h, alloc(&h->x0, (size_t)BT * 256 * 8 * es));
+    h->cat.assign(h->L + 1, nullptr);
+    for (int l = 1; l <= h->L; ++l) CRN_TRY(h, alloc(&h->cat[l], (size_t)BT * (256 >> l) * 2 * ch[l] * es));
+    CRN_TRY(h, alloc(&h->gx, (size_t)BT * h->S * h->CELLS * 4 * h->H * es));
+    CRN_TRY(h, alloc(&h->y, (size_t)BT * h->CELLS * h->S * h->H * es));
+    if (h->nrnn > 1) CRN_TRY(h, alloc(&h->xn, (size_t)BT * h->S * h->H * es));
+    CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->cst), (size_t)nB * h->CELLS * h->S * h->H * sizeof(float)));
+    CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->mask), (size_t)BT * 256 * 2 * sizeof(float)));
+    CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->d_len), (size_t)nB * sizeof(int64_t)));
+    h->ws_B = nB;
+    h->ws_T = nT;
+    return AEC_OK;
+}
+
+static void mark(aec_crn_handle* h, hipStream_t st) {
+    if (!h->profile) return;
+    if (h->ev_used == h->ev.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        h->ev.push_back(e);
+    }
+    (void)hipEventRecord(h->ev[h->ev_used++], st);
+}
+
+template <typename T>
+static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int32_t B, int64_t ld, int64_t Tmax,
+                      float* out, int64_t ld_out, float* spec, float* mask_out, hipStream_t st) {
+    using crn::RowEpi;
+    using crn::RowSrc;
+    const int* ch = h->cfg.conv_channels;
+    const int L = h->L;
+    const int64_t BT = (int64_t)B * Tmax;
+    mark(h, st);
+    // front: X0 [BT][256][8]
+    crn::FrontArgs fa{mic, far, ld, h->d_len, Tmax, h->d_tab, h->x0, nullptr};
+    CRN_TRY(h, crn::launch_front<T>(fa, B, st));
+    mark(h, st);
+    // encoder
+    for (int i = 0; i < L; ++i) {
+        const int Fin = 256 >> i, Fo = Fin / 2;
+        const int cin = i == 0 ? 8 : ch[i];
+        const int64_t ld_in = i == 0 ? 8 : 2 * ch[i];
+        const int64_t choff = i == 0 ? 0 : ch[i];
+        const Packed& pk = h->enc[i];
+        RowSrc a{};
+        a.src = i == 0 ? h->x0 : h->cat[i];
+        a.M = BT * Fo;
+        a.K = pk.K;
+        a.rshift = ilog2(Fo);
+        a.rs_hi = Fin * ld_in;
+        a.rs_lo = 2 * ld_in;
+        a.kshift = ilog2(cin);
+        a.ks = ld_in;
+        a.pmul = 2;
+        a.padd = -2;
+        a.plim = Fin;
+        a.base_off = choff - 2 * ld_in;
+        const int64_t ldo = 2 * ch[i + 1];
+        RowEpi e{h->cat[i + 1], a.M, pk.N, a.rshift, Fo * ldo, ldo, ch[i + 1], pk.bias, pk.alpha, pk.act};
+        CRN_TRY(h, (crn::launch_gemm_rows<T, T>(a, reinterpret_cast<const T*>(pk.w), pk.kpad,
+                                                 (int)(pk.kpad * sizeof(T) / crn::kStageBytes), e, pk.npad, st)));
+    }
+    mark(h, st);
+    // LSTM layers
+    const int H = h->H, S = h->S, C = h->CELLS, D = h->D, Q = h->Q;
+    for (int l = 0; l < h->nrnn; ++l) {
+        RowSrc a{};
+        int64_t ld_in, choff;
+        if (l == 0) {
+            a.src = h->cat[L];
+            ld_in = 2 * ch[L];
+            choff = ch[L];
+        } else {
+            a.src = h->xn;
+            ld_in = (int64_t)S * Q;
+            choff = 0;
+        }
+        a.M = BT * S;
+        a.K = H;
+        a.rshift = ilog2(S);
+        a.rs_hi = D * ld_in;
+        a.rs_lo = Q;
+        a.kshift = ilog2(Q);
+        a.ks = ld_in;
+        a.pmul = 0;
+        a.padd = 0;
+        a.plim = D;
+        a.base_off = choff;
+        const Packed& ih = h->lih[l];
+        RowEpi e{h->gx, a.M, ih.N, 0, (int64_t)C * 4 * H, 0, 0, ih.bias, 0.f, 0};
+        CRN_TRY(h, (crn::launch_gemm_rows<T, T>(a, reinterpret_cast<const T*>(ih.w), ih.kpad,
+                                                 (int)(ih.kpad * sizeof(T) / crn::kStageBytes), e, ih.npad, st)));
+        crn::StepArgs sa{h->lhh[l].w, h->gx, h->y, h->cst, B, H, Tmax, 0};
+        for (int64_t t = 0; t < Tmax; ++t) {
+            sa.t = (int)t;
+            CRN_TRY(h, crn::launch_lstm_step<T>(sa, C, S, st));
+        }
+        const bool last = l + 1 == h->nrnn;
+        T* dst = reinterpret_cast<T*>(last ? h->cat[L] : h->xn);
+        const int64_t ldd = last ? 2 * ch[L] : (int64_t)S * Q;
+        CRN_TRY(h, crn::launch_lstm_combine<T>(reinterpret_cast<const T*>(h->y), dst, BT, H, C, S, ilog2(Q),
+                                               D * ldd, ldd, st));
+    }
+    mark(h, st);
+    // decoder
+    for (int d = 0; d < L; ++d) {
+        const int cl = L - d;
+        const int Fin = 256 >> cl, Fo = 2 * Fin;
+        const int64_t ld_in = 2 * ch[cl];
+        for (int par = 0; par < 2; ++par) {
+            const Packed& pk = h->dec[2 * d + par];
+            RowSrc a{};
+            a.src = h->cat[cl];
+            a.M = BT * Fin;
+            a.K = pk.K;
+            a.rshift = ilog2(Fin);
+            a.rs_hi = Fin * ld_in;
+            a.rs_lo = ld_in;
+            a.kshift = ilog2(ld_in);
+            a.ks = ld_in;
+            a.pmul = 1;
+            a.padd = par == 0 ? -1 : 0;
+            a.plim = Fin;
+            a.base_off = a.padd * ld_in;
+            if (cl != 1) {
+                const int64_t ldo = 2 * ch[cl - 1];
+                RowEpi e{h->cat[cl - 1], a.M, pk.N, a.rshift, Fo * ldo, 2 * ldo, par * ldo, pk.bias, pk.alpha, pk.act};
+                CRN_TRY(h, (crn::launch_gemm_rows<T, T>(a, reinterpret_cast<const T*>(pk.w), pk.kpad,
+                                                         (int)(pk.kpad * sizeof(T) / crn::kStageBytes), e, pk.npad,
+                                                         st)));
+            } else {
+                RowEpi e{h->mask, a.M, pk.N, a.rshift, (int64_t)Fo * 2, 4, (int64_t)par * 2, pk.bias, pk.alpha, pk.act};
+                CRN_TRY(h, (crn::launch_gemm_rows<T, float>(a, reinterpret_cast<const T*>(pk.w), pk.kpad,
+                                                             (int)(pk.kpad * sizeof(T) / crn::kStageBytes), e,
+                                                             pk.npad, st)));
+            }
+        }
+    }
+    mark(h, st);
+    // back
+    const int mode = h->cfg.version == 1 ? 1 : (h->cfg.masking_mode == 'E' ? 0 : h->cfg.masking_mode == 'C' ? 1 : 2);
+    if (out || spec) {
+        crn::BackArgs ba{mic, ld, h->d_len, Tmax, h->d_tab, reinterpret_cast<const float2*>(h->mask), out, ld_out,
+                         reinterpret_cast<float2*>(spec)};
+        CRN_TRY(h, crn::launch_back(ba, B, mode, st));
+    }
+    if (mask_out)
+        CRN_TRY(h, hipMemcpyAsync(mask_out, h->mask, (size_t)BT * 256 * 2 * sizeof(float), hipMemcpyDeviceToDevice, st));
+    mark(h, st);
+    return AEC_OK;
+}
+
+extern "C" {
+
+size_t aec_crn_param_count(const aec_crn_config* cfg) { return cfg ? param_count(*cfg) : 0; }
+
+const char* aec_crn_last_error(const aec_crn_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+aec_status aec_crn_create(const aec_crn_config* cfg, const float* params, size_t n, int32_t device,
+                          aec_crn_handle** out) {
+    if (!cfg || !out) return AEC_ERR_INVALID_ARG;
+    *out = nullptr;
+    const std::string why = check_cfg(*cfg);
+    if (!why.empty()) return AEC_ERR_UNSUPPORTED;
+    aec_crn_handle* h = new (std::nothrow) aec_crn_handle();
+    if (!h) return AEC_ERR_OOM;
+    h->cfg = *cfg;
+    h->device = device;
+    h->L = cfg->n_layers;
+    h->D = 256 >> h->L;
+    h->es = cfg->dtype == 1 ? 2 : 4;
+    if (cfg->version == 1) {
+        h->H = cfg->conv_channels[h->L] * 4;
+        h->S = h->CELLS = 1;
+        h->nrnn = 1;
+    } else {
+        h->H = cfg->hidden_dim * cfg->conv_channels[h->L] / 2;
+        h->S = h->CELLS = 2;
+        h->nrnn = cfg->rnn_layers;
+    }
+    h->Q = h->H / h->D;
+    auto bail = [&](aec_status s) {
+        aec_crn_destroy(h);
+        return s;
+    };
+    if (h->H % 32 || ilog2(h->Q) < 0) return bail(AEC_ERR_UNSUPPORTED);
+    if (hipSetDevice(device) != hipSuccess) return bail(AEC_ERR_HIP);
+    if (hipMalloc(&h->d_tab, sizeof(aec::DevTables)) != hipSuccess) return bail(AEC_ERR_OOM);
+    aec::DevTables tab;
+    aec::build_dev_tables(tab);
+    if (hipMemcpy(h->d_tab, &tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess) return bail(AEC_ERR_HIP);
+    h->enc.assign(h->L, Packed{});
+    h->dec.assign(2 * h->L, Packed{});
+    h->lih.assign(h->nrnn, Packed{});
+    h->lhh.assign(h->nrnn, Packed{});
+    if (params) {
+        const aec_status s = load_params(h, params, n);
+        if (s != AEC_OK) return bail(s);
+    }
+    *out = h;
+    return AEC_OK;
+}
+
+aec_status aec_crn_set_params(aec_crn_handle* h, const float* params, size_t n) {
+    if (!h || !params) return AEC_ERR_INVALID_ARG;
+    if (hipSetDevice(h->device) != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
+    return load_params(h, params, n);
+}
+
+static aec_status prepare(aec_crn_handle* h, const int64_t* lengths, int32_t B, int64_t ld, int64_t* Tmax,
+                          hipStream_t st) {
+    if (!lengths || B <= 0 || ld <= 0) return crn_fail(h, AEC_ERR_INVALID_ARG, "bad lengths / B / ld");
+    int64_t mx = 0;
+    for (int b = 0; b < B; ++b) {
+        if (lengths[b] < 1 || lengths[b] > ld) return crn_fail(h, AEC_ERR_INVALID_ARG, "length out of [1, ld]");
+        mx = std::max(mx, lengths[b]);
+    }
+    if (mx >= (1ll << 31) / 4) return crn_fail(h, AEC_ERR_INVALID_ARG, "utterance too long");
+    *Tmax = mx / 256 + 1;
+    aec_status s = ensure_ws(h, B, *Tmax);
+    if (s != AEC_OK) return s;
+    // the lengths live in the handle (the copy's source outlives the async call);
+    // re-uploaded only when they change or the workspace was reallocated
+    if (h->last_lens.size() != (size_t)B ||
+        !std::equal(lengths, lengths + B, h->last_lens.begin())) {
+        h->last_lens.assign(lengths, lengths + B);
+        CRN_TRY(h, hipMemcpyAsync(h->d_len, h->last_lens.data(), (size_t)B * sizeof(int64_t), hipMemcpyHostToDevice,
+                                  st));
+    }
+    return AEC_OK;
+}
+
+aec_status aec_crn_process(aec_crn_handle* h, const float* mic, const float* far, const int64_t* lengths, int32_t B,
+                           int64_t ld, float* out, int64_t ld_out, float* spec, float* mask, void* stream) {
+    if (!h) return AEC_ERR_INVALID_ARG;
+    if (!h->have_params) return crn_fail(h, AEC_ERR_INVALID_ARG, "parameters not set");
+    if (!mic || !far) return crn_fail(h, AEC_ERR_INVALID_ARG, "null signal");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (hipSetDevice(h->device) != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
+    int64_t Tmax = 0;
+    aec_status s = prepare(h, lengths, B, ld, &Tmax, st);
+    if (s != AEC_OK) return s;
+    bool need_out = false;
+    for (int b = 0; b < B; ++b) need_out |= lengths[b] >= 256;
+    if (need_out && !out) return crn_fail(h, AEC_ERR_INVALID_ARG, "null out");
+    int64_t mx = 0;
+    for (int b = 0; b < B; ++b) mx = std::max(mx, 256 * (lengths[b] / 256));
+    if (out && ld_out < mx) return crn_fail(h, AEC_ERR_INVALID_ARG, "ld_out too small");
+    if (h->profile) h->ev_used = 0;
+    s = h->es == 4 ? run<float>(h, mic, far, B, ld, Tmax, out, ld_out, spec, mask, st)
+                   : run<bf16_t>(h, mic, far, B, ld, Tmax, out, ld_out, spec, mask, st);
+    if (s != AEC_OK) return s;
+    if (h->profile && h->ev_used == 6) {
+        CRN_TRY(h, hipEventSynchronize(h->ev[5]));
+        for (int k = 0; k < 5; ++k) {
+            float m = 0.f;
+            CRN_TRY(h, hipEventElapsedTime(&m, h->ev[k], h->ev[k + 1]));
+            h->ms[k] += m;
+        }
+        h->calls++;
+    }
+    return AEC_OK;
+}
+
+aec_status aec_crn_stft(aec_crn_handle* h, const float* x, const int64_t* lengths, int32_t B, int64_t ld, float* spec,
+                        void* stream) {
+    if (!h || !x || !spec) return AEC_ERR_INVALID_ARG;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (hipSetDevice(h->device) != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
+    int64_t Tmax = 0;
+    aec_status s = prepare(h, lengths, B, ld, &Tmax, st);
+    if (s != AEC_OK) return s;
+    crn::FrontArgs fa{x, x, ld, h->d_len, Tmax, h->d_tab, nullptr, reinterpret_cast<float2*>(spec)};
+    CRN_TRY(h, crn::launch_front<float>(fa, B, st));
+    return AEC_OK;
+}
+
+aec_status aec_crn_profile_enable(aec_crn_handle* h, int32_t enable) {
+    if (!h) return AEC_ERR_INVALID_ARG;
+    h->profile = enable != 0;
+    return AEC_OK;
+}
+
+aec_status aec_crn_profile_read(aec_crn_handle* h, double* ms5, int64_t* calls) {
+    if (!h || !ms5) return AEC_ERR_INVALID_ARG;
+    for (int k = 0; k < 5; ++k) {
+        ms5[k] = h->ms[k];
+        h->ms[k] = 0;
+    }
+    if (calls) *calls = h->calls;
+    h->calls = 0;
+    return AEC_OK;
+}
+
+void aec_crn_destroy(aec_crn_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    for (void* p : h->allocs) (void)hipFree(p);
+    for (auto* v : {&h->enc, &h->dec, &h->lih, &h->lhh})
+        for (Packed& pk : *v) {
+            if (pk.w) (void)hipFree(pk.w);
+            if (pk.bias) (void)hipFree(pk.bias);
+        }
+    if (h->d_tab) (void)hipFree(h->d_tab);
+    for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+    delete h;
+}
+
+}  // extern "C"

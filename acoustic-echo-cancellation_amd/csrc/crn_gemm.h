@@ -1,0 +1,169 @@
+// crn_gemm.h — MFMA building blocks of the DCCRN path (internal).
+//
+// Every dense block of the reference's complex CRN is a
+// GEMM whose operands are K-contiguous rows:
+//   encoder ComplexConv2d (k=(5,1), s=(2,1))   dccrn.py:103-153
+//   decoder ComplexConvTranspose2d (+skip)     dccrn.py:156-207, 386-395
+//   LSTM input projection                      dccrn.py:423-450 / :514
+//   LSTM recurrence W_hh h_{t-1}               (one launch per frame step)
+// The conv kernels have time extent 1, so a conv over the frequency axis is
+// an implicit GEMM over rows (frame, output bin) with k = (tap, in-channel)
+// on channels-last [frame][bin][channel] maps (no im2col buffer).
+//
+// Element type T is float (exact f32 MFMA, v_mfma_f32_16x16x4_f32) or
+// bf16 (v_mfma_f32_16x16x32_bf16, f32 accumulate).  Both read operand
+// fragments as one 16-byte chunk per lane: lane l holds row (l & 15) of a
+// 16-row fragment and the 16 bytes at byte offset 16 (l >> 4) of a 64-byte
+// k-chunk.  For bf16 that is exactly the 16x16x32 operand map (k = 8 (l>>4)
+// + j); for f32 the four elements feed four 16x16x4 steps with k = 4 (l>>4)
+// + j, the same permutation on A and B, so the sum over the chunk's 16 k is
+// unchanged.  Accumulator map (both): col = lane & 15, row = 4 (lane >> 4) + r.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace crn {
+
+typedef uint16_t bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T> struct Elem;
+template <> struct Elem<float> { static constexpr int kPer16 = 4; };
+template <> struct Elem<bf16_t> { static constexpr int kPer16 = 8; };
+
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+__device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float((uint32_t)h << 16); }
+
+template <typename T> __device__ __forceinline__ T to_elem(float v);
+template <> __device__ __forceinline__ float to_elem<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16_t to_elem<bf16_t>(float v) { return f2bf(v); }
+__device__ __forceinline__ float to_f32(float v) { return v; }
+__device__ __forceinline__ float to_f32(bf16_t v) { return bf2f(v); }
+
+// acc += A-chunk * B-chunk over one 64-byte k-chunk (see header)
+__device__ __forceinline__ void mma_chunk(f32x4& acc, const u32x4& a, const u32x4& b, bf16_t) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc,
+                                                 0, 0, 0);
+}
+__device__ __forceinline__ void mma_chunk(f32x4& acc, const u32x4& a, const u32x4& b, float) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[0]), __uint_as_float(b[0]), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[1]), __uint_as_float(b[1]), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[2]), __uint_as_float(b[2]), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[3]), __uint_as_float(b[3]), acc, 0, 0, 0);
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float tanhf_(float x) {
+    // tanh(x) = 1 - 2 / (exp(2x) + 1): saturates cleanly for |x| large
+    return 1.f - 2.f / (__expf(2.f * x) + 1.f);
+}
+
+constexpr int kStageBytes = 128;   // K bytes staged per main-loop step (two 64-B k-chunks)
+constexpr int kRowStride = 144;    // LDS bytes per staged row: 16 rows at one column hit 16 distinct 16-B bank slots
+
+// Implicit-GEMM row source shared by the conv, LSTM-input and dense loaders:
+//   row m -> (hi = m >> rshift, lo = m & (2^rshift - 1))
+//   k     -> (tap = k >> kshift, ci = k & (2^kshift - 1))
+//   element offset = hi*rs_hi + lo*rs_lo + tap*ks + ci + base_off
+//   valid iff m < M, k < K and 0 <= lo*pmul + tap + padd < plim  (zero otherwise:
+//   the conv's frequency padding and the K / M tails).
+struct RowSrc {
+    const void* src;
+    int64_t M;
+    int32_t K;
+    int32_t rshift;
+    int64_t rs_hi, rs_lo;
+    int32_t kshift;
+    int32_t pmul, padd, plim;
+    int64_t ks, base_off;
+};
+
+template <typename T>
+__device__ __forceinline__ u32x4 rowsrc_load(const RowSrc& a, int64_t m, int kbyte) {
+    constexpr int E = Elem<T>::kPer16;
+    const int k = kbyte / (int)sizeof(T);
+    const int64_t hi = m >> a.rshift;
+    const int lo = (int)(m & ((1ll << a.rshift) - 1));
+    const int tap = k >> a.kshift;
+    const int ci = k & ((1 << a.kshift) - 1);
+    const int pos = lo * a.pmul + tap + a.padd;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (m < a.M && k < a.K && pos >= 0 && pos < a.plim) {
+        const T* p = reinterpret_cast<const T*>(a.src) + hi * a.rs_hi + (int64_t)lo * a.rs_lo + (int64_t)tap * a.ks +
+                     ci + a.base_off;
+        v = *reinterpret_cast<const u32x4*>(p);
+    }
+    (void)E;
+    return v;
+}
+
+// Block-level main loop: acc[FM][FN] += A[wr0 + fm*16 + i][:] . B[wc0 + fn*16 + j][:]
+// over `nstages` stages of 128 K-bytes.  A / B rows are fetched through the
+// callables al(row, kbyte) / bl(row, kbyte) (block-relative rows) as 16-byte
+// chunks, staged global -> registers -> LDS with the next stage's loads in
+// flight during the current stage's MFMAs.  256 threads.
+template <typename T, int BM, int BN, int FM, int FN, class AL, class BL>
+__device__ __forceinline__ void gemm_core(f32x4 (&acc)[FM][FN], char* smem, const AL& al, const BL& bl, int nstages,
+                                          int wr0, int wc0) {
+    constexpr int NA = BM * 8, NB = BN * 8;                // 16-B chunks per stage
+    constexpr int CA = (NA + 255) / 256, CB = (NB + 255) / 256;
+    char* sA = smem;
+    char* sB = smem + BM * kRowStride;
+    const int tid = threadIdx.x, lane = tid & 63;
+    u32x4 ra[CA], rb[CB];
+    auto gload = [&](int st) {
+#pragma unroll
+        for (int i = 0; i < CA; ++i) {
+            const int c = tid + 256 * i;
+            if (NA % 256 == 0 || c < NA) ra[i] = al(c >> 3, st * kStageBytes + (c & 7) * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < CB; ++i) {
+            const int c = tid + 256 * i;
+            if (NB % 256 == 0 || c < NB) rb[i] = bl(c >> 3, st * kStageBytes + (c & 7) * 16);
+        }
+    };
+    auto sstore = [&]() {
+#pragma unroll
+        for (int i = 0; i < CA; ++i) {
+            const int c = tid + 256 * i;
+            if (NA % 256 == 0 || c < NA) *reinterpret_cast<u32x4*>(sA + (c >> 3) * kRowStride + (c & 7) * 16) = ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < CB; ++i) {
+            const int c = tid + 256 * i;
+            if (NB % 256 == 0 || c < NB) *reinterpret_cast<u32x4*>(sB + (c >> 3) * kRowStride + (c & 7) * 16) = rb[i];
+        }
+    };
+    gload(0);
+    sstore();
+    __syncthreads();
+    const int fr = lane & 15, fq = (lane >> 4) * 16;
+    for (int st = 0; st < nstages; ++st) {
+        const bool more = st + 1 < nstages;
+        if (more) gload(st + 1);
+#pragma unroll
+        for (int kc = 0; kc < 2; ++kc) {
+            u32x4 af[FM], bfr[FN];
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm)
+                af[fm] = *reinterpret_cast<const u32x4*>(sA + (wr0 + fm * 16 + fr) * kRowStride + kc * 64 + fq);
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn)
+                bfr[fn] = *reinterpret_cast<const u32x4*>(sB + (wc0 + fn * 16 + fr) * kRowStride + kc * 64 + fq);
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+                for (int fn = 0; fn < FN; ++fn) mma_chunk(acc[fm][fn], af[fm], bfr[fn], T{});
+        }
+        if (more) {
+            __syncthreads();
+            sstore();
+            __syncthreads();
+        }
+    }
+}
+
+}  // namespace crn

@@ -1,0 +1,497 @@
+// crn_kernels.hip — gfx950 kernels of the DCCRN (complex CRN) post-filter.
+//
+// Reference: Stage2_lhm/scripts/network/dccrn.py:453-594 (DCCRN v1) and
+// Stage2_lhm/scripts/network/dccrn2.py:10-218 (DCCRN v2), eval mode
+// (SURVEY.md §8 a14).  Per batch of B utterances (Tmax frames each):
+//
+//   crn_front_kernel     mic / far -> windowed rFFT-512 -> X0 [B*Tmax][256][8]
+//   gemm_rows_kernel x6  encoder ComplexConv2d + folded (Complex)BatchNorm + PReLU
+//   gemm_rows_kernel     LSTM input projection for every frame (hoisted)
+//   lstm_step_kernel xT  one frame of the recurrence, cell update fused
+//   lstm_combine_kernel  NavieComplexLSTM real/imag combination + reshape
+//   gemm_rows_kernel x12 decoder ComplexConvTranspose2d (even / odd output bins)
+//   crn_back_kernel      mask (E / C / R) on the mic spectrum -> irFFT + WOLA
+//
+// Feature maps are channels-last [frame][bin][channel] in the element type T
+// (float or bf16); the host (crn_api.hip) folds every BatchNorm into the conv
+// weights and permutes the weight rows / columns to the layouts used here.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "aec_fft.h"
+#include "aec_stft.h"
+#include "aec_tables.h"
+#include "crn_gemm.h"
+#include "crn_launch.h"
+
+namespace crn {
+
+using aec::kGroupFloats;
+using aec::kHop;
+using aec::kWaveFloats;
+using aec::kWaveFrames;
+using aec::kWavePf;
+
+// --------------------------------------------------------------------------
+// Front: 16 frames per block (4 waves x 4 frames, one 16-lane group per frame)
+// --------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void put_bin(T* row, int k, float2 m, float2 f);
+template <>
+__device__ __forceinline__ void put_bin<float>(float* row, int k, float2 m, float2 f) {
+    float4* p = reinterpret_cast<float4*>(row + (int64_t)(k - 1) * 8);
+    p[0] = make_float4(m.x, f.x, m.y, f.y);
+    p[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+template <>
+__device__ __forceinline__ void put_bin<bf16_t>(bf16_t* row, int k, float2 m, float2 f) {
+    u32x4 v;
+    v[0] = (uint32_t)f2bf(m.x) | ((uint32_t)f2bf(f.x) << 16);
+    v[1] = (uint32_t)f2bf(m.y) | ((uint32_t)f2bf(f.y) << 16);
+    v[2] = 0u;
+    v[3] = 0u;
+    *reinterpret_cast<u32x4*>(row + (int64_t)(k - 1) * 8) = v;
+}
+
+template <typename T, bool kSpec>
+__global__ __launch_bounds__(256) void crn_front_kernel(FrontArgs p) {
+    __shared__ __attribute__((aligned(16))) float smem[256 * 2 + 258 * 2 + 512 + 4 * kWaveFloats];
+    float2* sTwT = reinterpret_cast<float2*>(smem);
+    float2* sTw512 = sTwT + 256;
+    float* sHann = reinterpret_cast<float*>(sTw512 + 258);
+    float* sWave = sHann + 512;
+    const int tid = threadIdx.x;
+    sTwT[tid] = p.tab->twT[tid];
+    sTw512[tid] = p.tab->tw512[tid];
+    if (tid < 2) sTw512[256 + tid] = p.tab->tw512[256 + tid];
+    sHann[tid] = p.tab->hann[tid];
+    sHann[tid + 256] = p.tab->hann[tid + 256];
+    __syncthreads();
+
+    const int b = blockIdx.y;
+    const int wave = tid >> 6, lane = tid & 63, gg = lane >> 4, lb = lane & 15;
+    const int t0 = blockIdx.x * 16 + wave * kWaveFrames;
+    const int64_t t = t0 + gg;
+    const int n = (int)p.lens[b];
+    const int64_t Tn = n / kHop + 1;
+    float* wr = sWave + wave * kWaveFloats;
+    float* scr = wr + gg * kGroupFloats;
+    const bool aligned = ((p.ld & 3) == 0) && ((reinterpret_cast<uintptr_t>(p.mic) & 15) == 0) &&
+                         ((reinterpret_cast<uintptr_t>(p.far) & 15) == 0);
+
+    float2 ma[8], mb[8], m128;
+    float2 fa[8], fb[8], f128;
+#pragma unroll
+    for (int s = 0; s < (kSpec ? 1 : 2); ++s) {
+        const float* row = (s == 0 ? p.mic : p.far) + (int64_t)b * p.ld;
+        float4 pf[kWavePf];
+        aec::wave_prefetch(pf, row, n, t0, lane, aligned);
+        aec::wave_fence();
+        aec::wave_commit(wr, pf, 0.f, n, t0, lane);
+        aec::wave_fence();
+        float2 v[16];
+        aec::load_frame(v, wr, sHann, gg, lb);
+        aec::wave_fence();
+        aec::fft256<false>(v, lb, scr, sTwT);
+        if (s == 0)
+            aec::rfft_unpack(v, lb, sTw512, ma, mb, m128);
+        else
+            aec::rfft_unpack(v, lb, sTw512, fa, fb, f128);
+        aec::wave_fence();
+    }
+    if (t >= p.Tmax) return;
+    const bool live = t < Tn;
+    const float2 z = make_float2(0.f, 0.f);
+    if (kSpec) {   // complex spectrum [B][Tmax][257] of `mic` (ConvSTFT output, dccrn.py:45-52)
+        float2* srow = p.spec + ((int64_t)b * p.Tmax + t) * 257;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const int k = lb + 16 * m;
+            srow[k] = live ? ma[m] : z;
+            srow[256 - k] = live ? mb[m] : z;
+        }
+        if (lb == 0) srow[128] = live ? m128 : z;
+        return;
+    }
+    T* row = reinterpret_cast<T*>(p.x0) + ((int64_t)b * p.Tmax + t) * 256 * 8;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const int k = lb + 16 * m;
+        if (k != 0) put_bin<T>(row, k, live ? ma[m] : z, live ? fa[m] : z);
+        put_bin<T>(row, 256 - k, live ? mb[m] : z, live ? fb[m] : z);
+    }
+    if (lb == 0) put_bin<T>(row, 128, live ? m128 : z, live ? f128 : z);
+}
+
+// --------------------------------------------------------------------------
+// Back: one block per (stream, 15 output hops); re-derives the 16 frames'
+// mic spectra, applies the decoder's mask, inverse-transforms and
+// overlap-adds (structure of the Little_net synthesis kernel, aec_kernels.hip)
+// --------------------------------------------------------------------------
+template <int MODE>
+__device__ __forceinline__ float2 apply_mask(float2 x, float2 mk) {
+    if (MODE == 0) {   // 'E' (dccrn2.py:194-208): tanh(|M|) |X|_1e-8 * exp(i (arg X + arg M))
+        const float mags = sqrtf(x.x * x.x + x.y * x.y + 1e-8f);
+        const float ax = sqrtf(x.x * x.x + x.y * x.y);
+        const float am = sqrtf(mk.x * mk.x + mk.y * mk.y);
+        // atan2(0, 0) = 0 -> unit vector (1, 0)
+        const float cx = ax > 0.f ? x.x / ax : 1.f, sx = ax > 0.f ? x.y / ax : 0.f;
+        const float cm = am > 0.f ? mk.x / am : 1.f, sm = am > 0.f ? mk.y / am : 0.f;
+        const float e = tanhf(am) * mags;
+        return make_float2(e * (cx * cm - sx * sm), e * (sx * cm + cx * sm));
+    } else if (MODE == 1) {   // 'C' (dccrn.py:575, dccrn2.py:209)
+        return make_float2(x.x * mk.x - x.y * mk.y, x.x * mk.y + x.y * mk.x);
+    } else {                  // 'R' (dccrn2.py:210-211)
+        return make_float2(x.x * mk.x, x.y * mk.y);
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void crn_back_kernel(BackArgs p) {
+    __shared__ __attribute__((aligned(16))) float smem[258 * 2 + 256 * 2 + 512 + 256 + 4 * kWaveFloats];
+    float2* sTw512 = reinterpret_cast<float2*>(smem);
+    float2* sTwT = sTw512 + 258;
+    float* sHann = reinterpret_cast<float*>(sTwT + 256);
+    float* sCoff = sHann + 512;
+    float* sWave = sCoff + 256;
+    const int tid = threadIdx.x;
+    const int b = blockIdx.y;
+    const int64_t n = p.lens[b];
+    const int64_t nhop = n / kHop;                  // T - 1 output hops
+    const int64_t h0 = (int64_t)blockIdx.x * 15;
+    if (h0 > 0 && h0 >= nhop) return;               // block-uniform
+    sTwT[tid] = p.tab->twT[tid];
+    sTw512[tid] = p.tab->tw512[tid];
+    if (tid < 2) sTw512[256 + tid] = p.tab->tw512[256 + tid];
+    sHann[tid] = p.tab->hann[tid];
+    sHann[tid + 256] = p.tab->hann[tid + 256];
+    sCoff[tid] = p.tab->inv_coff[tid];
+    __syncthreads();
+
+    const int wave = tid >> 6, lane = tid & 63, gg = lane >> 4, lb = lane & 15;
+    const int g = tid >> 4;                         // frame h0 + g
+    float* wr = sWave + wave * kWaveFloats;
+    float* scr = wr + gg * kGroupFloats;
+    const bool aligned = ((p.ld & 3) == 0) && ((reinterpret_cast<uintptr_t>(p.mic) & 15) == 0);
+    const int tw0 = (int)(h0 + kWaveFrames * wave);
+    float4 pf[kWavePf];
+    aec::wave_prefetch(pf, p.mic + (int64_t)b * p.ld, (int)n, tw0, lane, aligned);
+    aec::wave_fence();
+    aec::wave_commit(wr, pf, 0.f, (int)n, tw0, lane);
+    aec::wave_fence();
+    float2 v[16];
+    float2 xa[8], xb[8], x128;
+    aec::load_frame(v, wr, sHann, gg, lb);
+    aec::wave_fence();
+    aec::fft256<false>(v, lb, scr, sTwT);
+    aec::rfft_unpack(v, lb, sTw512, xa, xb, x128);
+
+    // mask row of frame t (bins 1..256 -> index bin-1); DC has mask 0 (F.pad, dccrn.py:577-578)
+    const int64_t t = h0 + g;
+    const bool live = t <= nhop && t < p.Tmax;
+    const float2* mrow = p.mask + ((int64_t)b * p.Tmax + (live ? t : 0)) * 256;
+    const float2 z = make_float2(0.f, 0.f);
+    auto mk = [&](int bin) { return (live && bin > 0) ? mrow[bin - 1] : z; };
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const int kk = lb + 16 * m;
+        xa[m] = apply_mask<MODE>(xa[m], mk(kk));
+        xb[m] = apply_mask<MODE>(xb[m], mk(256 - kk));
+    }
+    x128 = apply_mask<MODE>(x128, mk(128));
+    if (p.spec && live) {
+        float2* srow = p.spec + ((int64_t)b * p.Tmax + t) * 257;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const int kk = lb + 16 * m;
+            srow[kk] = xa[m];
+            srow[256 - kk] = xb[m];
+        }
+        if (lb == 0) srow[128] = x128;
+    }
+
+    // inverse pack (as in aec_kernels.hip K4, with the masked spectrum as S)
+    float2 Zk[8], Zmk[8];
+    aec::static_for<0, 8>([&](auto mi) {
+        constexpr int m = decltype(mi)::value;
+        const int kk = lb + 16 * m;
+        float2 zk, zmk;
+        aec::irfft_pair(xa[m], xb[m], sTw512[kk], zk, zmk);
+        const float s0 = xa[m].x, s256 = xb[m].x;
+        Zk[m] = aec::csel(kk == 0, make_float2(s0 + s256, s0 - s256), zk);
+        Zmk[m] = aec::csel(kk == 0, Zk[m], zmk);
+    });
+    float2 z128 = make_float2(0.f, 0.f);
+    if (lb == 0) z128 = make_float2(2.f * x128.x, -2.f * x128.y);   // 2*conj(S[128])
+#pragma unroll
+    for (int a = 0; a < 8; ++a) v[a] = Zk[a];
+    aec::static_for<8, 16>([&](auto ai) {
+        constexpr int a = decltype(ai)::value;
+        const float2 mir = aec::mirror16(Zmk[15 - a]);
+        v[a] = aec::csel(lb != 0, mir, a == 8 ? z128 : Zmk[(16 - a) & 7]);
+    });
+    aec::wave_fence();
+    aec::fft256<true>(v, lb, scr, sTwT);
+    float2* s2 = reinterpret_cast<float2*>(scr);
+    const float2* h2 = reinterpret_cast<const float2*>(sHann);
+#pragma unroll
+    for (int m2 = 0; m2 < 16; ++m2) {
+        const float2 zz = v[aec::kP(m2)];
+        const float2 w = h2[lb + 16 * m2];
+        s2[lb + 16 * m2] = make_float2(zz.x * (w.x * (1.f / 512.f)), zz.y * (w.y * (1.f / 512.f)));
+    }
+    __syncthreads();
+    // overlap-add + WOLA normalisation + trim (dccrn.py:92-100); no +1e-9 here (ERB.py only)
+    float* orow = p.out + (int64_t)b * p.ld_out;
+    const int nh = (int)min((int64_t)15, nhop - h0);
+    for (int e = tid; e < nh * kHop; e += 256) {
+        const int i = e >> 8, r = e & 255;
+        const float a = sWave[i * kGroupFloats + 256 + r];
+        const float c = sWave[(i + 1) * kGroupFloats + r];
+        orow[(h0 + i) * kHop + r] = (a + c) * sCoff[r];
+    }
+}
+
+// --------------------------------------------------------------------------
+// Row GEMM (encoder / decoder convs, LSTM input projection)
+// --------------------------------------------------------------------------
+template <typename OutT>
+__device__ __forceinline__ void store_out(void* out, int64_t idx, float v) {
+    reinterpret_cast<OutT*>(out)[idx] = to_elem<OutT>(v);
+}
+
+template <typename T, typename OutT, int WM, int WN, int FM, int FN>
+__global__ __launch_bounds__(256) void gemm_rows_kernel(RowSrc a, const T* __restrict__ bt, int64_t ldb, int nstages,
+                                                         RowEpi e) {
+    constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
+    __shared__ __attribute__((aligned(16))) char smem[(BM + BN) * kRowStride];
+    const int64_t m0 = (int64_t)blockIdx.x * BM;
+    const int n0 = blockIdx.y * BN;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wr0 = (wave / WN) * FM * 16, wc0 = (wave % WN) * FN * 16;
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* bbase = reinterpret_cast<const char*>(bt + (int64_t)n0 * ldb);
+    auto al = [&](int r, int kb) { return rowsrc_load<T>(a, m0 + r, kb); };
+    auto bl = [&](int r, int kb) {
+        return *reinterpret_cast<const u32x4*>(bbase + (int64_t)r * ldb * (int64_t)sizeof(T) + kb);
+    };
+    gemm_core<T, BM, BN, FM, FN>(acc, smem, al, bl, nstages, wr0, wc0);
+
+    const int64_t omask = (1ll << e.oshift) - 1;
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t m = m0 + wr0 + fm * 16 + 4 * (lane >> 4) + r;
+            if (m >= e.M) continue;
+            const int64_t ob = (m >> e.oshift) * e.o_hi + (m & omask) * e.o_lo + e.o_add;
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) {
+                const int n = n0 + wc0 + fn * 16 + (lane & 15);
+                if (n >= e.N) continue;
+                float v = acc[fm][fn][r] + e.bias[n];
+                if (e.act == 1)
+                    v = v >= 0.f ? v : e.alpha * v;
+                else if (e.act == 2)
+                    v = tanhf(v);
+                store_out<OutT>(e.out, ob + n, v);
+            }
+        }
+}
+
+template <typename T, typename OutT>
+hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstages, const RowEpi& e, int npad,
+                            hipStream_t st) {
+    if (a.M <= 0) return hipSuccess;
+    const int bn = gemm_bn(e.N);
+    if (npad % bn) return hipErrorInvalidValue;
+#define CRN_GEMM(WM, WN, FM, FN)                                                                              \
+    do {                                                                                                      \
+        constexpr int BM = WM * FM * 16;                                                                      \
+        dim3 grid((unsigned)((a.M + BM - 1) / BM), (unsigned)(npad / (WN * FN * 16)));                        \
+        hipLaunchKernelGGL((gemm_rows_kernel<T, OutT, WM, WN, FM, FN>), grid, dim3(256), 0, st, a, bt, ldb,  \
+                           nstages, e);                                                                       \
+    } while (0)
+    switch (bn) {
+        case 16: CRN_GEMM(4, 1, 4, 1); break;
+        case 32: CRN_GEMM(2, 2, 4, 1); break;
+        case 64: CRN_GEMM(2, 2, 4, 2); break;
+        default: CRN_GEMM(2, 2, 4, 4); break;
+    }
+#undef CRN_GEMM
+    return hipGetLastError();
+}
+
+template hipError_t launch_gemm_rows<float, float>(const RowSrc&, const float*, int64_t, int, const RowEpi&, int,
+                                                   hipStream_t);
+template hipError_t launch_gemm_rows<bf16_t, bf16_t>(const RowSrc&, const bf16_t*, int64_t, int, const RowEpi&, int,
+                                                     hipStream_t);
+template hipError_t launch_gemm_rows<bf16_t, float>(const RowSrc&, const bf16_t*, int64_t, int, const RowEpi&, int,
+                                                    hipStream_t);
+
+// --------------------------------------------------------------------------
+// LSTM frame step.  Block = (32 units) x (SB streams); rows of the A tile are
+// h_{t-1} of every (cell, sequence, stream), the B tile the cells' W_hh rows
+// of those units (4 gates x 32 units per cell, packed i|f|g|o per 16 units).
+// Each wave owns 16 units x 4 gates of one cell, so the gate quadruple of a
+// (row, unit) lands in one lane: the cell update is fused.
+// --------------------------------------------------------------------------
+template <typename T, int CELLS, int S>
+__global__ __launch_bounds__(256) void lstm_step_kernel(StepArgs p) {
+    constexpr bool V2 = CELLS * S == 4;
+    constexpr int SB = V2 ? 32 : 64;
+    constexpr int U = 32;
+    constexpr int BM = SB * CELLS * S;
+    constexpr int BN = CELLS * 4 * U;
+    constexpr int FM = V2 ? 4 : 2, FN = 4;
+    __shared__ __attribute__((aligned(16))) char smem[(BM + BN) * kRowStride];
+    const int H = p.H;
+    const int unit0 = blockIdx.x * U, b0 = blockIdx.y * SB;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int cell = V2 ? (wave >> 1) : 0, uh = wave & 1;
+    const int wr0 = V2 ? cell * 64 : (wave >> 1) * 32;
+    const int wc0 = V2 ? cell * 128 + uh * 64 : uh * 64;
+    const int t = p.t;
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const T* Y = reinterpret_cast<const T*>(p.y);
+    if (t > 0) {
+        auto al = [&](int r, int kb) {
+            const int cr = V2 ? r >> 6 : 0, sr = V2 ? (r >> 5) & 1 : 0, bl = V2 ? r & 31 : r;
+            const int b = b0 + bl;
+            u32x4 v = {0u, 0u, 0u, 0u};
+            if (b < p.B) {
+                const T* row = Y + ((((int64_t)b * p.Tmax + t - 1) * CELLS + cr) * S + sr) * H;
+                v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(row) + kb);
+            }
+            return v;
+        };
+        const T* W = reinterpret_cast<const T*>(p.whh);
+        auto bl = [&](int c, int kb) {
+            const int cc = c / (4 * U), pl = c % (4 * U);
+            const T* row = W + ((int64_t)cc * 4 * H + (int64_t)unit0 * 4 + pl) * H;
+            return *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(row) + kb);
+        };
+        gemm_core<T, BM, BN, FM, FN>(acc, smem, al, bl, H * (int)sizeof(T) / kStageBytes, wr0, wc0);
+    }
+    const T* Gx = reinterpret_cast<const T*>(p.gx);
+    T* Yo = reinterpret_cast<T*>(p.y);
+    const int j = unit0 + uh * 16 + (lane & 15);
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int rloc = fm * 16 + 4 * (lane >> 4) + rr;     // within the wave's rows
+            const int s = V2 ? (rloc >> 5) : 0;
+            const int bl = V2 ? (rloc & 31) : (wr0 + rloc);
+            const int b = b0 + bl;
+            if (b >= p.B) continue;
+            const int64_t gb = (((int64_t)b * p.Tmax + t) * S + s) * (int64_t)(CELLS * 4 * H) + (int64_t)cell * 4 * H +
+                               (int64_t)(j >> 4) * 64 + (j & 15);
+            const float gi = acc[fm][0][rr] + to_f32(Gx[gb + 0]);
+            const float gf = acc[fm][1][rr] + to_f32(Gx[gb + 16]);
+            const float gg = acc[fm][2][rr] + to_f32(Gx[gb + 32]);
+            const float go = acc[fm][3][rr] + to_f32(Gx[gb + 48]);
+            const int64_t ci = (((int64_t)b * CELLS + cell) * S + s) * H + j;
+            const float cp = t > 0 ? p.cst[ci] : 0.f;
+            const float c = sigmoidf_(gf) * cp + sigmoidf_(gi) * tanhf(gg);
+            const float h = sigmoidf_(go) * tanhf(c);
+            p.cst[ci] = c;
+            Yo[((((int64_t)b * p.Tmax + t) * CELLS + cell) * S + s) * H + j] = to_elem<T>(h);
+        }
+}
+
+template <typename T>
+hipError_t launch_lstm_step(const StepArgs& a, int cells, int seqs, hipStream_t st) {
+    if (a.H % 32 || (a.H * (int)sizeof(T)) % kStageBytes) return hipErrorInvalidValue;
+    if (cells == 2 && seqs == 2) {
+        hipLaunchKernelGGL((lstm_step_kernel<T, 2, 2>), dim3(a.H / 32, (a.B + 31) / 32), dim3(256), 0, st, a);
+    } else if (cells == 1 && seqs == 1) {
+        hipLaunchKernelGGL((lstm_step_kernel<T, 1, 1>), dim3(a.H / 32, (a.B + 63) / 64), dim3(256), 0, st, a);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+template hipError_t launch_lstm_step<float>(const StepArgs&, int, int, hipStream_t);
+template hipError_t launch_lstm_step<bf16_t>(const StepArgs&, int, int, hipStream_t);
+
+// --------------------------------------------------------------------------
+// NavieComplexLSTM output (dccrn.py:443-446): real = rr - ii, imag = ir + ri
+// (v2), or the plain h (v1), written to dst[f*ldf + (j >> dshift)*ldd +
+// s*2^dshift + (j & mask)] — the [frame][d][s, c] map the next layer / the
+// decoder reads (dccrn2.py:153-157, dccrn.py:572-573).
+// --------------------------------------------------------------------------
+template <typename T, int CELLS, int S>
+__global__ __launch_bounds__(256) void lstm_combine_kernel(const T* __restrict__ y, T* __restrict__ dst,
+                                                           int64_t nframes, int H, int dshift, int64_t ldf,
+                                                           int64_t ldd) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;    // (frame, j)
+    if (idx >= nframes * H) return;
+    const int64_t f = idx / H;
+    const int j = (int)(idx - f * H);
+    const T* row = y + f * (CELLS * S) * (int64_t)H + j;
+    const int64_t o = f * ldf + (int64_t)(j >> dshift) * ldd + (j & ((1 << dshift) - 1));
+    if (CELLS * S == 4) {   // rows (cell, s): 0 = R(x_r), 1 = R(x_i), 2 = I(x_r), 3 = I(x_i)
+        const float rr = to_f32(row[0]), ri = to_f32(row[H]), ir = to_f32(row[2 * H]), ii = to_f32(row[3 * H]);
+        dst[o] = to_elem<T>(rr - ii);
+        dst[o + (1 << dshift)] = to_elem<T>(ri + ir);
+    } else {
+        dst[o] = row[0];
+    }
+}
+
+template <typename T>
+hipError_t launch_lstm_combine(const T* y, T* dst, int64_t nframes, int H, int cells, int seqs, int dshift,
+                               int64_t ldf, int64_t ldd, hipStream_t st) {
+    const int64_t n = nframes * H;
+    if (n <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + 255) / 256));
+    if (cells == 2 && seqs == 2)
+        hipLaunchKernelGGL((lstm_combine_kernel<T, 2, 2>), grid, dim3(256), 0, st, y, dst, nframes, H, dshift, ldf,
+                           ldd);
+    else
+        hipLaunchKernelGGL((lstm_combine_kernel<T, 1, 1>), grid, dim3(256), 0, st, y, dst, nframes, H, dshift, ldf,
+                           ldd);
+    return hipGetLastError();
+}
+template hipError_t launch_lstm_combine<float>(const float*, float*, int64_t, int, int, int, int, int64_t, int64_t,
+                                               hipStream_t);
+template hipError_t launch_lstm_combine<bf16_t>(const bf16_t*, bf16_t*, int64_t, int, int, int, int, int64_t,
+                                                int64_t, hipStream_t);
+
+// --------------------------------------------------------------------------
+template <typename T>
+hipError_t launch_front(const FrontArgs& a, int B, hipStream_t st) {
+    if (B <= 0 || a.Tmax <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((a.Tmax + 15) / 16), (unsigned)B);
+    if (a.spec)
+        hipLaunchKernelGGL((crn_front_kernel<T, true>), grid, dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((crn_front_kernel<T, false>), grid, dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+template hipError_t launch_front<float>(const FrontArgs&, int, hipStream_t);
+template hipError_t launch_front<bf16_t>(const FrontArgs&, int, hipStream_t);
+
+hipError_t launch_back(const BackArgs& a, int B, int mode, hipStream_t st) {
+    if (B <= 0) return hipSuccess;
+    const int64_t nb = (a.Tmax - 1 + 14) / 15;
+    const dim3 grid((unsigned)(nb > 0 ? nb : 1), (unsigned)B);
+    switch (mode) {
+        case 0: hipLaunchKernelGGL(crn_back_kernel<0>, grid, dim3(256), 0, st, a); break;
+        case 1: hipLaunchKernelGGL(crn_back_kernel<1>, grid, dim3(256), 0, st, a); break;
+        case 2: hipLaunchKernelGGL(crn_back_kernel<2>, grid, dim3(256), 0, st, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace crn

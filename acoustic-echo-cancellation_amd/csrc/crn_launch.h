@@ -1,0 +1,81 @@
+// crn_launch.h — DCCRN kernel argument blocks and host launchers (internal).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "aec_tables.h"
+#include "crn_gemm.h"
+
+namespace crn {
+
+// Front: frame + Hann + rFFT-512 of mic and far (ConvSTFT, dccrn.py:28-59)
+// -> the encoder input map X0 [B][Tmax][256][8] (bins 1..256; channels
+// mic_re, far_re, mic_im, far_im, 0, 0, 0, 0 — dccrn.py:559-561).
+struct FrontArgs {
+    const float* mic;
+    const float* far;
+    int64_t ld;
+    const int64_t* lens;        // device [B]
+    int64_t Tmax;
+    const aec::DevTables* tab;
+    void* x0;
+    float2* spec;               // non-null: write the complex spectrum [B][Tmax][257] of `mic` instead of X0
+};
+
+// Back: mask [B][Tmax][256] float2 (bins 1..256) applied to the re-derived
+// mic spectrum (mode 0 = 'E', 1 = 'C', 2 = 'R'; dccrn2.py:189-210), irFFT +
+// WOLA (ConviSTFT, dccrn.py:80-100) -> out [B][ld_out]; optionally the
+// masked spectrum [B][Tmax][257] float2 (out_spec).
+struct BackArgs {
+    const float* mic;
+    int64_t ld;
+    const int64_t* lens;
+    int64_t Tmax;
+    const aec::DevTables* tab;
+    const float2* mask;
+    float* out;
+    int64_t ld_out;
+    float2* spec;               // nullable
+};
+
+// Row-GEMM epilogue: out[(m >> oshift)*o_hi + (m & mask)*o_lo + o_add + n] =
+// act(acc + bias[n]) for m < M, n < N; act 0 none, 1 PReLU(alpha), 2 tanh.
+struct RowEpi {
+    void* out;
+    int64_t M;
+    int32_t N;
+    int32_t oshift;
+    int64_t o_hi, o_lo, o_add;
+    const float* bias;
+    float alpha;
+    int32_t act;
+};
+
+// One LSTM frame step for CELLS weight sets x S input sequences (v1: 1x1,
+// v2 NavieComplexLSTM: 2x2), gate columns packed per 16 units (i|f|g|o).
+struct StepArgs {
+    const void* whh;            // [CELLS*4H][H]
+    const void* gx;             // [B][Tmax][S][CELLS*4H]  (input projection + both biases)
+    void* y;                    // [B][Tmax][CELLS][S][H]
+    float* cst;                 // [B][CELLS][S][H]
+    int32_t B, H;
+    int64_t Tmax;
+    int32_t t;
+};
+
+template <typename T, typename OutT>
+hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstages, const RowEpi& e, int npad,
+                            hipStream_t st);
+template <typename T>
+hipError_t launch_front(const FrontArgs& a, int B, hipStream_t st);
+hipError_t launch_back(const BackArgs& a, int B, int mode, hipStream_t st);
+template <typename T>
+hipError_t launch_lstm_step(const StepArgs& a, int cells, int seqs, hipStream_t st);
+template <typename T>
+hipError_t launch_lstm_combine(const T* y, T* dst, int64_t nframes, int H, int cells, int seqs, int dshift,
+                               int64_t ldf, int64_t ldd, hipStream_t st);
+
+// tile width the host must pad the weight rows (N) to for a GEMM of N columns
+inline int gemm_bn(int N) { return N <= 16 ? 16 : N <= 32 ? 32 : N <= 64 ? 64 : 128; }
+
+}  // namespace crn

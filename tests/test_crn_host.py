@@ -1,0 +1,73 @@
+"""CPU: the DCCRN boundary — C-ABI exports (include/aec_crn.h), parameter
+blob layout, state_dict compatibility with the reference names and the
+no-CPU-fallback rule.  No GPU needed."""
+import copy
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+import aec_amd
+import crn_oracle as C
+from aec_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_clib_exports_every_crn_symbol():
+    hdr = open(os.path.join(REPO, 'include', 'aec_crn.h')).read()
+    declared = set(re.findall(r'^\s*(?:[A-Za-z_][\w\s\*]*?)\b(aec_crn_\w+)\s*\(', hdr, re.M))
+    assert declared == set(_lib.CRN_EXPORTS), declared ^ set(_lib.CRN_EXPORTS)
+    lib = _lib.load()
+    for s in declared:
+        assert hasattr(lib, s), s
+
+
+@pytest.mark.parametrize('version,over', [(1, {}), (2, {}), (2, {'use_cbn': False, 'masking_mode': 'C'}),
+                                          (2, {'masking_mode': 'R', 'rnn_layers': 1})])
+def test_param_blob_layout(version, over):
+    conf = copy.deepcopy(aec_amd.net_conf)
+    conf.update(over)
+    net = (aec_amd.dccrn if version == 1 else aec_amd.dccrn2).DCCRN(conf)
+    names = net.param_names()
+    # same names and order as the oracle's restatement of the reference state_dict
+    assert names == [n for n, _ in C.param_shapes(conf, version)]
+    sd = net.state_dict()
+    assert _lib.crn_param_count(version, conf) == sum(sd[n].numel() for n in names)
+    blob = net.params_blob()
+    assert blob.dtype == np.float32 and blob.size == _lib.crn_param_count(version, conf)
+
+
+def test_unsupported_configs_rejected():
+    bad = copy.deepcopy(aec_amd.net_conf)
+    bad['conv_channels'] = [4, 16, 32, 64, 128, 256]      # 256 >> 5 = 8 != 4
+    assert _lib.crn_param_count(2, bad) == 0
+    bad = copy.deepcopy(aec_amd.net_conf)
+    bad['hidden_dim'] = 8
+    assert _lib.crn_param_count(2, bad) == 0
+
+
+def test_fixture_weights_load_strictly_by_reference_names():
+    for version, mod in ((1, aec_amd.dccrn), (2, aec_amd.dccrn2)):
+        net = mod.DCCRN(aec_amd.net_conf)
+        w = C.make_weights(aec_amd.net_conf, version, 7)
+        sd = net.state_dict()
+        for k, v in w.items():
+            assert tuple(sd[k].shape) == v.shape, k
+            sd[k] = torch.from_numpy(v)
+        net.load_state_dict(sd, strict=True)
+        blob = net.params_blob()
+        exp = np.concatenate([w[n].reshape(-1) for n in net.param_names()])
+        assert np.array_equal(blob, exp)
+
+
+def test_crn_cpu_tensors_fail_loudly():
+    net = aec_amd.dccrn2.DCCRN(aec_amd.net_conf).eval()
+    x = torch.zeros(1, 1000)
+    with torch.no_grad(), pytest.raises(RuntimeError, match='HIP device'):
+        net(x, x, x, x)
+    net.train()
+    with torch.no_grad(), pytest.raises(NotImplementedError, match='eval'):
+        net(x, x, x, x)

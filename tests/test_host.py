@@ -81,7 +81,7 @@ def test_product_path_does_not_import_oracle():
         for f in files:
             if f.endswith(('.py', '.hip', '.h', '.cpp')):
                 src = open(os.path.join(root, f)).read()
-                assert 'aec_oracle' not in src and 'oracle/' not in src, f
+                assert 'aec_oracle' not in src and 'crn_oracle' not in src and 'oracle/' not in src, f
 
 
 def test_cpu_tensors_fail_loudly(golden_erb):
