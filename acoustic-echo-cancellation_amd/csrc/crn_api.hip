@@ -328,8 +328,9 @@ static aec_status pack_decoder(aec_crn_handle* h, Packed& pk, const RealConv& r,
     return upload_packed(h, pk, w, r.b);
 }
 
-// LSTM cell(s): unit order u' = d*Q + c <-> reference u = c*D + d; gate
-// column p(q, u') = ((u'/16)*4 + q)*16 + u'%16 (i|f|g|o per 16 units)
+// LSTM cell(s): unit order u' = d*Q + c <-> reference u = c*D + d; W_hh gate
+// row p(q, u') = ((u'/16)*4 + q)*16 + u'%16 (i|f|g|o per 16 units), W_ih /
+// bias gate row u'*4 + q (so Gx holds a unit's 4 gates contiguously)
 static aec_status pack_lstm(aec_crn_handle* h, Cursor& cur, Packed& ih, Packed& hh) {
     const int H = h->H, D = h->D, Q = h->Q, C = h->CELLS;
     const size_t G = (size_t)4 * H;
@@ -343,13 +344,16 @@ static aec_status pack_lstm(aec_crn_handle* h, Cursor& cur, Packed& ih, Packed& 
         if (!cur.ok) return crn_fail(h, AEC_ERR_INVALID_ARG, "parameter blob too short");
         for (int up = 0; up < H; ++up)
             for (int q = 0; q < 4; ++q) {
+                // W_hh rows: fragment order (16 units of one gate per 16-column fragment);
+                // W_ih rows / bias: the 4 gates of a unit adjacent (Gx read as one vector)
                 const size_t p = (size_t)cell * G + ((size_t)(up / 16) * 4 + q) * 16 + up % 16;
+                const size_t pi = (size_t)cell * G + (size_t)up * 4 + q;
                 const size_t src = (size_t)q * H + perm(up);
                 for (int kp = 0; kp < H; ++kp) {
-                    wih[p * H + kp] = Wih[src * H + perm(kp)];
+                    wih[pi * H + kp] = Wih[src * H + perm(kp)];
                     whh[p * H + kp] = Whh[src * H + perm(kp)];
                 }
-                bias[p] = (double)bih[src] + (double)bhh[src];
+                bias[pi] = (double)bih[src] + (double)bhh[src];
             }
     }
     ih.N = hh.N = (int)(C * G);
@@ -479,6 +483,7 @@ static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int
         a.padd = -2;
         a.plim = Fin;
         a.base_off = choff - 2 * ld_in;
+        a.src_elems = BT * Fin * ld_in;
         const int64_t ldo = 2 * ch[i + 1];
         RowEpi e{h->cat[i + 1], a.M, pk.N, a.rshift, Fo * ldo, ldo, ch[i + 1], pk.bias, pk.alpha, pk.act};
         CRN_TRY(h, (crn::launch_gemm_rows<T, T>(a, reinterpret_cast<const T*>(pk.w), pk.kpad,
@@ -510,11 +515,12 @@ static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int
         a.padd = 0;
         a.plim = D;
         a.base_off = choff;
+        a.src_elems = BT * D * ld_in;
         const Packed& ih = h->lih[l];
         RowEpi e{h->gx, a.M, ih.N, 0, (int64_t)C * 4 * H, 0, 0, ih.bias, 0.f, 0};
         CRN_TRY(h, (crn::launch_gemm_rows<T, T>(a, reinterpret_cast<const T*>(ih.w), ih.kpad,
                                                  (int)(ih.kpad * sizeof(T) / crn::kStageBytes), e, ih.npad, st)));
-        crn::StepArgs sa{h->lhh[l].w, h->gx, h->y, h->cst, B, H, Tmax, 0};
+        crn::StepArgs sa{h->lhh[l].w, h->gx, h->y, h->cst, B, H, Tmax, 0, 0};
         for (int64_t t = 0; t < Tmax; ++t) {
             sa.t = (int)t;
             CRN_TRY(h, crn::launch_lstm_step<T>(sa, C, S, st));
@@ -546,6 +552,7 @@ static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int
             a.padd = par == 0 ? -1 : 0;
             a.plim = Fin;
             a.base_off = a.padd * ld_in;
+            a.src_elems = BT * Fin * ld_in;
             if (cl != 1) {
                 const int64_t ldo = 2 * ch[cl - 1];
                 RowEpi e{h->cat[cl - 1], a.M, pk.N, a.rshift, Fo * ldo, 2 * ldo, par * ldo, pk.bias, pk.alpha, pk.act};
@@ -568,8 +575,11 @@ static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int
                          reinterpret_cast<float2*>(spec)};
         CRN_TRY(h, crn::launch_back(ba, B, mode, st));
     }
-    if (mask_out)
-        CRN_TRY(h, hipMemcpyAsync(mask_out, h->mask, (size_t)BT * 256 * 2 * sizeof(float), hipMemcpyDeviceToDevice, st));
+    if (mask_out)   // internal frames are t-major ([Tmax][B]); the ABI's mask is [B][Tmax]
+        for (int b = 0; b < B; ++b)
+            CRN_TRY(h, hipMemcpy2DAsync(mask_out + (size_t)b * Tmax * 512, 512 * sizeof(float), h->mask + (size_t)b * 512,
+                                        (size_t)B * 512 * sizeof(float), 512 * sizeof(float), (size_t)Tmax,
+                                        hipMemcpyDeviceToDevice, st));
     mark(h, st);
     return AEC_OK;
 }

@@ -78,6 +78,7 @@ struct RowSrc {
     int32_t kshift;
     int32_t pmul, padd, plim;
     int64_t ks, base_off;
+    int64_t src_elems;          // elements of the source tensor (buffer range of the DMA path)
 };
 
 template <typename T>
@@ -165,5 +166,96 @@ __device__ __forceinline__ void gemm_core(f32x4 (&acc)[FM][FN], char* smem, cons
         }
     }
 }
+
+
+// --------------------------------------------------------------------------
+// LDS-DMA main loop (buffer_load ... lds): no register staging, NBUF stage
+// buffers, one barrier per stage, counted vmcnt.  Each stage is 128 K-bytes
+// per row; LDS rows are 128 B, unpadded (the DMA writes 64 lanes x 16 B
+// contiguously), with the 16-B chunk q of row r stored at slot
+// q ^ ((r >> 1) & 7): the 16 rows of a fragment read then hit 16 distinct
+// bank slots.  A lane of DMA instruction i fills row 8i + (lane >> 3), slot
+// lane & 7, so it fetches logical chunk (lane & 7) ^ ((row >> 1) & 7).
+// aoff(i, kbyte) / boff(i, kbyte): the lane's byte offset into ra / rb for
+// its row of A / B instruction i (i < BM/32 resp. BN/32 per wave, rows
+// 8 (4 i + wave) + lane/8) at K-byte kbyte, or 0x80000000 (out of range ->
+// the hardware writes zeros).  BM, BN multiples of 32.
+// --------------------------------------------------------------------------
+__device__ __forceinline__ int swz_slot(int row, int q) { return q ^ ((row >> 1) & 7); }
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    // gfx9 s_waitcnt: vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt[5:4] << 14
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+template <typename T, int BM, int BN, int FM, int FN, int NBUF, class AO, class BO>
+__device__ __forceinline__ void gemm_core_dma(f32x4 (&acc)[FM][FN], char* smem, __amdgpu_buffer_rsrc_t ra,
+                                              __amdgpu_buffer_rsrc_t rb, const AO& aoff, const BO& boff,
+                                              int nstages, int wr0, int wc0) {
+    static_assert(BM % 32 == 0 && BN % 32 == 0 && NBUF >= 2, "tile");
+    constexpr int LA = BM / 32, LB = BN / 32;          // DMA instructions per wave per stage
+    constexpr int STAGE = (BM + BN) * 128;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int q_l = lane & 7;
+    auto issue = [&](int st) {
+        char* buf = smem + (st % NBUF) * STAGE;
+#pragma unroll
+        for (int i = 0; i < LA; ++i) {
+            const int row = 8 * (4 * i + wave) + (lane >> 3);
+            const uint32_t vo = aoff(i, st * 128 + swz_slot(row, q_l) * 16);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                ra, (__attribute__((address_space(3))) void*)(buf + 8 * (4 * i + wave) * 128), 16, vo, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < LB; ++i) {
+            const int row = 8 * (4 * i + wave) + (lane >> 3);
+            const uint32_t vo = boff(i, st * 128 + swz_slot(row, q_l) * 16);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rb, (__attribute__((address_space(3))) void*)(buf + BM * 128 + 8 * (4 * i + wave) * 128), 16, vo, 0,
+                0, 0);
+        }
+    };
+#pragma unroll
+    for (int s = 0; s < NBUF - 1; ++s)
+        if (s < nstages) issue(s);
+    const int fr = lane & 15, g = lane >> 4;
+    for (int st = 0; st < nstages; ++st) {
+        if (st + NBUF - 2 < nstages)
+            wait_vm<(NBUF - 2) * (LA + LB)>();
+        else
+            wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        if (st + NBUF - 1 < nstages) issue(st + NBUF - 1);
+        const char* sA = smem + (st % NBUF) * STAGE;
+        const char* sB = sA + BM * 128;
+#pragma unroll
+        for (int kc = 0; kc < 2; ++kc) {
+            u32x4 af[FM], bfr[FN];
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm) {
+                const int r = wr0 + fm * 16 + fr;
+                af[fm] = *reinterpret_cast<const u32x4*>(sA + r * 128 + swz_slot(r, kc * 4 + g) * 16);
+            }
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) {
+                const int r = wc0 + fn * 16 + fr;
+                bfr[fn] = *reinterpret_cast<const u32x4*>(sB + r * 128 + swz_slot(r, kc * 4 + g) * 16);
+            }
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+                for (int fn = 0; fn < FN; ++fn) mma_chunk(acc[fm][fn], af[fm], bfr[fn], T{});
+        }
+    }
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint64_t bytes) {
+    const uint32_t nr = bytes > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)bytes;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nr, 0x00020000);
+}
+
+constexpr uint32_t kOOB = 0x80000000u;
 
 }  // namespace crn

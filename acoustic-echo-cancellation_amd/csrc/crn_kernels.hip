@@ -12,11 +12,14 @@
 //   gemm_rows_kernel x12 decoder ComplexConvTranspose2d (even / odd output bins)
 //   crn_back_kernel      mask (E / C / R) on the mic spectrum -> irFFT + WOLA
 //
-// Feature maps are channels-last [frame][bin][channel] in the element type T
+// Frames are ordered time-major, f = t*B + b, so one LSTM step's rows (all
+// streams at frame t) are contiguous.  Feature maps are channels-last
+// [frame][bin][channel] in the element type T
 // (float or bf16); the host (crn_api.hip) folds every BatchNorm into the conv
 // weights and permutes the weight rows / columns to the layouts used here.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "aec_fft.h"
 #include "aec_stft.h"
@@ -113,7 +116,7 @@ __global__ __launch_bounds__(256) void crn_front_kernel(FrontArgs p) {
         if (lb == 0) srow[128] = live ? m128 : z;
         return;
     }
-    T* row = reinterpret_cast<T*>(p.x0) + ((int64_t)b * p.Tmax + t) * 256 * 8;
+    T* row = reinterpret_cast<T*>(p.x0) + ((int64_t)t * gridDim.y + b) * 256 * 8;   // frame f = t*B + b
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
         const int k = lb + 16 * m;
@@ -189,7 +192,7 @@ __global__ __launch_bounds__(256) void crn_back_kernel(BackArgs p) {
     // mask row of frame t (bins 1..256 -> index bin-1); DC has mask 0 (F.pad, dccrn.py:577-578)
     const int64_t t = h0 + g;
     const bool live = t <= nhop && t < p.Tmax;
-    const float2* mrow = p.mask + ((int64_t)b * p.Tmax + (live ? t : 0)) * 256;
+    const float2* mrow = p.mask + ((int64_t)(live ? t : 0) * gridDim.y + b) * 256;   // frame f = t*B + b
     const float2 z = make_float2(0.f, 0.f);
     auto mk = [&](int bin) { return (live && bin > 0) ? mrow[bin - 1] : z; };
 #pragma unroll
@@ -260,13 +263,94 @@ __device__ __forceinline__ void store_out(void* out, int64_t idx, float v) {
     reinterpret_cast<OutT*>(out)[idx] = to_elem<OutT>(v);
 }
 
+// Row-GEMM epilogue: bias (loaded once per column fragment), activation,
+// store.  Rows / columns beyond M / N are skipped.
+template <typename OutT, int FM, int FN>
+__device__ __forceinline__ void rows_epilogue(const f32x4 (&acc)[FM][FN], const RowEpi& e, int64_t mb, int nb,
+                                              int lane) {
+    float bias[FN];
+    bool nok[FN];
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+        const int n = nb + fn * 16 + (lane & 15);
+        nok[fn] = n < e.N;
+        bias[fn] = nok[fn] ? e.bias[n] : 0.f;
+    }
+    const int64_t omask = (1ll << e.oshift) - 1;
+    const int act = e.act;
+    const float alpha = e.alpha;
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t m = mb + fm * 16 + 4 * (lane >> 4) + r;
+            if (m >= e.M) continue;
+            OutT* orow = reinterpret_cast<OutT*>(e.out) + (m >> e.oshift) * e.o_hi + (m & omask) * e.o_lo + e.o_add +
+                         nb + (lane & 15);
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) {
+                float v = acc[fm][fn][r] + bias[fn];
+                v = act == 1 ? (v >= 0.f ? v : alpha * v) : act == 2 ? tanhf(v) : v;
+                if (nok[fn]) orow[fn * 16] = to_elem<OutT>(v);
+            }
+        }
+}
+
+// LDS-staged variant for the DMA kernel: the wave's (FM*16) x (FN*16) tile
+// goes through LDS (after bias + activation) and leaves as 16-byte row
+// chunks (N and the output channel offsets are multiples of 8).
+template <typename OutT, int FM, int FN>
+__device__ __forceinline__ void rows_epilogue_lds(const f32x4 (&acc)[FM][FN], const RowEpi& e, int64_t mb, int nb,
+                                                  int lane, char* wlds) {
+    constexpr int WR = FM * 16, WC = FN * 16;
+    constexpr int RB = WC * (int)sizeof(OutT);          // bytes per staged row
+    constexpr int CPR = RB / 16;                         // 16-B chunks per row
+    constexpr int EPC = 16 / (int)sizeof(OutT);          // elements per chunk
+    float bias[FN];
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+        const int n = nb + fn * 16 + (lane & 15);
+        bias[fn] = n < e.N ? e.bias[n] : 0.f;
+    }
+    const int act = e.act;
+    const float alpha = e.alpha;
+    OutT* st = reinterpret_cast<OutT*>(wlds);
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) {
+                float v = acc[fm][fn][r] + bias[fn];
+                v = act == 1 ? (v >= 0.f ? v : alpha * v) : act == 2 ? tanhf(v) : v;
+                st[(fm * 16 + 4 * (lane >> 4) + r) * WC + fn * 16 + (lane & 15)] = to_elem<OutT>(v);
+            }
+    aec::wave_fence();
+    const int64_t omask = (1ll << e.oshift) - 1;
+#pragma unroll
+    for (int it = 0; it < WR * CPR / 64; ++it) {
+        const int c = it * 64 + lane;
+        const int row = c / CPR, ch = c % CPR;
+        const int64_t m = mb + row;
+        const int n = nb + ch * EPC;
+        if (m < e.M && n < e.N) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(wlds + row * RB + ch * 16);
+            OutT* o = reinterpret_cast<OutT*>(e.out) + (m >> e.oshift) * e.o_hi + (m & omask) * e.o_lo + e.o_add + n;
+            *reinterpret_cast<u32x4*>(o) = v;
+        }
+    }
+}
+
 template <typename T, typename OutT, int WM, int WN, int FM, int FN>
 __global__ __launch_bounds__(256) void gemm_rows_kernel(RowSrc a, const T* __restrict__ bt, int64_t ldb, int nstages,
                                                          RowEpi e) {
     constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
     __shared__ __attribute__((aligned(16))) char smem[(BM + BN) * kRowStride];
-    const int64_t m0 = (int64_t)blockIdx.x * BM;
-    const int n0 = blockIdx.y * BN;
+    // 1-D grid, column blocks fastest: the column tiles of one row tile run
+    // together (the A rows are read once from HBM and re-used through L2/MALL)
+    const int nbn = (e.N + BN - 1) / BN;
+    const int64_t m0 = (int64_t)(blockIdx.x / nbn) * BM;
+    const int n0 = (int)(blockIdx.x % nbn) * BN;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wr0 = (wave / WN) * FM * 16, wc0 = (wave % WN) * FN * 16;
     f32x4 acc[FM][FN];
@@ -281,26 +365,65 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(RowSrc a, const T* __res
     };
     gemm_core<T, BM, BN, FM, FN>(acc, smem, al, bl, nstages, wr0, wc0);
 
-    const int64_t omask = (1ll << e.oshift) - 1;
+    rows_epilogue<OutT, FM, FN>(acc, e, m0 + wr0, n0 + wc0, lane);
+}
+
+// Same GEMM through the LDS-DMA main loop (tiles with BM, BN multiples of 32).
+template <typename T, typename OutT, int WM, int WN, int FM, int FN, int NBUF>
+__global__ __launch_bounds__(256) void gemm_rows_dma_kernel(RowSrc a, const T* __restrict__ bt, int64_t ldb,
+                                                             int nstages, RowEpi e) {
+    constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
+    constexpr int LA = BM / 32;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    // 1-D grid, column blocks fastest: the column tiles of one row tile run
+    // together (the A rows are read once from HBM and re-used through L2/MALL)
+    const int nbn = (e.N + BN - 1) / BN;
+    const int64_t m0 = (int64_t)(blockIdx.x / nbn) * BM;
+    const int n0 = (int)(blockIdx.x % nbn) * BN;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wr0 = (wave / WN) * FM * 16, wc0 = (wave % WN) * FN * 16;
+    constexpr int ES = (int)sizeof(T);
+    const int64_t hi0 = m0 >> a.rshift;
+    const T* abase = reinterpret_cast<const T*>(a.src) + hi0 * a.rs_hi;
+    const __amdgpu_buffer_rsrc_t ra = make_rsrc(abase, (uint64_t)(a.src_elems - hi0 * a.rs_hi) * ES);
+    const __amdgpu_buffer_rsrc_t rb = make_rsrc(bt + (int64_t)n0 * ldb, (uint64_t)BN * ldb * ES);
+    int32_t rowoff[LA], posb[LA];
+    bool mval[LA];
 #pragma unroll
-    for (int fm = 0; fm < FM; ++fm)
+    for (int i = 0; i < LA; ++i) {
+        const int64_t m = m0 + 8 * (4 * i + wave) + (lane >> 3);
+        const int64_t hi = m >> a.rshift;
+        const int lo = (int)(m & ((1ll << a.rshift) - 1));
+        rowoff[i] = (int32_t)((hi - hi0) * a.rs_hi + (int64_t)lo * a.rs_lo + a.base_off);
+        posb[i] = lo * a.pmul + a.padd;
+        mval[i] = m < a.M;
+    }
+    const int kmask = (1 << a.kshift) - 1;
+    auto aoff = [&](int i, int kbyte) -> uint32_t {
+        const int k = kbyte / ES;
+        const int tap = k >> a.kshift;
+        const int pos = posb[i] + tap;
+        const bool ok = mval[i] && k < a.K && pos >= 0 && pos < a.plim;
+        return ok ? (uint32_t)((rowoff[i] + tap * (int32_t)a.ks + (k & kmask)) * ES) : kOOB;
+    };
+    auto boff = [&](int i, int kbyte) -> uint32_t {
+        return (uint32_t)((8 * (4 * i + wave) + (lane >> 3)) * (int32_t)ldb * ES + kbyte);
+    };
+    f32x4 acc[FM][FN];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int64_t m = m0 + wr0 + fm * 16 + 4 * (lane >> 4) + r;
-            if (m >= e.M) continue;
-            const int64_t ob = (m >> e.oshift) * e.o_hi + (m & omask) * e.o_lo + e.o_add;
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-            for (int fn = 0; fn < FN; ++fn) {
-                const int n = n0 + wc0 + fn * 16 + (lane & 15);
-                if (n >= e.N) continue;
-                float v = acc[fm][fn][r] + e.bias[n];
-                if (e.act == 1)
-                    v = v >= 0.f ? v : e.alpha * v;
-                else if (e.act == 2)
-                    v = tanhf(v);
-                store_out<OutT>(e.out, ob + n, v);
-            }
-        }
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    gemm_core_dma<T, BM, BN, FM, FN, NBUF>(acc, smem, ra, rb, aoff, boff, nstages, wr0, wc0);
+    __syncthreads();                                   // every wave is done with the stage buffers
+    static_assert(4 * FM * 16 * FN * 16 * sizeof(OutT) <= (size_t)NBUF * (BM + BN) * 128, "epilogue LDS");
+    rows_epilogue_lds<OutT, FM, FN>(acc, e, m0 + wr0, n0 + wc0, lane,
+                                    smem + wave * (FM * 16 * FN * 16 * (int)sizeof(OutT)));
+}
+
+static int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v ? atoi(v) : dflt;
 }
 
 template <typename T, typename OutT>
@@ -308,21 +431,47 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
                             hipStream_t st) {
     if (a.M <= 0) return hipSuccess;
     const int bn = gemm_bn(e.N);
-    if (npad % bn) return hipErrorInvalidValue;
+    if (npad != (e.N + bn - 1) / bn * bn) return hipErrorInvalidValue;
 #define CRN_GEMM(WM, WN, FM, FN)                                                                              \
     do {                                                                                                      \
         constexpr int BM = WM * FM * 16;                                                                      \
-        dim3 grid((unsigned)((a.M + BM - 1) / BM), (unsigned)(npad / (WN * FN * 16)));                        \
+        const unsigned nbn_ = (unsigned)(npad / (WN * FN * 16));                                              \
+        dim3 grid((unsigned)((a.M + BM - 1) / BM) * nbn_);                                                    \
         hipLaunchKernelGGL((gemm_rows_kernel<T, OutT, WM, WN, FM, FN>), grid, dim3(256), 0, st, a, bt, ldb,  \
                            nstages, e);                                                                       \
     } while (0)
+#define CRN_GEMM_DMA(WM, WN, FM, FN, NBUF)                                                                     \
+    do {                                                                                                          \
+        constexpr int BM = WM * FM * 16, BN = WN * FN * 16;                                                       \
+        auto kern = gemm_rows_dma_kernel<T, OutT, WM, WN, FM, FN, NBUF>;                                          \
+        constexpr size_t lds = (size_t)NBUF * (BM + BN) * 128;                                                    \
+        static const hipError_t attr =                                                                            \
+            hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                (int)lds);                                                                        \
+        if (attr != hipSuccess) return attr;                                                                      \
+        const unsigned nbn_ = (unsigned)(npad / BN);                                                              \
+        dim3 grid((unsigned)((a.M + BM - 1) / BM) * nbn_);                                                        \
+        hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a, bt, ldb, nstages, e);                               \
+    } while (0)
+    static const int dma = env_int("CRN_GEMM_DMA", 2);    // 0 = register-staged core, else NBUF
     switch (bn) {
         case 16: CRN_GEMM(4, 1, 4, 1); break;
         case 32: CRN_GEMM(2, 2, 4, 1); break;
-        case 64: CRN_GEMM(2, 2, 4, 2); break;
-        default: CRN_GEMM(2, 2, 4, 4); break;
+        case 64:
+            if (dma == 2) CRN_GEMM_DMA(2, 2, 4, 2, 2);
+            else if (dma == 3) CRN_GEMM_DMA(2, 2, 4, 2, 3);
+            else if (dma >= 4) CRN_GEMM_DMA(2, 2, 4, 2, 4);
+            else CRN_GEMM(2, 2, 4, 2);
+            break;
+        default:
+            if (dma == 2) CRN_GEMM_DMA(2, 2, 4, 4, 2);
+            else if (dma == 3) CRN_GEMM_DMA(2, 2, 4, 4, 3);
+            else if (dma >= 4) CRN_GEMM_DMA(2, 2, 4, 4, 4);
+            else CRN_GEMM(2, 2, 4, 4);
+            break;
     }
 #undef CRN_GEMM
+#undef CRN_GEMM_DMA
     return hipGetLastError();
 }
 
@@ -336,88 +485,212 @@ template hipError_t launch_gemm_rows<bf16_t, float>(const RowSrc&, const bf16_t*
 // --------------------------------------------------------------------------
 // LSTM frame step.  Block = (32 units) x (SB streams); rows of the A tile are
 // h_{t-1} of every (cell, sequence, stream), the B tile the cells' W_hh rows
-// of those units (4 gates x 32 units per cell, packed i|f|g|o per 16 units).
-// Each wave owns 16 units x 4 gates of one cell, so the gate quadruple of a
-// (row, unit) lands in one lane: the cell update is fused.
+// of those units (4 gates x 32 units per cell, packed i|f|g|o per 16 units),
+// staged by LDS-DMA (gemm_core_dma).  Each wave owns 16 units x 4 gates of
+// one cell, so the gate quadruple of a (row, unit) lands in one lane and the
+// cell update is fused.  Gx holds the 4 gates of a (row, unit) contiguously
+// (one 8-B / 16-B load); every Gx / c load of the epilogue is issued before
+// the first use.
 // --------------------------------------------------------------------------
+__device__ __forceinline__ float4 load4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 load4(const bf16_t* p) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
+    return make_float4(__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xFFFF0000u), __uint_as_float(v.y << 16),
+                       __uint_as_float(v.y & 0xFFFF0000u));
+}
+
+__device__ __forceinline__ float fsigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float ftanh(float x) { return 2.f * fsigmoid(2.f * x) - 1.f; }
+
+// Block = one cell x 32 units x SB streams (v2: both sequences of each stream,
+// 128 rows; v1: 64 rows).  Weights of the block: 4 gates x 32 units = 128
+// W_hh rows.  grid = (H / 32, CELLS * ceil(B / SB)); consecutive blocks take
+// consecutive unit slices, so each XCD keeps the same 4 slices (2 MB of
+// weights) for every step.
+template <typename T, int CELLS, int S>
+struct StepCfg {
+    static constexpr int SB = CELLS * S == 4 ? 64 : 64;
+    static constexpr int U = 32;
+    static constexpr int BM = SB * S;                   // rows: (s, stream)
+    static constexpr int BN = 4 * U;
+    static constexpr int FM = BM / 32, FN = 4;          // 2 x 2 waves
+    static constexpr int NBUF = sizeof(T) == 2 ? 3 : 2;
+    static constexpr int GROW = U * 4 * (int)sizeof(T);            // Gx bytes per row
+    static constexpr size_t STAGES = (size_t)NBUF * (BM + BN) * 128;
+    static constexpr size_t LDS = STAGES + (size_t)BM * GROW + (size_t)BM * U * 4;
+};
+
 template <typename T, int CELLS, int S>
 __global__ __launch_bounds__(256) void lstm_step_kernel(StepArgs p) {
-    constexpr bool V2 = CELLS * S == 4;
-    constexpr int SB = V2 ? 32 : 64;
-    constexpr int U = 32;
-    constexpr int BM = SB * CELLS * S;
-    constexpr int BN = CELLS * 4 * U;
-    constexpr int FM = V2 ? 4 : 2, FN = 4;
-    __shared__ __attribute__((aligned(16))) char smem[(BM + BN) * kRowStride];
+    using C_ = StepCfg<T, CELLS, S>;
+    constexpr int SB = C_::SB, U = C_::U, BM = C_::BM, BN = C_::BN, FM = C_::FM, FN = C_::FN;
+    constexpr int LA = BM / 32;
+    constexpr int ES = (int)sizeof(T);
+    constexpr int GROW = C_::GROW;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* sG = smem + C_::STAGES;                       // Gx tile [BM][U][4]
+    char* sC = sG + BM * GROW;                          // c tile [BM][U] f32
     const int H = p.H;
-    const int unit0 = blockIdx.x * U, b0 = blockIdx.y * SB;
+    const int nsb = (int)gridDim.y / CELLS;
+    const int cell = (int)blockIdx.y / nsb;
+    const int unit0 = blockIdx.x * U, b0 = ((int)blockIdx.y % nsb) * SB;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int cell = V2 ? (wave >> 1) : 0, uh = wave & 1;
-    const int wr0 = V2 ? cell * 64 : (wave >> 1) * 32;
-    const int wc0 = V2 ? cell * 128 + uh * 64 : uh * 64;
+    const int uh = wave & 1;
+    const int wr0 = (wave >> 1) * (BM / 2), wc0 = uh * 64;
     const int t = p.t;
+    const int64_t ystride = (int64_t)CELLS * S * H;            // elements per (stream, frame)
+    const int64_t gstride = (int64_t)CELLS * 4 * H;            // Gx elements per (stream, frame, s)
+
+    // 1. DMA the epilogue's Gx (and c) tiles into LDS first: the oldest vector-memory
+    //    ops, retired by the main loop's first wait (or the explicit wait at t = 0)
+    if (!(p.mode & 4)) {
+        const T* gbase = reinterpret_cast<const T*>(p.gx) + ((int64_t)t * p.B + b0) * S * gstride;
+        const __amdgpu_buffer_rsrc_t rg =
+            make_rsrc(gbase, (uint64_t)((int64_t)(p.B - b0) * S * gstride) * ES);
+        constexpr int GCH = GROW / 16;                   // 16-B chunks per Gx row
+        constexpr int GI = BM * GCH / 256;               // DMA instructions per wave
+#pragma unroll
+        for (int i = 0; i < GI; ++i) {
+            const int c = (4 * i + wave) * 64 + lane;
+            const int r = c / GCH, ch = c % GCH;
+            const int s = r / SB, bl = r % SB;
+            const uint32_t vo = (b0 + bl < p.B)
+                ? (uint32_t)((((int64_t)bl * S + s) * gstride + (int64_t)cell * 4 * H + unit0 * 4) * ES +
+                             ch * 16)
+                : kOOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rg, (__attribute__((address_space(3))) void*)(sG + (4 * i + wave) * 1024), 16, vo, 0, 0, 2);
+        }
+        if (t > 0) {
+            const float* cbase = p.cst + (int64_t)b0 * CELLS * S * H;
+            const __amdgpu_buffer_rsrc_t rc = make_rsrc(cbase, (uint64_t)(p.B - b0) * CELLS * S * H * 4);
+            constexpr int CI = BM * (U * 4 / 16) / 256;
+#pragma unroll
+            for (int i = 0; i < CI; ++i) {
+                const int c = (4 * i + wave) * 64 + lane;
+                const int r = c / (U * 4 / 16), ch = c % (U * 4 / 16);
+                const int s = r / SB, bl = r % SB;
+                const uint32_t vo = (b0 + bl < p.B)
+                    ? (uint32_t)((((int64_t)bl * CELLS + cell) * S + s) * H * 4 + unit0 * 4 + ch * 16)
+                    : kOOB;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rc, (__attribute__((address_space(3))) void*)(sC + (4 * i + wave) * 1024), 16, vo, 0, 0, 2);
+            }
+        }
+    }
+    // 2. recurrent GEMM  gates = h_{t-1} W_hh^T  (tile rows (s, stream), cols (unit, gate))
     f32x4 acc[FM][FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const T* Y = reinterpret_cast<const T*>(p.y);
-    if (t > 0) {
-        auto al = [&](int r, int kb) {
-            const int cr = V2 ? r >> 6 : 0, sr = V2 ? (r >> 5) & 1 : 0, bl = V2 ? r & 31 : r;
-            const int b = b0 + bl;
-            u32x4 v = {0u, 0u, 0u, 0u};
-            if (b < p.B) {
-                const T* row = Y + ((((int64_t)b * p.Tmax + t - 1) * CELLS + cr) * S + sr) * H;
-                v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(row) + kb);
-            }
-            return v;
-        };
-        const T* W = reinterpret_cast<const T*>(p.whh);
-        auto bl = [&](int c, int kb) {
-            const int cc = c / (4 * U), pl = c % (4 * U);
-            const T* row = W + ((int64_t)cc * 4 * H + (int64_t)unit0 * 4 + pl) * H;
-            return *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(row) + kb);
-        };
-        gemm_core<T, BM, BN, FM, FN>(acc, smem, al, bl, H * (int)sizeof(T) / kStageBytes, wr0, wc0);
-    }
-    const T* Gx = reinterpret_cast<const T*>(p.gx);
-    T* Yo = reinterpret_cast<T*>(p.y);
-    const int j = unit0 + uh * 16 + (lane & 15);
+    if (t > 0 && !(p.mode & 2)) {
+        const T* ybase = reinterpret_cast<const T*>(p.y) + ((int64_t)(t - 1) * p.B + b0) * ystride;
+        const __amdgpu_buffer_rsrc_t ra = make_rsrc(ybase, (uint64_t)((int64_t)(p.B - b0) * ystride) * ES);
+        const __amdgpu_buffer_rsrc_t rb =
+            make_rsrc(reinterpret_cast<const T*>(p.whh) + ((int64_t)cell * 4 * H + (int64_t)unit0 * 4) * H,
+                      (uint64_t)BN * H * ES);
+        uint32_t arow[LA];
 #pragma unroll
-    for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-            const int rloc = fm * 16 + 4 * (lane >> 4) + rr;     // within the wave's rows
-            const int s = V2 ? (rloc >> 5) : 0;
-            const int bl = V2 ? (rloc & 31) : (wr0 + rloc);
-            const int b = b0 + bl;
-            if (b >= p.B) continue;
-            const int64_t gb = (((int64_t)b * p.Tmax + t) * S + s) * (int64_t)(CELLS * 4 * H) + (int64_t)cell * 4 * H +
-                               (int64_t)(j >> 4) * 64 + (j & 15);
-            const float gi = acc[fm][0][rr] + to_f32(Gx[gb + 0]);
-            const float gf = acc[fm][1][rr] + to_f32(Gx[gb + 16]);
-            const float gg = acc[fm][2][rr] + to_f32(Gx[gb + 32]);
-            const float go = acc[fm][3][rr] + to_f32(Gx[gb + 48]);
-            const int64_t ci = (((int64_t)b * CELLS + cell) * S + s) * H + j;
-            const float cp = t > 0 ? p.cst[ci] : 0.f;
-            const float c = sigmoidf_(gf) * cp + sigmoidf_(gi) * tanhf(gg);
-            const float h = sigmoidf_(go) * tanhf(c);
-            p.cst[ci] = c;
-            Yo[((((int64_t)b * p.Tmax + t) * CELLS + cell) * S + s) * H + j] = to_elem<T>(h);
+        for (int i = 0; i < LA; ++i) {
+            const int r = 8 * (4 * i + wave) + (lane >> 3);
+            const int s = r / SB, bl = r % SB;
+            arow[i] = (b0 + bl < p.B)
+                          ? (uint32_t)((((int64_t)bl * ystride) + ((int64_t)cell * S + s) * H) * ES)
+                          : kOOB;
         }
+        auto aoff = [&](int i, int kbyte) -> uint32_t { return arow[i] == kOOB ? kOOB : arow[i] + kbyte; };
+        auto boff = [&](int i, int kbyte) -> uint32_t {
+            return (uint32_t)((8 * (4 * i + wave) + (lane >> 3)) * H * ES + kbyte);
+        };
+        gemm_core_dma<T, BM, BN, FM, FN, C_::NBUF>(acc, smem, ra, rb, aoff, boff, H * ES / kStageBytes, wr0, wc0);
+    } else {
+        wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+    }
+    // 3. cell update (gate order i, f, g, o); c and h are staged in LDS (c over
+    //    the c-prev tile, h in the free stage buffers) and leave as 16-B rows
+    __syncthreads();                                   // stage buffers free, Gx / c tiles visible
+    char* sH = smem;                                   // h tile [BM][U] of T
+    const int jl = uh * 16 + (lane & 15);
+    if (!(p.mode & 1)) {
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int r = wr0 + fm * 16 + 4 * (lane >> 4) + rr;
+                float4 g;
+                if (ES == 2) {
+                    const uint2 v = *reinterpret_cast<const uint2*>(sG + r * GROW + jl * 8);
+                    g = make_float4(__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xFFFF0000u),
+                                    __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xFFFF0000u));
+                } else {
+                    g = *reinterpret_cast<const float4*>(sG + r * GROW + jl * 16);
+                }
+                float* cslot = reinterpret_cast<float*>(sC + r * U * 4 + jl * 4);
+                const float cp = t > 0 ? *cslot : 0.f;
+                const float c = fsigmoid(acc[fm][1][rr] + g.y) * cp +
+                                fsigmoid(acc[fm][0][rr] + g.x) * ftanh(acc[fm][2][rr] + g.z);
+                const float h = fsigmoid(acc[fm][3][rr] + g.w) * ftanh(c);
+                *cslot = c;
+                reinterpret_cast<T*>(sH)[r * U + jl] = to_elem<T>(h);
+            }
+    }
+    __syncthreads();
+    // c rows: U*4 bytes at cst[((b*CELLS + cell)*S + s)*H + unit0]; h rows: U*ES bytes at y[t]
+    T* Yo = reinterpret_cast<T*>(p.y);
+    constexpr int CCH = U * 4 / 16, HCH = U * ES / 16;
+#pragma unroll
+    for (int i = 0; i < BM * CCH / 256; ++i) {
+        const int c = i * 256 + threadIdx.x;
+        const int r = c / CCH, ch = c % CCH;
+        const int s = r / SB, bl = r % SB;
+        if (b0 + bl < p.B) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(sC + r * U * 4 + ch * 16);
+            *reinterpret_cast<u32x4*>(p.cst + (((int64_t)(b0 + bl) * CELLS + cell) * S + s) * H + unit0 + ch * 4) = v;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < (BM * HCH + 255) / 256; ++i) {
+        const int c = i * 256 + threadIdx.x;
+        if (BM * HCH % 256 != 0 && c >= BM * HCH) break;
+        const int r = c / HCH, ch = c % HCH;
+        const int s = r / SB, bl = r % SB;
+        if (b0 + bl < p.B) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(sH + r * U * ES + ch * 16);
+            *reinterpret_cast<u32x4*>(Yo + ((((int64_t)t * p.B + b0 + bl) * CELLS + cell) * S + s) * H + unit0 +
+                                      ch * (16 / ES)) = v;
+        }
+    }
 }
 
 template <typename T>
 hipError_t launch_lstm_step(const StepArgs& a, int cells, int seqs, hipStream_t st) {
+    // CRN_STEP_MODE (timing experiments only, results invalid unless 0): bit0 skip the
+    // cell update, bit1 skip the recurrent GEMM, bit2 skip the Gx / c DMA
+    static const int step_mode = env_int("CRN_STEP_MODE", 0);
     if (a.H % 32 || (a.H * (int)sizeof(T)) % kStageBytes) return hipErrorInvalidValue;
-    if (cells == 2 && seqs == 2) {
-        hipLaunchKernelGGL((lstm_step_kernel<T, 2, 2>), dim3(a.H / 32, (a.B + 31) / 32), dim3(256), 0, st, a);
-    } else if (cells == 1 && seqs == 1) {
-        hipLaunchKernelGGL((lstm_step_kernel<T, 1, 1>), dim3(a.H / 32, (a.B + 63) / 64), dim3(256), 0, st, a);
-    } else {
+#define CRN_STEP(C, S_)                                                                                           \
+    do {                                                                                                          \
+        auto kern = lstm_step_kernel<T, C, S_>;                                                                   \
+        constexpr size_t lds = StepCfg<T, C, S_>::LDS;                                                            \
+        static_assert(lds <= 160 * 1024, "LDS");                                                                  \
+        static const hipError_t attr =                                                                            \
+            hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                (int)lds);                                                                        \
+        if (attr != hipSuccess) return attr;                                                                      \
+        constexpr int SB = StepCfg<T, C, S_>::SB;                                                                 \
+        StepArgs a2 = a;                                                                                          \
+        a2.mode = step_mode;                                                                                      \
+        hipLaunchKernelGGL(kern, dim3(a.H / 32, C * ((a.B + SB - 1) / SB)), dim3(256), lds, st, a2);             \
+    } while (0)
+    if (cells == 2 && seqs == 2)
+        CRN_STEP(2, 2);
+    else if (cells == 1 && seqs == 1)
+        CRN_STEP(1, 1);
+    else
         return hipErrorInvalidValue;
-    }
+#undef CRN_STEP
     return hipGetLastError();
 }
 template hipError_t launch_lstm_step<float>(const StepArgs&, int, int, hipStream_t);

@@ -9,7 +9,7 @@
 namespace crn {
 
 // Front: frame + Hann + rFFT-512 of mic and far (ConvSTFT, dccrn.py:28-59)
-// -> the encoder input map X0 [B][Tmax][256][8] (bins 1..256; channels
+// -> the encoder input map X0 [Tmax][B][256][8] (bins 1..256; channels
 // mic_re, far_re, mic_im, far_im, 0, 0, 0, 0 — dccrn.py:559-561).
 struct FrontArgs {
     const float* mic;
@@ -22,7 +22,7 @@ struct FrontArgs {
     float2* spec;               // non-null: write the complex spectrum [B][Tmax][257] of `mic` instead of X0
 };
 
-// Back: mask [B][Tmax][256] float2 (bins 1..256) applied to the re-derived
+// Back: mask [Tmax][B][256] float2 (bins 1..256) applied to the re-derived
 // mic spectrum (mode 0 = 'E', 1 = 'C', 2 = 'R'; dccrn2.py:189-210), irFFT +
 // WOLA (ConviSTFT, dccrn.py:80-100) -> out [B][ld_out]; optionally the
 // masked spectrum [B][Tmax][257] float2 (out_spec).
@@ -55,12 +55,13 @@ struct RowEpi {
 // v2 NavieComplexLSTM: 2x2), gate columns packed per 16 units (i|f|g|o).
 struct StepArgs {
     const void* whh;            // [CELLS*4H][H]
-    const void* gx;             // [B][Tmax][S][CELLS*4H]  (input projection + both biases)
-    void* y;                    // [B][Tmax][CELLS][S][H]
+    const void* gx;             // [Tmax][B][S][CELLS*4H]  (input projection + both biases, gates of a unit adjacent)
+    void* y;                    // [Tmax][B][CELLS][S][H]
     float* cst;                 // [B][CELLS][S][H]
     int32_t B, H;
     int64_t Tmax;
     int32_t t;
+    int32_t mode;               // timing experiments only (CRN_STEP_MODE)
 };
 
 template <typename T, typename OutT>
