@@ -66,9 +66,12 @@ def parse():
     ap.add_argument('--seconds', type=float, default=10.0)
     ap.add_argument('--cpu-seconds', type=float, default=12.0, help='bounded CPU-baseline sample (wall s)')
     ap.add_argument('--no-cpu', action='store_true')
-    ap.add_argument('--pipeline', choices=['full', 'postfilter'], default='full',
+    ap.add_argument('--pipeline', choices=['full', 'postfilter', 'crn'], default='full',
                     help='full = STFT -> FD-NLMS -> ERB-GRU post-filter -> iSTFT (north_star); '
-                         'postfilter = the reference Little_net path alone (NLMS bypass)')
+                         'postfilter = the reference Little_net path alone (NLMS bypass); '
+                         'crn = BASELINE config 3: the DCCRN (dccrn2.py, configs.net_conf) post-filter')
+    ap.add_argument('--crn-dtype', choices=['bf16', 'f32'], default='bf16', help='--pipeline crn compute type')
+    ap.add_argument('--crn-version', type=int, choices=[1, 2], default=2, help='1 = dccrn.py, 2 = dccrn2.py')
     ap.add_argument('--no-rtf', action='store_true', help='skip the batch-1 latency probe (profiling runs)')
     ap.add_argument('--sweep', action='store_true', help='also report a batch sweep')
     return ap.parse_args()
@@ -122,8 +125,154 @@ def cpu_baseline(seconds, B=16, n=160000):
                        f'(reference op mix: conv1d DFT, nn.GRU, conv_transpose1d), {el:.1f} s wall')
 
 
+BF16_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
+CRN_STAGES = ['front', 'encoder', 'lstm', 'decoder', 'back']
+
+
+def crn_flops_per_frame(conf, version):
+    """Algorithmic MACs x 2 of the DCCRN per 256-sample frame (dense convs as
+    GEMMs, LSTMs), SURVEY.md §8(d)."""
+    ch = conf['conv_channels']
+    L = len(ch) - 1
+    enc = sum(2 * (256 >> (i + 1)) * ch[i + 1] * 5 * ch[i] for i in range(L))
+    dec = sum(2 * (256 >> c) * (2 * ch[c]) * (ch[c - 1] if c != 1 else 2) * 5 for c in range(L, 0, -1))
+    if version == 1:
+        H = ch[-1] * 4
+        rnn = 2 * 4 * H * (H + H)
+    else:
+        H = conf['hidden_dim'] * ch[-1] // 2
+        rnn = conf['rnn_layers'] * 4 * 2 * 4 * H * (H + H)
+    return dict(encoder=enc, decoder=dec, lstm=rnn, total=enc + dec + rnn)
+
+
+def cpu_baseline_crn(seconds, conf, version, n=160000, B=1):
+    """The reference op mix (oracle/torch_crn_port.py: conv2d / conv_transpose2d /
+    nn.LSTM, float32) on host cores, bounded sample."""
+    import torch
+    sys.path.insert(0, os.path.join(REPO, 'oracle'))
+    import crn_oracle
+    from torch_crn_port import TorchCrnPort
+    from aec_amd import synth
+    port = TorchCrnPort(crn_oracle.make_weights(conf, version, 1), conf, version)
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    mic, far, _ = (torch.from_numpy(a) for a in synth.batch(B, n, seed0=7000))
+    port(mic[:, :16000], far[:, :16000])             # warm-up
+    frames, reps = 0, 0
+    t0 = time.perf_counter()
+    while True:
+        port(mic, far)
+        reps += 1
+        frames += B * (n // 256 + 1)
+        el = time.perf_counter() - t0
+        if el >= seconds or reps >= 50:
+            break
+    return dict(value=round(frames / el, 1), unit='frames/s', cores=threads, kind='port',
+                sample=f'{reps} x [{B} stream x {n} samples] through oracle/torch_crn_port.py '
+                       f'(reference op mix: conv2d / conv_transpose2d / nn.LSTM, float32), {el:.1f} s wall')
+
+
+def main_crn(args):
+    """BASELINE config 3: the DCCRN post-filter (bf16 MFMA), B streams x 10 s."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    import aec_amd
+    from aec_amd import shard, synth
+    conf = dict(aec_amd.net_conf)
+    B = args.streams
+    n = int(round(args.seconds * 16000))
+    T = n // 256 + 1
+    torch.manual_seed(0)                         # the reference's own init (random weights, no checkpoint ships)
+    mod = aec_amd.dccrn if args.crn_version == 1 else aec_amd.dccrn2
+    net = mod.DCCRN(conf, dtype=args.crn_dtype).eval().to(dev)
+    mic, far, _ = (torch.from_numpy(a).to(dev) for a in synth.batch(B, n, seed0=1000 * rank))
+    lens = [n] * B
+
+    def step():
+        return net.forward_ragged(mic, far, lens, want_spec=False)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        h = net._handle(dev)
+        h.profile_enable(True)
+        h.profile_read()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        sms, calls = h.profile_read()
+        h.profile_enable(False)
+        el = shard.max_over_ranks(el)
+        lat = []
+        for _ in range(0 if args.no_rtf else 3):
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            net.forward_ragged(mic[:1], far[:1], [n], want_spec=False)
+            torch.cuda.synchronize(dev)
+            lat.append(time.perf_counter() - t1)
+        rtf1 = float(np.median(lat)) / args.seconds if lat else None
+    frames_total = world * B * T * args.steps
+    value = frames_total / el
+    ms_step = el / args.steps * 1e3
+    stage_ms = {k: sms[i] / max(calls, 1) for i, k in enumerate(CRN_STAGES)}
+    fl = crn_flops_per_frame(conf, args.crn_version)
+    peak = BF16_PEAK_TFLOPS if args.crn_dtype == 'bf16' else FP32_PEAK_TFLOPS
+    dom = max(stage_ms, key=stage_ms.get)
+    dom_fl = fl.get(dom, 0)
+    ach = dom_fl * B * T / (stage_ms[dom] * 1e-3) / 1e12 if dom_fl else 0.0
+    whole = fl['total'] * B * T / (ms_step * 1e-3 / 1) / 1e12
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline_crn(args.cpu_seconds, conf, args.crn_version, n=n)
+    if rank == 0:
+        line = {
+            'metric': '16kHz frames/sec/GPU (batched AEC) + RTF@batch=1; ERLE delta vs reference',
+            'value': round(value, 1), 'unit': 'frames/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(ms_step, 3), 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': args.crn_dtype, 'data': 'synthetic',
+            'config': {'workload': f'C3 (BASELINE configs[2]): DCCRN v{args.crn_version} '
+                                   f'({"dccrn2.py" if args.crn_version == 2 else "dccrn.py"}, configs.net_conf, '
+                                   f'{args.crn_dtype} MFMA) on {B} concurrent 10 s 16 kHz streams per GPU, '
+                                   'reference init (torch.manual_seed(0))',
+                       'streams_per_gpu': B, 'samples_per_stream': n, 'frames_per_stream': T,
+                       'frame': '256-sample hop', 'pipeline': 'crn',
+                       'parallelism': f'streams sharded, {world} rank(s)'},
+            'xRT': round(value * 256 / 16000, 1),
+            'rtf_batch1': rtf1,
+            'stage_ms_per_step': {k: round(v, 3) for k, v in stage_ms.items()},
+            'roofline': {'bound': 'mfma', 'achieved': round(ach, 1), 'peak': peak, 'unit': 'TFLOP/s',
+                         'frac': round(ach / peak, 4), 'traffic': None,
+                         'kernel': f'{dom} stage ({"input GEMM + per-frame recurrence steps + combine per layer" if dom == "lstm" else "GEMM launches"})',
+                         'alg_flops_per_frame': dom_fl, 'frames_per_launch': B * T},
+            'pipeline_roofline': {'alg_flops_per_frame': fl['total'], 'achieved_tflops': round(whole, 1),
+                                  'mfma_frac': round(whole / peak, 4)},
+            'cpu_baseline': cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.pipeline == 'crn':
+        return main_crn(args)
     import numpy as np
     import torch
     import torch.distributed as dist

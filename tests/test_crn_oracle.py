@@ -54,3 +54,18 @@ def test_param_shapes_cover_reference_names():
     n1 = sum(int(np.prod(s)) for k, s in C.param_shapes(C.NET_CONF, 1) if not k.split('.')[-1].startswith('running'))
     assert n2 == 34902237
     assert n1 == 34885105
+
+
+@pytest.mark.parametrize('name', ['v2E_2125', 'v1_2125', 'v2C_bn_2125', 'v2R_1000'])
+def test_torch_port_matches_reference(name):
+    # the CPU baseline of bench.py --pipeline crn (reference op mix, float32)
+    import torch
+    from torch_crn_port import TorchCrnPort
+    m = META[name]
+    d = np.load(os.path.join(GOLD, f'crn_{name}.npz'))
+    conf = dict(C.NET_CONF)
+    conf.update(m['overrides'])
+    port = TorchCrnPort(C.make_weights(conf, m['version'], m['weight_seed']), conf, m['version'])
+    out = port(torch.from_numpy(d['mic'])[None], torch.from_numpy(d['far'])[None])[0].numpy()
+    assert out.shape == d['out_wav'].shape
+    assert rel(out, d['out_wav']) <= 1e-4
