@@ -29,6 +29,7 @@ EXPORTS = ('aec_weights_count', 'aec_create', 'aec_set_weights', 'aec_set_erb', 
 
 # every symbol include/aec_crn.h declares
 CRN_EXPORTS = ('aec_crn_param_count', 'aec_crn_create', 'aec_crn_set_params', 'aec_crn_process', 'aec_crn_stft',
+               'aec_crn_stream_open', 'aec_crn_stream_reset', 'aec_crn_stream_step',
                'aec_crn_profile_enable', 'aec_crn_profile_read', 'aec_crn_last_error', 'aec_crn_destroy')
 
 
@@ -102,6 +103,12 @@ def load():
     lib.aec_crn_process.restype = ctypes.c_int
     lib.aec_crn_stft.argtypes = [P, P, P, ctypes.c_int32, ctypes.c_int64, P, P]
     lib.aec_crn_stft.restype = ctypes.c_int
+    lib.aec_crn_stream_open.argtypes = [P, ctypes.c_int32]
+    lib.aec_crn_stream_open.restype = ctypes.c_int
+    lib.aec_crn_stream_reset.argtypes = [P, ctypes.c_int32, P]
+    lib.aec_crn_stream_reset.restype = ctypes.c_int
+    lib.aec_crn_stream_step.argtypes = [P, P, P, ctypes.c_int64, P, ctypes.c_int64, P]
+    lib.aec_crn_stream_step.restype = ctypes.c_int
     lib.aec_crn_profile_enable.argtypes = [P, ctypes.c_int32]
     lib.aec_crn_profile_enable.restype = ctypes.c_int
     lib.aec_crn_profile_read.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
@@ -248,6 +255,16 @@ class CrnHandle:
         lens = np.ascontiguousarray(lengths, dtype=np.int64)
         check(self.lib.aec_crn_stft(self.h, x_ptr, lens.ctypes.data, int(B), int(ld), spec_ptr, stream), self.h,
               'aec_crn_stft', True)
+
+    def stream_open(self, B):
+        check(self.lib.aec_crn_stream_open(self.h, int(B)), self.h, 'aec_crn_stream_open', True)
+
+    def stream_reset(self, b, stream):
+        check(self.lib.aec_crn_stream_reset(self.h, int(b), stream), self.h, 'aec_crn_stream_reset', True)
+
+    def stream_step(self, mic_ptr, far_ptr, ld_in, out_ptr, ld_out, stream):
+        check(self.lib.aec_crn_stream_step(self.h, mic_ptr, far_ptr, int(ld_in), out_ptr, int(ld_out), stream),
+              self.h, 'aec_crn_stream_step', True)
 
     def profile_enable(self, on: bool):
         check(self.lib.aec_crn_profile_enable(self.h, int(bool(on))), self.h, 'aec_crn_profile_enable', True)

@@ -187,6 +187,39 @@ class _DCCRNBase(nn.Module):
             h.stft(x.data_ptr(), lengths, B, N, spec.data_ptr(), torch.cuda.current_stream(x.device).cuda_stream)
         return torch.cat([spec[..., 0], spec[..., 1]], dim=2).transpose(1, 2)
 
+    # ---- streaming (include/aec_crn.h aec_crn_stream_*) ------------------------
+    def stream_open(self, B, device='cuda'):
+        """Open B concurrent streams (state zeroed).  Then feed one 256-sample
+        hop per stream per ``stream_step``; the output of step k is hop k-1 of
+        the batch forward's out_wav (the first step's output is the trimmed
+        warm-up region).  Feed N//256 + 1 hops per utterance, the last one
+        zero-padded."""
+        self._check(torch.zeros(1, device=device))
+        dev = torch.device(device)
+        h = self._handle(dev)
+        h.stream_open(B)
+        self._stream = (h, dev, int(B))
+
+    def stream_reset(self, b=-1):
+        h, dev, _ = self._stream
+        with torch.cuda.device(dev):
+            h.stream_reset(b, torch.cuda.current_stream(dev).cuda_stream)
+
+    def stream_step(self, mic_hop, far_hop, out=None):
+        """mic_hop / far_hop [B, 256] (row stride may exceed 256) -> out [B, 256]."""
+        h, dev, B = self._stream                         # (parameters as of stream_open)
+        if mic_hop.shape != (B, 256) or far_hop.shape != (B, 256):
+            raise ValueError(f'hops must be [{B}, 256]')
+        mic_hop = mic_hop.float()
+        far_hop = far_hop.float()
+        if mic_hop.stride(1) != 1 or far_hop.stride(1) != 1 or mic_hop.stride(0) != far_hop.stride(0):
+            mic_hop, far_hop = mic_hop.contiguous(), far_hop.contiguous()
+        out = torch.empty(B, 256, device=dev, dtype=torch.float32) if out is None else out
+        with torch.cuda.device(dev):
+            h.stream_step(mic_hop.data_ptr(), far_hop.data_ptr(), mic_hop.stride(0), out.data_ptr(), out.stride(0),
+                          torch.cuda.current_stream(dev).cuda_stream)
+        return out
+
     def forward_ragged(self, mic, far, lengths, want_spec=True, want_mask=False):
         """Rows zero-padded to a common width with true ``lengths``.  Returns
         (out_wav [B, 256*(max//256)] (row b valid to 256*(lengths[b]//256)),

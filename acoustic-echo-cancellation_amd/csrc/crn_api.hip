@@ -63,6 +63,8 @@ struct Packed {
 
 }  // namespace
 
+struct StreamState;
+
 struct aec_crn_handle {
     aec_crn_config cfg{};
     int device = 0;
@@ -85,6 +87,7 @@ struct aec_crn_handle {
     int64_t* d_len = nullptr;
     std::vector<int64_t> last_lens;                // host copy of what d_len holds
     std::vector<void*> allocs;
+    StreamState* ss = nullptr;                     // aec_crn_stream_* state
     // profiling
     int profile = 0;
     std::vector<hipEvent_t> ev;
@@ -450,29 +453,29 @@ static void mark(aec_crn_handle* h, hipStream_t st) {
     (void)hipEventRecord(h->ev[h->ev_used++], st);
 }
 
+// Feature buffers of one pass over F frames (batch: F = B*Tmax; stream: F = B)
+struct Bufs {
+    void* x0;
+    void* const* cat;       // [L+1], index 1..L
+    void* gx;
+    void* xn;
+    float* mask;
+};
+
 template <typename T>
-static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int32_t B, int64_t ld, int64_t Tmax,
-                      float* out, int64_t ld_out, float* spec, float* mask_out, hipStream_t st) {
+static aec_status run_encoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipStream_t st) {
     using crn::RowEpi;
     using crn::RowSrc;
     const int* ch = h->cfg.conv_channels;
-    const int L = h->L;
-    const int64_t BT = (int64_t)B * Tmax;
-    mark(h, st);
-    // front: X0 [BT][256][8]
-    crn::FrontArgs fa{mic, far, ld, h->d_len, Tmax, h->d_tab, h->x0, nullptr};
-    CRN_TRY(h, crn::launch_front<T>(fa, B, st));
-    mark(h, st);
-    // encoder
-    for (int i = 0; i < L; ++i) {
+    for (int i = 0; i < h->L; ++i) {
         const int Fin = 256 >> i, Fo = Fin / 2;
         const int cin = i == 0 ? 8 : ch[i];
         const int64_t ld_in = i == 0 ? 8 : 2 * ch[i];
         const int64_t choff = i == 0 ? 0 : ch[i];
         const Packed& pk = h->enc[i];
         RowSrc a{};
-        a.src = i == 0 ? h->x0 : h->cat[i];
-        a.M = BT * Fo;
+        a.src = i == 0 ? bf.x0 : bf.cat[i];
+        a.M = F * Fo;
         a.K = pk.K;
         a.rshift = ilog2(Fo);
         a.rs_hi = Fin * ld_in;
@@ -483,56 +486,73 @@ static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int
         a.padd = -2;
         a.plim = Fin;
         a.base_off = choff - 2 * ld_in;
-        a.src_elems = BT * Fin * ld_in;
+        a.src_elems = F * Fin * ld_in;
         const int64_t ldo = 2 * ch[i + 1];
-        RowEpi e{h->cat[i + 1], a.M, pk.N, a.rshift, Fo * ldo, ldo, ch[i + 1], pk.bias, pk.alpha, pk.act};
+        RowEpi e{bf.cat[i + 1], a.M, pk.N, a.rshift, Fo * ldo, ldo, ch[i + 1], pk.bias, pk.alpha, pk.act};
         CRN_TRY(h, (crn::launch_gemm_rows<T, T>(a, reinterpret_cast<const T*>(pk.w), pk.kpad,
                                                  (int)(pk.kpad * sizeof(T) / crn::kStageBytes), e, pk.npad, st)));
     }
-    mark(h, st);
-    // LSTM layers
-    const int H = h->H, S = h->S, C = h->CELLS, D = h->D, Q = h->Q;
-    for (int l = 0; l < h->nrnn; ++l) {
-        RowSrc a{};
-        int64_t ld_in, choff;
-        if (l == 0) {
-            a.src = h->cat[L];
-            ld_in = 2 * ch[L];
-            choff = ch[L];
-        } else {
-            a.src = h->xn;
-            ld_in = (int64_t)S * Q;
-            choff = 0;
-        }
-        a.M = BT * S;
-        a.K = H;
-        a.rshift = ilog2(S);
-        a.rs_hi = D * ld_in;
-        a.rs_lo = Q;
-        a.kshift = ilog2(Q);
-        a.ks = ld_in;
-        a.pmul = 0;
-        a.padd = 0;
-        a.plim = D;
-        a.base_off = choff;
-        a.src_elems = BT * D * ld_in;
-        const Packed& ih = h->lih[l];
-        RowEpi e{h->gx, a.M, ih.N, 0, (int64_t)C * 4 * H, 0, 0, ih.bias, 0.f, 0};
-        CRN_TRY(h, (crn::launch_gemm_rows<T, T>(a, reinterpret_cast<const T*>(ih.w), ih.kpad,
-                                                 (int)(ih.kpad * sizeof(T) / crn::kStageBytes), e, ih.npad, st)));
-        crn::StepArgs sa{h->lhh[l].w, h->gx, h->y, h->cst, B, H, Tmax, 0, 0};
-        for (int64_t t = 0; t < Tmax; ++t) {
-            sa.t = (int)t;
-            CRN_TRY(h, crn::launch_lstm_step<T>(sa, C, S, st));
-        }
-        const bool last = l + 1 == h->nrnn;
-        T* dst = reinterpret_cast<T*>(last ? h->cat[L] : h->xn);
-        const int64_t ldd = last ? 2 * ch[L] : (int64_t)S * Q;
-        CRN_TRY(h, crn::launch_lstm_combine<T>(reinterpret_cast<const T*>(h->y), dst, BT, H, C, S, ilog2(Q),
-                                               D * ldd, ldd, st));
+    return AEC_OK;
+}
+
+// LSTM layer l input projection for F frames -> bf.gx [F][S][CELLS*4H]
+template <typename T>
+static aec_status run_lstm_input(aec_crn_handle* h, const Bufs& bf, int l, int64_t F, hipStream_t st) {
+    using crn::RowEpi;
+    using crn::RowSrc;
+    const int* ch = h->cfg.conv_channels;
+    const int L = h->L, H = h->H, S = h->S, C = h->CELLS, D = h->D, Q = h->Q;
+    RowSrc a{};
+    int64_t ld_in, choff;
+    if (l == 0) {
+        a.src = bf.cat[L];
+        ld_in = 2 * ch[L];
+        choff = ch[L];
+    } else {
+        a.src = bf.xn;
+        ld_in = (int64_t)S * Q;
+        choff = 0;
     }
-    mark(h, st);
-    // decoder
+    a.M = F * S;
+    a.K = H;
+    a.rshift = ilog2(S);
+    a.rs_hi = D * ld_in;
+    a.rs_lo = Q;
+    a.kshift = ilog2(Q);
+    a.ks = ld_in;
+    a.pmul = 0;
+    a.padd = 0;
+    a.plim = D;
+    a.base_off = choff;
+    a.src_elems = F * D * ld_in;
+    const Packed& ih = h->lih[l];
+    RowEpi e{bf.gx, a.M, ih.N, 0, (int64_t)C * 4 * H, 0, 0, ih.bias, 0.f, 0};
+    CRN_TRY(h, (crn::launch_gemm_rows<T, T>(a, reinterpret_cast<const T*>(ih.w), ih.kpad,
+                                             (int)(ih.kpad * sizeof(T) / crn::kStageBytes), e, ih.npad, st)));
+    return AEC_OK;
+}
+
+// NavieComplexLSTM combination of layer l's h rows y [F][C][S][H] -> the next
+// layer's input (xn) or the decoder's dec half of cat[L]
+template <typename T>
+static aec_status run_lstm_combine(aec_crn_handle* h, const Bufs& bf, int l, const void* y, int64_t F,
+                                   hipStream_t st) {
+    const int* ch = h->cfg.conv_channels;
+    const int L = h->L, S = h->S, Q = h->Q;
+    const bool last = l + 1 == h->nrnn;
+    T* dst = reinterpret_cast<T*>(last ? bf.cat[L] : bf.xn);
+    const int64_t ldd = last ? 2 * ch[L] : (int64_t)S * Q;
+    CRN_TRY(h, crn::launch_lstm_combine<T>(reinterpret_cast<const T*>(y), dst, F, h->H, h->CELLS, S, ilog2(Q),
+                                           h->D * ldd, ldd, st));
+    return AEC_OK;
+}
+
+template <typename T>
+static aec_status run_decoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipStream_t st) {
+    using crn::RowEpi;
+    using crn::RowSrc;
+    const int* ch = h->cfg.conv_channels;
+    const int L = h->L;
     for (int d = 0; d < L; ++d) {
         const int cl = L - d;
         const int Fin = 256 >> cl, Fo = 2 * Fin;
@@ -540,8 +560,8 @@ static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int
         for (int par = 0; par < 2; ++par) {
             const Packed& pk = h->dec[2 * d + par];
             RowSrc a{};
-            a.src = h->cat[cl];
-            a.M = BT * Fin;
+            a.src = bf.cat[cl];
+            a.M = F * Fin;
             a.K = pk.K;
             a.rshift = ilog2(Fin);
             a.rs_hi = Fin * ld_in;
@@ -552,28 +572,63 @@ static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int
             a.padd = par == 0 ? -1 : 0;
             a.plim = Fin;
             a.base_off = a.padd * ld_in;
-            a.src_elems = BT * Fin * ld_in;
+            a.src_elems = F * Fin * ld_in;
             if (cl != 1) {
                 const int64_t ldo = 2 * ch[cl - 1];
-                RowEpi e{h->cat[cl - 1], a.M, pk.N, a.rshift, Fo * ldo, 2 * ldo, par * ldo, pk.bias, pk.alpha, pk.act};
+                RowEpi e{bf.cat[cl - 1], a.M, pk.N, a.rshift, Fo * ldo, 2 * ldo, par * ldo, pk.bias, pk.alpha, pk.act};
                 CRN_TRY(h, (crn::launch_gemm_rows<T, T>(a, reinterpret_cast<const T*>(pk.w), pk.kpad,
                                                          (int)(pk.kpad * sizeof(T) / crn::kStageBytes), e, pk.npad,
                                                          st)));
             } else {
-                RowEpi e{h->mask, a.M, pk.N, a.rshift, (int64_t)Fo * 2, 4, (int64_t)par * 2, pk.bias, pk.alpha, pk.act};
+                RowEpi e{bf.mask, a.M, pk.N, a.rshift, (int64_t)Fo * 2, 4, (int64_t)par * 2, pk.bias, pk.alpha, pk.act};
                 CRN_TRY(h, (crn::launch_gemm_rows<T, float>(a, reinterpret_cast<const T*>(pk.w), pk.kpad,
                                                              (int)(pk.kpad * sizeof(T) / crn::kStageBytes), e,
                                                              pk.npad, st)));
             }
         }
     }
+    return AEC_OK;
+}
+
+static int mask_mode(const aec_crn_handle* h) {
+    return h->cfg.version == 1 ? 1 : (h->cfg.masking_mode == 'E' ? 0 : h->cfg.masking_mode == 'C' ? 1 : 2);
+}
+
+template <typename T>
+static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int32_t B, int64_t ld, int64_t Tmax,
+                      float* out, int64_t ld_out, float* spec, float* mask_out, hipStream_t st) {
+    const int64_t BT = (int64_t)B * Tmax;
+    const Bufs bf{h->x0, h->cat.data(), h->gx, h->xn, h->mask};
+    const int H = h->H, S = h->S, C = h->CELLS;
     mark(h, st);
-    // back
-    const int mode = h->cfg.version == 1 ? 1 : (h->cfg.masking_mode == 'E' ? 0 : h->cfg.masking_mode == 'C' ? 1 : 2);
+    // front: X0 [Tmax][B][256][8]
+    crn::FrontArgs fa{mic, far, ld, h->d_len, Tmax, h->d_tab, h->x0, nullptr};
+    CRN_TRY(h, crn::launch_front<T>(fa, B, st));
+    mark(h, st);
+    aec_status s = run_encoder<T>(h, bf, BT, st);
+    if (s != AEC_OK) return s;
+    mark(h, st);
+    for (int l = 0; l < h->nrnn; ++l) {
+        s = run_lstm_input<T>(h, bf, l, BT, st);
+        if (s != AEC_OK) return s;
+        const int64_t ystride = (int64_t)B * C * S * H, gstride = (int64_t)B * S * C * 4 * H;   // per frame
+        for (int64_t t = 0; t < Tmax; ++t) {
+            crn::StepArgs sa{h->lhh[l].w, reinterpret_cast<const T*>(h->gx) + t * gstride,
+                             reinterpret_cast<const T*>(h->y) + (t > 0 ? t - 1 : 0) * ystride,
+                             reinterpret_cast<T*>(h->y) + t * ystride, h->cst, B, H, t == 0, 0};
+            CRN_TRY(h, crn::launch_lstm_step<T>(sa, C, S, st));
+        }
+        s = run_lstm_combine<T>(h, bf, l, h->y, BT, st);
+        if (s != AEC_OK) return s;
+    }
+    mark(h, st);
+    s = run_decoder<T>(h, bf, BT, st);
+    if (s != AEC_OK) return s;
+    mark(h, st);
     if (out || spec) {
         crn::BackArgs ba{mic, ld, h->d_len, Tmax, h->d_tab, reinterpret_cast<const float2*>(h->mask), out, ld_out,
                          reinterpret_cast<float2*>(spec)};
-        CRN_TRY(h, crn::launch_back(ba, B, mode, st));
+        CRN_TRY(h, crn::launch_back(ba, B, mask_mode(h), st));
     }
     if (mask_out)   // internal frames are t-major ([Tmax][B]); the ABI's mask is [B][Tmax]
         for (int b = 0; b < B; ++b)
@@ -584,6 +639,64 @@ static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int
     return AEC_OK;
 }
 
+// --------------------------------------------------------------------------
+// streaming: one 256-sample hop per stream per call (aec_crn_stream_*)
+// --------------------------------------------------------------------------
+struct StreamState {
+    int32_t B = 0;
+    int64_t k = 0;                       // hops consumed since open / reset-all
+    std::vector<void*> allocs;
+    void* x0 = nullptr;
+    std::vector<void*> cat;
+    void* gx = nullptr;
+    void* xn = nullptr;
+    float* mask = nullptr;
+    void* ring_y[8][2] = {};             // per LSTM layer: h ring (two frames)
+    float* cst[8] = {};                  // per LSTM layer: c
+    float* hop = nullptr;                // [2 parity][2 signal][B][256] input hop ring (mic, far)
+    float* tail = nullptr;               // [B][256] overlap-add tail
+    float* out = nullptr;                // [B][256] output hop
+    hipGraphExec_t graph[2] = {nullptr, nullptr};
+    hipStream_t cap = nullptr;           // capture stream
+};
+
+static void stream_free(aec_crn_handle* h) {
+    if (!h->ss) return;
+    for (int p = 0; p < 2; ++p)
+        if (h->ss->graph[p]) (void)hipGraphExecDestroy(h->ss->graph[p]);
+    for (void* p : h->ss->allocs) (void)hipFree(p);
+    if (h->ss->cap) (void)hipStreamDestroy(h->ss->cap);
+    delete h->ss;
+    h->ss = nullptr;
+}
+
+template <typename T>
+static aec_status stream_launches(aec_crn_handle* h, int par, hipStream_t st) {
+    StreamState& ss = *h->ss;
+    const int B = ss.B;
+    const Bufs bf{ss.x0, ss.cat.data(), ss.gx, ss.xn, ss.mask};
+    const float* cur_mic = ss.hop + (size_t)(par * 2 + 0) * B * 256;
+    const float* cur_far = ss.hop + (size_t)(par * 2 + 1) * B * 256;
+    const float* prev_mic = ss.hop + (size_t)((1 - par) * 2 + 0) * B * 256;
+    const float* prev_far = ss.hop + (size_t)((1 - par) * 2 + 1) * B * 256;
+    crn::StreamFrontArgs fa{prev_mic, cur_mic, prev_far, cur_far, h->d_tab, ss.x0, B};
+    CRN_TRY(h, crn::launch_stream_front<T>(fa, st));
+    aec_status s = run_encoder<T>(h, bf, B, st);
+    if (s != AEC_OK) return s;
+    for (int l = 0; l < h->nrnn; ++l) {
+        s = run_lstm_input<T>(h, bf, l, B, st);
+        if (s != AEC_OK) return s;
+        crn::StepArgs sa{h->lhh[l].w, ss.gx, ss.ring_y[l][1 - par], ss.ring_y[l][par], ss.cst[l], B, h->H, 0, 0};
+        CRN_TRY(h, crn::launch_lstm_step<T>(sa, h->CELLS, h->S, st));
+        s = run_lstm_combine<T>(h, bf, l, ss.ring_y[l][par], B, st);
+        if (s != AEC_OK) return s;
+    }
+    s = run_decoder<T>(h, bf, B, st);
+    if (s != AEC_OK) return s;
+    crn::StreamBackArgs ba{prev_mic, cur_mic, h->d_tab, reinterpret_cast<const float2*>(ss.mask), ss.tail, ss.out, B};
+    CRN_TRY(h, crn::launch_stream_back(ba, mask_mode(h), st));
+    return AEC_OK;
+}
 extern "C" {
 
 size_t aec_crn_param_count(const aec_crn_config* cfg) { return cfg ? param_count(*cfg) : 0; }
@@ -709,6 +822,118 @@ aec_status aec_crn_stft(aec_crn_handle* h, const float* x, const int64_t* length
     return AEC_OK;
 }
 
+aec_status aec_crn_stream_open(aec_crn_handle* h, int32_t B) {
+    if (!h || B <= 0) return AEC_ERR_INVALID_ARG;
+    if (!h->have_params) return crn_fail(h, AEC_ERR_INVALID_ARG, "parameters not set");
+    if (h->nrnn > 8) return crn_fail(h, AEC_ERR_UNSUPPORTED, "too many LSTM layers for streaming");
+    if (hipSetDevice(h->device) != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
+    stream_free(h);
+    h->ss = new (std::nothrow) StreamState();
+    if (!h->ss) return AEC_ERR_OOM;
+    StreamState& ss = *h->ss;
+    ss.B = B;
+    const size_t es = h->es;
+    const int* ch = h->cfg.conv_channels;
+    const int C = h->CELLS, S = h->S, H = h->H;
+    auto alloc = [&](void** p, size_t bytes) {
+        hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 16));
+        if (e == hipSuccess) {
+            ss.allocs.push_back(*p);
+            e = hipMemset(*p, 0, std::max<size_t>(bytes, 16));
+        }
+        return e;
+    };
+    CRN_TRY(h, alloc(&ss.x0, (size_t)B * 256 * 8 * es));
+    ss.cat.assign(h->L + 1, nullptr);
+    for (int l = 1; l <= h->L; ++l) CRN_TRY(h, alloc(&ss.cat[l], (size_t)B * (256 >> l) * 2 * ch[l] * es));
+    CRN_TRY(h, alloc(&ss.gx, (size_t)B * S * C * 4 * H * es));
+    if (h->nrnn > 1) CRN_TRY(h, alloc(&ss.xn, (size_t)B * S * H * es));
+    CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.mask), (size_t)B * 256 * 2 * sizeof(float)));
+    for (int l = 0; l < h->nrnn; ++l) {
+        CRN_TRY(h, alloc(&ss.ring_y[l][0], (size_t)B * C * S * H * es));
+        CRN_TRY(h, alloc(&ss.ring_y[l][1], (size_t)B * C * S * H * es));
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.cst[l]), (size_t)B * C * S * H * sizeof(float)));
+    }
+    CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.hop), (size_t)4 * B * 256 * sizeof(float)));
+    CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.tail), (size_t)B * 256 * sizeof(float)));
+    CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.out), (size_t)B * 256 * sizeof(float)));
+    CRN_TRY(h, hipStreamCreateWithFlags(&ss.cap, hipStreamNonBlocking));
+    CRN_TRY(h, hipDeviceSynchronize());
+    ss.k = 0;
+    return AEC_OK;
+}
+
+aec_status aec_crn_stream_reset(aec_crn_handle* h, int32_t b, void* stream) {
+    if (!h || !h->ss) return AEC_ERR_INVALID_ARG;
+    StreamState& ss = *h->ss;
+    if (b < -1 || b >= ss.B) return crn_fail(h, AEC_ERR_INVALID_ARG, "stream index out of range");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const size_t es = h->es;
+    const size_t hrow = (size_t)h->CELLS * h->S * h->H;       // elements of one stream's h / c rows
+    const int b0 = b < 0 ? 0 : b, nb = b < 0 ? ss.B : 1;
+    for (int l = 0; l < h->nrnn; ++l) {
+        for (int r = 0; r < 2; ++r)
+            CRN_TRY(h, hipMemsetAsync(reinterpret_cast<char*>(ss.ring_y[l][r]) + b0 * hrow * es, 0, nb * hrow * es, st));
+        CRN_TRY(h, hipMemsetAsync(ss.cst[l] + b0 * hrow, 0, nb * hrow * sizeof(float), st));
+    }
+    for (int q = 0; q < 4; ++q)
+        CRN_TRY(h, hipMemsetAsync(ss.hop + ((size_t)q * ss.B + b0) * 256, 0, (size_t)nb * 256 * sizeof(float), st));
+    CRN_TRY(h, hipMemsetAsync(ss.tail + (size_t)b0 * 256, 0, (size_t)nb * 256 * sizeof(float), st));
+    if (b < 0) ss.k = 0;
+    return AEC_OK;
+}
+
+aec_status aec_crn_stream_step(aec_crn_handle* h, const float* mic, const float* far, int64_t ld_in, float* out,
+                               int64_t ld_out, void* stream) {
+    if (!h || !h->ss) return AEC_ERR_INVALID_ARG;
+    if (!mic || !far || !out || ld_in < 256 || ld_out < 256) return crn_fail(h, AEC_ERR_INVALID_ARG, "bad hop buffers");
+    StreamState& ss = *h->ss;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (hipSetDevice(h->device) != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
+    const int par = (int)(ss.k & 1);
+    const int B = ss.B;
+    CRN_TRY(h, hipMemcpy2DAsync(ss.hop + (size_t)(par * 2 + 0) * B * 256, 256 * sizeof(float), mic,
+                                (size_t)ld_in * sizeof(float), 256 * sizeof(float), (size_t)B, hipMemcpyDeviceToDevice,
+                                st));
+    CRN_TRY(h, hipMemcpy2DAsync(ss.hop + (size_t)(par * 2 + 1) * B * 256, 256 * sizeof(float), far,
+                                (size_t)ld_in * sizeof(float), 256 * sizeof(float), (size_t)B, hipMemcpyDeviceToDevice,
+                                st));
+    static const int use_graph = [] {
+        const char* v = getenv("AEC_CRN_GRAPH");
+        return v ? atoi(v) : 1;
+    }();
+    bool launched = false;
+    if (use_graph) {
+        if (!ss.graph[par]) {
+            // capture the ~26 launches of one frame once per ring parity; replay every hop
+            hipGraph_t g = nullptr;
+            if (hipStreamBeginCapture(ss.cap, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+                const aec_status s = h->es == 4 ? stream_launches<float>(h, par, ss.cap)
+                                                : stream_launches<bf16_t>(h, par, ss.cap);
+                const hipError_t e = hipStreamEndCapture(ss.cap, &g);
+                if (s == AEC_OK && e == hipSuccess && g) {
+                    if (hipGraphInstantiate(&ss.graph[par], g, nullptr, nullptr, 0) != hipSuccess)
+                        ss.graph[par] = nullptr;
+                }
+                if (g) (void)hipGraphDestroy(g);
+                (void)hipGetLastError();
+            }
+        }
+        if (ss.graph[par]) {
+            CRN_TRY(h, hipGraphLaunch(ss.graph[par], st));
+            launched = true;
+        }
+    }
+    if (!launched) {
+        const aec_status s = h->es == 4 ? stream_launches<float>(h, par, st) : stream_launches<bf16_t>(h, par, st);
+        if (s != AEC_OK) return s;
+    }
+    CRN_TRY(h, hipMemcpy2DAsync(out, (size_t)ld_out * sizeof(float), ss.out, 256 * sizeof(float), 256 * sizeof(float),
+                                (size_t)B, hipMemcpyDeviceToDevice, st));
+    ss.k++;
+    return AEC_OK;
+}
+
 aec_status aec_crn_profile_enable(aec_crn_handle* h, int32_t enable) {
     if (!h) return AEC_ERR_INVALID_ARG;
     h->profile = enable != 0;
@@ -729,6 +954,7 @@ aec_status aec_crn_profile_read(aec_crn_handle* h, double* ms5, int64_t* calls) 
 void aec_crn_destroy(aec_crn_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
+    stream_free(h);
     for (void* p : h->allocs) (void)hipFree(p);
     for (auto* v : {&h->enc, &h->dec, &h->lih, &h->lhh})
         for (Packed& pk : *v) {

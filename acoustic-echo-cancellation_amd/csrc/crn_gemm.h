@@ -177,9 +177,9 @@ __device__ __forceinline__ void gemm_core(f32x4 (&acc)[FM][FN], char* smem, cons
 // bank slots.  A lane of DMA instruction i fills row 8i + (lane >> 3), slot
 // lane & 7, so it fetches logical chunk (lane & 7) ^ ((row >> 1) & 7).
 // aoff(i, kbyte) / boff(i, kbyte): the lane's byte offset into ra / rb for
-// its row of A / B instruction i (i < BM/32 resp. BN/32 per wave, rows
-// 8 (4 i + wave) + lane/8) at K-byte kbyte, or 0x80000000 (out of range ->
-// the hardware writes zeros).  BM, BN multiples of 32.
+// its row of A / B instruction i (i < BM/(8 NW) resp. BN/(8 NW) per wave,
+// rows 8 (NW i + wave) + lane/8, NW waves) at K-byte kbyte, or 0x80000000
+// (out of range -> the hardware writes zeros).  BM, BN multiples of 8 NW.
 // --------------------------------------------------------------------------
 __device__ __forceinline__ int swz_slot(int row, int q) { return q ^ ((row >> 1) & 7); }
 
@@ -190,12 +190,12 @@ __device__ __forceinline__ void wait_vm() {
     __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
-template <typename T, int BM, int BN, int FM, int FN, int NBUF, class AO, class BO>
+template <typename T, int BM, int BN, int FM, int FN, int NBUF, class AO, class BO, int NW = 4>
 __device__ __forceinline__ void gemm_core_dma(f32x4 (&acc)[FM][FN], char* smem, __amdgpu_buffer_rsrc_t ra,
                                               __amdgpu_buffer_rsrc_t rb, const AO& aoff, const BO& boff,
                                               int nstages, int wr0, int wc0) {
-    static_assert(BM % 32 == 0 && BN % 32 == 0 && NBUF >= 2, "tile");
-    constexpr int LA = BM / 32, LB = BN / 32;          // DMA instructions per wave per stage
+    static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0 && NBUF >= 2, "tile");
+    constexpr int LA = BM / (8 * NW), LB = BN / (8 * NW);   // DMA instructions per wave per stage
     constexpr int STAGE = (BM + BN) * 128;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int q_l = lane & 7;
@@ -203,17 +203,17 @@ __device__ __forceinline__ void gemm_core_dma(f32x4 (&acc)[FM][FN], char* smem, 
         char* buf = smem + (st % NBUF) * STAGE;
 #pragma unroll
         for (int i = 0; i < LA; ++i) {
-            const int row = 8 * (4 * i + wave) + (lane >> 3);
+            const int row = 8 * (NW * i + wave) + (lane >> 3);
             const uint32_t vo = aoff(i, st * 128 + swz_slot(row, q_l) * 16);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                ra, (__attribute__((address_space(3))) void*)(buf + 8 * (4 * i + wave) * 128), 16, vo, 0, 0, 0);
+                ra, (__attribute__((address_space(3))) void*)(buf + 8 * (NW * i + wave) * 128), 16, vo, 0, 0, 0);
         }
 #pragma unroll
         for (int i = 0; i < LB; ++i) {
-            const int row = 8 * (4 * i + wave) + (lane >> 3);
+            const int row = 8 * (NW * i + wave) + (lane >> 3);
             const uint32_t vo = boff(i, st * 128 + swz_slot(row, q_l) * 16);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rb, (__attribute__((address_space(3))) void*)(buf + BM * 128 + 8 * (4 * i + wave) * 128), 16, vo, 0,
+                rb, (__attribute__((address_space(3))) void*)(buf + BM * 128 + 8 * (NW * i + wave) * 128), 16, vo, 0,
                 0, 0);
         }
     };

@@ -256,6 +256,169 @@ __global__ __launch_bounds__(256) void crn_back_kernel(BackArgs p) {
 }
 
 // --------------------------------------------------------------------------
+// Streaming front / back: one 16-lane group per stream, 16 streams per block.
+// The group stages its frame [prev hop | cur hop] in its own LDS region (the
+// hop layout load_frame reads) and runs the same transform code as the
+// batch kernels, so a streamed frame is bit-identical to the batch frame.
+// --------------------------------------------------------------------------
+__device__ __forceinline__ void stage_frame(float* reg, const float* prev, const float* cur, int lb) {
+    const float4* p4 = reinterpret_cast<const float4*>(prev) + lb * 4;
+    const float4* c4 = reinterpret_cast<const float4*>(cur) + lb * 4;
+    float4* r0 = reinterpret_cast<float4*>(reg) + lb * 4;
+    float4* r1 = reinterpret_cast<float4*>(reg + aec::kHopStride) + lb * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        r0[i] = p4[i];
+        r1[i] = c4[i];
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void crn_stream_front_kernel(StreamFrontArgs p) {
+    __shared__ __attribute__((aligned(16))) float smem[256 * 2 + 258 * 2 + 512 + 16 * kGroupFloats];
+    float2* sTwT = reinterpret_cast<float2*>(smem);
+    float2* sTw512 = sTwT + 256;
+    float* sHann = reinterpret_cast<float*>(sTw512 + 258);
+    float* sGrp = sHann + 512;
+    const int tid = threadIdx.x;
+    sTwT[tid] = p.tab->twT[tid];
+    sTw512[tid] = p.tab->tw512[tid];
+    if (tid < 2) sTw512[256 + tid] = p.tab->tw512[256 + tid];
+    sHann[tid] = p.tab->hann[tid];
+    sHann[tid + 256] = p.tab->hann[tid + 256];
+    __syncthreads();
+    const int g = tid >> 4, lb = tid & 15;
+    const int b = blockIdx.x * 16 + g;
+    const int bb = b < p.B ? b : p.B - 1;
+    float* reg = sGrp + g * kGroupFloats;
+    float2 ma[8], mb[8], m128, fa[8], fb[8], f128;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        stage_frame(reg, (s == 0 ? p.prev_mic : p.prev_far) + (int64_t)bb * 256,
+                    (s == 0 ? p.cur_mic : p.cur_far) + (int64_t)bb * 256, lb);
+        aec::wave_fence();
+        float2 v[16];
+        aec::load_frame(v, reg, sHann, 0, lb);
+        aec::wave_fence();
+        aec::fft256<false>(v, lb, reg, sTwT);
+        if (s == 0)
+            aec::rfft_unpack(v, lb, sTw512, ma, mb, m128);
+        else
+            aec::rfft_unpack(v, lb, sTw512, fa, fb, f128);
+        aec::wave_fence();
+    }
+    if (b >= p.B) return;
+    T* row = reinterpret_cast<T*>(p.x0) + (int64_t)b * 256 * 8;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const int k = lb + 16 * m;
+        if (k != 0) put_bin<T>(row, k, ma[m], fa[m]);
+        put_bin<T>(row, 256 - k, mb[m], fb[m]);
+    }
+    if (lb == 0) put_bin<T>(row, 128, m128, f128);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void crn_stream_back_kernel(StreamBackArgs p) {
+    __shared__ __attribute__((aligned(16))) float smem[258 * 2 + 256 * 2 + 512 + 256 + 16 * kGroupFloats];
+    float2* sTw512 = reinterpret_cast<float2*>(smem);
+    float2* sTwT = sTw512 + 258;
+    float* sHann = reinterpret_cast<float*>(sTwT + 256);
+    float* sCoff = sHann + 512;
+    float* sGrp = sCoff + 256;
+    const int tid = threadIdx.x;
+    sTwT[tid] = p.tab->twT[tid];
+    sTw512[tid] = p.tab->tw512[tid];
+    if (tid < 2) sTw512[256 + tid] = p.tab->tw512[256 + tid];
+    sHann[tid] = p.tab->hann[tid];
+    sHann[tid + 256] = p.tab->hann[tid + 256];
+    sCoff[tid] = p.tab->inv_coff[tid];
+    __syncthreads();
+    const int g = tid >> 4, lb = tid & 15;
+    const int b = blockIdx.x * 16 + g;
+    const int bb = b < p.B ? b : p.B - 1;
+    float* reg = sGrp + g * kGroupFloats;
+    stage_frame(reg, p.prev_mic + (int64_t)bb * 256, p.cur_mic + (int64_t)bb * 256, lb);
+    aec::wave_fence();
+    float2 v[16];
+    float2 xa[8], xb[8], x128;
+    aec::load_frame(v, reg, sHann, 0, lb);
+    aec::wave_fence();
+    aec::fft256<false>(v, lb, reg, sTwT);
+    aec::rfft_unpack(v, lb, sTw512, xa, xb, x128);
+    const float2* mrow = p.mask + (int64_t)bb * 256;
+    const float2 z = make_float2(0.f, 0.f);
+    auto mk = [&](int bin) { return bin > 0 ? mrow[bin - 1] : z; };
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const int kk = lb + 16 * m;
+        xa[m] = apply_mask<MODE>(xa[m], mk(kk));
+        xb[m] = apply_mask<MODE>(xb[m], mk(256 - kk));
+    }
+    x128 = apply_mask<MODE>(x128, mk(128));
+    float2 Zk[8], Zmk[8];
+    aec::static_for<0, 8>([&](auto mi) {
+        constexpr int m = decltype(mi)::value;
+        const int kk = lb + 16 * m;
+        float2 zk, zmk;
+        aec::irfft_pair(xa[m], xb[m], sTw512[kk], zk, zmk);
+        const float s0 = xa[m].x, s256 = xb[m].x;
+        Zk[m] = aec::csel(kk == 0, make_float2(s0 + s256, s0 - s256), zk);
+        Zmk[m] = aec::csel(kk == 0, Zk[m], zmk);
+    });
+    float2 z128 = make_float2(0.f, 0.f);
+    if (lb == 0) z128 = make_float2(2.f * x128.x, -2.f * x128.y);
+#pragma unroll
+    for (int a = 0; a < 8; ++a) v[a] = Zk[a];
+    aec::static_for<8, 16>([&](auto ai) {
+        constexpr int a = decltype(ai)::value;
+        const float2 mir = aec::mirror16(Zmk[15 - a]);
+        v[a] = aec::csel(lb != 0, mir, a == 8 ? z128 : Zmk[(16 - a) & 7]);
+    });
+    aec::wave_fence();
+    aec::fft256<true>(v, lb, reg, sTwT);
+    float2* s2 = reinterpret_cast<float2*>(reg);
+    const float2* h2 = reinterpret_cast<const float2*>(sHann);
+#pragma unroll
+    for (int m2 = 0; m2 < 16; ++m2) {
+        const float2 zz = v[aec::kP(m2)];
+        const float2 w = h2[lb + 16 * m2];
+        s2[lb + 16 * m2] = make_float2(zz.x * (w.x * (1.f / 512.f)), zz.y * (w.y * (1.f / 512.f)));
+    }
+    aec::wave_fence();
+    if (b >= p.B) return;
+    float* tail = p.tail + (int64_t)b * 256;
+    float* out = p.out + (int64_t)b * 256;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int r = lb + 16 * i;
+        out[r] = (tail[r] + reg[r]) * sCoff[r];
+        tail[r] = reg[256 + r];
+    }
+}
+
+template <typename T>
+hipError_t launch_stream_front(const StreamFrontArgs& a, hipStream_t st) {
+    if (a.B <= 0) return hipSuccess;
+    hipLaunchKernelGGL((crn_stream_front_kernel<T>), dim3((unsigned)((a.B + 15) / 16)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+template hipError_t launch_stream_front<float>(const StreamFrontArgs&, hipStream_t);
+template hipError_t launch_stream_front<bf16_t>(const StreamFrontArgs&, hipStream_t);
+
+hipError_t launch_stream_back(const StreamBackArgs& a, int mode, hipStream_t st) {
+    if (a.B <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((a.B + 15) / 16));
+    switch (mode) {
+        case 0: hipLaunchKernelGGL(crn_stream_back_kernel<0>, grid, dim3(256), 0, st, a); break;
+        case 1: hipLaunchKernelGGL(crn_stream_back_kernel<1>, grid, dim3(256), 0, st, a); break;
+        case 2: hipLaunchKernelGGL(crn_stream_back_kernel<2>, grid, dim3(256), 0, st, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// --------------------------------------------------------------------------
 // Row GEMM (encoder / decoder convs, LSTM input projection)
 // --------------------------------------------------------------------------
 template <typename OutT>
@@ -296,13 +459,15 @@ __device__ __forceinline__ void rows_epilogue(const f32x4 (&acc)[FM][FN], const 
         }
 }
 
-// LDS-staged variant for the DMA kernel: the wave's (FM*16) x (FN*16) tile
-// goes through LDS (after bias + activation) and leaves as 16-byte row
-// chunks (N and the output channel offsets are multiples of 8).
-template <typename OutT, int FM, int FN>
+// LDS-staged variant: the wave's (FM*16) x (FN*16) tile goes through LDS
+// (after bias + activation) in passes of PF row fragments and leaves as
+// 16-byte row chunks (N and the output channel offsets are multiples of 16
+// bytes).  wlds: the wave's PF*16 x FN*16 staging area.
+template <typename OutT, int FM, int FN, int PF>
 __device__ __forceinline__ void rows_epilogue_lds(const f32x4 (&acc)[FM][FN], const RowEpi& e, int64_t mb, int nb,
                                                   int lane, char* wlds) {
-    constexpr int WR = FM * 16, WC = FN * 16;
+    static_assert(FM % PF == 0, "passes");
+    constexpr int WC = FN * 16;
     constexpr int RB = WC * (int)sizeof(OutT);          // bytes per staged row
     constexpr int CPR = RB / 16;                         // 16-B chunks per row
     constexpr int EPC = 16 / (int)sizeof(OutT);          // elements per chunk
@@ -314,31 +479,44 @@ __device__ __forceinline__ void rows_epilogue_lds(const f32x4 (&acc)[FM][FN], co
     }
     const int act = e.act;
     const float alpha = e.alpha;
+    const int64_t omask = (1ll << e.oshift) - 1;
     OutT* st = reinterpret_cast<OutT*>(wlds);
 #pragma unroll
-    for (int fm = 0; fm < FM; ++fm)
+    for (int p0 = 0; p0 < FM; p0 += PF) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+        for (int f = 0; f < PF; ++f)
 #pragma unroll
-            for (int fn = 0; fn < FN; ++fn) {
-                float v = acc[fm][fn][r] + bias[fn];
-                v = act == 1 ? (v >= 0.f ? v : alpha * v) : act == 2 ? tanhf(v) : v;
-                st[(fm * 16 + 4 * (lane >> 4) + r) * WC + fn * 16 + (lane & 15)] = to_elem<OutT>(v);
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int fn = 0; fn < FN; ++fn) {
+                    float v = acc[p0 + f][fn][r] + bias[fn];
+                    v = act == 1 ? (v >= 0.f ? v : alpha * v) : act == 2 ? tanhf(v) : v;
+                    st[(f * 16 + 4 * (lane >> 4) + r) * WC + fn * 16 + (lane & 15)] = to_elem<OutT>(v);
+                }
+        aec::wave_fence();
+#pragma unroll
+        for (int it = 0; it < PF * 16 * CPR / 64; ++it) {
+            const int c = it * 64 + lane;
+            const int row = c / CPR, ch = c % CPR;
+            const int64_t m = mb + p0 * 16 + row;
+            const int n = nb + ch * EPC;
+            if (m < e.M && n < e.N) {
+                const u32x4 v = *reinterpret_cast<const u32x4*>(wlds + row * RB + ch * 16);
+                OutT* o =
+                    reinterpret_cast<OutT*>(e.out) + (m >> e.oshift) * e.o_hi + (m & omask) * e.o_lo + e.o_add + n;
+                *reinterpret_cast<u32x4*>(o) = v;
             }
-    aec::wave_fence();
-    const int64_t omask = (1ll << e.oshift) - 1;
-#pragma unroll
-    for (int it = 0; it < WR * CPR / 64; ++it) {
-        const int c = it * 64 + lane;
-        const int row = c / CPR, ch = c % CPR;
-        const int64_t m = mb + row;
-        const int n = nb + ch * EPC;
-        if (m < e.M && n < e.N) {
-            const u32x4 v = *reinterpret_cast<const u32x4*>(wlds + row * RB + ch * 16);
-            OutT* o = reinterpret_cast<OutT*>(e.out) + (m >> e.oshift) * e.o_hi + (m & omask) * e.o_lo + e.o_add + n;
-            *reinterpret_cast<u32x4*>(o) = v;
         }
+        aec::wave_fence();
     }
+}
+
+// largest pass count PF (dividing FM) whose NW staging areas fit in `bytes`
+template <typename OutT, int FM, int FN, int NW>
+constexpr int epi_passes(size_t bytes) {
+    int pf = FM;
+    while (pf > 1 && (size_t)NW * pf * 16 * FN * 16 * sizeof(OutT) > bytes) pf /= 2;
+    return pf;
 }
 
 template <typename T, typename OutT, int WM, int WN, int FM, int FN>
@@ -364,16 +542,24 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(RowSrc a, const T* __res
         return *reinterpret_cast<const u32x4*>(bbase + (int64_t)r * ldb * (int64_t)sizeof(T) + kb);
     };
     gemm_core<T, BM, BN, FM, FN>(acc, smem, al, bl, nstages, wr0, wc0);
-
-    rows_epilogue<OutT, FM, FN>(acc, e, m0 + wr0, n0 + wc0, lane);
+    if (e.N % (16 / (int)sizeof(OutT)) == 0) {          // 16-B row chunks stay inside the N columns
+        __syncthreads();
+        constexpr int PF = epi_passes<OutT, FM, FN, 4>((size_t)(BM + BN) * kRowStride);
+        static_assert(4 * PF * 16 * FN * 16 * sizeof(OutT) <= (size_t)(BM + BN) * kRowStride, "epilogue LDS");
+        rows_epilogue_lds<OutT, FM, FN, PF>(acc, e, m0 + wr0, n0 + wc0, lane,
+                                            smem + wave * (PF * 16 * FN * 16 * (int)sizeof(OutT)));
+    } else {
+        rows_epilogue<OutT, FM, FN>(acc, e, m0 + wr0, n0 + wc0, lane);
+    }
 }
 
 // Same GEMM through the LDS-DMA main loop (tiles with BM, BN multiples of 32).
 template <typename T, typename OutT, int WM, int WN, int FM, int FN, int NBUF>
-__global__ __launch_bounds__(256) void gemm_rows_dma_kernel(RowSrc a, const T* __restrict__ bt, int64_t ldb,
-                                                             int nstages, RowEpi e) {
+__global__ __launch_bounds__(64 * WM * WN) void gemm_rows_dma_kernel(RowSrc a, const T* __restrict__ bt, int64_t ldb,
+                                                                     int nstages, RowEpi e) {
     constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
-    constexpr int LA = BM / 32;
+    constexpr int NW = WM * WN;
+    constexpr int LA = BM / (8 * NW);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // 1-D grid, column blocks fastest: the column tiles of one row tile run
     // together (the A rows are read once from HBM and re-used through L2/MALL)
@@ -391,7 +577,7 @@ __global__ __launch_bounds__(256) void gemm_rows_dma_kernel(RowSrc a, const T* _
     bool mval[LA];
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
-        const int64_t m = m0 + 8 * (4 * i + wave) + (lane >> 3);
+        const int64_t m = m0 + 8 * (NW * i + wave) + (lane >> 3);
         const int64_t hi = m >> a.rshift;
         const int lo = (int)(m & ((1ll << a.rshift) - 1));
         rowoff[i] = (int32_t)((hi - hi0) * a.rs_hi + (int64_t)lo * a.rs_lo + a.base_off);
@@ -407,18 +593,20 @@ __global__ __launch_bounds__(256) void gemm_rows_dma_kernel(RowSrc a, const T* _
         return ok ? (uint32_t)((rowoff[i] + tap * (int32_t)a.ks + (k & kmask)) * ES) : kOOB;
     };
     auto boff = [&](int i, int kbyte) -> uint32_t {
-        return (uint32_t)((8 * (4 * i + wave) + (lane >> 3)) * (int32_t)ldb * ES + kbyte);
+        return (uint32_t)((8 * (NW * i + wave) + (lane >> 3)) * (int32_t)ldb * ES + kbyte);
     };
     f32x4 acc[FM][FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gemm_core_dma<T, BM, BN, FM, FN, NBUF>(acc, smem, ra, rb, aoff, boff, nstages, wr0, wc0);
+    gemm_core_dma<T, BM, BN, FM, FN, NBUF, decltype(aoff), decltype(boff), NW>(acc, smem, ra, rb, aoff, boff, nstages,
+                                                                               wr0, wc0);
     __syncthreads();                                   // every wave is done with the stage buffers
-    static_assert(4 * FM * 16 * FN * 16 * sizeof(OutT) <= (size_t)NBUF * (BM + BN) * 128, "epilogue LDS");
-    rows_epilogue_lds<OutT, FM, FN>(acc, e, m0 + wr0, n0 + wc0, lane,
-                                    smem + wave * (FM * 16 * FN * 16 * (int)sizeof(OutT)));
+    constexpr int PF = epi_passes<OutT, FM, FN, NW>((size_t)NBUF * (BM + BN) * 128);
+    static_assert(NW * PF * 16 * FN * 16 * sizeof(OutT) <= (size_t)NBUF * (BM + BN) * 128, "epilogue LDS");
+    rows_epilogue_lds<OutT, FM, FN, PF>(acc, e, m0 + wr0, n0 + wc0, lane,
+                                        smem + wave * (PF * 16 * FN * 16 * (int)sizeof(OutT)));
 }
 
 static int env_int(const char* name, int dflt) {
@@ -451,9 +639,10 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
         if (attr != hipSuccess) return attr;                                                                      \
         const unsigned nbn_ = (unsigned)(npad / BN);                                                              \
         dim3 grid((unsigned)((a.M + BM - 1) / BM) * nbn_);                                                        \
-        hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a, bt, ldb, nstages, e);                               \
+        hipLaunchKernelGGL(kern, grid, dim3(64 * WM * WN), lds, st, a, bt, ldb, nstages, e);                      \
     } while (0)
     static const int dma = env_int("CRN_GEMM_DMA", 2);    // 0 = register-staged core, else NBUF
+    static const int big = env_int("CRN_GEMM_BIG", 0);    // 256x128 tiles (8 waves) for large M (measured slower)
     switch (bn) {
         case 16: CRN_GEMM(4, 1, 4, 1); break;
         case 32: CRN_GEMM(2, 2, 4, 1); break;
@@ -464,7 +653,8 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
             else CRN_GEMM(2, 2, 4, 2);
             break;
         default:
-            if (dma == 2) CRN_GEMM_DMA(2, 2, 4, 4, 2);
+            if (big && a.M >= 256 * 1024) CRN_GEMM_DMA(4, 2, 4, 4, 2);
+            else if (dma == 2) CRN_GEMM_DMA(2, 2, 4, 4, 2);
             else if (dma == 3) CRN_GEMM_DMA(2, 2, 4, 4, 3);
             else if (dma >= 4) CRN_GEMM_DMA(2, 2, 4, 4, 4);
             else CRN_GEMM(2, 2, 4, 4);
@@ -537,14 +727,14 @@ __global__ __launch_bounds__(256) void lstm_step_kernel(StepArgs p) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int uh = wave & 1;
     const int wr0 = (wave >> 1) * (BM / 2), wc0 = uh * 64;
-    const int t = p.t;
+    const bool first = p.first != 0;
     const int64_t ystride = (int64_t)CELLS * S * H;            // elements per (stream, frame)
     const int64_t gstride = (int64_t)CELLS * 4 * H;            // Gx elements per (stream, frame, s)
 
     // 1. DMA the epilogue's Gx (and c) tiles into LDS first: the oldest vector-memory
     //    ops, retired by the main loop's first wait (or the explicit wait at t = 0)
     if (!(p.mode & 4)) {
-        const T* gbase = reinterpret_cast<const T*>(p.gx) + ((int64_t)t * p.B + b0) * S * gstride;
+        const T* gbase = reinterpret_cast<const T*>(p.gx) + (int64_t)b0 * S * gstride;
         const __amdgpu_buffer_rsrc_t rg =
             make_rsrc(gbase, (uint64_t)((int64_t)(p.B - b0) * S * gstride) * ES);
         constexpr int GCH = GROW / 16;                   // 16-B chunks per Gx row
@@ -561,7 +751,7 @@ __global__ __launch_bounds__(256) void lstm_step_kernel(StepArgs p) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
                 rg, (__attribute__((address_space(3))) void*)(sG + (4 * i + wave) * 1024), 16, vo, 0, 0, 2);
         }
-        if (t > 0) {
+        if (!first) {
             const float* cbase = p.cst + (int64_t)b0 * CELLS * S * H;
             const __amdgpu_buffer_rsrc_t rc = make_rsrc(cbase, (uint64_t)(p.B - b0) * CELLS * S * H * 4);
             constexpr int CI = BM * (U * 4 / 16) / 256;
@@ -584,8 +774,8 @@ __global__ __launch_bounds__(256) void lstm_step_kernel(StepArgs p) {
     for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (t > 0 && !(p.mode & 2)) {
-        const T* ybase = reinterpret_cast<const T*>(p.y) + ((int64_t)(t - 1) * p.B + b0) * ystride;
+    if (!first && !(p.mode & 2)) {
+        const T* ybase = reinterpret_cast<const T*>(p.y_prev) + (int64_t)b0 * ystride;
         const __amdgpu_buffer_rsrc_t ra = make_rsrc(ybase, (uint64_t)((int64_t)(p.B - b0) * ystride) * ES);
         const __amdgpu_buffer_rsrc_t rb =
             make_rsrc(reinterpret_cast<const T*>(p.whh) + ((int64_t)cell * 4 * H + (int64_t)unit0 * 4) * H,
@@ -628,7 +818,7 @@ __global__ __launch_bounds__(256) void lstm_step_kernel(StepArgs p) {
                     g = *reinterpret_cast<const float4*>(sG + r * GROW + jl * 16);
                 }
                 float* cslot = reinterpret_cast<float*>(sC + r * U * 4 + jl * 4);
-                const float cp = t > 0 ? *cslot : 0.f;
+                const float cp = first ? 0.f : *cslot;
                 const float c = fsigmoid(acc[fm][1][rr] + g.y) * cp +
                                 fsigmoid(acc[fm][0][rr] + g.x) * ftanh(acc[fm][2][rr] + g.z);
                 const float h = fsigmoid(acc[fm][3][rr] + g.w) * ftanh(c);
@@ -638,7 +828,7 @@ __global__ __launch_bounds__(256) void lstm_step_kernel(StepArgs p) {
     }
     __syncthreads();
     // c rows: U*4 bytes at cst[((b*CELLS + cell)*S + s)*H + unit0]; h rows: U*ES bytes at y[t]
-    T* Yo = reinterpret_cast<T*>(p.y);
+    T* Yo = reinterpret_cast<T*>(p.y_cur);
     constexpr int CCH = U * 4 / 16, HCH = U * ES / 16;
 #pragma unroll
     for (int i = 0; i < BM * CCH / 256; ++i) {
@@ -658,7 +848,7 @@ __global__ __launch_bounds__(256) void lstm_step_kernel(StepArgs p) {
         const int s = r / SB, bl = r % SB;
         if (b0 + bl < p.B) {
             const u32x4 v = *reinterpret_cast<const u32x4*>(sH + r * U * ES + ch * 16);
-            *reinterpret_cast<u32x4*>(Yo + ((((int64_t)t * p.B + b0 + bl) * CELLS + cell) * S + s) * H + unit0 +
+            *reinterpret_cast<u32x4*>(Yo + ((((int64_t)b0 + bl) * CELLS + cell) * S + s) * H + unit0 +
                                       ch * (16 / ES)) = v;
         }
     }

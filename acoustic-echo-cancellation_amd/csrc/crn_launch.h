@@ -55,14 +55,39 @@ struct RowEpi {
 // v2 NavieComplexLSTM: 2x2), gate columns packed per 16 units (i|f|g|o).
 struct StepArgs {
     const void* whh;            // [CELLS*4H][H]
-    const void* gx;             // [Tmax][B][S][CELLS*4H]  (input projection + both biases, gates of a unit adjacent)
-    void* y;                    // [Tmax][B][CELLS][S][H]
-    float* cst;                 // [B][CELLS][S][H]
+    const void* gx;             // this frame's Gx rows [B][S][CELLS*4H] (input projection + both biases,
+                                // the 4 gates of a unit adjacent)
+    const void* y_prev;         // h_{t-1} [B][CELLS][S][H]  (unused when first)
+    void* y_cur;                // h_t     [B][CELLS][S][H]
+    float* cst;                 // c       [B][CELLS][S][H]  (read unless first, written)
     int32_t B, H;
-    int64_t Tmax;
-    int32_t t;
+    int32_t first;              // frame 0: h_{-1} = c_{-1} = 0
     int32_t mode;               // timing experiments only (CRN_STEP_MODE)
 };
+
+// Streaming (one hop per stream): frame = [prev hop, cur hop] of each stream
+struct StreamFrontArgs {
+    const float* prev_mic;      // [B][256]
+    const float* cur_mic;
+    const float* prev_far;
+    const float* cur_far;
+    const aec::DevTables* tab;
+    void* x0;                   // [B][256][8]
+    int32_t B;
+};
+struct StreamBackArgs {
+    const float* prev_mic;
+    const float* cur_mic;
+    const aec::DevTables* tab;
+    const float2* mask;         // [B][256]
+    float* tail;                // [B][256] overlap-add state (in / out)
+    float* out;                 // [B][256] output hop (the previous hop of the stream)
+    int32_t B;
+};
+
+template <typename T>
+hipError_t launch_stream_front(const StreamFrontArgs& a, hipStream_t st);
+hipError_t launch_stream_back(const StreamBackArgs& a, int mode, hipStream_t st);
 
 template <typename T, typename OutT>
 hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstages, const RowEpi& e, int npad,

@@ -93,6 +93,27 @@ aec_status aec_crn_process(aec_crn_handle* h, const float* mic, const float* far
 aec_status aec_crn_stft(aec_crn_handle* h, const float* x, const int64_t* lengths, int32_t B, int64_t ld,
                         float* spec, void* stream);
 
+/* Streaming (serving): one 256-sample hop per stream per call, the per-frame
+ * loop of the same network (the DCCRN has no utterance-global statistic, so a
+ * streamed utterance equals the batch result: frame t needs hops t-1 and t,
+ * ConvSTFT framing dccrn.py:45-52).  The ~26 launches of one frame are
+ * captured once in a hipGraph per ring parity and replayed (AEC_CRN_GRAPH=0:
+ * direct launches).
+ *   aec_crn_stream_open(h, B)        B concurrent streams; state zeroed
+ *   aec_crn_stream_reset(h, b, st)   zero stream b's state (-1: all, and the hop counter)
+ *   aec_crn_stream_step(h, mic, far, ld_in, out, ld_out, st)
+ *        mic, far: device [B, ld_in] float32, hop k of every stream (samples
+ *        256k .. 256k+255; zero-pad a final partial hop);
+ *        out: device [B, ld_out] float32 receives output hop k-1 (the
+ *        reference's out_wav[256(k-1) : 256k]); the output of a stream's first
+ *        step is the warm-up region the reference trims (dccrn.py:99), and
+ *        one extra all-zero hop after the last input hop flushes the final
+ *        output hop. */
+aec_status aec_crn_stream_open(aec_crn_handle* h, int32_t B);
+aec_status aec_crn_stream_reset(aec_crn_handle* h, int32_t b, void* stream);
+aec_status aec_crn_stream_step(aec_crn_handle* h, const float* mic, const float* far, int64_t ld_in, float* out,
+                               int64_t ld_out, void* stream);
+
 /* Kernel timing (HIP events on `stream`): ms[0..4] = front, encoder,
  * lstm (input projection + steps + combine), decoder, back; summed over the
  * calls since the previous read. */
