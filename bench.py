@@ -172,6 +172,24 @@ def cpu_baseline_crn(seconds, conf, version, n=160000, B=1):
                        f'(reference op mix: conv2d / conv_transpose2d / nn.LSTM, float32), {el:.1f} s wall')
 
 
+def erle_check(run_gpu, run_ref, n, streams=2):
+    """ERLE (10 log10(sum mic^2 / sum out^2), first 0.5 s
+    skipped) of the GPU path and of the CPU reference restatement on the same
+    far-end single-talk scenes; delta = GPU - reference (north_star: <= 0.1 dB)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, 'oracle'))
+    from aec_oracle import erle_db
+    from aec_amd import synth
+    g, r = [], []
+    for i in range(streams):
+        mic, ref, near = synth.scene(n, 90000 + i, double_talk=False)
+        g.append(erle_db(mic, run_gpu(mic, ref, near)))
+        r.append(erle_db(mic, run_ref(mic, ref, near)))
+    return dict(gpu_db=round(float(np.mean(g)), 4), reference_db=round(float(np.mean(r)), 4),
+                delta_db=round(float(np.mean(g) - np.mean(r)), 5), streams=streams,
+                scene='far-end single talk (near = 0), 10 s, synthetic RIR echo')
+
+
 def main_crn(args):
     """BASELINE config 3: the DCCRN post-filter (bf16 MFMA), B streams x 10 s."""
     import numpy as np
@@ -238,8 +256,21 @@ def main_crn(args):
     ach = dom_fl * B * T / (stage_ms[dom] * 1e-3) / 1e12 if dom_fl else 0.0
     whole = fl['total'] * B * T / (ms_step * 1e-3 / 1) / 1e12
     cpu = None
+    erle = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline_crn(args.cpu_seconds, conf, args.crn_version, n=n)
+        sys.path.insert(0, os.path.join(REPO, 'oracle'))
+        from torch_crn_port import TorchCrnPort
+        wref = {k: v.detach().cpu().numpy() for k, v in net.state_dict().items()}
+        port = TorchCrnPort(wref, conf, args.crn_version)
+
+        def gpu1(m_, f_, _n):
+            with torch.no_grad():
+                o, _, _ = net.forward_ragged(torch.from_numpy(m_)[None].to(dev), torch.from_numpy(f_)[None].to(dev),
+                                             [len(m_)], want_spec=False)
+            return o[0].cpu().numpy()
+
+        erle = erle_check(gpu1, lambda m_, f_, _n: port(torch.from_numpy(m_)[None], torch.from_numpy(f_)[None])[0].numpy(), n)
     if rank == 0:
         line = {
             'metric': '16kHz frames/sec/GPU (batched AEC) + RTF@batch=1; ERLE delta vs reference',
@@ -262,6 +293,7 @@ def main_crn(args):
                          'alg_flops_per_frame': dom_fl, 'frames_per_launch': B * T},
             'pipeline_roofline': {'alg_flops_per_frame': fl['total'], 'achieved_tflops': round(whole, 1),
                                   'mfma_frac': round(whole / peak, 4)},
+            'erle': erle,
             'cpu_baseline': cpu,
         }
         print(json.dumps(line), flush=True)
@@ -367,8 +399,19 @@ def main():
     pipe_gbs = PIPE['bytes'] * B * T / pipe_t / 1e9
     pipe_tfl = PIPE['flops'] * B * T / pipe_t / 1e12
     cpu = None
+    erle = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_seconds)
+        sys.path.insert(0, os.path.join(REPO, 'oracle'))
+        import aec_oracle
+        erb_np = aec_amd.erb_matrix().astype(np.float32)
+
+        def gpu1(m_, r_, n_):
+            with torch.no_grad():
+                o, _ = net.forward_ragged(*(torch.from_numpy(x)[None].to(dev) for x in (m_, r_, n_)), erb, [len(m_)])
+            return o[0].cpu().numpy()
+
+        erle = erle_check(gpu1, lambda m_, r_, n_: aec_oracle.aec_forward(m_, r_, n_, erb_np, w, nlms)[0], n)
     if rank == 0:
         line = {
             'metric': '16kHz frames/sec/GPU (batched AEC) + RTF@batch=1; ERLE delta vs reference',
@@ -387,6 +430,7 @@ def main():
             'pipeline_roofline': {'alg_bytes_per_frame': PIPE['bytes'], 'alg_flops_per_frame': PIPE['flops'],
                                   'hbm_frac': round(pipe_gbs / HBM_PEAK_GBS, 4),
                                   'fp32_frac': round(pipe_tfl / FP32_PEAK_TFLOPS, 4)},
+            'erle': erle,
             'cpu_baseline': cpu,
         }
         if sweep:
