@@ -697,22 +697,22 @@ __device__ __forceinline__ float ftanh(float x) { return 2.f * fsigmoid(2.f * x)
 // W_hh rows.  grid = (H / 32, CELLS * ceil(B / SB)); consecutive blocks take
 // consecutive unit slices, so each XCD keeps the same 4 slices (2 MB of
 // weights) for every step.
-template <typename T, int CELLS, int S>
+template <typename T, int CELLS, int S, int SB_, int NBUF_>
 struct StepCfg {
-    static constexpr int SB = CELLS * S == 4 ? 64 : 64;
+    static constexpr int SB = SB_;                      // streams per block
     static constexpr int U = 32;
     static constexpr int BM = SB * S;                   // rows: (s, stream)
     static constexpr int BN = 4 * U;
     static constexpr int FM = BM / 32, FN = 4;          // 2 x 2 waves
-    static constexpr int NBUF = sizeof(T) == 2 ? 3 : 2;
+    static constexpr int NBUF = NBUF_;
     static constexpr int GROW = U * 4 * (int)sizeof(T);            // Gx bytes per row
     static constexpr size_t STAGES = (size_t)NBUF * (BM + BN) * 128;
     static constexpr size_t LDS = STAGES + (size_t)BM * GROW + (size_t)BM * U * 4;
 };
 
-template <typename T, int CELLS, int S>
+template <typename T, int CELLS, int S, int SB_, int NBUF_>
 __global__ __launch_bounds__(256) void lstm_step_kernel(StepArgs p) {
-    using C_ = StepCfg<T, CELLS, S>;
+    using C_ = StepCfg<T, CELLS, S, SB_, NBUF_>;
     constexpr int SB = C_::SB, U = C_::U, BM = C_::BM, BN = C_::BN, FM = C_::FM, FN = C_::FN;
     constexpr int LA = BM / 32;
     constexpr int ES = (int)sizeof(T);
@@ -860,26 +860,36 @@ hipError_t launch_lstm_step(const StepArgs& a, int cells, int seqs, hipStream_t 
     // cell update, bit1 skip the recurrent GEMM, bit2 skip the Gx / c DMA
     static const int step_mode = env_int("CRN_STEP_MODE", 0);
     if (a.H % 32 || (a.H * (int)sizeof(T)) % kStageBytes) return hipErrorInvalidValue;
-#define CRN_STEP(C, S_)                                                                                           \
+#define CRN_STEP(C, S_, SB_, NB_)                                                                                 \
     do {                                                                                                          \
-        auto kern = lstm_step_kernel<T, C, S_>;                                                                   \
-        constexpr size_t lds = StepCfg<T, C, S_>::LDS;                                                            \
+        auto kern = lstm_step_kernel<T, C, S_, SB_, NB_>;                                                         \
+        constexpr size_t lds = StepCfg<T, C, S_, SB_, NB_>::LDS;                                                  \
         static_assert(lds <= 160 * 1024, "LDS");                                                                  \
         static const hipError_t attr =                                                                            \
             hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                 (int)lds);                                                                        \
         if (attr != hipSuccess) return attr;                                                                      \
-        constexpr int SB = StepCfg<T, C, S_>::SB;                                                                 \
         StepArgs a2 = a;                                                                                          \
         a2.mode = step_mode;                                                                                      \
-        hipLaunchKernelGGL(kern, dim3(a.H / 32, C * ((a.B + SB - 1) / SB)), dim3(256), lds, st, a2);             \
+        hipLaunchKernelGGL(kern, dim3(a.H / 32, C * ((a.B + SB_ - 1) / SB_)), dim3(256), lds, st, a2);           \
     } while (0)
-    if (cells == 2 && seqs == 2)
-        CRN_STEP(2, 2);
-    else if (cells == 1 && seqs == 1)
-        CRN_STEP(1, 1);
-    else
+    // CRN_STEP_CFG: 0 = 64 streams per block, 3 (bf16) / 2 (f32) stage buffers (1 block per CU);
+    // 1 (default, fastest measured) = 32 streams, 2 buffers (2 blocks per CU); 2 = 32 streams,
+    // 3 buffers; 3 = 16 streams, 2 buffers (3 blocks per CU, v2 only)
+    static const int cfg = env_int("CRN_STEP_CFG", 1);
+    constexpr int NB0 = sizeof(T) == 2 ? 3 : 2;
+    if (cells == 2 && seqs == 2) {
+        if (cfg == 1) CRN_STEP(2, 2, 32, 2);
+        else if (cfg == 2) CRN_STEP(2, 2, 32, 3);
+        else if (cfg == 3) CRN_STEP(2, 2, 16, 2);
+        else CRN_STEP(2, 2, 64, NB0);
+    } else if (cells == 1 && seqs == 1) {
+        if (cfg == 1) CRN_STEP(1, 1, 32, 2);
+        else if (cfg == 2) CRN_STEP(1, 1, 32, 3);
+        else CRN_STEP(1, 1, 64, NB0);
+    } else {
         return hipErrorInvalidValue;
+    }
 #undef CRN_STEP
     return hipGetLastError();
 }
