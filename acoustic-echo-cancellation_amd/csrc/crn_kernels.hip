@@ -643,6 +643,7 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
     } while (0)
     static const int dma = env_int("CRN_GEMM_DMA", 2);    // 0 = register-staged core, else NBUF
     static const int big = env_int("CRN_GEMM_BIG", 0);    // 256x128 tiles (8 waves) for large M (measured slower)
+    static const int sq = env_int("CRN_GEMM_SQ", 1);      // 256x256 tiles (8 waves) when N % 256 == 0
     switch (bn) {
         case 16: CRN_GEMM(4, 1, 4, 1); break;
         case 32: CRN_GEMM(2, 2, 4, 1); break;
@@ -653,7 +654,9 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
             else CRN_GEMM(2, 2, 4, 2);
             break;
         default:
-            if (big && a.M >= 256 * 1024) CRN_GEMM_DMA(4, 2, 4, 4, 2);
+            if (e.N % 256 == 0 && a.M >= 4096 && sq >= 1)
+                CRN_GEMM_DMA(2, 4, 8, 4, 2);                             // 256 x 256 tile, 8 waves, 128 KB LDS
+            else if (big && a.M >= 256 * 1024) CRN_GEMM_DMA(4, 2, 4, 4, 2);
             else if (dma == 2) CRN_GEMM_DMA(2, 2, 4, 4, 2);
             else if (dma == 3) CRN_GEMM_DMA(2, 2, 4, 4, 3);
             else if (dma >= 4) CRN_GEMM_DMA(2, 2, 4, 4, 4);
