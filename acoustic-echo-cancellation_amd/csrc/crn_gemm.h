@@ -181,7 +181,13 @@ __device__ __forceinline__ void gemm_core(f32x4 (&acc)[FM][FN], char* smem, cons
 // rows 8 (NW i + wave) + lane/8, NW waves) at K-byte kbyte, or 0x80000000
 // (out of range -> the hardware writes zeros).  BM, BN multiples of 8 NW.
 // --------------------------------------------------------------------------
-__device__ __forceinline__ int swz_slot(int row, int q) { return q ^ ((row >> 1) & 7); }
+// 16-B slot of logical chunk q in LDS row `row`: 128-B rows use q ^ ((row >> 1) & 7),
+// 64-B rows (4 rows per 256-B bank window) q ^ ((row >> 2) & 3): either way the 16
+// rows of one fragment read land on 16 distinct bank slots.
+template <int RB = 128>
+__device__ __forceinline__ int swz_slot(int row, int q) {
+    return RB == 128 ? (q ^ ((row >> 1) & 7)) : (q ^ ((row >> 2) & 3));
+}
 
 template <int N>
 __device__ __forceinline__ void wait_vm() {
@@ -190,30 +196,34 @@ __device__ __forceinline__ void wait_vm() {
     __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
-template <typename T, int BM, int BN, int FM, int FN, int NBUF, class AO, class BO, int NW = 4>
+// RB = bytes of K per row per stage (128: two 64-B k-chunks; 64: one).  A DMA
+// instruction writes 64 lanes x 16 B = 1 KiB = 1024 / RB rows.
+template <typename T, int BM, int BN, int FM, int FN, int NBUF, class AO, class BO, int NW = 4, int RB = 128>
 __device__ __forceinline__ void gemm_core_dma(f32x4 (&acc)[FM][FN], char* smem, __amdgpu_buffer_rsrc_t ra,
                                               __amdgpu_buffer_rsrc_t rb, const AO& aoff, const BO& boff,
                                               int nstages, int wr0, int wc0) {
-    static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0 && NBUF >= 2, "tile");
-    constexpr int LA = BM / (8 * NW), LB = BN / (8 * NW);   // DMA instructions per wave per stage
-    constexpr int STAGE = (BM + BN) * 128;
+    constexpr int RPI = 1024 / RB;                       // rows per DMA instruction
+    constexpr int CPR = RB / 16;                         // 16-B chunks per row
+    static_assert(BM % (RPI * NW) == 0 && BN % (RPI * NW) == 0 && NBUF >= 2, "tile");
+    constexpr int LA = BM / (RPI * NW), LB = BN / (RPI * NW);   // DMA instructions per wave per stage
+    constexpr int STAGE = (BM + BN) * RB;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int q_l = lane & 7;
+    const int q_l = lane & (CPR - 1);
     auto issue = [&](int st) {
         char* buf = smem + (st % NBUF) * STAGE;
 #pragma unroll
         for (int i = 0; i < LA; ++i) {
-            const int row = 8 * (NW * i + wave) + (lane >> 3);
-            const uint32_t vo = aoff(i, st * 128 + swz_slot(row, q_l) * 16);
+            const int row = RPI * (NW * i + wave) + lane / CPR;
+            const uint32_t vo = aoff(i, st * RB + swz_slot<RB>(row, q_l) * 16);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                ra, (__attribute__((address_space(3))) void*)(buf + 8 * (NW * i + wave) * 128), 16, vo, 0, 0, 0);
+                ra, (__attribute__((address_space(3))) void*)(buf + RPI * (NW * i + wave) * RB), 16, vo, 0, 0, 0);
         }
 #pragma unroll
         for (int i = 0; i < LB; ++i) {
-            const int row = 8 * (NW * i + wave) + (lane >> 3);
-            const uint32_t vo = boff(i, st * 128 + swz_slot(row, q_l) * 16);
+            const int row = RPI * (NW * i + wave) + lane / CPR;
+            const uint32_t vo = boff(i, st * RB + swz_slot<RB>(row, q_l) * 16);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rb, (__attribute__((address_space(3))) void*)(buf + BM * 128 + 8 * (NW * i + wave) * 128), 16, vo, 0,
+                rb, (__attribute__((address_space(3))) void*)(buf + BM * RB + RPI * (NW * i + wave) * RB), 16, vo, 0,
                 0, 0);
         }
     };
@@ -229,19 +239,19 @@ __device__ __forceinline__ void gemm_core_dma(f32x4 (&acc)[FM][FN], char* smem, 
         __builtin_amdgcn_s_barrier();
         if (st + NBUF - 1 < nstages) issue(st + NBUF - 1);
         const char* sA = smem + (st % NBUF) * STAGE;
-        const char* sB = sA + BM * 128;
+        const char* sB = sA + BM * RB;
 #pragma unroll
-        for (int kc = 0; kc < 2; ++kc) {
+        for (int kc = 0; kc < RB / 64; ++kc) {
             u32x4 af[FM], bfr[FN];
 #pragma unroll
             for (int fm = 0; fm < FM; ++fm) {
                 const int r = wr0 + fm * 16 + fr;
-                af[fm] = *reinterpret_cast<const u32x4*>(sA + r * 128 + swz_slot(r, kc * 4 + g) * 16);
+                af[fm] = *reinterpret_cast<const u32x4*>(sA + r * RB + swz_slot<RB>(r, kc * 4 + g) * 16);
             }
 #pragma unroll
             for (int fn = 0; fn < FN; ++fn) {
                 const int r = wc0 + fn * 16 + fr;
-                bfr[fn] = *reinterpret_cast<const u32x4*>(sB + r * 128 + swz_slot(r, kc * 4 + g) * 16);
+                bfr[fn] = *reinterpret_cast<const u32x4*>(sB + r * RB + swz_slot<RB>(r, kc * 4 + g) * 16);
             }
 #pragma unroll
             for (int fm = 0; fm < FM; ++fm)

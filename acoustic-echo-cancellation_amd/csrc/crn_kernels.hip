@@ -554,12 +554,13 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(RowSrc a, const T* __res
 }
 
 // Same GEMM through the LDS-DMA main loop (tiles with BM, BN multiples of 32).
-template <typename T, typename OutT, int WM, int WN, int FM, int FN, int NBUF>
+template <typename T, typename OutT, int WM, int WN, int FM, int FN, int NBUF, int RB>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_rows_dma_kernel(RowSrc a, const T* __restrict__ bt, int64_t ldb,
                                                                      int nstages, RowEpi e) {
     constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
     constexpr int NW = WM * WN;
-    constexpr int LA = BM / (8 * NW);
+    constexpr int RPI = 1024 / RB;
+    constexpr int LA = BM / (RPI * NW);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // 1-D grid, column blocks fastest: the column tiles of one row tile run
     // together (the A rows are read once from HBM and re-used through L2/MALL)
@@ -577,7 +578,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_rows_dma_kernel(RowSrc a, c
     bool mval[LA];
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
-        const int64_t m = m0 + 8 * (NW * i + wave) + (lane >> 3);
+        const int64_t m = m0 + RPI * (NW * i + wave) + lane / (RB / 16);
         const int64_t hi = m >> a.rshift;
         const int lo = (int)(m & ((1ll << a.rshift) - 1));
         rowoff[i] = (int32_t)((hi - hi0) * a.rs_hi + (int64_t)lo * a.rs_lo + a.base_off);
@@ -593,18 +594,18 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_rows_dma_kernel(RowSrc a, c
         return ok ? (uint32_t)((rowoff[i] + tap * (int32_t)a.ks + (k & kmask)) * ES) : kOOB;
     };
     auto boff = [&](int i, int kbyte) -> uint32_t {
-        return (uint32_t)((8 * (NW * i + wave) + (lane >> 3)) * (int32_t)ldb * ES + kbyte);
+        return (uint32_t)((RPI * (NW * i + wave) + lane / (RB / 16)) * (int32_t)ldb * ES + kbyte);
     };
     f32x4 acc[FM][FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gemm_core_dma<T, BM, BN, FM, FN, NBUF, decltype(aoff), decltype(boff), NW>(acc, smem, ra, rb, aoff, boff, nstages,
-                                                                               wr0, wc0);
+    gemm_core_dma<T, BM, BN, FM, FN, NBUF, decltype(aoff), decltype(boff), NW, RB>(acc, smem, ra, rb, aoff, boff,
+                                                                                   nstages, wr0, wc0);
     __syncthreads();                                   // every wave is done with the stage buffers
-    constexpr int PF = epi_passes<OutT, FM, FN, NW>((size_t)NBUF * (BM + BN) * 128);
-    static_assert(NW * PF * 16 * FN * 16 * sizeof(OutT) <= (size_t)NBUF * (BM + BN) * 128, "epilogue LDS");
+    constexpr int PF = epi_passes<OutT, FM, FN, NW>((size_t)NBUF * (BM + BN) * RB);
+    static_assert(NW * PF * 16 * FN * 16 * sizeof(OutT) <= (size_t)NBUF * (BM + BN) * RB, "epilogue LDS");
     rows_epilogue_lds<OutT, FM, FN, PF>(acc, e, m0 + wr0, n0 + wc0, lane,
                                         smem + wave * (PF * 16 * FN * 16 * (int)sizeof(OutT)));
 }
@@ -628,22 +629,24 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
         hipLaunchKernelGGL((gemm_rows_kernel<T, OutT, WM, WN, FM, FN>), grid, dim3(256), 0, st, a, bt, ldb,  \
                            nstages, e);                                                                       \
     } while (0)
-#define CRN_GEMM_DMA(WM, WN, FM, FN, NBUF)                                                                     \
+#define CRN_GEMM_DMA_RB(WM, WN, FM, FN, NBUF, RB)                                                               \
     do {                                                                                                          \
         constexpr int BM = WM * FM * 16, BN = WN * FN * 16;                                                       \
-        auto kern = gemm_rows_dma_kernel<T, OutT, WM, WN, FM, FN, NBUF>;                                          \
-        constexpr size_t lds = (size_t)NBUF * (BM + BN) * 128;                                                    \
+        auto kern = gemm_rows_dma_kernel<T, OutT, WM, WN, FM, FN, NBUF, RB>;                                      \
+        constexpr size_t lds = (size_t)NBUF * (BM + BN) * RB;                                                     \
         static const hipError_t attr =                                                                            \
             hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                 (int)lds);                                                                        \
         if (attr != hipSuccess) return attr;                                                                      \
         const unsigned nbn_ = (unsigned)(npad / BN);                                                              \
         dim3 grid((unsigned)((a.M + BM - 1) / BM) * nbn_);                                                        \
-        hipLaunchKernelGGL(kern, grid, dim3(64 * WM * WN), lds, st, a, bt, ldb, nstages, e);                      \
+        hipLaunchKernelGGL(kern, grid, dim3(64 * WM * WN), lds, st, a, bt, ldb, nstages * (128 / RB), e);         \
     } while (0)
+#define CRN_GEMM_DMA(WM, WN, FM, FN, NBUF) CRN_GEMM_DMA_RB(WM, WN, FM, FN, NBUF, 128)
     static const int dma = env_int("CRN_GEMM_DMA", 2);    // 0 = register-staged core, else NBUF
     static const int big = env_int("CRN_GEMM_BIG", 0);    // 256x128 tiles (8 waves) for large M (measured slower)
     static const int sq = env_int("CRN_GEMM_SQ", 1);      // 256x256 tiles (8 waves) when N % 256 == 0
+    static const int rb64 = env_int("CRN_GEMM_RB64", 0);  // 128x128 tiles with 64-B K slices, 4 buffers
     switch (bn) {
         case 16: CRN_GEMM(4, 1, 4, 1); break;
         case 32: CRN_GEMM(2, 2, 4, 1); break;
@@ -654,8 +657,10 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
             else CRN_GEMM(2, 2, 4, 2);
             break;
         default:
-            if (e.N % 256 == 0 && a.M >= 4096 && sq >= 1)
-                CRN_GEMM_DMA(2, 4, 8, 4, 2);                             // 256 x 256 tile, 8 waves, 128 KB LDS
+            if (e.N % 256 == 0 && a.M >= 4096 && sq >= 1) {
+                if (sq == 2) CRN_GEMM_DMA_RB(2, 4, 8, 4, 4, 64);          // 64-B K slices, 4 buffers
+                else CRN_GEMM_DMA(2, 4, 8, 4, 2);                         // 256 x 256 tile, 8 waves, 128 KB LDS
+            } else if (rb64) CRN_GEMM_DMA_RB(2, 2, 4, 4, 4, 64);
             else if (big && a.M >= 256 * 1024) CRN_GEMM_DMA(4, 2, 4, 4, 2);
             else if (dma == 2) CRN_GEMM_DMA(2, 2, 4, 4, 2);
             else if (dma == 3) CRN_GEMM_DMA(2, 2, 4, 4, 3);
@@ -665,6 +670,7 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
     }
 #undef CRN_GEMM
 #undef CRN_GEMM_DMA
+#undef CRN_GEMM_DMA_RB
     return hipGetLastError();
 }
 
