@@ -23,6 +23,7 @@ _STATUS = {0: 'AEC_OK', 1: 'AEC_ERR_INVALID_ARG', 2: 'AEC_ERR_OOM', 3: 'AEC_ERR_
 
 # every symbol include/aec_hip.h declares
 EXPORTS = ('aec_weights_count', 'aec_create', 'aec_set_weights', 'aec_set_erb', 'aec_process',
+           'aec_stream_open', 'aec_stream_reset', 'aec_stream_step',
            'aec_set_debug', 'aec_debug_copy', 'aec_profile_enable', 'aec_profile_read',
            'aec_erb_tables_check', 'aec_num_frames', 'aec_out_len', 'aec_last_error', 'aec_destroy')
 
@@ -73,6 +74,12 @@ def load():
     lib.aec_set_erb.restype = ctypes.c_int
     lib.aec_process.argtypes = [P, P, P, P, P, ctypes.c_int32, ctypes.c_int64, P, ctypes.c_int64, P, P]
     lib.aec_process.restype = ctypes.c_int
+    lib.aec_stream_open.argtypes = [P, ctypes.c_int32]
+    lib.aec_stream_open.restype = ctypes.c_int
+    lib.aec_stream_reset.argtypes = [P, ctypes.c_int32, P]
+    lib.aec_stream_reset.restype = ctypes.c_int
+    lib.aec_stream_step.argtypes = [P, P, P, ctypes.c_int64, P, ctypes.c_int64, P]
+    lib.aec_stream_step.restype = ctypes.c_int
     lib.aec_set_debug.argtypes = [P, ctypes.c_int32]
     lib.aec_set_debug.restype = ctypes.c_int
     lib.aec_debug_copy.argtypes = [P, ctypes.c_int32, P, ctypes.c_size_t, P]
@@ -181,6 +188,16 @@ class Handle:
         st = self.lib.aec_process(self.h, mic_ptr, ref_ptr, near_ptr, lens.ctypes.data, int(B), int(ld),
                                   out_ptr, int(ld_out), loss_ptr, stream)
         check(st, self.h, 'aec_process')
+
+    def stream_open(self, B):
+        check(self.lib.aec_stream_open(self.h, int(B)), self.h, 'aec_stream_open')
+
+    def stream_reset(self, b, stream):
+        check(self.lib.aec_stream_reset(self.h, int(b), stream), self.h, 'aec_stream_reset')
+
+    def stream_step(self, mic_ptr, ref_ptr, ld_in, out_ptr, ld_out, stream):
+        check(self.lib.aec_stream_step(self.h, mic_ptr, ref_ptr, int(ld_in), out_ptr, int(ld_out), stream), self.h,
+              'aec_stream_step')
 
     def debug_copy(self, what, dst_ptr, n, stream):
         check(self.lib.aec_debug_copy(self.h, int(what), dst_ptr, int(n), stream), self.h, 'aec_debug_copy')

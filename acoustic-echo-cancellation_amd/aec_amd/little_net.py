@@ -191,6 +191,51 @@ class Little_net(nn.Module):
                           stream)
         return out, loss
 
+    # --- streaming (include/aec_hip.h aec_stream_*) ------------------------------
+    def stream_open(self, B, erb, device=None):
+        """Open B concurrent streams (state zeroed) on ``device``: afterwards
+        ``stream_step`` advances every stream by one 256-sample hop."""
+        if torch.is_grad_enabled() and self.training:
+            raise NotImplementedError('Little_net (gfx950) is inference-only: use net.eval() and torch.no_grad()')
+        device = torch.device(device or 'cuda')
+        if device.type != 'cuda':
+            raise RuntimeError(f'Little_net (gfx950) streams live on a HIP device, got {device}')
+        if erb.shape != (257, 32):
+            raise ValueError(f'erb must be [257, 32], got {tuple(erb.shape)}')
+        h, idx = self._handle(device)
+        self._sync_erb(h, idx, erb)
+        h.stream_open(B)
+        self._stream = (h, torch.device('cuda', idx), int(B))
+
+    def _stream_state(self):
+        st = getattr(self, '_stream', None)
+        if st is None:
+            raise RuntimeError('call stream_open first')
+        return st
+
+    def stream_reset(self, b=-1):
+        """Zero stream b's state (b = -1: every stream) for a new utterance."""
+        h, device, _ = self._stream_state()
+        h.stream_reset(b, torch.cuda.current_stream(device).cuda_stream)
+
+    def stream_step(self, mic, ref):
+        """mic, ref [B, 256] float32 (hop k of every stream, already normalised
+        — see aec_stream_step) -> output hop k-1 [B, 256]."""
+        h, device, B = self._stream_state()
+        for t in (mic, ref):
+            if t.device != device or t.dim() != 2 or t.shape[0] != B or t.shape[1] < HOP:
+                raise ValueError(f'hops must be [{B}, >= 256] on {device}')
+        mic = mic.float()
+        ref = ref.float()
+        if mic.stride(1) != 1 or ref.stride(1) != 1 or mic.stride(0) != ref.stride(0):
+            mic, ref = mic.contiguous(), ref.contiguous()
+        self._handle(device)            # weights may have changed
+        out = torch.empty(B, HOP, device=device, dtype=torch.float32)
+        with torch.cuda.device(device):
+            h.stream_step(mic.data_ptr(), ref.data_ptr(), mic.stride(0), out.data_ptr(), HOP,
+                          torch.cuda.current_stream(device).cuda_stream)
+        return out
+
     def debug_intermediate(self, what, B, T, device=None):
         """Copy an intermediate of the last forward: 'mic_erb', 'ref_erb',
         'near_erb', 'gru_out', 'mask', 'est_erb' -> [B, T, 32]."""

@@ -216,6 +216,10 @@ struct aec_handle {
     int profile = 0;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
+    // streaming (aec_stream_*): per-stream state [stream_B][stream_stride]
+    float* d_state = nullptr;
+    int32_t stream_B = 0;
+    int64_t stream_stride = 0;
 };
 
 static hipEvent_t next_event(aec_handle* h) {
@@ -589,6 +593,50 @@ aec_status aec_erb_tables_check(const float* erb, const float* mags, const float
     return AEC_OK;
 }
 
+aec_status aec_stream_open(aec_handle* h, int32_t B) {
+    if (!h) return AEC_ERR_INVALID_ARG;
+    if (B < 1) return fail(h, AEC_ERR_INVALID_ARG, "stream count must be >= 1");
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, hipDeviceSynchronize());   // a previous state may still be in use
+    if (h->d_state) { HIP_TRY(h, hipFree(h->d_state)); h->d_state = nullptr; }
+    h->stream_B = 0;
+    const int64_t stride = stream_state_floats(h->cfg.nlms_taps);
+    HIP_TRY(h, hipMalloc(&h->d_state, (size_t)B * stride * sizeof(float)));
+    HIP_TRY(h, hipMemset(h->d_state, 0, (size_t)B * stride * sizeof(float)));
+    h->stream_B = B;
+    h->stream_stride = stride;
+    return AEC_OK;
+}
+
+aec_status aec_stream_reset(aec_handle* h, int32_t b, void* stream) {
+    if (!h) return AEC_ERR_INVALID_ARG;
+    if (!h->d_state) return fail(h, AEC_ERR_INVALID_ARG, "aec_stream_open first");
+    if (b < -1 || b >= h->stream_B) return fail(h, AEC_ERR_INVALID_ARG, "stream index out of range");
+    HIP_TRY(h, hipSetDevice(h->device));
+    const int64_t first = b < 0 ? 0 : b, count = b < 0 ? h->stream_B : 1;
+    HIP_TRY(h, hipMemsetAsync(h->d_state + first * h->stream_stride, 0, (size_t)count * h->stream_stride * sizeof(float),
+                              reinterpret_cast<hipStream_t>(stream)));
+    return AEC_OK;
+}
+
+aec_status aec_stream_step(aec_handle* h, const float* mic, const float* ref, int64_t ld_in, float* out,
+                           int64_t ld_out, void* stream) {
+    if (!h) return AEC_ERR_INVALID_ARG;
+    if (!h->d_state) return fail(h, AEC_ERR_INVALID_ARG, "aec_stream_open first");
+    if (!h->have_w || !h->have_erb) return fail(h, AEC_ERR_INVALID_ARG, "weights / erb not set");
+    if (!mic || !ref || !out) return fail(h, AEC_ERR_INVALID_ARG, "null mic / ref / out");
+    if (ld_in < 256 || ld_out < 256) return fail(h, AEC_ERR_INVALID_ARG, "ld_in / ld_out must be >= 256");
+    HIP_TRY(h, hipSetDevice(h->device));
+    StreamStepArgs a{};
+    a.mic = mic; a.ref = ref; a.ld_in = ld_in; a.out = out; a.ld_out = ld_out;
+    a.state = h->d_state; a.state_stride = h->stream_stride;
+    a.w = h->d_w; a.tables = reinterpret_cast<const float*>(h->d_tab);
+    a.sched = h->d_sched; a.sched_len = h->sched_len; a.bintab = h->d_bintab;
+    a.mu = h->cfg.nlms_mu; a.beta = h->cfg.nlms_beta; a.delta = h->cfg.nlms_delta;
+    HIP_TRY(h, launch_stream_step(a, h->stream_B, h->cfg.nlms_taps, reinterpret_cast<hipStream_t>(stream)));
+    return AEC_OK;
+}
+
 void aec_destroy(aec_handle* h) {
     if (!h) return;
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
@@ -601,7 +649,8 @@ void aec_destroy(aec_handle* h) {
     (void)hipSetDevice(h->device);
     (void)hipFree(h->d_w); (void)hipFree(h->d_tab); (void)hipFree(h->d_sched); (void)hipFree(h->d_bintab);
     (void)hipFree(h->d_mom); (void)hipFree(h->d_cvals); (void)hipFree(h->d_items); (void)hipFree(h->d_sitems); (void)hipFree(h->d_len);
-    (void)hipFree(h->d_feats); (void)hipFree(h->d_est); (void)hipFree(h->d_dbg);
+    (void)hipFree(h->d_feats); (void)hipFree(h->d_est); (void)hipFree(h->d_dbg); (void)hipFree(h->d_spec);
+    (void)hipFree(h->d_state);
     delete h;
 }
 

@@ -16,16 +16,10 @@
 #include <stdint.h>
 
 #include "aec_fft.h"
+#include "aec_frame.h"
 #include "aec_launch.h"
 
 namespace aec {
-
-__device__ __forceinline__ float sigmoidf_(float x) {
-    return __builtin_amdgcn_rcpf(1.f + __expf(-x));
-}
-__device__ __forceinline__ float tanhf_(float x) {
-    return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x));
-}
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 

@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include "aec_fft.h"
+#include "aec_frame.h"
 #include "aec_launch.h"
 #include "aec_stft.h"
 #include "aec_tables.h"
@@ -117,50 +118,6 @@ __global__ __launch_bounds__(256) void norm_finalize_kernel(const double2* __res
     if (i >= b1 * 3) return;
     const int b = i / 3, s = i % 3;
     cvals[i] = s < nsig ? norm_scalar(mom, b, s, lens[b]) : 0.f;
-}
-
-// --------------------------------------------------------------------------
-// shared helpers for K2 / K4
-// --------------------------------------------------------------------------
-
-// |X| = sqrt(re^2 + im^2 + 1e-9) (ERB.py:277-279).  The argument is >= 1e-9,
-// never denormal, so the hardware v_sqrt_f32 (<= 1 ulp) needs no IEEE fix-up.
-__device__ __forceinline__ float mag(float2 x) {
-    return __builtin_amdgcn_sqrtf(fmaf(x.x, x.x, fmaf(x.y, x.y, 1e-9f)));
-}
-
-// Balanced ERB projection of one frame's magnitudes (scr[k ^ sw], k = 0..256)
-// onto the 32 bands (ERB.py:282-284): L scheduled entries per lane, three
-// partial sums, pieces of split bands combined through comb.  fo = the
-// frame's 32-float feature row, or null (frame beyond the stream: compute
-// nothing visible).  Leaves the wave fenced.
-__device__ __forceinline__ void erb_project(float* scr, const float4* sSched, const int2* sComb, int L, int lb,
-                                            int sw, float* fo) {
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-    for (int e = 0; e < L; e += 4) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const float4 en = sSched[(e + u) * 16 + lb];
-            const float mg = scr[__float_as_int(en.x) ^ sw];
-            a0 = fmaf(en.y, mg, a0);
-            a1 = fmaf(en.z, mg, a1);
-            a2 = fmaf(en.w, mg, a2);
-        }
-    }
-    float* part = scr + 512;
-    part[3 * lb + 0] = a0;
-    part[3 * lb + 1] = a1;
-    part[3 * lb + 2] = a2;
-    wave_fence();
-    if (fo) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int band = lb + 16 * h;
-            const int2 cb = sComb[band];
-            fo[band] = part[cb.x] + (cb.y >= 0 ? part[cb.y] : 0.f);
-        }
-    }
-    wave_fence();
 }
 
 // --------------------------------------------------------------------------
@@ -288,72 +245,6 @@ constexpr int kSpecRow = 256;          // float2 per spectrum row
 constexpr int kNlmsWaves = 12;
 constexpr int kERow = 512 + 48;        // floats per LDS error row: 256 float2, then ERB partials
 
-// Packed-FP32 complex helpers for the recursion: a complex value is a
-// float2 vector, so the products below map to v_pk_mul_f32 / v_pk_fma_f32
-// (two lanes of arithmetic per instruction slot).
-typedef float v2f __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ v2f vfma(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ v2f vsplat(float a) { return v2f{a, a}; }
-__device__ __forceinline__ v2f vrot(v2f a) { return v2f{-a.y, a.x}; }       // i * a
-
-// One lane's NLMS.  A lane runs either one complex bin or, on the lane that
-// owns row slot 0, the two real bins 0 and 256 side by side (x, y halves).
-// Both cases are the same instruction stream over per-tap operands
-//   complex: A = h, B = i h              dual real: A = (h.x, 0), B = (0, h.y)
-//   y  = sum_l w.x A + w.y B             (complex W h  /  (w.x h.x, w.y h.y))
-//   W += ge.x conj(A) + ge.y (-B.x, B.y) (ge conj(h)   /  (ge.x h.x, ge.y h.y))
-//   pw = sum_l A*A + B*B                 (|h|^2 in both halves / (h.x^2, h.y^2))
-// with ge = e * mu / (P + delta) per half.
-template <int TAPS>
-struct NlmsBin {
-    v2f w[TAPS];
-    v2f a[TAPS], bq[TAPS], qq[TAPS];   // operands A, B and A*A + B*B of R[t], R[t-1], ...
-    v2f p;
-    v2f ma, mb, mc;                    // operand masks: complex (1,1), (-1,1), (0,0); dual (1,0), (0,0), (0,1)
-    __device__ __forceinline__ void reset(bool dual) {
-#pragma unroll
-        for (int l = 0; l < TAPS; ++l) w[l] = a[l] = bq[l] = qq[l] = vsplat(0.f);
-        p = vsplat(0.f);
-        ma = dual ? v2f{1.f, 0.f} : v2f{1.f, 1.f};
-        mb = dual ? v2f{0.f, 0.f} : v2f{-1.f, 1.f};
-        mc = dual ? v2f{0.f, 1.f} : v2f{0.f, 0.f};
-    }
-    // One frame: returns E = D - sum_l W[l] R[t-l] and adapts W.
-    __device__ __forceinline__ float2 step(float2 d2, float2 r2, float mu, float beta, float delta) {
-        const v2f d{d2.x, d2.y}, r{r2.x, r2.y};
-#pragma unroll
-        for (int l = TAPS - 1; l >= 1; --l) {
-            a[l] = a[l - 1];
-            bq[l] = bq[l - 1];
-            qq[l] = qq[l - 1];
-        }
-        a[0] = r * ma;
-        bq[0] = vfma(v2f{r.y, r.x}, mb, r * mc);
-        qq[0] = vfma(a[0], a[0], bq[0] * bq[0]);
-        // independent per-tap products summed as a tree (short dependency chain)
-        v2f pr[TAPS];
-        v2f pw = qq[0];
-#pragma unroll
-        for (int l = 0; l < TAPS; ++l) pr[l] = vfma(vsplat(w[l].y), bq[l], vsplat(w[l].x) * a[l]);
-#pragma unroll
-        for (int l = 1; l < TAPS; ++l) pw = pw + qq[l];
-#pragma unroll
-        for (int s = 1; s < TAPS; s *= 2)
-#pragma unroll
-            for (int l = 0; l + s < TAPS; l += 2 * s) pr[l] = pr[l] + pr[l + s];
-        const v2f e = d - pr[0];
-        p = vfma(vsplat(beta), p, vsplat(1.f - beta) * pw);
-        const v2f g = v2f{__builtin_amdgcn_rcpf(p.x + delta), __builtin_amdgcn_rcpf(p.y + delta)} * vsplat(mu);
-        const v2f ge = e * g;
-#pragma unroll
-        for (int l = 0; l < TAPS; ++l) {
-            w[l] = vfma(vsplat(ge.x), v2f{a[l].x, -a[l].y}, w[l]);
-            w[l] = vfma(vsplat(ge.y), v2f{-bq[l].x, bq[l].y}, w[l]);
-        }
-        return make_float2(e.x, e.y);
-    }
-};
-
 // One transform pass of a wave: commit the prefetched samples of (signal,
 // 4 frames at wt), prefetch the next task, window + rFFT -> xa / xb / x128.
 __device__ __forceinline__ void nlms_transform(float* wr, float* scr, float4 (&pf)[kWavePf], float cval, int n, int wt,
@@ -369,33 +260,6 @@ __device__ __forceinline__ void nlms_transform(float* wr, float* scr, float4 (&p
     wave_fence();
     fft256<false>(v, lb, scr, sTwT);
     rfft_unpack(v, lb, sTw512, xa, xb, x128);
-}
-
-__device__ __forceinline__ void mags_to_scr(float* scr, int lb, int sw, const float2 (&xa)[8], const float2 (&xb)[8],
-                                            float2 x128) {
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-        const int kk = lb + 16 * m;
-        scr[kk ^ sw] = mag(xa[m]);
-        scr[(kk == 0 ? 256 : 256 - kk) ^ sw] = mag(xb[m]);
-    }
-    if (lb == 0) scr[128 ^ sw] = mag(x128);
-}
-
-__device__ __forceinline__ void row_to_scr(float* scr, int lb, const float2 (&xa)[8], const float2 (&xb)[8],
-                                           float2 x128) {
-    float2* row = reinterpret_cast<float2*>(scr);
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-        const int kk = lb + 16 * m;
-        if (kk == 0) {
-            row[0] = make_float2(xa[0].x, xb[0].x);                   // (X[0], X[256]), both real
-        } else {
-            row[kk] = xa[m];
-            row[256 - kk] = xb[m];
-        }
-    }
-    if (lb == 0) row[128] = x128;
 }
 
 template <int TAPS>
@@ -639,51 +503,7 @@ __global__ __launch_bounds__(256) void synthesis_kernel(SynthArgs p) {
             rfft_unpack(v, lb, sTw512, xa, xb, x128);
         }
 
-        // ERB gain per bin: g[k] = sum_j est_erb[j] erb[k][j] over the <= 2 bands
-        // covering bin k (ERB.py:306-307), applied to the mic spectrum (:309-310)
-        const float* est = sEst + g * kEstStride;
-        auto gain = [&](int kk) {
-            const float4 e = sBin[kk];
-            return e.y * est[__float_as_int(e.x)] + e.w * est[__float_as_int(e.z)];
-        };
-        // inverse pack: lane lb forms 2Z'[k] and 2Z'[256-k] for k = lb + 16 m; the
-        // inverse FFT wants v[a] = 2Z'[16a + lb]: a <= 7 is this lane's own Zk[a],
-        // a >= 8 is Zmk[15-a] of lane (16-lb)&15 (DPP), lane 0 patched.
-        float2 Zk[8], Zmk[8];
-        static_for<0, 8>([&](auto mi) {
-            constexpr int m = decltype(mi)::value;
-            const int kk = lb + 16 * m;
-            // kk == 0 (lane 0, m = 0): DC / Nyquist, irfft ignores their imaginary parts;
-            // gain(256 - 0) indexes bin 256 = Nyquist, as required
-            const float ga = gain(kk), gb = gain(256 - kk);
-            float2 zk, zmk;
-            irfft_pair(cscale(xa[m], ga), cscale(xb[m], gb), sTw512[kk], zk, zmk);
-            const float s0 = ga * xa[m].x, s256 = gb * xb[m].x;
-            Zk[m] = csel(kk == 0, make_float2(s0 + s256, s0 - s256), zk);
-            Zmk[m] = csel(kk == 0, Zk[m], zmk);
-        });
-        float2 z128 = make_float2(0.f, 0.f);
-        if (lb == 0) {
-            const float2 S = cscale(x128, gain(128));
-            z128 = make_float2(2.f * S.x, -2.f * S.y);   // 2*conj(S[128])
-        }
-#pragma unroll
-        for (int a = 0; a < 8; ++a) v[a] = Zk[a];
-        static_for<8, 16>([&](auto ai) {
-            constexpr int a = decltype(ai)::value;
-            const float2 mir = mirror16(Zmk[15 - a]);
-            v[a] = csel(lb != 0, mir, a == 8 ? z128 : Zmk[(16 - a) & 7]);
-        });
-        fft256<true>(v, lb, scr, sTwT);
-        // v[kP(m2)] = 512 * (x[2m] + i x[2m+1]), m = lb + 16 m2 ; window + 1/512
-        float2* s2 = reinterpret_cast<float2*>(scr);
-        const float2* h2 = reinterpret_cast<const float2*>(sHann);
-#pragma unroll
-        for (int m2 = 0; m2 < 16; ++m2) {
-            const float2 z = v[kP(m2)];
-            const float2 w = h2[lb + 16 * m2];
-            s2[lb + 16 * m2] = make_float2(z.x * (w.x * (1.f / 512.f)), z.y * (w.y * (1.f / 512.f)));
-        }
+        synth_frame(xa, xb, x128, sEst + g * kEstStride, sBin, sTw512, sTwT, sHann, scr, lb);
         __syncthreads();
         // overlap-add + WOLA normalisation + trim (attention_ccrn.py:92-99) + 1e-9 (ERB.py:316)
         float* orow = p.out + (int64_t)b * p.ld_out;

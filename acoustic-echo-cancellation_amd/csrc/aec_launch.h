@@ -86,6 +86,35 @@ struct SynthArgs {
     const float2* spec;      // NLMS error spectrum [B][Tmax][256], or null: re-derive the mic spectrum
 };
 
+// Fused streaming step (aec_stream.hip): one 256-sample hop of B streams.
+// Per-stream state, floats (stride = stream_state_floats(taps)):
+//   [0, 512)     previous input hop: mic (256), ref (256)
+//   [512, 768)   OLA tail: second half of the previous synthesis frame
+//   [768, 800)   GRU h
+//   [1024, ...)  NLMS, float2[2*taps][256] by field: w[0..taps-1],
+//                far-end history r[t-1 .. t-taps+1], power p
+constexpr int kStPrev = 0;
+constexpr int kStTail = 512;
+constexpr int kStH = 768;
+constexpr int kStNlms = 1024;
+inline int64_t stream_state_floats(int taps) { return 1024 + (int64_t)1024 * taps; }
+
+struct StreamStepArgs {
+    const float* mic;        // [B][ld_in] hop k of every stream
+    const float* ref;
+    int64_t ld_in;
+    float* out;              // [B][ld_out] output hop k-1
+    int64_t ld_out;
+    float* state;            // [B][state_stride]
+    int64_t state_stride;
+    const float* w;          // weights blob
+    const float* tables;     // DevTables
+    const float* sched;
+    int sched_len;
+    const float* bintab;
+    float mu, beta, delta;
+};
+
 // dynamic LDS bytes (must match the carve in the kernels)
 inline size_t analysis_smem_bytes(int sched_len) {
     return (size_t)sched_len * 16 * 16 + 32 * 8 + (258 * 2 + 256 * 2 + 512 + (size_t)kFPB * kGroupFloats) * 4;
@@ -108,5 +137,6 @@ hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t st);
 hipError_t launch_nlms_analysis(const NlmsArgs& a, int nb, hipStream_t st);
 hipError_t launch_gru(const GruArgs& a, int B, hipStream_t st);
 hipError_t launch_synthesis(const SynthArgs& a, hipStream_t st);
+hipError_t launch_stream_step(const StreamStepArgs& a, int B, int taps, hipStream_t st);
 
 }  // namespace aec

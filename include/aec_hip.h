@@ -95,6 +95,26 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
                        const int64_t* lengths, int32_t B, int64_t ld,
                        float* out, int64_t ld_out, float* loss, void* stream);
 
+/* Streaming (serving): the reference's per-frame loop (Little_net.forward,
+ * ERB.py:252-334) advanced by one 256-sample hop per stream per call, as ONE
+ * fused kernel launch (frame -> rFFT -> [FD-NLMS] -> ERB -> GRU step -> head
+ * -> gains -> irFFT -> overlap-add).  Frame t needs hops t-1 and t
+ * (ConvSTFT framing, attention_ccrn.py:45-52), so step k emits output hop
+ * k-1; the first step's output is the warm-up region the reference trims
+ * (attention_ccrn.py:99).  Feeding hops 0 .. n/256 (the last one zero-padded
+ * past n) reproduces aec_process's out row for that stream.  The hops must
+ * already be normalised: x - mean(x)/std(x) (ERB.py:254-256) needs the whole
+ * utterance, which a stream does not have; near / loss are not computed.
+ *   aec_stream_open(h, B)        B concurrent streams; state zeroed
+ *   aec_stream_reset(h, b, st)   zero stream b's state (-1: all streams)
+ *   aec_stream_step(h, mic, ref, ld_in, out, ld_out, st)
+ *        mic, ref: device [B, ld_in] float32, hop k of every stream;
+ *        out: device [B, ld_out] float32 receives output hop k-1 (256 samples). */
+aec_status aec_stream_open(aec_handle* h, int32_t B);
+aec_status aec_stream_reset(aec_handle* h, int32_t b, void* stream);
+aec_status aec_stream_step(aec_handle* h, const float* mic, const float* ref, int64_t ld_in,
+                           float* out, int64_t ld_out, void* stream);
+
 /* Debug / parity: copy an intermediate of the LAST aec_process call into the
  * device buffer dst ([B, T_max, 32] float32, frames beyond a stream's T left
  * unspecified).  Requires aec_set_debug(h, 1) before that call.
