@@ -2,10 +2,13 @@
 
 Utterances are independent: the normaliser, NLMS taps, GRU state and OLA
 tail are all per stream. So one process per GPU processes its own shard and
-no data crosses GPUs during compute. The only collectives are scalar ones
-outside the data path:
+no data crosses GPUs during compute. The collectives sit outside the data
+path:
 - `max_over_ranks` for the bench clock;
-- `sum_over_ranks` for run-level metric sums (frames, Σmic², Σout²).
+- `sum_over_ranks` for run-level metric sums (frames, Σmic², Σout²);
+- `gather_to_root`: the end-of-run gather of enhanced waveforms to rank 0
+  (north_star: RCCL over xGMI only gathers the enhanced waveforms), used by
+  the CLI's ``--gather`` mode.
 
 Both use the process group's backend: RCCL ("nccl") on the GPU box, gloo in
 the CPU tests.
@@ -13,8 +16,9 @@ the CPU tests.
 from __future__ import annotations
 
 import heapq
-from typing import List, Sequence
+from typing import Dict, List, Optional, Sequence
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -67,3 +71,48 @@ def sum_over_ranks(values: Sequence[float]) -> List[float]:
     t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=_dev())
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [float(v) for v in t.tolist()]
+
+
+def gather_to_root(outputs: Dict[int, np.ndarray], root: int = 0) -> Optional[Dict[int, np.ndarray]]:
+    """Gather every rank's {utterance index: float32 waveform} to `root`.
+
+    Two collectives on the process group's device (RCCL over xGMI on the GPU
+    box, gloo in the CPU tests): an all_gather of the per-rank sample counts,
+    then one gather of each rank's waveforms packed into a flat float32 buffer
+    (padded to the largest rank) with an int64 (index, length) table.
+    Returns the merged dict on `root`, None elsewhere; identity when not
+    distributed."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return dict(outputs)
+    dev = _dev()
+    world, rank = dist.get_world_size(), dist.get_rank()
+    keys = sorted(outputs)
+    table = np.array([[k, len(outputs[k])] for k in keys], np.int64).reshape(-1, 2)
+    counts = torch.tensor([len(keys), int(table[:, 1].sum()) if len(keys) else 0], dtype=torch.int64, device=dev)
+    allc = [torch.zeros_like(counts) for _ in range(world)]
+    dist.all_gather(allc, counts)
+    allc = [c.tolist() for c in allc]
+    max_utt = max(1, max(c[0] for c in allc))
+    max_smp = max(1, max(c[1] for c in allc))
+    tab = torch.full((max_utt, 2), -1, dtype=torch.int64)
+    tab[:len(keys)] = torch.from_numpy(table)
+    flat = torch.zeros(max_smp, dtype=torch.float32)
+    if keys:
+        flat[:int(table[:, 1].sum())] = torch.from_numpy(np.concatenate([np.asarray(outputs[k], np.float32)
+                                                                          for k in keys]))
+    tab, flat = tab.to(dev), flat.to(dev)
+    tabs = [torch.empty_like(tab) for _ in range(world)] if rank == root else None
+    flats = [torch.empty_like(flat) for _ in range(world)] if rank == root else None
+    dist.gather(tab, tabs, dst=root)
+    dist.gather(flat, flats, dst=root)
+    if rank != root:
+        return None
+    merged: Dict[int, np.ndarray] = {}
+    for r in range(world):
+        t = tabs[r].cpu().numpy()
+        f = flats[r].cpu().numpy()
+        off = 0
+        for k, n in t[:allc[r][0]]:
+            merged[int(k)] = f[off:off + int(n)].copy()
+            off += int(n)
+    return merged

@@ -20,12 +20,16 @@ What differs is how the work is scheduled. Utterances are batched per GPU
 call: the results are bit-identical to running them one at a time, which
 `tests/test_gpu_parity.py` checks as batch invariance. Under torchrun, each
 rank processes a length-balanced shard of the utterances and writes its own
-files. The only collective is a scalar sum of run metrics.
+files; the only collective is then a scalar sum of run
+metrics. With `--gather`, the enhanced waveforms are gathered to rank 0 over
+the process group (RCCL over xGMI, `shard.gather_to_root`) and rank 0
+writes every file.
 
 Extra flags (all optional):
 - `--nlms` puts the FD-NLMS stage in front of the post-filter;
 - `--streams` sets the utterances per GPU call;
-- `--device` picks the GPU.
+- `--device` picks the GPU;
+- `--gather` writes every file on rank 0 (waveforms gathered over RCCL).
 """
 from __future__ import annotations
 
@@ -71,6 +75,8 @@ def build_parser():
     p.add_argument('--nlms', action='store_true', help='FD-NLMS linear AEC in front of the post-filter')
     p.add_argument('--streams', type=int, default=64, help='utterances per GPU call')
     p.add_argument('--device', type=int, default=None, help='GPU index (default: LOCAL_RANK or 0)')
+    p.add_argument('--gather', action='store_true',
+                   help='under torchrun: gather the enhanced waveforms to rank 0, which writes every file')
     return p
 
 
@@ -141,6 +147,8 @@ class Tester(object):
             f.readlines()
         pool = ThreadPoolExecutor(max_workers=8)
         n_utt = n_frames = 0
+        gather = bool(getattr(self.args, 'gather', False)) and world > 1
+        local = {}
         t0 = time.perf_counter()
         for i in range(len(self.tt_list)):
             reader = h5lite.File(self.tt_list[0])                    # test.py:138 reads tt_list[0] every time
@@ -163,9 +171,18 @@ class Tester(object):
                 outs = enhance(rows['nearend_mic'], rows['farend_speech'], rows['nearend_speech'],
                                [e['n_samples'] for e in egs])
                 for k, e, out in zip(ks, egs, outs):
-                    futs.append(pool.submit(self._write, est_subdir, k, out, e))
+                    if gather:
+                        local[k] = out
+                    else:
+                        futs.append(pool.submit(self._write, est_subdir, k, out, e))
                     n_utt += 1
                     n_frames += e['n_samples'] // 256 + 1
+            if gather:
+                merged = shard.gather_to_root(local)
+                local = {}
+                if merged is not None:
+                    for k in sorted(merged):
+                        futs.append(pool.submit(self._write, est_subdir, k, merged[k], self._load(reader, k)))
             for fu in futs:
                 fu.result()
             reader.close()

@@ -135,10 +135,10 @@ def _oracle_enhancer(weights, erb):
     return enhance
 
 
-def _args(tmp_path, lst, fl, streams=3):
+def _args(tmp_path, lst, fl, streams=3, extra=()):
     return build_parser().parse_args(['--tt_list', lst, '--filename_list', fl, '--ckpt_dir',
                                       str(tmp_path / 'exp'), '--est_path', str(tmp_path / 'est'),
-                                      '--streams', str(streams)])
+                                      '--streams', str(streams), *extra])
 
 
 def test_cli_file_tree_and_contents(tmp_path, golden_weights, golden_erb):
@@ -174,26 +174,28 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, tmp, lst, fl, weights, erb, q):
+def _rank_main(rank, world, port, tmp, lst, fl, weights, erb, q, extra=()):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
                       LOCAL_RANK=str(rank))
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
         import pathlib
         tmp = pathlib.Path(tmp)
-        res = _Tester(_args(tmp, lst, fl, streams=2), enhance=_oracle_enhancer(weights, erb)).test()
+        res = _Tester(_args(tmp, lst, fl, streams=2, extra=extra), enhance=_oracle_enhancer(weights, erb)).test()
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
 
 
-def test_cli_two_ranks_gloo(tmp_path, golden_weights, golden_erb):
-    _, lst, fl = _make_set(tmp_path, seed=50)
+@pytest.mark.parametrize('gather', [False, True], ids=['per-rank-writes', 'gather-to-rank0'])
+def test_cli_two_ranks_gloo(tmp_path, golden_weights, golden_erb, gather):
+    utts, lst, fl = _make_set(tmp_path, seed=50)
+    extra = ('--gather',) if gather else ()
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
     erb = golden_erb.astype(np.float32)
-    ps = [ctx.Process(target=_rank_main, args=(r, 2, port, str(tmp_path), lst, fl, golden_weights, erb, q))
+    ps = [ctx.Process(target=_rank_main, args=(r, 2, port, str(tmp_path), lst, fl, golden_weights, erb, q, extra))
           for r in range(2)]
     for p in ps:
         p.start()
@@ -205,3 +207,9 @@ def test_cli_two_ranks_gloo(tmp_path, golden_weights, golden_erb):
     assert res[0][1] == res[1][1] == (2 * len(LENS), 2 * sum(n // 256 + 1 for n in LENS))
     names = os.listdir(tmp_path / 'est' / 'test')
     assert len(names) == 5 * len(LENS) and len(set(names)) == len(names)
+    # the estimates are the single-utterance results whichever rank produced them
+    for k in (0, 2, 6):
+        est, _ = wavio.read_wav(str(tmp_path / 'est' / 'test' / f'{k}_near_est.wav'))
+        o, _ = O.little_net_forward(utts[k]['nearend_mic'], utts[k]['farend_speech'], utts[k]['nearend_speech'],
+                                    erb, golden_weights)
+        assert np.abs(wavio.pcm16(o).astype(int) - (est * 32768).astype(int)).max() <= 1

@@ -64,6 +64,43 @@ def test_gloo_shards_and_reductions(world):
         assert sums[1] == float(world)
 
 
+def _gather_worker(rank, world, port, lengths, q):
+    import numpy as np
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        mine = shard.balanced_shards(lengths, world)[rank]
+        outs = {k: (np.arange(256 * (lengths[k] // 256), dtype=np.float32) * 1e-3 + k) for k in mine}
+        got = shard.gather_to_root(outs)
+        q.put((rank, None if got is None else {k: v.tolist() for k, v in got.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_gloo_gather_to_root(world):
+    # 3 ranks over 2 utterances: one rank has nothing to send
+    import numpy as np
+    lengths = [1000, 70000] if world == 3 else [1000, 70000, 255, 9000, 513]
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gather_worker, args=(r, world, port, lengths, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=120) for _ in range(world)), key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(r[1] is None for r in res[1:])
+    got = res[0][1]
+    assert sorted(got) == list(range(len(lengths)))
+    for k, n in enumerate(lengths):
+        exp = np.arange(256 * (n // 256), dtype=np.float32) * 1e-3 + k
+        assert np.array_equal(np.asarray(got[k], np.float32), exp)
+
+
 def test_balanced_shards_properties():
     import random
     rng = random.Random(0)
