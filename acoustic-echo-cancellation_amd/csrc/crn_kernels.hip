@@ -706,7 +706,7 @@ __device__ __forceinline__ float ftanh(float x) { return 2.f * fsigmoid(2.f * x)
 // W_hh rows.  grid = (H / 32, CELLS * ceil(B / SB)); consecutive blocks take
 // consecutive unit slices, so each XCD keeps the same 4 slices (2 MB of
 // weights) for every step.
-template <typename T, int CELLS, int S, int SB_, int NBUF_>
+template <typename T, int CELLS, int S, int SB_, int NBUF_, int RB_ = 128>
 struct StepCfg {
     static constexpr int SB = SB_;                      // streams per block
     static constexpr int U = 32;
@@ -714,16 +714,18 @@ struct StepCfg {
     static constexpr int BN = 4 * U;
     static constexpr int FM = BM / 32, FN = 4;          // 2 x 2 waves
     static constexpr int NBUF = NBUF_;
+    static constexpr int RB = RB_;                      // K bytes per row per stage
     static constexpr int GROW = U * 4 * (int)sizeof(T);            // Gx bytes per row
-    static constexpr size_t STAGES = (size_t)NBUF * (BM + BN) * 128;
+    static constexpr size_t STAGES = (size_t)NBUF * (BM + BN) * RB;
     static constexpr size_t LDS = STAGES + (size_t)BM * GROW + (size_t)BM * U * 4;
 };
 
-template <typename T, int CELLS, int S, int SB_, int NBUF_>
+template <typename T, int CELLS, int S, int SB_, int NBUF_, int RB_>
 __global__ __launch_bounds__(256) void lstm_step_kernel(StepArgs p) {
-    using C_ = StepCfg<T, CELLS, S, SB_, NBUF_>;
+    using C_ = StepCfg<T, CELLS, S, SB_, NBUF_, RB_>;
     constexpr int SB = C_::SB, U = C_::U, BM = C_::BM, BN = C_::BN, FM = C_::FM, FN = C_::FN;
-    constexpr int LA = BM / 32;
+    constexpr int RB = C_::RB, RPI = 1024 / RB, CPR = RB / 16;   // DMA rows per instruction, chunks per row
+    constexpr int LA = BM / (RPI * 4);
     constexpr int ES = (int)sizeof(T);
     constexpr int GROW = C_::GROW;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -792,7 +794,7 @@ __global__ __launch_bounds__(256) void lstm_step_kernel(StepArgs p) {
         uint32_t arow[LA];
 #pragma unroll
         for (int i = 0; i < LA; ++i) {
-            const int r = 8 * (4 * i + wave) + (lane >> 3);
+            const int r = RPI * (4 * i + wave) + lane / CPR;
             const int s = r / SB, bl = r % SB;
             arow[i] = (b0 + bl < p.B)
                           ? (uint32_t)((((int64_t)bl * ystride) + ((int64_t)cell * S + s) * H) * ES)
@@ -800,9 +802,10 @@ __global__ __launch_bounds__(256) void lstm_step_kernel(StepArgs p) {
         }
         auto aoff = [&](int i, int kbyte) -> uint32_t { return arow[i] == kOOB ? kOOB : arow[i] + kbyte; };
         auto boff = [&](int i, int kbyte) -> uint32_t {
-            return (uint32_t)((8 * (4 * i + wave) + (lane >> 3)) * H * ES + kbyte);
+            return (uint32_t)((RPI * (4 * i + wave) + lane / CPR) * H * ES + kbyte);
         };
-        gemm_core_dma<T, BM, BN, FM, FN, C_::NBUF>(acc, smem, ra, rb, aoff, boff, H * ES / kStageBytes, wr0, wc0);
+        gemm_core_dma<T, BM, BN, FM, FN, C_::NBUF, decltype(aoff), decltype(boff), 4, RB>(acc, smem, ra, rb, aoff,
+                                                                                         boff, H * ES / RB, wr0, wc0);
     } else {
         wait_vm<0>();
         __builtin_amdgcn_s_barrier();
@@ -869,10 +872,10 @@ hipError_t launch_lstm_step(const StepArgs& a, int cells, int seqs, hipStream_t 
     // cell update, bit1 skip the recurrent GEMM, bit2 skip the Gx / c DMA
     static const int step_mode = env_int("CRN_STEP_MODE", 0);
     if (a.H % 32 || (a.H * (int)sizeof(T)) % kStageBytes) return hipErrorInvalidValue;
-#define CRN_STEP(C, S_, SB_, NB_)                                                                                 \
+#define CRN_STEP(C, S_, SB_, NB_, RB_)                                                                            \
     do {                                                                                                          \
-        auto kern = lstm_step_kernel<T, C, S_, SB_, NB_>;                                                         \
-        constexpr size_t lds = StepCfg<T, C, S_, SB_, NB_>::LDS;                                                  \
+        auto kern = lstm_step_kernel<T, C, S_, SB_, NB_, RB_>;                                                    \
+        constexpr size_t lds = StepCfg<T, C, S_, SB_, NB_, RB_>::LDS;                                             \
         static_assert(lds <= 160 * 1024, "LDS");                                                                  \
         static const hipError_t attr =                                                                            \
             hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, \
@@ -883,19 +886,24 @@ hipError_t launch_lstm_step(const StepArgs& a, int cells, int seqs, hipStream_t 
         hipLaunchKernelGGL(kern, dim3(a.H / 32, C * ((a.B + SB_ - 1) / SB_)), dim3(256), lds, st, a2);           \
     } while (0)
     // CRN_STEP_CFG: 0 = 64 streams per block, 3 (bf16) / 2 (f32) stage buffers (1 block per CU);
-    // 1 (default, fastest measured) = 32 streams, 2 buffers (2 blocks per CU); 2 = 32 streams,
-    // 3 buffers; 3 = 16 streams, 2 buffers (3 blocks per CU, v2 only)
+    // 1 = 32 streams, 2 buffers of 128-B K slices (2 blocks per CU); 2 = 32 streams, 3 buffers;
+    // 3 = 16 streams, 2 buffers (3 blocks per CU, v2 only); 4 = 32 streams, 4 buffers of 64-B K
+    // slices (2 blocks per CU, 3 slices in flight per block: slower, 37.8 vs 32.8 ms of LSTM per
+    // 256 x 10 s batch — the step GEMM is not bound by the slices in flight)
     static const int cfg = env_int("CRN_STEP_CFG", 1);
     constexpr int NB0 = sizeof(T) == 2 ? 3 : 2;
+    if ((a.H * (int)sizeof(T)) % 64) return hipErrorInvalidValue;
     if (cells == 2 && seqs == 2) {
-        if (cfg == 1) CRN_STEP(2, 2, 32, 2);
-        else if (cfg == 2) CRN_STEP(2, 2, 32, 3);
-        else if (cfg == 3) CRN_STEP(2, 2, 16, 2);
-        else CRN_STEP(2, 2, 64, NB0);
+        if (cfg == 1) CRN_STEP(2, 2, 32, 2, 128);
+        else if (cfg == 2) CRN_STEP(2, 2, 32, 3, 128);
+        else if (cfg == 3) CRN_STEP(2, 2, 16, 2, 128);
+        else if (cfg == 4) CRN_STEP(2, 2, 32, 4, 64);
+        else CRN_STEP(2, 2, 64, NB0, 128);
     } else if (cells == 1 && seqs == 1) {
-        if (cfg == 1) CRN_STEP(1, 1, 32, 2);
-        else if (cfg == 2) CRN_STEP(1, 1, 32, 3);
-        else CRN_STEP(1, 1, 64, NB0);
+        if (cfg == 1) CRN_STEP(1, 1, 32, 2, 128);
+        else if (cfg == 2) CRN_STEP(1, 1, 32, 3, 128);
+        else if (cfg == 4) CRN_STEP(1, 1, 64, 4, 64);
+        else CRN_STEP(1, 1, 64, NB0, 128);
     } else {
         return hipErrorInvalidValue;
     }
