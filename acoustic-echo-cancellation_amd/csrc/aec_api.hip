@@ -211,6 +211,8 @@ struct aec_handle {
     int debug = 0;
     int gru_mode = 0;            // AEC_GRU_MODE (timing experiments; results invalid unless 0)
     int nlms_mode = 0;           // AEC_NLMS_MODE (timing experiments; results invalid unless 0)
+    int nlms_prio = 0;           // AEC_NLMS_PRIO: wave priorities mic|ref|nlms digits (0: all equal, fastest measured)
+    int nlms_erb = 1;            // AEC_NLMS_ERB: role running the mic_erb pass (1 ref, 2 nlms)
     int64_t last_B = 0, last_T = 0;
     // kernel timing (aec_profile_*)
     int profile = 0;
@@ -323,6 +325,8 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
     h->device = device;
     if (const char* m = std::getenv("AEC_GRU_MODE")) h->gru_mode = std::atoi(m);
     if (const char* m = std::getenv("AEC_NLMS_MODE")) h->nlms_mode = std::atoi(m);
+    if (const char* m = std::getenv("AEC_NLMS_PRIO")) h->nlms_prio = std::atoi(m);
+    if (const char* m = std::getenv("AEC_NLMS_ERB")) h->nlms_erb = std::atoi(m);
     if (const char* m = std::getenv("AEC_SUBBATCH")) h->sub_max = std::max(1, std::min(aec_handle::kMaxSub, std::atoi(m)));
     {
         int cus = 0;
@@ -468,6 +472,8 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
             a.feats = h->d_feats; a.Tmax = Tmax; a.spec = h->d_spec;
             a.taps = h->cfg.nlms_taps; a.mu = h->cfg.nlms_mu; a.beta = h->cfg.nlms_beta; a.delta = h->cfg.nlms_delta;
             a.mode = h->nlms_mode;
+            a.prio = h->nlms_prio;
+            a.erb_role = h->nlms_erb;
             mark(h, ks);
             HIP_TRY(h, launch_nlms_analysis(a, b1 - b0, ks));
         } else {

@@ -291,6 +291,16 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
     }
     const int wave = tid >> 6, lane = tid & 63;
     const int role = wave >> 2, q = wave & 3;                        // 0 mic, 1 ref, 2 nlms
+    {
+        // VALU issue between the three waves of a SIMD goes by priority, then age
+        const int pr = role == 0 ? p.prio / 100 : (role == 1 ? (p.prio / 10) % 10 : p.prio % 10);
+        switch (pr) {
+            case 1: __builtin_amdgcn_s_setprio(1); break;
+            case 2: __builtin_amdgcn_s_setprio(2); break;
+            case 3: __builtin_amdgcn_s_setprio(3); break;
+            default: break;
+        }
+    }
     const int gg = lane >> 4, lb = lane & 15, sw = 16 * (gg & 1);
     float* wr = sWave + (role < 2 ? wave : 0) * kWaveFloats;
     float* scr = wr + gg * kGroupFloats;
@@ -310,6 +320,29 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
     float2* spec = p.spec + (int64_t)b * p.Tmax * kSpecRow;
     float* feats = p.feats + (int64_t)b * p.Tmax * 96;
     const float mu = p.mu, beta = p.beta, delta = p.delta;
+    // mic_erb of chunk c2 from its error rows (complete since the barriers of
+    // tick c2 + 1); this group's frame 4 q + gg.  Run by the ref waves
+    // (erb_role 1) or by the nlms waves after their recursion (erb_role 2).
+    const int erb_role = p.erb_role == 2 ? 2 : 1;
+    auto mic_erb_pass = [&](int c2) {
+        const int64_t t2 = (int64_t)c2 * kFPB + 4 * q + gg;
+        float* er = sE + (c2 & 1) * kFPB * kERow + (4 * q + gg) * kERow;
+        const float2* row = reinterpret_cast<const float2*>(er);
+        float2 xa[8], xb[8], x128;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const int kk = lb + 16 * m;
+            xa[m] = row[kk];
+            xb[m] = row[(256 - kk) & 255];
+        }
+        x128 = row[128];
+        xa[0] = lb == 0 ? make_float2(xa[0].x, 0.f) : xa[0];
+        xb[0] = lb == 0 ? make_float2(xb[0].y, 0.f) : xb[0];     // slot 0 = (E[0], E[256])
+        wave_fence();
+        mags_to_scr(er, lb, sw, xa, xb, x128);
+        wave_fence();
+        erb_project(er, sSched, sComb, L, lb, sw, t2 < T ? feats + t2 * 96 : nullptr);
+    };
     __syncthreads();
 
     // The nlms waves and the transform waves run separate loops with the same
@@ -335,6 +368,7 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
                     if (t0 + i < T) spec[(t0 + i) * kSpecRow + k] = e;
                 }
             }
+            if (erb_role == 2 && c >= 2 && !(p.mode & 4)) mic_erb_pass(c - 2);
             __syncthreads();                                          // rows of chunk c complete
             if (c < nch) {
 #pragma unroll
@@ -379,27 +413,7 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
                 row_to_scr(scr, lb, xa, xb, x128);
             }
         } else {
-            const int c2 = c - 2;
-            if (c2 >= 0 && !(p.mode & 4)) {
-                // mic_erb of chunk c-2 from its error rows (complete since the
-                // barriers of tick c-1); this group's frame 4 q + gg
-                const int64_t t2 = (int64_t)c2 * kFPB + 4 * q + gg;
-                float* er = sE + (c2 & 1) * kFPB * kERow + (4 * q + gg) * kERow;
-                const float2* row = reinterpret_cast<const float2*>(er);
-#pragma unroll
-                for (int m = 0; m < 8; ++m) {
-                    const int kk = lb + 16 * m;
-                    xa[m] = row[kk];
-                    xb[m] = row[(256 - kk) & 255];
-                }
-                x128 = row[128];
-                xa[0] = lb == 0 ? make_float2(xa[0].x, 0.f) : xa[0];
-                xb[0] = lb == 0 ? make_float2(xb[0].y, 0.f) : xb[0];     // slot 0 = (E[0], E[256])
-                wave_fence();
-                mags_to_scr(er, lb, sw, xa, xb, x128);
-                wave_fence();
-                erb_project(er, sSched, sComb, L, lb, sw, t2 < T ? feats + t2 * 96 : nullptr);
-            }
+            if (erb_role == 1 && c >= 2 && !(p.mode & 4)) mic_erb_pass(c - 2);
             if (c < nch && !(p.mode & 8)) {
                 nlms_transform(wr, scr, pf, p.cvals[b * 3 + 1], n, wt, lane, gg, lb, sHann, sTwT, sTw512,
                                c + 1 < nch ? row_ref : nullptr, wt + kFPB, al_ref, xa, xb, x128);
