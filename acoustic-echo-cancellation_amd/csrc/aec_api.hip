@@ -213,6 +213,8 @@ struct aec_handle {
     int nlms_mode = 0;           // AEC_NLMS_MODE (timing experiments; results invalid unless 0)
     int nlms_prio = 0;           // AEC_NLMS_PRIO: wave priorities mic|ref|nlms digits (0: all equal, fastest measured)
     int nlms_erb = 1;            // AEC_NLMS_ERB: role running the mic_erb pass (1 ref, 2 nlms)
+    int fused = 1;               // AEC_FUSED_SYNTH: GRU + synthesis in one kernel (NLMS path)
+    int fused_mode = 0;          // AEC_FUSED_MODE (timing experiments; results invalid unless 0)
     int64_t last_B = 0, last_T = 0;
     // kernel timing (aec_profile_*)
     int profile = 0;
@@ -327,6 +329,8 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
     if (const char* m = std::getenv("AEC_NLMS_MODE")) h->nlms_mode = std::atoi(m);
     if (const char* m = std::getenv("AEC_NLMS_PRIO")) h->nlms_prio = std::atoi(m);
     if (const char* m = std::getenv("AEC_NLMS_ERB")) h->nlms_erb = std::atoi(m);
+    if (const char* m = std::getenv("AEC_FUSED_SYNTH")) h->fused = std::atoi(m);
+    if (const char* m = std::getenv("AEC_FUSED_MODE")) h->fused_mode = std::atoi(m);
     if (const char* m = std::getenv("AEC_SUBBATCH")) h->sub_max = std::max(1, std::min(aec_handle::kMaxSub, std::atoi(m)));
     {
         int cus = 0;
@@ -497,8 +501,6 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
         g.dbg_mask = h->debug ? h->d_dbg + B * Tmax * 32 : nullptr;
         g.mode = h->gru_mode;
         g.b0 = b0;
-        HIP_TRY(h, launch_gru(g, b1 - b0, ks));
-        mark(h, ks);
 
         SynthArgs y{};
         y.mic = mic; y.ld = ld; y.items = h->d_sitems + h->sitem_off[b0];
@@ -508,8 +510,18 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
         y.bintab = h->d_bintab; y.est = h->d_est; y.Tmax = Tmax;
         y.out = out; y.ld_out = ld_out;
         y.spec = h->cfg.nlms_taps > 0 ? h->d_spec : nullptr;
-        HIP_TRY(h, launch_synthesis(y, ks));
-        mark(h, ks);
+        y.fmode = h->fused_mode;
+        if (y.spec && h->fused && h->gru_mode == 0) {
+            // one kernel: the synthesis runs two chunks behind the recurrence
+            HIP_TRY(h, launch_gru_synth(g, y, b1 - b0, ks));
+            mark(h, ks);
+            mark(h, ks);
+        } else {
+            HIP_TRY(h, launch_gru(g, b1 - b0, ks));
+            mark(h, ks);
+            HIP_TRY(h, launch_synthesis(y, ks));
+            mark(h, ks);
+        }
         if (S > 1) HIP_TRY(h, hipEventRecord(h->ev_done[k], ks));
     }
     if (S > 1)

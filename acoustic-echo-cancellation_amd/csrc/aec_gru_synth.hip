@@ -1,0 +1,409 @@
+// aec_gru_synth.hip — K3+K4 fused: the post-filter recurrence and the
+// synthesis of the same stream in one block (gfx950).
+//
+// Reference: nn.GRU + linear1/relu + linear2/sigmoid + mask + loss
+// (Stage2_lhm/scripts/network/ERB.py:213-217, 287-323), then the ERB gains,
+// conv-iSTFT and WOLA (ERB.py:304-316, attention_ccrn.py:82-101).
+//
+// The GRU is one dependent step per frame (latency-bound: ~680 cycles a
+// step on one wave), so gru_kernel leaves its CU mostly idle while the
+// separate synthesis kernel then streams the error spectrum back in.  Here
+// the synthesis waves of the stream run inside the GRU's own tick pipeline,
+// two chunks behind the recurrence:
+//
+//   wave 0       recurrence, chunk c                     (gru_kernel's code)
+//   waves 1..3   stage feats of chunk c+2, load chunk c+3, gi = W_ih x + b of chunk c+1
+//   waves 4..6   head / mask / est_erb / loss of chunk c-1 -> est (HBM + LDS ring);
+//                OLA + WOLA of chunk c-3 from the frame ring -> out
+//   waves 7..10  synthesis (gains, irFFT, window) of chunk c-2 into the LDS
+//                frame ring;  E rows of chunk c-1 into registers
+//
+// one block barrier per tick of 16 frames.  The arithmetic of every output
+// sample is the unfused path's (synth_frame, the same OLA expression), so
+// the result is bit-identical to gru_kernel + synthesis_kernel
+// (tests/test_gpu_parity.py::test_fused_synthesis_bit_exact).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "aec_fft.h"
+#include "aec_frame.h"
+#include "aec_launch.h"
+#include "aec_tables.h"
+
+namespace aec {
+
+namespace {
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+constexpr int kGiWaves = 3, kHeadWaves = 3, kSynWaves = 4;
+constexpr int kFusedWaves = 1 + kGiWaves + kHeadWaves + kSynWaves;    // 11
+constexpr int kFusedThreads = 64 * kFusedWaves;
+constexpr int kGiLanes = 64 * kGiWaves;                               // 192
+constexpr int kHeadLanes = 64 * kHeadWaves;                           // 192
+constexpr int kHeadGrp = kHeadLanes / 32;                             // 6 groups of 32 lanes
+constexpr int kEstS = 33;                                             // est ring row stride
+
+// LDS carve (floats)
+constexpr int oX = 0;                                   // [2][16][64]
+constexpr int oGi = oX + 2 * kCH * 64;                  // [2][16][96]
+constexpr int oH = oGi + 2 * kCH * 96;                  // [2][16][32]
+constexpr int oMic = oH + 2 * kCH * 32;                 // [4][16][32]
+constexpr int oNear = oMic + 4 * kCH * 32;              // [4][16][32]
+constexpr int oO = oNear + 4 * kCH * 32;                // [6][32]
+constexpr int oLoss = oO + kHeadGrp * 32;               // [8]
+constexpr int oHb = oLoss + 8;                          // [32]
+constexpr int oEst = oHb + 32;                          // [2][16][33] (+2 pad)
+constexpr int oBin = (oEst + 2 * kCH * kEstS + 2 + 3) & ~3;   // float4[257] (+3)
+constexpr int oTw512 = oBin + 260 * 4;                  // float2[258]
+constexpr int oTwT = oTw512 + 258 * 2;                  // float2[256]
+constexpr int oHann = oTwT + 256 * 2;                   // [512]
+constexpr int oCoff = oHann + 512;                      // [256]
+constexpr int oTail = oCoff + 256;                      // [2][256]
+constexpr int oOut = oTail + 2 * 256;                   // [2][4 waves][4 groups][576] frame ring
+constexpr int kFusedFloats = oOut + 2 * kSynWaves * 4 * kGroupFloats;
+static_assert(oOut % 4 == 0 && oBin % 4 == 0, "16-B alignment");
+}  // namespace
+
+size_t gru_synth_smem_bytes() { return (size_t)kFusedFloats * 4; }
+
+// The tick barrier: LDS traffic drained (lgkmcnt(0)), global loads and
+// stores left in flight.  __syncthreads would also drain vmcnt, exposing the
+// HBM latency of the loads issued for the NEXT tick (feats, E rows) once per
+// tick; the compiler waits for those registers where they are used.  The
+// empty asm keeps the compiler from moving memory accesses across it.
+__device__ __forceinline__ void tick_barrier() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);        // gfx9: vmcnt 63, expcnt 7, lgkmcnt 0
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+__global__ __launch_bounds__(kFusedThreads, 1) void gru_synth_kernel(GruArgs p, SynthArgs y) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* sX = smem + oX;
+    float* sGi = smem + oGi;
+    float* sH = smem + oH;
+    float* sMic = smem + oMic;
+    float* sNear = smem + oNear;
+    float* sO = smem + oO;
+    float* sLoss = smem + oLoss;
+    float* sHb = smem + oHb;
+    float* sEst = smem + oEst;
+    float4* sBin = reinterpret_cast<float4*>(smem + oBin);
+    float2* sTw512 = reinterpret_cast<float2*>(smem + oTw512);
+    float2* sTwT = reinterpret_cast<float2*>(smem + oTwT);
+    float* sHann = smem + oHann;
+    float* sCoff = smem + oCoff;
+    float* sTail = smem + oTail;
+    float* sOut = smem + oOut;
+
+    const int b = p.b0 + blockIdx.x;
+    const int64_t n = p.lens[b];
+    const int T = (int)(n / kHop + 1);
+    const int64_t nhop = n / kHop;                       // output hops (T - 1)
+    const int nch = (T + kCH - 1) / kCH;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const float* W_ih = p.w;                  // [96][64]
+    const float* W_hh = p.w + 96 * 64;        // [96][32]
+    const float* b_ih = W_hh + 96 * 32;       // [96]
+    const float* b_hh = b_ih + 96;            // [96]
+    const float* W1 = b_hh + 96;              // [32][64]
+    const float* b1 = W1 + 32 * 64;           // [32]
+    const float* W2 = b1 + 32;                // [32][32]
+    const float* b2 = W2 + 32 * 32;           // [32]
+    const float* fb = p.feats + (int64_t)b * p.Tmax * 96;
+
+    // synthesis tables (read after the first tick barrier)
+    {
+        const DevTables* tb = reinterpret_cast<const DevTables*>(y.tables);
+        const float4* bt = reinterpret_cast<const float4*>(y.bintab);
+        for (int i = tid; i < 257; i += kFusedThreads) sBin[i] = bt[i];
+        for (int i = tid; i < 258; i += kFusedThreads) sTw512[i] = tb->tw512[i];
+        for (int i = tid; i < 256; i += kFusedThreads) {
+            sTwT[i] = tb->twT[i];
+            sCoff[i] = tb->inv_coff[i];
+            sTail[i] = 0.f;
+            sTail[256 + i] = 0.f;
+        }
+        for (int i = tid; i < 512; i += kFusedThreads) sHann[i] = tb->hann[i];
+    }
+
+    if (wave == 0) {
+        // ---------------- recurrence wave (gru_kernel wave 0) ----------------
+        __builtin_amdgcn_s_setprio(3);
+        const int j = lane & 31, kh = lane >> 5;
+        f2v wrz[16], wn[8];
+        {
+            const float* rR = W_hh + j * 32 + 16 * kh;
+            const float* rZ = W_hh + (32 + j) * 32 + 16 * kh;
+            const float* rN = W_hh + (64 + j) * 32 + 16 * kh;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) wrz[k] = f2v{rR[k], rZ[k]};
+#pragma unroll
+            for (int i = 0; i < 8; ++i) wn[i] = f2v{rN[2 * i], rN[2 * i + 1]};
+        }
+        const float bhn = b_hh[64 + j];
+        float hj = 0.f;
+        float* hb = sHb;
+        if (lane < 32) hb[lane] = 0.f;
+        for (int c = -3; c <= nch + 2; ++c) {
+            if (c >= 0 && c < nch) {
+                const int f_end = min(kCH, T - c * kCH);
+                const float* gi = sGi + (c & 1) * kCH * 96;
+                float gr = gi[j], gz = gi[32 + j], gn = gi[64 + j];
+                for (int f = 0; f < f_end; ++f) {
+                    const int fn = f + 1 < f_end ? f + 1 : f;
+                    const float ngr = gi[fn * 96 + j], ngz = gi[fn * 96 + 32 + j], ngn = gi[fn * 96 + 64 + j];
+                    const float4* h4 = reinterpret_cast<const float4*>(hb + 16 * kh);
+                    const float4 q0 = h4[0], q1 = h4[1], q2 = h4[2], q3 = h4[3];
+                    const float hk[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                                          q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+                    f2v arz[4] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}};
+                    f2v an[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
+#pragma unroll
+                    for (int k = 0; k < 16; ++k)
+                        arz[k & 3] = __builtin_elementwise_fma(wrz[k], f2v{hk[k], hk[k]}, arz[k & 3]);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        an[i & 1] = __builtin_elementwise_fma(wn[i], f2v{hk[2 * i], hk[2 * i + 1]}, an[i & 1]);
+                    const f2v rz = (arz[0] + arz[1]) + (arz[2] + arz[3]);
+                    const f2v n2 = an[0] + an[1];
+                    const float pr = rz.x, pz = rz.y, pn = n2.x + n2.y;
+                    const auto sr = __builtin_amdgcn_permlane32_swap(__float_as_uint(pr), __float_as_uint(pr), false, false);
+                    const auto sz = __builtin_amdgcn_permlane32_swap(__float_as_uint(pz), __float_as_uint(pz), false, false);
+                    const auto sn = __builtin_amdgcn_permlane32_swap(__float_as_uint(pn), __float_as_uint(pn), false, false);
+                    const float rdot = pr + __uint_as_float(kh ? sr[0] : sr[1]);
+                    const float zdot = pz + __uint_as_float(kh ? sz[0] : sz[1]);
+                    const float ndot = pn + __uint_as_float(kh ? sn[0] : sn[1]);
+                    const float r = sigmoidf_(gr + rdot);
+                    const float z = sigmoidf_(gz + zdot);
+                    const float nn = tanhf_(gn + r * (ndot + bhn));
+                    hj = (1.f - z) * nn + z * hj;
+                    if (kh == 0) {
+                        hb[j] = hj;
+                        sH[((c & 1) * kCH + f) * 32 + j] = hj;
+                    }
+                    gr = ngr; gz = ngz; gn = ngn;
+                }
+            }
+            tick_barrier();
+        }
+    } else if (wave <= kGiWaves) {
+        // ---------------- feats staging + input projection ----------------
+        const int hl = tid - 64;                              // 0..191
+        const int grow = hl % 96, fq = hl / 96;               // frames fq, fq + 2, ...
+        float wih[64];
+#pragma unroll
+        for (int k = 0; k < 64; ++k) wih[k] = W_ih[grow * 64 + k];
+        const float gbias = b_ih[grow] + (grow < 64 ? b_hh[grow] : 0.f);
+        constexpr int kStU = (kCH * 32 + kGiLanes - 1) / kGiLanes;    // 3 elements per lane
+        float pm[kStU], pr[kStU], pn[kStU];
+        auto load_chunk = [&](int cc) {
+#pragma unroll
+            for (int u = 0; u < kStU; ++u) {
+                const int e = hl + u * kGiLanes;
+                const int t = cc * kCH + (e >> 5);
+                const bool ok = e < kCH * 32 && t < T;
+                const float* f = fb + (int64_t)t * 96 + (e & 31);
+                pm[u] = ok ? f[0] : 0.f;
+                pr[u] = ok ? f[32] : 0.f;
+                pn[u] = ok && p.has_near ? f[64] : 0.f;
+            }
+        };
+#pragma unroll
+        for (int u = 0; u < kStU; ++u) pm[u] = pr[u] = pn[u] = 0.f;
+        for (int c = -3; c <= nch + 2; ++c) {
+            const int cs = c + 2;
+            if (cs >= 0 && cs < nch) {
+#pragma unroll
+                for (int u = 0; u < kStU; ++u) {
+                    const int e = hl + u * kGiLanes;
+                    if (e < kCH * 32) {
+                        const int f = e >> 5, jj = e & 31;
+                        sX[((cs & 1) * kCH + f) * 64 + jj] = pm[u];
+                        sX[((cs & 1) * kCH + f) * 64 + 32 + jj] = fabsf(pm[u] - pr[u]);
+                        sMic[((cs & 3) * kCH + f) * 32 + jj] = pm[u];
+                        sNear[((cs & 3) * kCH + f) * 32 + jj] = pn[u];
+                    }
+                }
+            }
+            if (c + 3 < nch) load_chunk(c + 3);
+            const int cg = c + 1;
+            if (cg >= 0 && cg < nch) {
+#pragma unroll 2
+                for (int i = 0; i < kCH / 2; ++i) {
+                    const int f = fq + 2 * i;
+                    const float4* x4 = reinterpret_cast<const float4*>(sX + ((cg & 1) * kCH + f) * 64);
+                    f2v a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const float4 xv = x4[q];
+                        a0 = __builtin_elementwise_fma(f2v{wih[4 * q], wih[4 * q + 1]}, f2v{xv.x, xv.y}, a0);
+                        a1 = __builtin_elementwise_fma(f2v{wih[4 * q + 2], wih[4 * q + 3]}, f2v{xv.z, xv.w}, a1);
+                    }
+                    const f2v s2 = a0 + a1;
+                    sGi[((cg & 1) * kCH + f) * 96 + grow] = gbias + (s2.x + s2.y);
+                }
+            }
+            tick_barrier();
+        }
+    } else if (wave <= kGiWaves + kHeadWaves) {
+        // ---------------- head / mask / est_erb / loss ----------------
+        const int hh = tid - 64 * (1 + kGiWaves);             // 0..191
+        const int hj_ = hh & 31, fg = hh >> 5;                // frames fg, fg + 6, fg + 12
+        float w1[64], w2[32];
+#pragma unroll
+        for (int k = 0; k < 64; ++k) w1[k] = W1[hj_ * 64 + k];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) w2[k] = W2[hj_ * 32 + k];
+        const float b1j = b1[hj_], b2j = b2[hj_];
+        float lacc = 0.f;
+        float* orow = y.out + (int64_t)b * y.ld_out;
+        const bool oal = ((y.ld_out & 3) == 0) && ((reinterpret_cast<uintptr_t>(y.out) & 15) == 0);
+        for (int c = -3; c <= nch + 2; ++c) {
+            const int ch = c - 1;
+            if (ch >= 0 && ch < nch) {
+                for (int f = fg; f < kCH; f += kHeadGrp) {
+                    const int t = ch * kCH + f;
+                    const float4* h4 = reinterpret_cast<const float4*>(sH + ((ch & 1) * kCH + f) * 32);
+                    const float4* m4 = reinterpret_cast<const float4*>(sMic + ((ch & 3) * kCH + f) * 32);
+                    float est = 0.f;
+                    if (t < T) {                              // uniform within the 32-lane group
+                        f2v a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) {
+                            const float4 hv = h4[q];
+                            const float4 mv = m4[q];
+                            a0 = __builtin_elementwise_fma(f2v{w1[4 * q], w1[4 * q + 1]}, f2v{hv.x, hv.y}, a0);
+                            a1 = __builtin_elementwise_fma(f2v{w1[4 * q + 2], w1[4 * q + 3]}, f2v{hv.z, hv.w}, a1);
+                            a0 = __builtin_elementwise_fma(f2v{w1[32 + 4 * q], w1[32 + 4 * q + 1]}, f2v{mv.x, mv.y}, a0);
+                            a1 = __builtin_elementwise_fma(f2v{w1[32 + 4 * q + 2], w1[32 + 4 * q + 3]}, f2v{mv.z, mv.w}, a1);
+                        }
+                        const f2v s1 = a0 + a1;
+                        sO[fg * 32 + hj_] = fmaxf(b1j + (s1.x + s1.y), 0.f);
+                        wave_fence();
+                        const float4* o4 = reinterpret_cast<const float4*>(sO + fg * 32);
+                        f2v c0 = {0.f, 0.f}, c1 = {0.f, 0.f};
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) {
+                            const float4 ov = o4[q];
+                            c0 = __builtin_elementwise_fma(f2v{w2[4 * q], w2[4 * q + 1]}, f2v{ov.x, ov.y}, c0);
+                            c1 = __builtin_elementwise_fma(f2v{w2[4 * q + 2], w2[4 * q + 3]}, f2v{ov.z, ov.w}, c1);
+                        }
+                        wave_fence();
+                        const f2v s2 = c0 + c1;
+                        const float mask = sigmoidf_(b2j + (s2.x + s2.y));
+                        const float me = sMic[((ch & 3) * kCH + f) * 32 + hj_];
+                        est = mask * me;
+                        const int64_t o_idx = ((int64_t)b * p.Tmax + t) * 32 + hj_;
+                        p.est[o_idx] = est;
+                        if (p.dbg_h) p.dbg_h[o_idx] = sH[((ch & 1) * kCH + f) * 32 + hj_];
+                        if (p.dbg_mask) p.dbg_mask[o_idx] = mask;
+                        if (p.has_near) {
+                            const float d = sqrtf(sNear[((ch & 3) * kCH + f) * 32 + hj_]) - sqrtf(est);
+                            lacc += d * d;
+                        }
+                    }
+                    sEst[((ch & 1) * kCH + f) * kEstS + hj_] = est;   // frames past the end: gain 0
+                }
+            }
+            // OLA + WOLA of chunk k = c - 3 (frames 16k .. 16k+15 in ring k & 1):
+            //     hops 16k-1 .. 16k+14; hop 16k-1 uses the tail of frame 16k-1
+            const int k = c - 3;
+            if (k >= 0 && k < nch && !(y.fmode & 2)) {
+                const float* ring = sOut + (k & 1) * (kSynWaves * 4 * kGroupFloats);
+                const float* tail_in = sTail + (k & 1) * 256;
+                const int64_t j0 = (int64_t)k * kCH - 1;
+                const int nh = (int)min((int64_t)kCH, nhop - j0);       // hops j0 .. j0 + nh - 1 below nhop
+                if (oal) {
+                    for (int e = hh; e < kCH * (kHop / 4); e += kHeadLanes) {
+                        const int i = e >> 6, r = (e & 63) * 4;         // hop j0 + i = frame i-1 (2nd half) + frame i
+                        if (i >= nh || j0 + i < 0) continue;
+                        const float4 a = i == 0 ? *reinterpret_cast<const float4*>(tail_in + r)
+                                                : *reinterpret_cast<const float4*>(ring + (i - 1) * kGroupFloats + 256 + r);
+                        const float4 cv = *reinterpret_cast<const float4*>(ring + i * kGroupFloats + r);
+                        const float4 cf = *reinterpret_cast<const float4*>(sCoff + r);
+                        float4 o;
+                        o.x = (a.x + cv.x) * cf.x + 1e-9f;
+                        o.y = (a.y + cv.y) * cf.y + 1e-9f;
+                        o.z = (a.z + cv.z) * cf.z + 1e-9f;
+                        o.w = (a.w + cv.w) * cf.w + 1e-9f;
+                        *reinterpret_cast<float4*>(orow + (j0 + i) * kHop + r) = o;
+                    }
+                } else {
+                    for (int e = hh; e < kCH * kHop; e += kHeadLanes) {
+                        const int i = e >> 8, r = e & 255;
+                        if (i >= nh || j0 + i < 0) continue;
+                        const float a = i == 0 ? tail_in[r] : ring[(i - 1) * kGroupFloats + 256 + r];
+                        const float cv = ring[i * kGroupFloats + r];
+                        orow[(j0 + i) * kHop + r] = (a + cv) * sCoff[r] + 1e-9f;
+                    }
+                }
+                for (int r = hh; r < 256; r += kHeadLanes)
+                    sTail[((k + 1) & 1) * 256 + r] = ring[(kCH - 1) * kGroupFloats + 256 + r];
+            }
+            tick_barrier();
+        }
+        if (p.loss) {
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) lacc += __shfl_xor(lacc, o);
+            if (lane == 0) sLoss[wave - 1 - kGiWaves] = lacc;
+        }
+    } else {
+        // ---------------- synthesis waves ----------------
+        const int sw = wave - (1 + kGiWaves + kHeadWaves);    // 0..3
+        const int gg = lane >> 4, lb = lane & 15;
+        const int fl = 4 * sw + gg;                           // frame of the chunk this group synthesises
+        const float2* spec = y.spec + (int64_t)b * y.Tmax * 256;
+        float2 xa[8] = {}, xb[8] = {}, x128 = {};
+        auto load_rows = [&](int cc) {
+            // E rows of chunk cc.  A frame past the last one (t > nhop) feeds no
+            // written hop (hop j reads frames j and j + 1 <= nhop), so it may
+            // read any valid row: the index is clamped, the loads stay plain
+            // global loads with no per-lane select.
+            const int64_t t = min((int64_t)cc * kCH + fl, nhop);
+            const float2* row = spec + t * 256;
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const int kk = lb + 16 * m;
+                const float2 a = row[kk];
+                const float2 c2 = row[(256 - kk) & 255];
+                xa[m] = kk == 0 ? make_float2(a.x, 0.f) : a;
+                xb[m] = kk == 0 ? make_float2(a.y, 0.f) : c2;
+            }
+            x128 = row[128];
+        };
+        for (int c = -3; c <= nch + 2; ++c) {
+            // (2) synthesis of chunk c - 2 into ring (c - 2) & 1 (rows loaded last tick)
+            const int cs = c - 2;
+            if (cs >= 0 && cs < nch && !(y.fmode & 1)) {
+                float* scr = sOut + (cs & 1) * (kSynWaves * 4 * kGroupFloats) + fl * kGroupFloats;
+                synth_frame(xa, xb, x128, sEst + ((cs & 1) * kCH + fl) * kEstS, sBin, sTw512, sTwT, sHann, scr, lb);
+            }
+            // (3) E rows of chunk c - 1 for the next tick
+            if (c - 1 >= 0 && c - 1 < nch && !(y.fmode & 4)) load_rows(c - 1);
+            tick_barrier();
+        }
+    }
+    if (p.loss) {
+        __syncthreads();
+        if (tid == 0) {
+            float s = 0.f;
+            for (int w = 0; w < kHeadWaves; ++w) s += sLoss[w];
+            p.loss[b] = s / (float)(T * 32);
+        }
+    }
+}
+
+hipError_t launch_gru_synth(const GruArgs& g, const SynthArgs& y, int B, hipStream_t st) {
+    if (B <= 0) return hipSuccess;
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gru_synth_kernel),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)gru_synth_smem_bytes());
+    if (attr != hipSuccess) return attr;
+    hipLaunchKernelGGL(gru_synth_kernel, dim3(B), dim3(kFusedThreads), gru_synth_smem_bytes(), st, g, y);
+    return hipGetLastError();
+}
+
+}  // namespace aec

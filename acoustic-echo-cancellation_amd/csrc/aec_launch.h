@@ -86,6 +86,8 @@ struct SynthArgs {
     float* out;
     int64_t ld_out;
     const float2* spec;      // NLMS error spectrum [B][Tmax][256], or null: re-derive the mic spectrum
+    int fmode;               // fused kernel timing experiments only (AEC_FUSED_MODE; results invalid
+                             // unless 0): bit0 skip the synthesis, bit1 skip the OLA, bit2 skip the E loads
 };
 
 // Fused streaming step (aec_stream.hip): one 256-sample hop of B streams.
@@ -140,5 +142,8 @@ hipError_t launch_nlms_analysis(const NlmsArgs& a, int nb, hipStream_t st);
 hipError_t launch_gru(const GruArgs& a, int B, hipStream_t st);
 hipError_t launch_synthesis(const SynthArgs& a, hipStream_t st);
 hipError_t launch_stream_step(const StreamStepArgs& a, int B, int taps, hipStream_t st);
+// K3+K4 fused (aec_gru_synth.hip): GRU + head + synthesis of the NLMS error spectrum
+hipError_t launch_gru_synth(const GruArgs& g, const SynthArgs& y, int B, hipStream_t st);
+size_t gru_synth_smem_bytes();
 
 }  // namespace aec
