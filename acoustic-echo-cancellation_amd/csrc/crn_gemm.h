@@ -198,7 +198,9 @@ __device__ __forceinline__ void wait_vm() {
 
 // RB = bytes of K per row per stage (128: two 64-B k-chunks; 64: one).  A DMA
 // instruction writes 64 lanes x 16 B = 1 KiB = 1024 / RB rows.
-template <typename T, int BM, int BN, int FM, int FN, int NBUF, class AO, class BO, int NW = 4, int RB = 128>
+// AUXA: cache policy bits of the A-operand DMA (2 = nt: streamed operand, keep L2 for B)
+template <typename T, int BM, int BN, int FM, int FN, int NBUF, class AO, class BO, int NW = 4, int RB = 128,
+          int AUXA = 0>
 __device__ __forceinline__ void gemm_core_dma(f32x4 (&acc)[FM][FN], char* smem, __amdgpu_buffer_rsrc_t ra,
                                               __amdgpu_buffer_rsrc_t rb, const AO& aoff, const BO& boff,
                                               int nstages, int wr0, int wc0) {
@@ -216,7 +218,7 @@ __device__ __forceinline__ void gemm_core_dma(f32x4 (&acc)[FM][FN], char* smem, 
             const int row = RPI * (NW * i + wave) + lane / CPR;
             const uint32_t vo = aoff(i, st * RB + swz_slot<RB>(row, q_l) * 16);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                ra, (__attribute__((address_space(3))) void*)(buf + RPI * (NW * i + wave) * RB), 16, vo, 0, 0, 0);
+                ra, (__attribute__((address_space(3))) void*)(buf + RPI * (NW * i + wave) * RB), 16, vo, 0, 0, AUXA);
         }
 #pragma unroll
         for (int i = 0; i < LB; ++i) {

@@ -706,13 +706,27 @@ __device__ __forceinline__ float ftanh(float x) { return 2.f * fsigmoid(2.f * x)
 // W_hh rows.  grid = (H / 32, CELLS * ceil(B / SB)); consecutive blocks take
 // consecutive unit slices, so each XCD keeps the same 4 slices (2 MB of
 // weights) for every step.
-template <typename T, int CELLS, int S, int SB_, int NBUF_, int RB_ = 128>
+// L2 policy of the step's streamed operands (compile-time A/B knobs).  Marking
+// the h_{t-1} DMA and the c / h stores nt to keep W_hh (2 MB per XCD)
+// L2-resident was measured slower (LSTM 39.8 vs 33.3 ms per 256 x 10 s
+// batch; L2 hit rate 0.77 vs 0.76), so both default off.
+#ifndef CRN_STEP_AUXA
+#define CRN_STEP_AUXA 0
+#endif
+#ifndef CRN_STEP_NTST
+#define CRN_STEP_NTST 0
+#endif
+constexpr int kStepAuxA = CRN_STEP_AUXA;
+constexpr bool kStepNtStores = CRN_STEP_NTST != 0;
+
+template <typename T, int CELLS, int S, int SB_, int NBUF_, int RB_ = 128, int NW_ = 4>
 struct StepCfg {
     static constexpr int SB = SB_;                      // streams per block
     static constexpr int U = 32;
     static constexpr int BM = SB * S;                   // rows: (s, stream)
     static constexpr int BN = 4 * U;
-    static constexpr int FM = BM / 32, FN = 4;          // 2 x 2 waves
+    static constexpr int NW = NW_;                      // waves: (NW / 2) row groups x 2 column halves
+    static constexpr int FM = BM / (NW / 2) / 16, FN = 4;
     static constexpr int NBUF = NBUF_;
     static constexpr int RB = RB_;                      // K bytes per row per stage
     static constexpr int GROW = U * 4 * (int)sizeof(T);            // Gx bytes per row
@@ -720,12 +734,13 @@ struct StepCfg {
     static constexpr size_t LDS = STAGES + (size_t)BM * GROW + (size_t)BM * U * 4;
 };
 
-template <typename T, int CELLS, int S, int SB_, int NBUF_, int RB_>
-__global__ __launch_bounds__(256) void lstm_step_kernel(StepArgs p) {
-    using C_ = StepCfg<T, CELLS, S, SB_, NBUF_, RB_>;
+template <typename T, int CELLS, int S, int SB_, int NBUF_, int RB_, int NW_>
+__global__ __launch_bounds__(64 * NW_) void lstm_step_kernel(StepArgs p) {
+    using C_ = StepCfg<T, CELLS, S, SB_, NBUF_, RB_, NW_>;
+    constexpr int NW = NW_, NT = 64 * NW_;
     constexpr int SB = C_::SB, U = C_::U, BM = C_::BM, BN = C_::BN, FM = C_::FM, FN = C_::FN;
     constexpr int RB = C_::RB, RPI = 1024 / RB, CPR = RB / 16;   // DMA rows per instruction, chunks per row
-    constexpr int LA = BM / (RPI * 4);
+    constexpr int LA = BM / (RPI * NW);
     constexpr int ES = (int)sizeof(T);
     constexpr int GROW = C_::GROW;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -737,7 +752,7 @@ __global__ __launch_bounds__(256) void lstm_step_kernel(StepArgs p) {
     const int unit0 = blockIdx.x * U, b0 = ((int)blockIdx.y % nsb) * SB;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int uh = wave & 1;
-    const int wr0 = (wave >> 1) * (BM / 2), wc0 = uh * 64;
+    const int wr0 = (wave >> 1) * (BM / (NW / 2)), wc0 = uh * 64;
     const bool first = p.first != 0;
     const int64_t ystride = (int64_t)CELLS * S * H;            // elements per (stream, frame)
     const int64_t gstride = (int64_t)CELLS * 4 * H;            // Gx elements per (stream, frame, s)
@@ -749,10 +764,10 @@ __global__ __launch_bounds__(256) void lstm_step_kernel(StepArgs p) {
         const __amdgpu_buffer_rsrc_t rg =
             make_rsrc(gbase, (uint64_t)((int64_t)(p.B - b0) * S * gstride) * ES);
         constexpr int GCH = GROW / 16;                   // 16-B chunks per Gx row
-        constexpr int GI = BM * GCH / 256;               // DMA instructions per wave
+        constexpr int GI = BM * GCH / NT;                // DMA instructions per wave
 #pragma unroll
         for (int i = 0; i < GI; ++i) {
-            const int c = (4 * i + wave) * 64 + lane;
+            const int c = (NW * i + wave) * 64 + lane;
             const int r = c / GCH, ch = c % GCH;
             const int s = r / SB, bl = r % SB;
             const uint32_t vo = (b0 + bl < p.B)
@@ -760,22 +775,22 @@ __global__ __launch_bounds__(256) void lstm_step_kernel(StepArgs p) {
                              ch * 16)
                 : kOOB;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rg, (__attribute__((address_space(3))) void*)(sG + (4 * i + wave) * 1024), 16, vo, 0, 0, 2);
+                rg, (__attribute__((address_space(3))) void*)(sG + (NW * i + wave) * 1024), 16, vo, 0, 0, 2);
         }
         if (!first) {
             const float* cbase = p.cst + (int64_t)b0 * CELLS * S * H;
             const __amdgpu_buffer_rsrc_t rc = make_rsrc(cbase, (uint64_t)(p.B - b0) * CELLS * S * H * 4);
-            constexpr int CI = BM * (U * 4 / 16) / 256;
+            constexpr int CI = BM * (U * 4 / 16) / NT;
 #pragma unroll
             for (int i = 0; i < CI; ++i) {
-                const int c = (4 * i + wave) * 64 + lane;
+                const int c = (NW * i + wave) * 64 + lane;
                 const int r = c / (U * 4 / 16), ch = c % (U * 4 / 16);
                 const int s = r / SB, bl = r % SB;
                 const uint32_t vo = (b0 + bl < p.B)
                     ? (uint32_t)((((int64_t)bl * CELLS + cell) * S + s) * H * 4 + unit0 * 4 + ch * 16)
                     : kOOB;
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    rc, (__attribute__((address_space(3))) void*)(sC + (4 * i + wave) * 1024), 16, vo, 0, 0, 2);
+                    rc, (__attribute__((address_space(3))) void*)(sC + (NW * i + wave) * 1024), 16, vo, 0, 0, 2);
             }
         }
     }
@@ -794,7 +809,7 @@ __global__ __launch_bounds__(256) void lstm_step_kernel(StepArgs p) {
         uint32_t arow[LA];
 #pragma unroll
         for (int i = 0; i < LA; ++i) {
-            const int r = RPI * (4 * i + wave) + lane / CPR;
+            const int r = RPI * (NW * i + wave) + lane / CPR;
             const int s = r / SB, bl = r % SB;
             arow[i] = (b0 + bl < p.B)
                           ? (uint32_t)((((int64_t)bl * ystride) + ((int64_t)cell * S + s) * H) * ES)
@@ -802,9 +817,9 @@ __global__ __launch_bounds__(256) void lstm_step_kernel(StepArgs p) {
         }
         auto aoff = [&](int i, int kbyte) -> uint32_t { return arow[i] == kOOB ? kOOB : arow[i] + kbyte; };
         auto boff = [&](int i, int kbyte) -> uint32_t {
-            return (uint32_t)((RPI * (4 * i + wave) + lane / CPR) * H * ES + kbyte);
+            return (uint32_t)((RPI * (NW * i + wave) + lane / CPR) * H * ES + kbyte);
         };
-        gemm_core_dma<T, BM, BN, FM, FN, C_::NBUF, decltype(aoff), decltype(boff), 4, RB>(acc, smem, ra, rb, aoff,
+        gemm_core_dma<T, BM, BN, FM, FN, C_::NBUF, decltype(aoff), decltype(boff), NW, RB, kStepAuxA>(acc, smem, ra, rb, aoff,
                                                                                          boff, H * ES / RB, wr0, wc0);
     } else {
         wait_vm<0>();
@@ -843,25 +858,29 @@ __global__ __launch_bounds__(256) void lstm_step_kernel(StepArgs p) {
     T* Yo = reinterpret_cast<T*>(p.y_cur);
     constexpr int CCH = U * 4 / 16, HCH = U * ES / 16;
 #pragma unroll
-    for (int i = 0; i < BM * CCH / 256; ++i) {
-        const int c = i * 256 + threadIdx.x;
+    for (int i = 0; i < BM * CCH / NT; ++i) {
+        const int c = i * NT + threadIdx.x;
         const int r = c / CCH, ch = c % CCH;
         const int s = r / SB, bl = r % SB;
         if (b0 + bl < p.B) {
             const u32x4 v = *reinterpret_cast<const u32x4*>(sC + r * U * 4 + ch * 16);
-            *reinterpret_cast<u32x4*>(p.cst + (((int64_t)(b0 + bl) * CELLS + cell) * S + s) * H + unit0 + ch * 4) = v;
+            u32x4* dst = reinterpret_cast<u32x4*>(p.cst + (((int64_t)(b0 + bl) * CELLS + cell) * S + s) * H + unit0 + ch * 4);
+            if (kStepNtStores) __builtin_nontemporal_store(v, dst);
+            else *dst = v;
         }
     }
 #pragma unroll
-    for (int i = 0; i < (BM * HCH + 255) / 256; ++i) {
-        const int c = i * 256 + threadIdx.x;
-        if (BM * HCH % 256 != 0 && c >= BM * HCH) break;
+    for (int i = 0; i < (BM * HCH + NT - 1) / NT; ++i) {
+        const int c = i * NT + threadIdx.x;
+        if (BM * HCH % NT != 0 && c >= BM * HCH) break;
         const int r = c / HCH, ch = c % HCH;
         const int s = r / SB, bl = r % SB;
         if (b0 + bl < p.B) {
             const u32x4 v = *reinterpret_cast<const u32x4*>(sH + r * U * ES + ch * 16);
-            *reinterpret_cast<u32x4*>(Yo + ((((int64_t)b0 + bl) * CELLS + cell) * S + s) * H + unit0 +
-                                      ch * (16 / ES)) = v;
+            u32x4* dst = reinterpret_cast<u32x4*>(Yo + ((((int64_t)b0 + bl) * CELLS + cell) * S + s) * H + unit0 +
+                                                  ch * (16 / ES));
+            if (kStepNtStores) __builtin_nontemporal_store(v, dst);
+            else *dst = v;
         }
     }
 }
@@ -872,10 +891,10 @@ hipError_t launch_lstm_step(const StepArgs& a, int cells, int seqs, hipStream_t 
     // cell update, bit1 skip the recurrent GEMM, bit2 skip the Gx / c DMA
     static const int step_mode = env_int("CRN_STEP_MODE", 0);
     if (a.H % 32 || (a.H * (int)sizeof(T)) % kStageBytes) return hipErrorInvalidValue;
-#define CRN_STEP(C, S_, SB_, NB_, RB_)                                                                            \
+#define CRN_STEP(C, S_, SB_, NB_, RB_, NW_)                                                                            \
     do {                                                                                                          \
-        auto kern = lstm_step_kernel<T, C, S_, SB_, NB_, RB_>;                                                    \
-        constexpr size_t lds = StepCfg<T, C, S_, SB_, NB_, RB_>::LDS;                                             \
+        auto kern = lstm_step_kernel<T, C, S_, SB_, NB_, RB_, NW_>;                                                    \
+        constexpr size_t lds = StepCfg<T, C, S_, SB_, NB_, RB_, NW_>::LDS;                                             \
         static_assert(lds <= 160 * 1024, "LDS");                                                                  \
         static const hipError_t attr =                                                                            \
             hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, \
@@ -883,7 +902,7 @@ hipError_t launch_lstm_step(const StepArgs& a, int cells, int seqs, hipStream_t 
         if (attr != hipSuccess) return attr;                                                                      \
         StepArgs a2 = a;                                                                                          \
         a2.mode = step_mode;                                                                                      \
-        hipLaunchKernelGGL(kern, dim3(a.H / 32, C * ((a.B + SB_ - 1) / SB_)), dim3(256), lds, st, a2);           \
+        hipLaunchKernelGGL(kern, dim3(a.H / 32, C * ((a.B + SB_ - 1) / SB_)), dim3(64 * NW_), lds, st, a2);           \
     } while (0)
     // CRN_STEP_CFG: 0 = 64 streams per block, 3 (bf16) / 2 (f32) stage buffers (1 block per CU);
     // 1 = 32 streams, 2 buffers of 128-B K slices (2 blocks per CU); 2 = 32 streams, 3 buffers;
@@ -894,16 +913,26 @@ hipError_t launch_lstm_step(const StepArgs& a, int cells, int seqs, hipStream_t 
     constexpr int NB0 = sizeof(T) == 2 ? 3 : 2;
     if ((a.H * (int)sizeof(T)) % 64) return hipErrorInvalidValue;
     if (cells == 2 && seqs == 2) {
-        if (cfg == 1) CRN_STEP(2, 2, 32, 2, 128);
-        else if (cfg == 2) CRN_STEP(2, 2, 32, 3, 128);
-        else if (cfg == 3) CRN_STEP(2, 2, 16, 2, 128);
-        else if (cfg == 4) CRN_STEP(2, 2, 32, 4, 64);
-        else CRN_STEP(2, 2, 64, NB0, 128);
+        if (cfg == 1) CRN_STEP(2, 2, 32, 2, 128, 4);
+        else if (cfg == 2) CRN_STEP(2, 2, 32, 3, 128, 4);
+        else if (cfg == 3) CRN_STEP(2, 2, 16, 2, 128, 4);
+        else if (cfg == 4) CRN_STEP(2, 2, 32, 4, 64, 4);
+        else if (cfg == 6) CRN_STEP(2, 2, 64, 2, 128, 8);
+        else if (cfg == 7) {
+            if constexpr (sizeof(T) == 2) CRN_STEP(2, 2, 64, 3, 128, 8);
+            else CRN_STEP(2, 2, 64, 2, 128, 8);
+        }
+        else CRN_STEP(2, 2, 64, NB0, 128, 4);
     } else if (cells == 1 && seqs == 1) {
-        if (cfg == 1) CRN_STEP(1, 1, 32, 2, 128);
-        else if (cfg == 2) CRN_STEP(1, 1, 32, 3, 128);
-        else if (cfg == 4) CRN_STEP(1, 1, 64, 4, 64);
-        else CRN_STEP(1, 1, 64, NB0, 128);
+        if (cfg == 1) CRN_STEP(1, 1, 32, 2, 128, 4);
+        else if (cfg == 2) CRN_STEP(1, 1, 32, 3, 128, 4);
+        else if (cfg == 4) CRN_STEP(1, 1, 64, 4, 64, 4);
+        else if (cfg == 6) CRN_STEP(1, 1, 128, 2, 128, 8);
+        else if (cfg == 7) {
+            if constexpr (sizeof(T) == 2) CRN_STEP(1, 1, 128, 3, 128, 8);
+            else CRN_STEP(1, 1, 128, 2, 128, 8);
+        }
+        else CRN_STEP(1, 1, 64, NB0, 128, 4);
     } else {
         return hipErrorInvalidValue;
     }
