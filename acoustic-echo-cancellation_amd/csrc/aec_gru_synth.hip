@@ -129,6 +129,17 @@ __global__ __launch_bounds__(kFusedThreads, 1) void gru_synth_kernel(GruArgs p, 
         for (int i = tid; i < 512; i += kFusedThreads) sHann[i] = tb->hann[i];
     }
 
+    {
+        // role priorities (AEC_FUSED_MODE bits 3-4 synthesis, 5-6 head, 7-8 gi; timing experiments)
+        const int role_prio = wave == 0 ? 0 : (wave <= kGiWaves ? (y.fmode >> 7) & 3
+                              : (wave <= kGiWaves + kHeadWaves ? (y.fmode >> 5) & 3 : (y.fmode >> 3) & 3));
+        switch (role_prio) {
+            case 1: __builtin_amdgcn_s_setprio(1); break;
+            case 2: __builtin_amdgcn_s_setprio(2); break;
+            case 3: __builtin_amdgcn_s_setprio(3); break;
+            default: break;
+        }
+    }
     if (wave == 0) {
         // ---------------- recurrence wave (gru_kernel wave 0) ----------------
         __builtin_amdgcn_s_setprio(3);
