@@ -224,4 +224,93 @@ __device__ __forceinline__ float tanhf_(float x) {
     return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x));
 }
 
+// ---------------------------------------------------------------------------
+// GRU cell pieces (nn.GRU(64, 32) gate order r, z, n; ERB.py:213, 293) and
+// the head (linear1 / relu / linear2 / sigmoid, ERB.py:295-301), shared by
+// gru_kernel, gru_synth_kernel and stream_step_kernel so the three run the
+// same accumulation order (bit-identical results).
+// ---------------------------------------------------------------------------
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// gi = W_ih[row] . x + bias (x: 64 floats in LDS, 16-B aligned)
+__device__ __forceinline__ float gru_gi(const float (&wih)[64], const float* x, float gbias) {
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    f2v a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const float4 xv = x4[q];
+        a0 = __builtin_elementwise_fma(f2v{wih[4 * q], wih[4 * q + 1]}, f2v{xv.x, xv.y}, a0);
+        a1 = __builtin_elementwise_fma(f2v{wih[4 * q + 2], wih[4 * q + 3]}, f2v{xv.z, xv.w}, a1);
+    }
+    const f2v s2 = a0 + a1;
+    return gbias + (s2.x + s2.y);
+}
+
+// One recurrence step on a wave: lane l owns unit j = l & 31 and the k-half
+// kh = l >> 5 of rows r_j, z_j, n_j of W_hh (wrz[k] = (W_r[j][16kh+k],
+// W_z[j][16kh+k]), wn[i] = W_n[j][16kh+2i .. +1]); hb = h_{t-1} (32 floats in
+// LDS); the halves' partial dots meet through v_permlane32_swap.  Returns h_t[j]
+// (identical in both halves).
+__device__ __forceinline__ float gru_step(const f2v (&wrz)[16], const f2v (&wn)[8], const float* hb, int kh, float gr,
+                                         float gz, float gn, float bhn, float hprev) {
+    const float4* h4 = reinterpret_cast<const float4*>(hb + 16 * kh);
+    const float4 q0 = h4[0], q1 = h4[1], q2 = h4[2], q3 = h4[3];
+    const float hk[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                          q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+    f2v arz[4] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}};
+    f2v an[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) arz[k & 3] = __builtin_elementwise_fma(wrz[k], f2v{hk[k], hk[k]}, arz[k & 3]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) an[i & 1] = __builtin_elementwise_fma(wn[i], f2v{hk[2 * i], hk[2 * i + 1]}, an[i & 1]);
+    const f2v rz = (arz[0] + arz[1]) + (arz[2] + arz[3]);
+    const f2v n2 = an[0] + an[1];
+    const float pr = rz.x, pz = rz.y, pn = n2.x + n2.y;
+    // v_permlane32_swap: lanes 32..63 of vdst <-> lanes 0..31 of vsrc, so the
+    // other half's value is res[1] in lanes 0..31 and res[0] in lanes 32..63
+    const auto sr = __builtin_amdgcn_permlane32_swap(__float_as_uint(pr), __float_as_uint(pr), false, false);
+    const auto sz = __builtin_amdgcn_permlane32_swap(__float_as_uint(pz), __float_as_uint(pz), false, false);
+    const auto sn = __builtin_amdgcn_permlane32_swap(__float_as_uint(pn), __float_as_uint(pn), false, false);
+    const float rdot = pr + __uint_as_float(kh ? sr[0] : sr[1]);
+    const float zdot = pz + __uint_as_float(kh ? sz[0] : sz[1]);
+    const float ndot = pn + __uint_as_float(kh ? sn[0] : sn[1]);
+    const float r = sigmoidf_(gr + rdot);
+    const float z = sigmoidf_(gz + zdot);
+    const float nn = tanhf_(gn + r * (ndot + bhn));
+    return (1.f - z) * nn + z * hprev;
+}
+
+// Head of unit j for one frame, by a group of 32 lanes (lane j of the group):
+// o = relu(W1[j] . [h, mic_erb] + b1) through the group's 32-float LDS row,
+// mask = sigmoid(W2[j] . o + b2).  h, mic: 32 floats each in LDS (16-B aligned).
+__device__ __forceinline__ float head_mask(const float (&w1)[64], const float (&w2)[32], float b1j, float b2j,
+                                          const float* h, const float* mic, float* orow, int j) {
+    const float4* h4 = reinterpret_cast<const float4*>(h);
+    const float4* m4 = reinterpret_cast<const float4*>(mic);
+    f2v a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const float4 hv = h4[q];
+        const float4 mv = m4[q];
+        a0 = __builtin_elementwise_fma(f2v{w1[4 * q], w1[4 * q + 1]}, f2v{hv.x, hv.y}, a0);
+        a1 = __builtin_elementwise_fma(f2v{w1[4 * q + 2], w1[4 * q + 3]}, f2v{hv.z, hv.w}, a1);
+        a0 = __builtin_elementwise_fma(f2v{w1[32 + 4 * q], w1[32 + 4 * q + 1]}, f2v{mv.x, mv.y}, a0);
+        a1 = __builtin_elementwise_fma(f2v{w1[32 + 4 * q + 2], w1[32 + 4 * q + 3]}, f2v{mv.z, mv.w}, a1);
+    }
+    const f2v s1 = a0 + a1;
+    orow[j] = fmaxf(b1j + (s1.x + s1.y), 0.f);
+    wave_fence();
+    const float4* o4 = reinterpret_cast<const float4*>(orow);
+    f2v c0 = {0.f, 0.f}, c1 = {0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const float4 ov = o4[q];
+        c0 = __builtin_elementwise_fma(f2v{w2[4 * q], w2[4 * q + 1]}, f2v{ov.x, ov.y}, c0);
+        c1 = __builtin_elementwise_fma(f2v{w2[4 * q + 2], w2[4 * q + 3]}, f2v{ov.z, ov.w}, c1);
+    }
+    wave_fence();                                   // the row is reused by the group's next frame
+    const f2v s2 = c0 + c1;
+    return sigmoidf_(b2j + (s2.x + s2.y));
+}
+
 }  // namespace aec

@@ -21,8 +21,6 @@
 
 namespace aec {
 
-typedef float f2v __attribute__((ext_vector_type(2)));
-
 constexpr int kGruHelpers = 6;
 constexpr int kGruThreads = 64 * (1 + kGruHelpers);
 constexpr int kHL = 64 * kGruHelpers;                 // helper lanes (384)
@@ -92,33 +90,7 @@ __global__ __launch_bounds__(kGruThreads) void gru_kernel(GruArgs p) {
                     // h_{t-1}[16 kh .. 16 kh + 15] (LDS ops of one wave execute in order;
                     // measured faster than a permlane16_swap + 16 DPP row_newbcast
                     // broadcast: 0.177 vs 0.197 ms recurrence-only)
-                    const float4* h4 = reinterpret_cast<const float4*>(hb + 16 * kh);
-                    const float4 q0 = h4[0], q1 = h4[1], q2 = h4[2], q3 = h4[3];
-                    const float hk[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
-                                          q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
-                    f2v arz[4] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}};
-                    f2v an[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
-#pragma unroll
-                    for (int k = 0; k < 16; ++k)
-                        arz[k & 3] = __builtin_elementwise_fma(wrz[k], f2v{hk[k], hk[k]}, arz[k & 3]);
-#pragma unroll
-                    for (int i = 0; i < 8; ++i)
-                        an[i & 1] = __builtin_elementwise_fma(wn[i], f2v{hk[2 * i], hk[2 * i + 1]}, an[i & 1]);
-                    const f2v rz = (arz[0] + arz[1]) + (arz[2] + arz[3]);
-                    const f2v n2 = an[0] + an[1];
-                    const float pr = rz.x, pz = rz.y, pn = n2.x + n2.y;
-                    // v_permlane32_swap: lanes 32..63 of vdst <-> lanes 0..31 of vsrc, so the
-                    // other half's value is res[1] in lanes 0..31 and res[0] in lanes 32..63
-                    const auto sr = __builtin_amdgcn_permlane32_swap(__float_as_uint(pr), __float_as_uint(pr), false, false);
-                    const auto sz = __builtin_amdgcn_permlane32_swap(__float_as_uint(pz), __float_as_uint(pz), false, false);
-                    const auto sn = __builtin_amdgcn_permlane32_swap(__float_as_uint(pn), __float_as_uint(pn), false, false);
-                    const float rdot = pr + __uint_as_float(kh ? sr[0] : sr[1]);
-                    const float zdot = pz + __uint_as_float(kh ? sz[0] : sz[1]);
-                    const float ndot = pn + __uint_as_float(kh ? sn[0] : sn[1]);
-                    const float r = sigmoidf_(gr + rdot);
-                    const float z = sigmoidf_(gz + zdot);
-                    const float nn = tanhf_(gn + r * (ndot + bhn));
-                    hj = (1.f - z) * nn + z * hj;
+                    hj = gru_step(wrz, wn, hb, kh, gr, gz, gn, bhn, hj);
                     if (kh == 0) {
                         hb[j] = hj;                            // broadcast slot for the next step
                         sH[c & 1][f][j] = hj;                  // for the head (off the chain)
@@ -187,16 +159,7 @@ __global__ __launch_bounds__(kGruThreads) void gru_kernel(GruArgs p) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const int f = fq + 4 * i;
-                        const float4* x4 = reinterpret_cast<const float4*>(&sX[cg & 1][f][0]);
-                        f2v a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
-#pragma unroll
-                        for (int q = 0; q < 16; ++q) {
-                            const float4 xv = x4[q];
-                            a0 = __builtin_elementwise_fma(f2v{wih[4 * q], wih[4 * q + 1]}, f2v{xv.x, xv.y}, a0);
-                            a1 = __builtin_elementwise_fma(f2v{wih[4 * q + 2], wih[4 * q + 3]}, f2v{xv.z, xv.w}, a1);
-                        }
-                        const f2v s2 = a0 + a1;
-                        sGi[cg & 1][f][grow] = gbias + (s2.x + s2.y);
+                        sGi[cg & 1][f][grow] = gru_gi(wih, &sX[cg & 1][f][0], gbias);
                     }
                 }
                 // (c) head for chunk c-1
@@ -205,33 +168,7 @@ __global__ __launch_bounds__(kGruThreads) void gru_kernel(GruArgs p) {
                     for (int f = fg; f < kCH; f += kHeadGroups) {
                         const int t = ch * kCH + f;
                         if (t >= T) break;               // uniform within the 32-lane group
-                        const float4* h4 = reinterpret_cast<const float4*>(&sH[ch & 1][f][0]);
-                        const float4* m4 = reinterpret_cast<const float4*>(&sMic[ch & 3][f][0]);
-                        f2v a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
-#pragma unroll
-                        for (int q = 0; q < 8; ++q) {
-                            const float4 hv = h4[q];
-                            const float4 mv = m4[q];
-                            a0 = __builtin_elementwise_fma(f2v{w1[4 * q], w1[4 * q + 1]}, f2v{hv.x, hv.y}, a0);
-                            a1 = __builtin_elementwise_fma(f2v{w1[4 * q + 2], w1[4 * q + 3]}, f2v{hv.z, hv.w}, a1);
-                            a0 = __builtin_elementwise_fma(f2v{w1[32 + 4 * q], w1[32 + 4 * q + 1]}, f2v{mv.x, mv.y}, a0);
-                            a1 = __builtin_elementwise_fma(f2v{w1[32 + 4 * q + 2], w1[32 + 4 * q + 3]}, f2v{mv.z, mv.w}, a1);
-                        }
-                        const f2v s1 = a0 + a1;
-                        const float o = fmaxf(b1j + (s1.x + s1.y), 0.f);
-                        sO[fg][hj_] = o;
-                        wave_fence();
-                        const float4* o4 = reinterpret_cast<const float4*>(&sO[fg][0]);
-                        f2v c0 = {0.f, 0.f}, c1 = {0.f, 0.f};
-#pragma unroll
-                        for (int q = 0; q < 8; ++q) {
-                            const float4 ov = o4[q];
-                            c0 = __builtin_elementwise_fma(f2v{w2[4 * q], w2[4 * q + 1]}, f2v{ov.x, ov.y}, c0);
-                            c1 = __builtin_elementwise_fma(f2v{w2[4 * q + 2], w2[4 * q + 3]}, f2v{ov.z, ov.w}, c1);
-                        }
-                        wave_fence();
-                        const f2v s2 = c0 + c1;
-                        const float mask = sigmoidf_(b2j + (s2.x + s2.y));
+                        const float mask = head_mask(w1, w2, b1j, b2j, &sH[ch & 1][f][0], &sMic[ch & 3][f][0], &sO[fg][0], hj_);
                         const float me = sMic[ch & 3][f][hj_];
                         const float est = mask * me;
                         const int64_t o_idx = ((int64_t)b * p.Tmax + t) * 32 + hj_;

@@ -18,9 +18,8 @@
 // One block of 4 waves per stream; per-stream state lives in HBM between
 // calls (prev hop, NLMS taps / far-end history / power, GRU h, OLA tail) and
 // is read once and written once per hop.  The arithmetic is the batch path's
-// own (aec_frame.h helpers; the GRU step and head restate gru_kernel's
-// accumulation order), so stream and batch agree to the last bit up to the
-// compiler's FMA contraction choices.
+// own (the aec_frame.h helpers, GRU step and head included), so a streamed
+// utterance reproduces aec_process bit for bit (tests/test_gpu_stream.py).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -31,8 +30,6 @@
 #include "aec_tables.h"
 
 namespace aec {
-
-typedef float f2v __attribute__((ext_vector_type(2)));
 
 constexpr int kStreamThreads = 256;
 constexpr int kSchedMax = 48;                 // ErbTables: L <= 48
@@ -217,44 +214,13 @@ __global__ __launch_bounds__(kStreamThreads) void stream_step_kernel(StreamStepA
 
     // ---- P4: gi = W_ih x + b_ih (+ b_hh for r, z) — gru_kernel's helper order ----
     if (wave != 0 && grow < 96) {
-        const float4* x4 = reinterpret_cast<const float4*>(sX);
-        f2v a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const float4 xv = x4[q];
-            a0 = __builtin_elementwise_fma(f2v{wih[4 * q], wih[4 * q + 1]}, f2v{xv.x, xv.y}, a0);
-            a1 = __builtin_elementwise_fma(f2v{wih[4 * q + 2], wih[4 * q + 3]}, f2v{xv.z, xv.w}, a1);
-        }
-        const f2v s2 = a0 + a1;
-        sGi[grow] = gbias + (s2.x + s2.y);
+        sGi[grow] = gru_gi(wih, sX, gbias);
     }
     __syncthreads();
 
     // ---- P5: the GRU step (gru_kernel wave 0, one frame) ----
     if (wave == 0) {
-        const float4* h4 = reinterpret_cast<const float4*>(sH + 16 * kh);
-        const float4 q0 = h4[0], q1 = h4[1], q2 = h4[2], q3 = h4[3];
-        const float hk[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
-                              q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
-        f2v arz[4] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}};
-        f2v an[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
-#pragma unroll
-        for (int k = 0; k < 16; ++k) arz[k & 3] = __builtin_elementwise_fma(wrz[k], f2v{hk[k], hk[k]}, arz[k & 3]);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) an[i & 1] = __builtin_elementwise_fma(wn[i], f2v{hk[2 * i], hk[2 * i + 1]}, an[i & 1]);
-        const f2v rz = (arz[0] + arz[1]) + (arz[2] + arz[3]);
-        const f2v n2 = an[0] + an[1];
-        const float pr = rz.x, pz = rz.y, pn = n2.x + n2.y;
-        const auto sr = __builtin_amdgcn_permlane32_swap(__float_as_uint(pr), __float_as_uint(pr), false, false);
-        const auto sz = __builtin_amdgcn_permlane32_swap(__float_as_uint(pz), __float_as_uint(pz), false, false);
-        const auto sn = __builtin_amdgcn_permlane32_swap(__float_as_uint(pn), __float_as_uint(pn), false, false);
-        const float rdot = pr + __uint_as_float(kh ? sr[0] : sr[1]);
-        const float zdot = pz + __uint_as_float(kh ? sz[0] : sz[1]);
-        const float ndot = pn + __uint_as_float(kh ? sn[0] : sn[1]);
-        const float r = sigmoidf_(sGi[j] + rdot);
-        const float z = sigmoidf_(sGi[32 + j] + zdot);
-        const float nn = tanhf_(sGi[64 + j] + r * (ndot + bhn));
-        const float hj = (1.f - z) * nn + z * sH[j];
+        const float hj = gru_step(wrz, wn, sH, kh, sGi[j], sGi[32 + j], sGi[64 + j], bhn, sH[j]);
         if (kh == 0) {
             sHn[j] = hj;
             st[kStH + j] = hj;
@@ -264,31 +230,7 @@ __global__ __launch_bounds__(kStreamThreads) void stream_step_kernel(StreamStepA
 
     // ---- P6: head (linear1 / relu / linear2 / sigmoid) -> est_erb (gru_kernel order) ----
     if (wave == 3 && lane < 32) {
-        const float4* h4 = reinterpret_cast<const float4*>(sHn);
-        const float4* m4 = reinterpret_cast<const float4*>(sMicErb);
-        f2v a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const float4 hv = h4[q];
-            const float4 mv = m4[q];
-            a0 = __builtin_elementwise_fma(f2v{w1[4 * q], w1[4 * q + 1]}, f2v{hv.x, hv.y}, a0);
-            a1 = __builtin_elementwise_fma(f2v{w1[4 * q + 2], w1[4 * q + 3]}, f2v{hv.z, hv.w}, a1);
-            a0 = __builtin_elementwise_fma(f2v{w1[32 + 4 * q], w1[32 + 4 * q + 1]}, f2v{mv.x, mv.y}, a0);
-            a1 = __builtin_elementwise_fma(f2v{w1[32 + 4 * q + 2], w1[32 + 4 * q + 3]}, f2v{mv.z, mv.w}, a1);
-        }
-        const f2v s1 = a0 + a1;
-        sO[lane] = fmaxf(b1j + (s1.x + s1.y), 0.f);
-        wave_fence();
-        const float4* o4 = reinterpret_cast<const float4*>(sO);
-        f2v c0 = {0.f, 0.f}, c1 = {0.f, 0.f};
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const float4 ov = o4[q];
-            c0 = __builtin_elementwise_fma(f2v{w2[4 * q], w2[4 * q + 1]}, f2v{ov.x, ov.y}, c0);
-            c1 = __builtin_elementwise_fma(f2v{w2[4 * q + 2], w2[4 * q + 3]}, f2v{ov.z, ov.w}, c1);
-        }
-        const f2v s2 = c0 + c1;
-        const float mask = sigmoidf_(b2j + (s2.x + s2.y));
+        const float mask = head_mask(w1, w2, b1j, b2j, sHn, sMicErb, sO, lane);
         sEst[lane] = mask * sMicErb[lane];
     }
     __syncthreads();
