@@ -48,7 +48,8 @@ def _scenes(lens, seed0):
     return [synth.scene(n, seed0 + i) for i, n in enumerate(lens)]
 
 
-@pytest.mark.parametrize('nlms', [None, NLMS], ids=['postfilter', 'nlms4'])
+@pytest.mark.parametrize('nlms', [None, NLMS, dict(NLMS, taps=1), dict(NLMS, taps=8)],
+                         ids=['postfilter', 'nlms4', 'nlms1', 'nlms8'])
 def test_stream_equals_batch(golden_weights, golden_erb, nlms):
     if not torch.cuda.is_available():
         pytest.skip('no HIP device')
@@ -109,3 +110,32 @@ def test_stream_argument_errors(golden_weights, golden_erb):
         net.stream_step(torch.zeros(3, 256, device=dev), torch.zeros(3, 256, device=dev))
     with pytest.raises(RuntimeError):
         net.stream_reset(5)
+
+
+def test_stream_single_stream_strided_hops(golden_weights, golden_erb):
+    """B = 1 with hops taken from a wider buffer at an odd row stride (ld_in =
+    257 floats): the kernel reads rows at any stride; output bit-exact."""
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+    net = _net(golden_weights, NLMS)
+    dev = 'cuda:0'
+    erb = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
+    n = 5000
+    (s,) = _scenes([n], 900)
+    with torch.no_grad():
+        ref_out, _ = net.forward_ragged(torch.tensor(s[0], device=dev)[None], torch.tensor(s[1], device=dev)[None],
+                                        None, erb, [n])
+    nh = n // 256 + 1
+    mic = np.zeros(256 * nh, np.float32)
+    far = np.zeros_like(mic)
+    mic[:n], far[:n] = _normalised(s[0]), _normalised(s[1])
+    buf = torch.zeros(2, nh, 257, device=dev)              # row stride 257: odd, not 16-B aligned
+    buf[0, :, :256] = torch.tensor(mic.reshape(nh, 256), device=dev)
+    buf[1, :, :256] = torch.tensor(far.reshape(nh, 256), device=dev)
+    with torch.no_grad():
+        net.stream_open(1, erb)
+        outs = [net.stream_step(buf[0, k:k + 1, :256], buf[1, k:k + 1, :256]) for k in range(nh)]
+    torch.cuda.synchronize()
+    got = torch.cat(outs[1:], dim=1)[0].cpu().numpy()
+    no = 256 * (n // 256)
+    assert np.array_equal(got[:no], ref_out[0, :no].cpu().numpy())
