@@ -603,6 +603,15 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_rows_dma_kernel(RowSrc a, c
         for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     gemm_core_dma<T, BM, BN, FM, FN, NBUF, decltype(aoff), decltype(boff), NW, RB>(acc, smem, ra, rb, aoff, boff,
                                                                                    nstages, wr0, wc0);
+    if (e.mode & 1) {                                  // timing only: keep the MFMAs alive, skip the epilogue
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) sum += acc[i][j][0];
+        if (sum == 1234.5f) reinterpret_cast<float*>(e.out)[0] = sum;
+        return;
+    }
     __syncthreads();                                   // every wave is done with the stage buffers
     constexpr int PF = epi_passes<OutT, FM, FN, NW>((size_t)NBUF * (BM + BN) * RB);
     static_assert(NW * PF * 16 * FN * 16 * sizeof(OutT) <= (size_t)NBUF * (BM + BN) * RB, "epilogue LDS");
@@ -640,13 +649,16 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
         if (attr != hipSuccess) return attr;                                                                      \
         const unsigned nbn_ = (unsigned)(npad / BN);                                                              \
         dim3 grid((unsigned)((a.M + BM - 1) / BM) * nbn_);                                                        \
-        hipLaunchKernelGGL(kern, grid, dim3(64 * WM * WN), lds, st, a, bt, ldb, nstages * (128 / RB), e);         \
+        hipLaunchKernelGGL(kern, grid, dim3(64 * WM * WN), lds, st, a, bt, ldb, nstages * (128 / RB), ee);        \
     } while (0)
 #define CRN_GEMM_DMA(WM, WN, FM, FN, NBUF) CRN_GEMM_DMA_RB(WM, WN, FM, FN, NBUF, 128)
     static const int dma = env_int("CRN_GEMM_DMA", 2);    // 0 = register-staged core, else NBUF
     static const int big = env_int("CRN_GEMM_BIG", 0);    // 256x128 tiles (8 waves) for large M (measured slower)
     static const int sq = env_int("CRN_GEMM_SQ", 1);      // 256x256 tiles (8 waves) when N % 256 == 0
     static const int rb64 = env_int("CRN_GEMM_RB64", 0);  // 128x128 tiles with 64-B K slices, 4 buffers
+    static const int gmode = env_int("CRN_GEMM_MODE", 0);  // timing experiments only (results invalid unless 0)
+    RowEpi ee = e;
+    ee.mode = gmode;
     switch (bn) {
         case 16: CRN_GEMM(4, 1, 4, 1); break;
         case 32: CRN_GEMM(2, 2, 4, 1); break;

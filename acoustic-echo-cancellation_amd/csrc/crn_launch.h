@@ -49,6 +49,7 @@ struct RowEpi {
     const float* bias;
     float alpha;
     int32_t act;
+    int32_t mode = 0;           // timing experiments only (CRN_GEMM_MODE): bit0 skip the epilogue
 };
 
 // One LSTM frame step for CELLS weight sets x S input sequences (v1: 1x1,
