@@ -215,6 +215,11 @@ struct aec_handle {
     int nlms_erb = 1;            // AEC_NLMS_ERB: role running the mic_erb pass (1 ref, 2 nlms)
     int fused = 1;               // AEC_FUSED_SYNTH: GRU + synthesis in one kernel (NLMS path)
     int fused_mode = 0;          // AEC_FUSED_MODE (timing experiments; results invalid unless 0)
+    int small_b = 64;            // AEC_SMALLB: NLMS batches up to this many streams take the split path
+                                 // (per 10 s step: B = 1 0.477 -> 0.336 ms, B = 16 0.486 -> 0.354,
+                                 // B = 64 0.504 -> 0.485; B = 128 slower)
+    float2* d_rows = nullptr;    // split path: packed mic / ref rows [B][T][2][256]
+    size_t rows_cap = 0;         // float2 elements
     int64_t last_B = 0, last_T = 0;
     // kernel timing (aec_profile_*)
     int profile = 0;
@@ -331,6 +336,7 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
     if (const char* m = std::getenv("AEC_NLMS_ERB")) h->nlms_erb = std::atoi(m);
     if (const char* m = std::getenv("AEC_FUSED_SYNTH")) h->fused = std::atoi(m);
     if (const char* m = std::getenv("AEC_FUSED_MODE")) h->fused_mode = std::atoi(m);
+    if (const char* m = std::getenv("AEC_SMALLB")) h->small_b = std::atoi(m);
     if (const char* m = std::getenv("AEC_SUBBATCH")) h->sub_max = std::max(1, std::min(aec_handle::kMaxSub, std::atoi(m)));
     {
         int cus = 0;
@@ -465,7 +471,32 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
         HIP_TRY(h, launch_moments(mic, ref, near, ld, h->d_len, h->d_mom, b0, b1 - b0, nsig, ks));
         HIP_TRY(h, launch_norm_finalize(h->d_mom, h->d_len, h->d_cvals, b0, b1, nsig, ks));
 
-        if (h->cfg.nlms_taps > 0) {
+        if (h->cfg.nlms_taps > 0 && B <= h->small_b && h->nlms_mode == 0) {
+            // few streams: transforms frame-parallel (K2 + rows), recursion per stream, mic_erb frame-parallel
+            const size_t need = (size_t)B * Tmax * 512 + (size_t)B * 256;      // + one dummy row per stream
+            if (need > h->rows_cap) {
+                HIP_TRY(h, hipStreamSynchronize(ks));
+                if (h->d_rows) HIP_TRY(h, hipFree(h->d_rows));
+                h->d_rows = nullptr;
+                h->rows_cap = 0;
+                HIP_TRY(h, hipMalloc(&h->d_rows, need * sizeof(float2)));
+                h->rows_cap = need;
+            }
+            AnalysisArgs a{};
+            a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
+            a.ld = ld; a.items = h->d_items + h->item_off[b0]; a.nitems = h->item_off[b1] - h->item_off[b0];
+            a.num_cus = h->num_cus; a.cvals = h->d_cvals;
+            a.tables = reinterpret_cast<const float*>(h->d_tab);
+            a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
+            a.feats = h->d_feats; a.Tmax = Tmax; a.rows = h->d_rows;
+            mark(h, ks);
+            HIP_TRY(h, launch_analysis(a, ks));
+            HIP_TRY(h, launch_nlms_recursion(h->d_rows, h->d_spec, h->d_len, Tmax, h->cfg.nlms_taps, h->cfg.nlms_mu,
+                                             h->cfg.nlms_beta, h->cfg.nlms_delta, b0, b1 - b0,
+                                             h->d_rows + (size_t)B * Tmax * 512, ks));
+            HIP_TRY(h, launch_mic_erb(h->d_spec, h->d_feats, h->d_len, Tmax, h->d_sched, h->sched_len,
+                                      h->d_items + h->item_off[b0], h->item_off[b1] - h->item_off[b0], ks));
+        } else if (h->cfg.nlms_taps > 0) {
             if (nlms_smem_bytes(h->sched_len, h->cfg.nlms_taps) > 160 * 1024)
                 return fail(h, AEC_ERR_UNSUPPORTED, "erb schedule too long for the NLMS kernel's LDS budget");
             NlmsArgs a{};
@@ -668,7 +699,7 @@ void aec_destroy(aec_handle* h) {
     (void)hipFree(h->d_w); (void)hipFree(h->d_tab); (void)hipFree(h->d_sched); (void)hipFree(h->d_bintab);
     (void)hipFree(h->d_mom); (void)hipFree(h->d_cvals); (void)hipFree(h->d_items); (void)hipFree(h->d_sitems); (void)hipFree(h->d_len);
     (void)hipFree(h->d_feats); (void)hipFree(h->d_est); (void)hipFree(h->d_dbg); (void)hipFree(h->d_spec);
-    (void)hipFree(h->d_state);
+    (void)hipFree(h->d_state); (void)hipFree(h->d_rows);
     delete h;
 }
 

@@ -197,6 +197,21 @@ __global__ __launch_bounds__(256, 3) void analysis_kernel(AnalysisArgs p) {
             fft256<false>(v, lb, scr, sTwT);
             float2 xa[8], xb[8], x128;
             rfft_unpack(v, lb, sTw512, xa, xb, x128);
+            if (p.rows && s < 2 && t < T) {
+                // packed row of mic / ref for the small-batch NLMS recursion (row_to_scr's layout)
+                float2* row = p.rows + (((int64_t)it.b * p.Tmax + t) * 2 + s) * 256;
+#pragma unroll
+                for (int m = 0; m < 8; ++m) {
+                    const int kk = lb + 16 * m;
+                    if (kk == 0) {
+                        row[0] = make_float2(xa[0].x, xb[0].x);
+                    } else {
+                        row[kk] = xa[m];
+                        row[256 - kk] = xb[m];
+                    }
+                }
+                if (lb == 0) row[128] = x128;
+            }
             // magnitudes (ERB.py:277-279) -> scr[k ^ sw], k = 0..256
 #pragma unroll
             for (int m = 0; m < 8; ++m) {
@@ -545,6 +560,102 @@ __global__ __launch_bounds__(256) void synthesis_kernel(SynthArgs p) {
             }
         }
     }
+}
+
+// --------------------------------------------------------------------------
+// Small-batch NLMS path.  K2n runs one block per stream; with few streams the
+// chip idles and a 10 s stream takes ~0.26 ms (40 ticks).  Here the
+// transforms run frame-parallel in K2 (which also writes the packed mic / ref
+// rows), the recursion is one block per stream over all frames (bin per
+// lane, rows prefetched kRecP frames ahead), and mic_erb = ERB(|E|) runs
+// frame-parallel again.  The per-frame arithmetic is K2n's own (NlmsBin,
+// the same row layout and ERB pass), so the output is bit-identical.
+// --------------------------------------------------------------------------
+constexpr int kRecP = 8;
+
+template <int TAPS>
+__global__ __launch_bounds__(256) void nlms_recursion_kernel(const float2* __restrict__ rows, float2* __restrict__ spec,
+                                                             const int64_t* __restrict__ lens, int64_t Tmax, float mu,
+                                                             float beta, float delta, int b0, float2* dummy_rows) {
+    const int b = b0 + blockIdx.x;
+    const int64_t T = lens[b] / kHop + 1;
+    const int k = threadIdx.x;
+    const float2* r0 = rows + (int64_t)b * Tmax * 512;
+    float2* e0 = spec + (int64_t)b * Tmax * kSpecRow;
+    NlmsBin<TAPS> st;
+    st.reset(k == 0);
+    float2 dd[kRecP], rr[kRecP];
+    auto fetch = [&](int64_t t, int i) {                  // rows past the end: any valid row (results unused)
+        const int64_t tc = t < T ? t : T - 1;
+        dd[i] = r0[tc * 512 + k];
+        rr[i] = r0[tc * 512 + 256 + k];
+    };
+    // frames past the end store to this stream's dummy row (after the [B][Tmax][2][256]
+    // rows): every store is unconditional, so the compiler's vmcnt bookkeeping
+    // stays exact across the loop and the prefetched rows are not waited for early
+    float2* dummy = dummy_rows + (int64_t)b * 256 + k;
+#pragma unroll
+    for (int i = 0; i < kRecP; ++i) fetch(i, i);
+    for (int64_t t0 = 0; t0 < T; t0 += kRecP) {
+#pragma unroll
+        for (int i = 0; i < kRecP; ++i) {
+            const float2 e = st.step(dd[i], rr[i], mu, beta, delta);
+            *(t0 + i < T ? e0 + (t0 + i) * kSpecRow + k : dummy) = e;
+            fetch(t0 + i + kRecP, i);
+        }
+    }
+}
+
+// mic_erb of every frame from its E row (K2n's mic_erb pass, frame-parallel):
+// one 4-frame work item per wave, 4 waves per block
+__global__ __launch_bounds__(256) void mic_erb_kernel(const float2* __restrict__ spec, float* __restrict__ feats,
+                                                      const int64_t* __restrict__ lens, int64_t Tmax,
+                                                      const float* __restrict__ sched, int L,
+                                                      const WorkItem* __restrict__ items, int64_t nitems) {
+    __shared__ __attribute__((aligned(16))) float4 sSched[48 * 16];
+    __shared__ int2 sComb[32];
+    __shared__ __attribute__((aligned(16))) float sScr[16][kERow];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < L * 16; i += 256) sSched[i] = reinterpret_cast<const float4*>(sched)[i];
+    if (tid < 32) sComb[tid] = reinterpret_cast<const int2*>(sched + 4 * 16 * L)[tid];
+    __syncthreads();
+    const int wave = tid >> 6, lane = tid & 63;
+    const int gg = lane >> 4, lb = lane & 15, sw = 16 * (gg & 1);
+    const int64_t item = (int64_t)blockIdx.x * 4 + wave;
+    if (item >= nitems) return;
+    const WorkItem it = items[item];
+    const int64_t T = it.n / kHop + 1;
+    const int64_t t = it.wt + gg;
+    float* er = sScr[4 * wave + gg];
+    float2 xa[8], xb[8], x128;
+    row_to_pairs(spec + ((int64_t)it.b * Tmax + (t < T ? t : 0)) * kSpecRow, lb, true, xa, xb, x128);
+    mags_to_scr(er, lb, sw, xa, xb, x128);
+    wave_fence();
+    erb_project(er, sSched, sComb, L, lb, sw, t < T ? feats + ((int64_t)it.b * Tmax + t) * 96 : nullptr);
+}
+
+hipError_t launch_nlms_recursion(const float2* rows, float2* spec, const int64_t* lens, int64_t Tmax, int taps,
+                                 float mu, float beta, float delta, int b0, int nb, float2* dummy_rows, hipStream_t st) {
+    if (nb <= 0) return hipSuccess;
+    switch (taps) {
+#define AEC_REC_CASE(T)                                                                                       \
+        case T: hipLaunchKernelGGL(nlms_recursion_kernel<T>, dim3(nb), dim3(256), 0, st, rows, spec, lens, Tmax, mu, \
+                                   beta, delta, b0, dummy_rows); break;
+        AEC_REC_CASE(1) AEC_REC_CASE(2) AEC_REC_CASE(3) AEC_REC_CASE(4)
+        AEC_REC_CASE(5) AEC_REC_CASE(6) AEC_REC_CASE(7) AEC_REC_CASE(8)
+#undef AEC_REC_CASE
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_mic_erb(const float2* spec, float* feats, const int64_t* lens, int64_t Tmax, const float* sched,
+                          int sched_len, const WorkItem* items, int64_t nitems, hipStream_t st) {
+    if (nitems <= 0) return hipSuccess;
+    if (sched_len > 48) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(mic_erb_kernel, dim3((unsigned)((nitems + 3) / 4)), dim3(256), 0, st, spec, feats, lens, Tmax,
+                       sched, sched_len, items, nitems);
+    return hipGetLastError();
 }
 
 // --------------------------------------------------------------------------

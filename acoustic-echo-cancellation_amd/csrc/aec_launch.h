@@ -34,6 +34,8 @@ struct AnalysisArgs {
     int nsig;
     float* feats;            // [B][Tmax][96]
     int64_t Tmax;
+    float2* rows;            // small-batch NLMS path: packed spectrum rows [B][Tmax][2][256] of mic and
+                             // ref (slot 0 = (X[0], X[256])), or null
 };
 
 // K2n: per-stream analysis with the FD-NLMS canceller (one block per stream).
@@ -139,6 +141,13 @@ hipError_t launch_norm_finalize(const double2* mom, const int64_t* lens, float* 
                                 hipStream_t st);
 hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t st);
 hipError_t launch_nlms_analysis(const NlmsArgs& a, int nb, hipStream_t st);
+// small-batch NLMS path (few streams: the per-stream K2n block would leave the
+// chip idle): K2 with spectrum rows, then the recursion per (stream, bin) and
+// the mic_erb pass over all frames
+hipError_t launch_nlms_recursion(const float2* rows, float2* spec, const int64_t* lens, int64_t Tmax, int taps,
+                                 float mu, float beta, float delta, int b0, int nb, float2* dummy_rows, hipStream_t st);
+hipError_t launch_mic_erb(const float2* spec, float* feats, const int64_t* lens, int64_t Tmax, const float* sched,
+                          int sched_len, const WorkItem* items, int64_t nitems, hipStream_t st);
 hipError_t launch_gru(const GruArgs& a, int B, hipStream_t st);
 hipError_t launch_synthesis(const SynthArgs& a, hipStream_t st);
 hipError_t launch_stream_step(const StreamStepArgs& a, int B, int taps, hipStream_t st);

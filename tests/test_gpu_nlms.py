@@ -185,3 +185,37 @@ def test_fused_synthesis_bit_exact(golden_weights, golden_erb, monkeypatch):
     for i, n in enumerate(lens):
         assert np.array_equal(e0[i, :n // 256 + 1], e1[i, :n // 256 + 1])
     np.testing.assert_allclose(l1, l0, rtol=1e-6)
+
+
+def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatch):
+    """Few streams take the split NLMS path (frame-parallel transforms + rows,
+    per-stream recursion, frame-parallel mic_erb; AEC_SMALLB) instead of the
+    per-stream K2n block: the same per-frame arithmetic, so the waveform,
+    the features and the loss are bit-identical to the K2n path."""
+    from aec_amd import synth
+    lens = [33333, 4097, 255, 16000, 256]
+    L = max(lens)
+    rows = [synth.scene(n, 800 + i) for i, n in enumerate(lens)]
+    mic, ref, near = (np.zeros((len(lens), L), np.float32) for _ in range(3))
+    for i, (m, r, nn_) in enumerate(rows):
+        mic[i, :lens[i]], ref[i, :lens[i]], near[i, :lens[i]] = m, r, nn_
+    dev = 'cuda:0'
+    erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
+    M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
+    res = {}
+    for small in ('0', '64'):
+        monkeypatch.setenv('AEC_SMALLB', small)                 # read when the handle is created
+        net = _net(golden_weights, NLMS)
+        net.set_debug(True)
+        with torch.no_grad():
+            out, loss = net.forward_ragged(M, R, N, erb_t, lens)
+        T = L // 256 + 1
+        feats = {k: net.debug_intermediate(k, len(lens), T).cpu().numpy() for k in ('mic_erb', 'ref_erb', 'est_erb')}
+        torch.cuda.synchronize()
+        res[small] = (out.cpu().numpy(), loss.cpu().numpy(), feats)
+    (o0, l0, f0), (o1, l1, f1) = res['0'], res['64']
+    assert np.array_equal(o0, o1)
+    assert np.array_equal(l0, l1, equal_nan=True)       # the 256-sample row's loss is the reference's 0/0 NaN
+    for k in f0:
+        for i, n in enumerate(lens):
+            assert np.array_equal(f0[k][i, :n // 256 + 1], f1[k][i, :n // 256 + 1]), (k, i)
