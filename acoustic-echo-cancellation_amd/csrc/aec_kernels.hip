@@ -6,16 +6,23 @@
 //   K1 moments_kernel   partial sums for x <- x - mean(x)/std(x) (ERB.py:254-256)
 //   K2 analysis_kernel  frame + Hann + rFFT-512 (attention_ccrn.py:45-52) -> |X| (ERB.py:277-279)
 //                       -> ERB band energies (ERB.py:282-284) for mic / ref / near
+//   K2n nlms_analysis_kernel  K2 with the FD-NLMS canceller (one block per stream);
+//                       for few streams the split path: K2 + spectrum rows,
+//                       nlms_recursion_kernel, mic_erb_kernel
 //   K3 gru_kernel       (aec_gru.hip) GRU + head + mask -> est_erb, loss
 //   K4 synthesis_kernel gain = est_erb @ erb^T (ERB.py:306-310) * mic spectrum
 //                       -> irFFT-512 + Hann + overlap-add / WOLA (attention_ccrn.py:82-101)
 //                       -> + 1e-9 (ERB.py:316)
+//   (K3 + K4 fused on the NLMS path: aec_gru_synth.hip; the per-hop streaming
+//    step: aec_stream.hip)
 //
 // HBM layout (row-major, float32 unless noted):
 //   signals  [B][ld]              caller-owned
 //   mom      [B][3][8] double2    per-chunk (sum x, sum x^2)
 //   feats    [B][Tmax][96]        mic_erb | ref_erb | near_erb per frame
 //   est      [B][Tmax][32]        est_erb per frame
+//   spec     [B][Tmax][256] float2  NLMS error spectrum E (slot 0 = (E[0], E[256]))
+//   rows     [B][Tmax][2][256] float2  split path only: mic / ref spectrum rows
 //   out      [B][ld_out]          caller-owned, 256*(N_b/256) samples per row
 #include <hip/hip_runtime.h>
 #include <stdint.h>
