@@ -235,7 +235,7 @@ def crn_config(version, conf, dtype):
     c.rnn_layers = int(conf.get('rnn_layers', 1))
     c.use_cbn = int(bool(conf.get('use_cbn', False)))
     c.masking_mode = ord(conf.get('masking_mode', 'C')[0]) if version == 2 else ord('C')
-    c.dtype = {'f32': 0, 'float32': 0, 'bf16': 1, 'bfloat16': 1}[dtype]
+    c.dtype = {'f32': 0, 'float32': 0, 'bf16': 1, 'bfloat16': 1, 'fp8': 2, 'mxfp8': 2}[dtype]
     return c
 
 

@@ -16,8 +16,11 @@ order, and the same ``forward(mic, far, near, echo)`` outputs:
 Eval-mode inference only (BatchNorm running statistics, as
 ``net.eval()``); it raises in training mode or under autograd.  The whole
 network runs in ``libaec_hip.so`` (include/aec_crn.h): ``dtype='f32'``
-(exact f32 MFMA, the parity path) or ``dtype='bf16'`` (bf16 MFMA with f32
-accumulation, the throughput path of BASELINE config 3).  No CPU fallback.
+(exact f32 MFMA, the parity path), ``dtype='bf16'`` (bf16 MFMA with f32
+accumulation, the throughput path of BASELINE config 3) or ``dtype='fp8'``
+(bf16, with the LSTM input projections -- half the weights -- as MX-fp8:
+OCP e4m3 weights and activations with an E8M0 scale per 32 k on the gfx950
+scaled MFMA; BASELINE config 5).  No CPU fallback.
 
 Rows of a [B, N] batch are independent in eval mode (nothing couples
 utterances), so batching is exact; ``forward_ragged`` takes per-row lengths.

@@ -59,6 +59,8 @@ struct Packed {
     int npad = 0, kpad = 0, N = 0, K = 0;
     float alpha = 0.f;
     int act = 0;
+    uint8_t* wq = nullptr;      // dtype 2 (LSTM input projections): e4m3 [npad][kpad]
+    uint8_t* wsc = nullptr;     //   and E8M0 scales [npad][kpad / 32]
 };
 
 }  // namespace
@@ -71,6 +73,7 @@ struct aec_crn_handle {
     std::string err;
     int L = 6, D = 4, H = 0, S = 1, CELLS = 1, Q = 0, nrnn = 1;
     size_t es = 4;                                 // element size
+    bool mx8 = false;                              // dtype 2: MX-fp8 LSTM input projections
     aec::DevTables* d_tab = nullptr;
     std::vector<Packed> enc, dec;                  // dec: 2 per level (even, odd)
     std::vector<Packed> lih, lhh;                  // per LSTM layer
@@ -82,6 +85,8 @@ struct aec_crn_handle {
     void* gx = nullptr;
     void* y = nullptr;
     void* xn = nullptr;
+    uint8_t* aq = nullptr;                         // dtype 2: quantized LSTM input rows + scales
+    uint8_t* as = nullptr;
     float* cst = nullptr;
     float* mask = nullptr;
     int64_t* d_len = nullptr;
@@ -120,7 +125,7 @@ static std::string check_cfg(const aec_crn_config& c) {
     if (c.conv_channels[0] != 4) return "conv_channels[0] must be 4 (mic/far real/imag)";
     for (int i = 1; i <= c.n_layers; ++i)
         if (c.conv_channels[i] < 8 || ilog2(c.conv_channels[i]) < 0) return "conv_channels must be powers of two >= 8";
-    if (c.dtype != 0 && c.dtype != 1) return "dtype must be 0 (f32) or 1 (bf16)";
+    if (c.dtype < 0 || c.dtype > 2) return "dtype must be 0 (f32), 1 (bf16) or 2 (bf16 + MX-fp8 LSTM input)";
     if (c.version == 2) {
         if (c.hidden_dim != 4) return "hidden_dim must equal the encoder output width (4)";
         if (c.rnn_layers < 1 || c.rnn_layers > 8) return "rnn_layers out of range";
@@ -280,6 +285,49 @@ static aec_status upload_packed(aec_crn_handle* h, Packed& pk, const std::vector
     return AEC_OK;
 }
 
+// OCP e4m3 (e4m3fn) of x, round to nearest even, saturating at +-448
+static uint8_t host_e4m3(double x) {
+    const uint8_t sg = x < 0 ? 0x80 : 0;
+    const double a = std::fabs(x);
+    if (!(a < 448.0)) return sg | 0x7E;
+    if (a < std::ldexp(1.0, -6)) return sg | (uint8_t)std::nearbyint(a * 512.0);   // subnormal: m * 2^-9
+    int e2;
+    (void)std::frexp(a, &e2);
+    const int E = e2 - 1;                                                          // floor(log2 a), -6 .. 8
+    const int m = (int)std::nearbyint((a / std::ldexp(1.0, E) - 1.0) * 8.0);      // 0 .. 8 (8 carries)
+    const int code = std::min(((E + 7) << 3) + m, 0x7E);
+    return sg | (uint8_t)code;
+}
+
+// dtype 2: the packed weight rows [npad][kpad] as MX-fp8 (E8M0 scale per 32 k:
+// 2^(floor(log2 amax) - 8), the same rule as the device's activation quantizer)
+static aec_status upload_mx8(aec_crn_handle* h, Packed& pk, const std::vector<double>& w) {
+    const size_t n = (size_t)pk.npad * pk.kpad, kb = (size_t)pk.kpad / 32;
+    std::vector<uint8_t> q(n, 0), sc((size_t)pk.npad * kb, 0);
+    for (int r = 0; r < pk.N; ++r)
+        for (size_t b = 0; b < kb; ++b) {
+            const double* x = &w[(size_t)r * pk.kpad + b * 32];
+            double amax = 0;
+            for (int j = 0; j < 32; ++j) amax = std::max(amax, std::fabs((double)(float)x[j]));
+            int code = 0;
+            if (amax > 0) {
+                int e2;
+                (void)std::frexp((double)(float)amax, &e2);
+                code = std::max(0, std::min(254, (e2 - 1) + 127 - 8));
+            }
+            sc[(size_t)r * kb + b] = (uint8_t)code;
+            for (int j = 0; j < 32; ++j)
+                q[(size_t)r * pk.kpad + b * 32 + j] = host_e4m3(std::ldexp((double)(float)x[j], 127 - code));
+        }
+    if (!pk.wq) {
+        CRN_TRY(h, hipMalloc(&pk.wq, n));
+        CRN_TRY(h, hipMalloc(&pk.wsc, sc.size()));
+    }
+    CRN_TRY(h, hipMemcpy(pk.wq, q.data(), n, hipMemcpyHostToDevice));
+    CRN_TRY(h, hipMemcpy(pk.wsc, sc.data(), sc.size(), hipMemcpyHostToDevice));
+    return AEC_OK;
+}
+
 static int kpad_for(int K, size_t es) {
     const int per = (int)(crn::kStageBytes / es);
     return (K + per - 1) / per * per;
@@ -366,6 +414,10 @@ static aec_status pack_lstm(aec_crn_handle* h, Cursor& cur, Packed& ih, Packed& 
     ih.act = 0;
     aec_status s = upload_packed(h, ih, wih, bias);
     if (s != AEC_OK) return s;
+    if (h->mx8) {
+        s = upload_mx8(h, ih, wih);
+        if (s != AEC_OK) return s;
+    }
     return upload_packed(h, hh, whh, bias);
 }
 
@@ -435,6 +487,10 @@ static aec_status ensure_ws(aec_crn_handle* h, int64_t B, int64_t T) {
     CRN_TRY(h, alloc(&h->gx, (size_t)BT * h->S * h->CELLS * 4 * h->H * es));
     CRN_TRY(h, alloc(&h->y, (size_t)BT * h->CELLS * h->S * h->H * es));
     if (h->nrnn > 1) CRN_TRY(h, alloc(&h->xn, (size_t)BT * h->S * h->H * es));
+    if (h->mx8) {
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->aq), (size_t)BT * h->S * h->H));
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->as), (size_t)BT * h->S * h->H / 32));
+    }
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->cst), (size_t)nB * h->CELLS * h->S * h->H * sizeof(float)));
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->mask), (size_t)BT * 256 * 2 * sizeof(float)));
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->d_len), (size_t)nB * sizeof(int64_t)));
@@ -460,6 +516,8 @@ struct Bufs {
     void* gx;
     void* xn;
     float* mask;
+    uint8_t* aq;            // dtype 2: quantized LSTM input rows [F*S][H] + scales [F*S][H/32]
+    uint8_t* as;
 };
 
 template <typename T>
@@ -527,6 +585,11 @@ static aec_status run_lstm_input(aec_crn_handle* h, const Bufs& bf, int l, int64
     a.src_elems = F * D * ld_in;
     const Packed& ih = h->lih[l];
     RowEpi e{bf.gx, a.M, ih.N, 0, (int64_t)C * 4 * H, 0, 0, ih.bias, 0.f, 0};
+    if (h->mx8) {                          // e4m3 rows + E8M0 scales, then the scaled-MFMA GEMM
+        CRN_TRY(h, crn::launch_mx8_quant(a, bf.aq, bf.as, st));
+        CRN_TRY(h, crn::launch_gemm_mx8<T>(bf.aq, bf.as, ih.wq, ih.wsc, ih.kpad, e, ih.npad, st));
+        return AEC_OK;
+    }
     CRN_TRY(h, (crn::launch_gemm_rows<T, T>(a, reinterpret_cast<const T*>(ih.w), ih.kpad,
                                              (int)(ih.kpad * sizeof(T) / crn::kStageBytes), e, ih.npad, st)));
     return AEC_OK;
@@ -598,7 +661,7 @@ template <typename T>
 static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int32_t B, int64_t ld, int64_t Tmax,
                       float* out, int64_t ld_out, float* spec, float* mask_out, hipStream_t st) {
     const int64_t BT = (int64_t)B * Tmax;
-    const Bufs bf{h->x0, h->cat.data(), h->gx, h->xn, h->mask};
+    const Bufs bf{h->x0, h->cat.data(), h->gx, h->xn, h->mask, h->aq, h->as};
     const int H = h->H, S = h->S, C = h->CELLS;
     mark(h, st);
     // front: X0 [Tmax][B][256][8]
@@ -651,6 +714,8 @@ struct StreamState {
     void* gx = nullptr;
     void* xn = nullptr;
     float* mask = nullptr;
+    uint8_t* aq = nullptr;               // dtype 2 (see Bufs)
+    uint8_t* as = nullptr;
     void* ring_y[8][2] = {};             // per LSTM layer: h ring (two frames)
     float* cst[8] = {};                  // per LSTM layer: c
     float* hop = nullptr;                // [2 parity][2 signal][B][256] input hop ring (mic, far)
@@ -674,7 +739,7 @@ template <typename T>
 static aec_status stream_launches(aec_crn_handle* h, int par, hipStream_t st) {
     StreamState& ss = *h->ss;
     const int B = ss.B;
-    const Bufs bf{ss.x0, ss.cat.data(), ss.gx, ss.xn, ss.mask};
+    const Bufs bf{ss.x0, ss.cat.data(), ss.gx, ss.xn, ss.mask, ss.aq, ss.as};
     const float* cur_mic = ss.hop + (size_t)(par * 2 + 0) * B * 256;
     const float* cur_far = ss.hop + (size_t)(par * 2 + 1) * B * 256;
     const float* prev_mic = ss.hop + (size_t)((1 - par) * 2 + 0) * B * 256;
@@ -715,7 +780,8 @@ aec_status aec_crn_create(const aec_crn_config* cfg, const float* params, size_t
     h->device = device;
     h->L = cfg->n_layers;
     h->D = 256 >> h->L;
-    h->es = cfg->dtype == 1 ? 2 : 4;
+    h->es = cfg->dtype == 0 ? 4 : 2;
+    h->mx8 = cfg->dtype == 2;
     if (cfg->version == 1) {
         h->H = cfg->conv_channels[h->L] * 4;
         h->S = h->CELLS = 1;
@@ -726,6 +792,10 @@ aec_status aec_crn_create(const aec_crn_config* cfg, const float* params, size_t
         h->nrnn = cfg->rnn_layers;
     }
     h->Q = h->H / h->D;
+    if (h->mx8 && (h->H % 128 || h->Q % 32)) {     // MX blocks of 32 k inside one tap, 128-k stages
+        delete h;
+        return AEC_ERR_UNSUPPORTED;
+    }
     auto bail = [&](aec_status s) {
         aec_crn_destroy(h);
         return s;
@@ -848,6 +918,10 @@ aec_status aec_crn_stream_open(aec_crn_handle* h, int32_t B) {
     for (int l = 1; l <= h->L; ++l) CRN_TRY(h, alloc(&ss.cat[l], (size_t)B * (256 >> l) * 2 * ch[l] * es));
     CRN_TRY(h, alloc(&ss.gx, (size_t)B * S * C * 4 * H * es));
     if (h->nrnn > 1) CRN_TRY(h, alloc(&ss.xn, (size_t)B * S * H * es));
+    if (h->mx8) {
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.aq), (size_t)B * S * H));
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.as), (size_t)B * S * H / 32));
+    }
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.mask), (size_t)B * 256 * 2 * sizeof(float)));
     for (int l = 0; l < h->nrnn; ++l) {
         CRN_TRY(h, alloc(&ss.ring_y[l][0], (size_t)B * C * S * H * es));
@@ -960,6 +1034,8 @@ void aec_crn_destroy(aec_crn_handle* h) {
         for (Packed& pk : *v) {
             if (pk.w) (void)hipFree(pk.w);
             if (pk.bias) (void)hipFree(pk.bias);
+            if (pk.wq) (void)hipFree(pk.wq);
+            if (pk.wsc) (void)hipFree(pk.wsc);
         }
     if (h->d_tab) (void)hipFree(h->d_tab);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);

@@ -199,11 +199,18 @@ __device__ __forceinline__ void wait_vm() {
 // RB = bytes of K per row per stage (128: two 64-B k-chunks; 64: one).  A DMA
 // instruction writes 64 lanes x 16 B = 1 KiB = 1024 / RB rows.
 // AUXA: cache policy bits of the A-operand DMA (2 = nt: streamed operand, keep L2 for B)
+// Tail hook: at the first iteration that issues no further stage (st =
+// nstages - NBUF + 1, after its barrier) the buffer of stage st - 1 is free
+// for the rest of the loop; tail(buf) may issue HK DMA instructions per wave
+// into it (the epilogue operands), which the remaining waits leave in flight.
+struct NoTail {
+    __device__ __forceinline__ void operator()(char*) const {}
+};
 template <typename T, int BM, int BN, int FM, int FN, int NBUF, class AO, class BO, int NW = 4, int RB = 128,
-          int AUXA = 0>
+          int AUXA = 0, class TAIL = NoTail, int HK = 0>
 __device__ __forceinline__ void gemm_core_dma(f32x4 (&acc)[FM][FN], char* smem, __amdgpu_buffer_rsrc_t ra,
                                               __amdgpu_buffer_rsrc_t rb, const AO& aoff, const BO& boff,
-                                              int nstages, int wr0, int wc0) {
+                                              int nstages, int wr0, int wc0, const TAIL& tail = TAIL{}) {
     constexpr int RPI = 1024 / RB;                       // rows per DMA instruction
     constexpr int CPR = RB / 16;                         // 16-B chunks per row
     static_assert(BM % (RPI * NW) == 0 && BN % (RPI * NW) == 0 && NBUF >= 2, "tile");
@@ -233,13 +240,17 @@ __device__ __forceinline__ void gemm_core_dma(f32x4 (&acc)[FM][FN], char* smem, 
     for (int s = 0; s < NBUF - 1; ++s)
         if (s < nstages) issue(s);
     const int fr = lane & 15, g = lane >> 4;
+    const int st_tail = nstages - NBUF + 1;              // first iteration without a stage issue
     for (int st = 0; st < nstages; ++st) {
         if (st + NBUF - 2 < nstages)
             wait_vm<(NBUF - 2) * (LA + LB)>();
+        else if (HK > 0 && st > st_tail)
+            wait_vm<HK>();                                   // the tail DMAs stay in flight
         else
             wait_vm<0>();
         __builtin_amdgcn_s_barrier();
         if (st + NBUF - 1 < nstages) issue(st + NBUF - 1);
+        if (HK > 0 && st == (st_tail > 0 ? st_tail : 0)) tail(smem + ((st + NBUF - 1) % NBUF) * STAGE);
         const char* sA = smem + (st % NBUF) * STAGE;
         const char* sB = sA + BM * RB;
 #pragma unroll
@@ -269,5 +280,96 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
 }
 
 constexpr uint32_t kOOB = 0x80000000u;
+
+// --------------------------------------------------------------------------
+// MX-fp8 main loop: OCP e4m3 operands with an E8M0 scale per 32 k of every
+// row, v_mfma_scale_f32_16x16x128_f8f6f4 (2x the bf16 MFMA rate per clock).
+// Operand map, measured on gfx950 (tools/probes/mx8_probe.hip, one-hot
+// probes over all 2048 lane/byte slots): lane l = (g = l >> 4, r = l & 15)
+// holds row r's bytes [16g, 16g+16) in operand regs 0-3 and [64+16g,
+// 64+16g+16) in regs 4-7, and its scale operand is the E8M0 of (row r,
+// k-block [32g, 32g+32)); C/D as the bf16 16x16 form.  So a 128-byte K stage
+// staged exactly as in gemm_core_dma feeds ONE MX MFMA per fragment pair from
+// the two 16-B chunks the bf16 loop reads (slots g and 4+g).
+// Stage layout: [A BM x 128 B][B BN x 128 B][A scales BM x 4 B][B scales BN x
+// 4 B]; a stage's scales (bytes 4 st .. 4 st+3 of every row's scale row) come
+// by one 4-byte DMA per lane: wave w, lane l fetches row 64 w + l of [A | B]
+// (BM + BN == 64 NW), so every wave issues LA + LB + 1 DMAs per stage.
+// rs / soff: the wave's scale descriptor (A or B, wave-uniform) and the lane's
+// byte offset of its scale row (kOOB: zero scale byte, row out of range).
+// --------------------------------------------------------------------------
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+template <int BM, int BN, int FM, int FN, int NBUF, class AO, class BO, int NW>
+__device__ __forceinline__ void gemm_core_mx8(f32x4 (&acc)[FM][FN], char* smem, __amdgpu_buffer_rsrc_t ra,
+                                              __amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rs, const AO& aoff,
+                                              const BO& boff, uint32_t soff, int nstages, int wr0, int wc0) {
+    constexpr int RB = 128, RPI = 8;
+    static_assert(BM % (RPI * NW) == 0 && BN % (RPI * NW) == 0 && NBUF >= 2 && BM + BN == 64 * NW, "tile");
+    constexpr int LA = BM / (RPI * NW), LB = BN / (RPI * NW);
+    constexpr int STAGE = (BM + BN) * (RB + 4);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int q_l = lane & 7;
+    auto issue = [&](int st) {
+        char* buf = smem + (st % NBUF) * STAGE;
+#pragma unroll
+        for (int i = 0; i < LA; ++i) {
+            const int row = RPI * (NW * i + wave) + lane / 8;
+            const uint32_t vo = aoff(i, st * RB + swz_slot<RB>(row, q_l) * 16);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                ra, (__attribute__((address_space(3))) void*)(buf + RPI * (NW * i + wave) * RB), 16, vo, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < LB; ++i) {
+            const int row = RPI * (NW * i + wave) + lane / 8;
+            const uint32_t vo = boff(i, st * RB + swz_slot<RB>(row, q_l) * 16);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rb, (__attribute__((address_space(3))) void*)(buf + BM * RB + RPI * (NW * i + wave) * RB), 16, vo, 0,
+                0, 0);
+        }
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs, (__attribute__((address_space(3))) void*)(buf + (BM + BN) * RB + wave * 256), 4,
+            soff == kOOB ? kOOB : soff + 4 * st, 0, 0, 0);
+    };
+#pragma unroll
+    for (int s = 0; s < NBUF - 1; ++s)
+        if (s < nstages) issue(s);
+    const int fr = lane & 15, g = lane >> 4;
+    for (int st = 0; st < nstages; ++st) {
+        if (st + NBUF - 2 < nstages)
+            wait_vm<(NBUF - 2) * (LA + LB + 1)>();
+        else
+            wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        if (st + NBUF - 1 < nstages) issue(st + NBUF - 1);
+        const char* sA = smem + (st % NBUF) * STAGE;
+        const char* sB = sA + BM * RB;
+        const uint32_t* sS = reinterpret_cast<const uint32_t*>(sA + (BM + BN) * RB);
+        i32x8 bfr[FN];
+        int sb[FN];
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+            const int r = wc0 + fn * 16 + fr;
+            const u32x4 lo = *reinterpret_cast<const u32x4*>(sB + r * RB + swz_slot<RB>(r, g) * 16);
+            const u32x4 hi = *reinterpret_cast<const u32x4*>(sB + r * RB + swz_slot<RB>(r, 4 + g) * 16);
+            bfr[fn] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2],
+                            (int)hi[3]};
+            sb[fn] = (int)((sS[BM + r] >> (8 * g)) & 0xFFu);
+        }
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+            const int r = wr0 + fm * 16 + fr;
+            const u32x4 lo = *reinterpret_cast<const u32x4*>(sA + r * RB + swz_slot<RB>(r, g) * 16);
+            const u32x4 hi = *reinterpret_cast<const u32x4*>(sA + r * RB + swz_slot<RB>(r, 4 + g) * 16);
+            const i32x8 af = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1],
+                                   (int)hi[2], (int)hi[3]};
+            const int sa = (int)((sS[r] >> (8 * g)) & 0xFFu);
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn)
+                acc[fm][fn] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bfr[fn], acc[fm][fn], 0, 0, 0, sa,
+                                                                               0, sb[fn]);
+        }
+    }
+}
 
 }  // namespace crn

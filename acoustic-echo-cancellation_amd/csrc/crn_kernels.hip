@@ -686,6 +686,135 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
     return hipGetLastError();
 }
 
+// --------------------------------------------------------------------------
+// MX-fp8 (dtype 2): LSTM input projections with e4m3 operands and E8M0
+// scales per 32 k (OCP MX: scale = 2^(floor(log2 amax) - 8), values clamped
+// to +-448, round to nearest even by v_cvt_pk_fp8_f32).
+// mx8_quant_kernel: one thread per (row, 32-k block) of a RowSrc (the block
+// lies inside one tap: 2^kshift % 32 == 0, checked by the host), reading 64
+// contiguous bytes of bf16 -> q [M][K] bytes, s [M][K/32] E8M0 codes.
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void mx8_quant_kernel(RowSrc a, uint8_t* __restrict__ q, uint8_t* __restrict__ s) {
+    const int KB = a.K / 32;
+    const int64_t total = a.M * KB;
+    const int kmask = (1 << a.kshift) - 1;
+    const int64_t lomask = (1ll << a.rshift) - 1;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t m = t / KB;
+        const int k0 = (int)(t - m * KB) * 32;
+        const int64_t off = (m >> a.rshift) * a.rs_hi + (m & lomask) * a.rs_lo + (int64_t)(k0 >> a.kshift) * a.ks +
+                            (k0 & kmask) + a.base_off;
+        const u32x4* src = reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(a.src) + off);
+        u32x4 raw[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) raw[i] = src[i];
+        float v[32];
+        float amax = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t w = raw[i >> 2][i & 3];
+            v[2 * i] = __uint_as_float(w << 16);
+            v[2 * i + 1] = __uint_as_float(w & 0xFFFF0000u);
+            amax = fmaxf(amax, fmaxf(fabsf(v[2 * i]), fabsf(v[2 * i + 1])));
+        }
+        const int ebits = (int)((__float_as_uint(amax) >> 23) & 0xFF);   // floor(log2 amax) + 127
+        const int code = ebits > 8 ? ebits - 8 : 0;                        // E8M0: 2^(code - 127)
+        uint32_t pk[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float x[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[j] = fminf(fmaxf(ldexpf(v[4 * i + j], 127 - code), -448.f), 448.f);
+            int w = __builtin_amdgcn_cvt_pk_fp8_f32(x[0], x[1], 0, false);
+            w = __builtin_amdgcn_cvt_pk_fp8_f32(x[2], x[3], w, true);
+            pk[i] = (uint32_t)w;
+        }
+        u32x4* dst = reinterpret_cast<u32x4*>(q + m * a.K + k0);
+        dst[0] = u32x4{pk[0], pk[1], pk[2], pk[3]};
+        dst[1] = u32x4{pk[4], pk[5], pk[6], pk[7]};
+        s[t] = (uint8_t)code;
+    }
+}
+
+hipError_t launch_mx8_quant(const RowSrc& a, uint8_t* q, uint8_t* s, hipStream_t st) {
+    if (a.M <= 0) return hipSuccess;
+    if (a.K % 128 || ((1 << a.kshift) % 32) || a.pmul != 0) return hipErrorInvalidValue;
+    const int64_t total = a.M * (a.K / 32);
+    const unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 256 * 64);
+    hipLaunchKernelGGL(mx8_quant_kernel, dim3(grid), dim3(256), 0, st, a, q, s);
+    return hipGetLastError();
+}
+
+// C[M][N] = dequant(A) dequant(B)^T (+ bias, RowEpi) with A q [M][K] / s [M][K/32],
+// B (weights, rows n) q [npad][K] / s [npad][K/32]; 1-D grid, column blocks fastest.
+template <typename OutT, int WM, int WN, int FM, int FN, int NBUF>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_mx8_kernel(const uint8_t* __restrict__ aq,
+                                                                const uint8_t* __restrict__ as,
+                                                                const uint8_t* __restrict__ bq,
+                                                                const uint8_t* __restrict__ bs, int K, RowEpi e) {
+    constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
+    constexpr int NW = WM * WN;
+    constexpr int LA = BM / (8 * NW);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int nbn = (e.N + BN - 1) / BN;
+    const int64_t m0 = (int64_t)(blockIdx.x / nbn) * BM;
+    const int n0 = (int)(blockIdx.x % nbn) * BN;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const int wr0 = (wave / WN) * FM * 16, wc0 = (wave % WN) * FN * 16;
+    const int KB = K / 32;
+    const int64_t mrem = e.M - m0;
+    const __amdgpu_buffer_rsrc_t ra = make_rsrc(aq + m0 * K, (uint64_t)mrem * K);
+    const __amdgpu_buffer_rsrc_t rb = make_rsrc(bq + (int64_t)n0 * K, (uint64_t)BN * K);
+    const __amdgpu_buffer_rsrc_t rsa = make_rsrc(as + m0 * KB, (uint64_t)mrem * KB);
+    const __amdgpu_buffer_rsrc_t rsb = make_rsrc(bs + (int64_t)n0 * KB, (uint64_t)BN * KB);
+    const bool sc_a = wv * 64 < BM;                      // wave-uniform: this wave fetches A (else B) scales
+    const int srow = wave * 64 + lane - (sc_a ? 0 : BM);
+    const uint32_t soff = (sc_a && srow >= mrem) ? kOOB : (uint32_t)(srow * KB);
+    uint32_t arow[LA];
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+        const int r = 8 * (NW * i + wave) + lane / 8;
+        arow[i] = r < mrem ? (uint32_t)(r * K) : kOOB;
+    }
+    auto aoff = [&](int i, int kbyte) -> uint32_t { return arow[i] == kOOB ? kOOB : arow[i] + kbyte; };
+    auto boff = [&](int i, int kbyte) -> uint32_t { return (uint32_t)((8 * (NW * i + wave) + lane / 8) * K + kbyte); };
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    gemm_core_mx8<BM, BN, FM, FN, NBUF, decltype(aoff), decltype(boff), NW>(acc, smem, ra, rb, sc_a ? rsa : rsb, aoff,
+                                                                          boff, soff, K / 128, wr0, wc0);
+    __syncthreads();
+    constexpr int PF = epi_passes<OutT, FM, FN, NW>((size_t)NBUF * (BM + BN) * 132);
+    rows_epilogue_lds<OutT, FM, FN, PF>(acc, e, m0 + wr0, n0 + wc0, lane,
+                                        smem + wave * (PF * 16 * FN * 16 * (int)sizeof(OutT)));
+}
+
+template <typename OutT>
+hipError_t launch_gemm_mx8(const uint8_t* aq, const uint8_t* as, const uint8_t* bq, const uint8_t* bs, int K,
+                           const RowEpi& e, int npad, hipStream_t st) {
+    if (e.M <= 0) return hipSuccess;
+    // 256 x 256 tiles, 8 waves (2 x 4, 128 x 64 per wave), 2 stage buffers of 132 B per row
+    constexpr int WM = 2, WN = 4, FM = 8, FN = 4, NBUF = 2;
+    constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
+    if (K % 128 || npad % BN || e.N > npad) return hipErrorInvalidValue;
+    auto kern = gemm_mx8_kernel<OutT, WM, WN, FM, FN, NBUF>;
+    constexpr size_t lds = (size_t)NBUF * (BM + BN) * 132;
+    static_assert(lds <= 160 * 1024, "LDS");
+    static const hipError_t attr =
+        hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (attr != hipSuccess) return attr;
+    const unsigned grid = (unsigned)((e.M + BM - 1) / BM) * (unsigned)(npad / BN);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WM * WN), lds, st, aq, as, bq, bs, K, e);
+    return hipGetLastError();
+}
+template hipError_t launch_gemm_mx8<bf16_t>(const uint8_t*, const uint8_t*, const uint8_t*, const uint8_t*, int,
+                                            const RowEpi&, int, hipStream_t);
+template hipError_t launch_gemm_mx8<float>(const uint8_t*, const uint8_t*, const uint8_t*, const uint8_t*, int,
+                                           const RowEpi&, int, hipStream_t);
+
 template hipError_t launch_gemm_rows<float, float>(const RowSrc&, const float*, int64_t, int, const RowEpi&, int,
                                                    hipStream_t);
 template hipError_t launch_gemm_rows<bf16_t, bf16_t>(const RowSrc&, const bf16_t*, int64_t, int, const RowEpi&, int,

@@ -93,6 +93,12 @@ hipError_t launch_stream_back(const StreamBackArgs& a, int mode, hipStream_t st)
 template <typename T, typename OutT>
 hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstages, const RowEpi& e, int npad,
                             hipStream_t st);
+// MX-fp8 (dtype 2): quantize bf16 rows of a RowSrc to e4m3 + E8M0 per 32 k,
+// and the scaled-MFMA GEMM over such operands (B = packed weight rows)
+hipError_t launch_mx8_quant(const RowSrc& a, uint8_t* q, uint8_t* s, hipStream_t st);
+template <typename OutT>
+hipError_t launch_gemm_mx8(const uint8_t* aq, const uint8_t* as, const uint8_t* bq, const uint8_t* bs, int K,
+                           const RowEpi& e, int npad, hipStream_t st);
 template <typename T>
 hipError_t launch_front(const FrontArgs& a, int B, hipStream_t st);
 hipError_t launch_back(const BackArgs& a, int B, int mode, hipStream_t st);

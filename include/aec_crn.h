@@ -53,7 +53,10 @@ typedef struct {
     int32_t rnn_layers;         /* v2: number of NavieComplexLSTM layers                     */
     int32_t use_cbn;            /* v2: ComplexBatchNorm (1) or BatchNorm2d (0)               */
     int32_t masking_mode;       /* v2: 'E', 'C' or 'R' (character code); v1 uses 'C'         */
-    int32_t dtype;              /* compute / storage type: 0 = float32, 1 = bfloat16         */
+    int32_t dtype;              /* compute / storage type: 0 = float32, 1 = bfloat16,
+                                   2 = bfloat16 with MX-fp8 LSTM input projections (OCP e4m3
+                                   weights and activations, E8M0 scale per 32 k; needs
+                                   H % 128 == 0 and H / (256 >> n_layers) % 32 == 0)       */
 } aec_crn_config;
 
 /* Number of floats in the parameter blob: the reference state_dict entries

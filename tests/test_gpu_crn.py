@@ -7,8 +7,12 @@ Tolerances (relative RMS, written here):
   (observed float32-reference vs float64-oracle: ~6e-7);
 * bf16 path (bf16 storage / MFMA, f32 accumulate): out_wav <= BF16_WAV_TOL,
   mask <= BF16_MASK_TOL (reduced precision; the f32 path is the parity gate);
+* fp8 path (bf16 + MX-fp8 LSTM input projections: e4m3 weights and
+  activations, E8M0 scale per 32 k): out_wav <= FP8_WAV_TOL, mask <=
+  FP8_MASK_TOL against the reference, and within FP8_VS_BF16_TOL of the bf16
+  path (the only change is the input projection's operand rounding);
 * integer framing (T, output length) bit-exact; batch composition (ragged
-  rows in one call vs one call per row) bit-exact on the f32 path.
+  rows in one call vs one call per row) bit-exact on every path.
 """
 import copy
 import json
@@ -28,6 +32,9 @@ META = json.load(open(os.path.join(GOLD, 'crn_meta.json')))
 F32_TOL = 1e-4
 BF16_WAV_TOL = 5e-2
 BF16_MASK_TOL = 5e-2
+FP8_WAV_TOL = 1e-1
+FP8_MASK_TOL = 1e-1
+FP8_VS_BF16_TOL = 1e-1
 
 
 def rel(a, b):
@@ -92,7 +99,26 @@ def test_bf16_close_to_reference(name):
     assert rel(mask[0].cpu().numpy(), d['mask']) <= BF16_MASK_TOL
 
 
-@pytest.mark.parametrize('dtype', ['f32', 'bf16'])
+@pytest.mark.parametrize('name', ['v2E_2125', 'v1_2125', 'v2E_16000'])
+def test_fp8_close_to_reference(name):
+    d = np.load(os.path.join(GOLD, f'crn_{name}.npz'))
+    outs = {}
+    for dt in ('bf16', 'fp8'):
+        net, m, _ = build(name, dt)
+        with torch.no_grad():
+            out, _, mask = net.forward_ragged(T(d['mic']), T(d['far']), [m['n']], want_spec=False, want_mask=True)
+        torch.cuda.synchronize()
+        outs[dt] = (out[0].cpu().numpy(), mask[0].cpu().numpy())
+    out, mask = outs['fp8']
+    assert out.shape == d['out_wav'].shape
+    assert np.isfinite(out).all()
+    assert rel(out, d['out_wav']) <= FP8_WAV_TOL
+    assert rel(mask, d['mask']) <= FP8_MASK_TOL
+    assert rel(out, outs['bf16'][0]) <= FP8_VS_BF16_TOL
+    assert not np.array_equal(out, outs['bf16'][0])       # the MX path really ran
+
+
+@pytest.mark.parametrize('dtype', ['f32', 'bf16', 'fp8'])
 def test_ragged_batch_equals_single_calls(dtype):
     net, m, conf = build('v2E_2125', dtype)
     from aec_amd import synth
@@ -129,7 +155,7 @@ def test_f32_long_utterance_against_oracle():
     assert rel(spec[0].cpu().numpy(), r['out_spec']) <= F32_TOL
 
 
-@pytest.mark.parametrize('dtype', ['f32', 'bf16'])
+@pytest.mark.parametrize('dtype', ['f32', 'bf16', 'fp8'])
 def test_streaming_equals_batch(dtype):
     """aec_crn_stream_step (hipGraph-replayed per-frame loop) reproduces the
     batch forward hop by hop, with per-stream reset mid-run.  The GEMMs, LSTM
@@ -161,7 +187,7 @@ def test_streaming_equals_batch(dtype):
             outs.append(net.stream_step(mic[:, 256 * k:256 * (k + 1)], far[:, 256 * k:256 * (k + 1)]).clone())
     torch.cuda.synchronize()
     got = torch.cat(outs[1:], dim=1)                    # step k emits hop k-1
-    tol = 1e-5 if dtype == 'f32' else 1e-2
+    tol = {'f32': 1e-5, 'bf16': 1e-2, 'fp8': 2e-2}[dtype]
     for b, n in enumerate(lens):
         no = 256 * (n // 256)
         assert rel(got[b, :no].cpu(), ref_out[b, :no].cpu()) <= tol, (dtype, b)

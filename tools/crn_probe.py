@@ -53,7 +53,7 @@ def main():
             d = np.load(os.path.join(GOLD, f'crn_{name}.npz'))
             conf = copy.deepcopy(aec_amd.net_conf)
             conf.update(m['overrides'])
-            for dt in ('f32', 'bf16'):
+            for dt in ('f32', 'bf16', 'fp8'):
                 net = build(m['version'], conf, dt, m['weight_seed'])
                 T = lambda x: torch.as_tensor(x, device='cuda')[None]
                 with torch.no_grad():
