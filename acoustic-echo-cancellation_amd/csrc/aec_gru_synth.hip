@@ -22,6 +22,9 @@
 // sample is the unfused path's (synth_frame, the same OLA expression), so
 // the result is bit-identical to gru_kernel + synthesis_kernel
 // (tests/test_gpu_parity.py::test_fused_synthesis_bit_exact).
+#ifndef AEC_SPEC_LD_NT
+#define AEC_SPEC_LD_NT 0   // E-spectrum row loads nt (A/B builds only)
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -319,8 +322,15 @@ __global__ __launch_bounds__(kFusedThreads, 1) void gru_synth_kernel(GruArgs p, 
 #pragma unroll
             for (int m = 0; m < 8; ++m) {
                 const int kk = lb + 16 * m;
+#if AEC_SPEC_LD_NT
+                typedef float f2v __attribute__((ext_vector_type(2)));
+                const f2v av = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(row + kk));
+                const f2v cv = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(row + ((256 - kk) & 255)));
+                const float2 a = make_float2(av.x, av.y), c2 = make_float2(cv.x, cv.y);
+#else
                 const float2 a = row[kk];
                 const float2 c2 = row[(256 - kk) & 255];
+#endif
                 xa[m] = kk == 0 ? make_float2(a.x, 0.f) : a;
                 xb[m] = kk == 0 ? make_float2(a.y, 0.f) : c2;
             }

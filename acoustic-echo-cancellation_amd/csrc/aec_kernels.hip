@@ -26,6 +26,11 @@
 //   out      [B][ld_out]          caller-owned, 256*(N_b/256) samples per row
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
+
+#ifndef AEC_SPEC_ST_NT
+#define AEC_SPEC_ST_NT 0   // E-spectrum stores nt (A/B builds only)
+#endif
 
 #include "aec_fft.h"
 #include "aec_frame.h"
@@ -40,8 +45,8 @@ namespace aec {
 // scalar c = mean/std (unbiased) is finished by every consumer from the
 // kMomChunks partials in a fixed order (deterministic, no atomics).
 // --------------------------------------------------------------------------
-template <int U>
-__global__ __launch_bounds__(256) void moments_kernel(const float* __restrict__ mic,
+template <int U, int NT, bool NTL>
+__global__ __launch_bounds__(NT) void moments_kernel(const float* __restrict__ mic,
                                                       const float* __restrict__ ref,
                                                       const float* __restrict__ near, int64_t ld,
                                                       const int64_t* __restrict__ lens,
@@ -68,17 +73,25 @@ __global__ __launch_bounds__(256) void moments_kernel(const float* __restrict__ 
             const float4* x4 = reinterpret_cast<const float4*>(x);
             const int64_t end4 = hi / 4;
             int64_t i4 = lo / 4 + tid;
-            for (; i4 + 256 * (U - 1) < end4; i4 += 256 * U) {
+            for (; i4 + NT * (U - 1) < end4; i4 += NT * U) {
                 float4 v[U];
 #pragma unroll
-                for (int u = 0; u < U; ++u) v[u] = x4[i4 + 256 * u];
+                for (int u = 0; u < U; ++u) {
+                    if constexpr (NTL) {
+                        typedef float f4v __attribute__((ext_vector_type(4)));
+                        const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(x4 + i4 + NT * u));
+                        v[u] = make_float4(t.x, t.y, t.z, t.w);
+                    } else {
+                        v[u] = x4[i4 + NT * u];
+                    }
+                }
 #pragma unroll
                 for (int u = 0; u < U; ++u) acc4(v[u]);
             }
-            for (; i4 < end4; i4 += 256) acc4(x4[i4]);
+            for (; i4 < end4; i4 += NT) acc4(x4[i4]);
             i = end4 * 4 + tid;
         }
-        for (; i < hi; i += 256) {
+        for (; i < hi; i += NT) {
             const double a = x[i];
             s1 += a;
             s2 += a * a;
@@ -89,15 +102,24 @@ __global__ __launch_bounds__(256) void moments_kernel(const float* __restrict__ 
         s1 += __shfl_xor(s1, o);
         s2 += __shfl_xor(s2, o);
     }
-    __shared__ double r1[4], r2[4];
+    constexpr int W = NT / 64;
+    __shared__ double r1[W], r2[W];
     if ((tid & 63) == 0) {
         r1[tid >> 6] = s1;
         r2[tid >> 6] = s2;
     }
     __syncthreads();
-    if (tid == 0)
-        mom[((int64_t)b * 3 + s) * kMomChunks + ch] =
-            make_double2((r1[0] + r1[1]) + (r1[2] + r1[3]), (r2[0] + r2[1]) + (r2[2] + r2[3]));
+    if (tid == 0) {
+        // pairwise over the block's waves in a fixed order
+        double t1[W], t2[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) { t1[w] = r1[w]; t2[w] = r2[w]; }
+#pragma unroll
+        for (int st = 1; st < W; st <<= 1)        // (r0 + r1) + (r2 + r3) at W = 4
+#pragma unroll
+            for (int w = 0; w + st < W; w += 2 * st) { t1[w] += t1[w + st]; t2[w] += t2[w + st]; }
+        mom[((int64_t)b * 3 + s) * kMomChunks + ch] = make_double2(t1[0], t2[0]);
+    }
 }
 
 // c = mean(x)/std(x, unbiased) from the partials (ERB.py:254-256).
@@ -388,7 +410,15 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
                 for (int i = 0; i < kFPB; ++i) {
                     const float2 e = st.step(dd[i], rr[i], mu, beta, delta);
                     reinterpret_cast<float2*>(eb + i * kERow)[k] = e;
-                    if (t0 + i < T) spec[(t0 + i) * kSpecRow + k] = e;
+                    if (t0 + i < T) {
+#if AEC_SPEC_ST_NT
+                        typedef float f2v __attribute__((ext_vector_type(2)));
+                        f2v ev; ev.x = e.x; ev.y = e.y;
+                        __builtin_nontemporal_store(ev, reinterpret_cast<f2v*>(spec + (t0 + i) * kSpecRow + k));
+#else
+                        spec[(t0 + i) * kSpecRow + k] = e;
+#endif
+                    }
                 }
             }
             if (erb_role == 2 && c >= 2 && !(p.mode & 4)) mic_erb_pass(c - 2);
@@ -671,10 +701,17 @@ hipError_t launch_mic_erb(const float2* spec, float* feats, const int64_t* lens,
 hipError_t launch_moments(const float* mic, const float* ref, const float* near, int64_t ld,
                           const int64_t* lens, double2* mom, int b0, int nb, int nsig, hipStream_t st) {
     if (nb <= 0) return hipSuccess;
-    // 4 float4 in flight per thread; 2 and 8 measured the same (the kernel runs at
-    // ~4.7 TB/s either way)
-    hipLaunchKernelGGL(moments_kernel<4>, dim3(kMomChunks, nsig, nb), dim3(256), 0, st, mic, ref, near, ld, lens, mom,
-                       b0);
+    // 4 float4 in flight per thread, nontemporal loads (each sample is read once
+    // here; the analysis pass re-reads it from HBM anyway).  256 x 10 s x 3
+    // signals: 0.104 ms (4.7 TB/s) with default-policy loads, 0.080 ms
+    // (6.1 TB/s) with nt; 8 float4 / 512-thread / 1024-thread blocks measured
+    // 0.085-0.091 ms.  AEC_MOM_CFG=1 selects the default-policy loads (A/B).
+    static const int cfg = [] { const char* e = std::getenv("AEC_MOM_CFG"); return e ? std::atoi(e) : 0; }();
+    const dim3 g(kMomChunks, nsig, nb);
+    if (cfg == 1)
+        hipLaunchKernelGGL((moments_kernel<4, 256, false>), g, dim3(256), 0, st, mic, ref, near, ld, lens, mom, b0);
+    else
+        hipLaunchKernelGGL((moments_kernel<4, 256, true>), g, dim3(256), 0, st, mic, ref, near, ld, lens, mom, b0);
     return hipGetLastError();
 }
 

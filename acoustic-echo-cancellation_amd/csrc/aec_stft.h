@@ -59,6 +59,9 @@ constexpr int kWavePf = kWaveHops;                          // float4 per lane p
 // out-of-range), so the reference's zero padding needs no branches;
 // wave_commit re-applies the exact [0, n) mask.  Rows that are not 16-B
 // aligned take dword loads (wave-uniform branch).
+#ifndef AEC_LOAD_CPOL
+#define AEC_LOAD_CPOL 2   // sample loads are nt (each hop is read once per transform); 0 = default policy (A/B)
+#endif
 __device__ __forceinline__ void wave_prefetch(float4 (&pf)[kWavePf], const float* __restrict__ row, int n,
                                               int t, int lane, bool aligned) {
     // the row / length are wave-uniform (one item per wave); make that provable so
@@ -73,7 +76,7 @@ __device__ __forceinline__ void wave_prefetch(float4 (&pf)[kWavePf], const float
     if (__builtin_expect(aligned, 1)) {
 #pragma unroll
         for (int u = 0; u < kWavePf; ++u) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, base + u * kHop * 4, 0, 0);
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, base + u * kHop * 4, 0, AEC_LOAD_CPOL);
             pf[u] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
                                 __uint_as_float(v[3]));
         }
@@ -81,10 +84,10 @@ __device__ __forceinline__ void wave_prefetch(float4 (&pf)[kWavePf], const float
 #pragma unroll
         for (int u = 0; u < kWavePf; ++u) {
             const int o = base + u * kHop * 4;
-            pf[u] = make_float4(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + 0, 0, 0)),
-                                __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + 4, 0, 0)),
-                                __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + 8, 0, 0)),
-                                __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + 12, 0, 0)));
+            pf[u] = make_float4(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + 0, 0, AEC_LOAD_CPOL)),
+                                __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + 4, 0, AEC_LOAD_CPOL)),
+                                __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + 8, 0, AEC_LOAD_CPOL)),
+                                __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + 12, 0, AEC_LOAD_CPOL)));
         }
     }
 }
