@@ -219,3 +219,33 @@ def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatc
     for k in f0:
         for i, n in enumerate(lens):
             assert np.array_equal(f0[k][i, :n // 256 + 1], f1[k][i, :n // 256 + 1]), (k, i)
+
+
+def test_max_batch_4096_streams_matches_single_calls(nlms_net, golden_erb):
+    """BASELINE C4/C5's 4,096-stream sweep point at 10 s: > 4 GiB spectrum and
+    input buffers (64-bit row / spectrum offsets), ragged lengths.  Sampled
+    streams of the 4,096-stream call must be bit-identical to the same
+    streams run alone (batch=1 semantics, Tester.test scripts/test.py:137-169);
+    the single-stream path is itself held to the oracle above."""
+    B, N = 4096, 160000
+    dev = 'cuda:0'
+    g = torch.Generator(device=dev).manual_seed(4096)
+    ref = 0.1 * torch.randn(B, N, device=dev, generator=g)
+    near = 0.05 * torch.randn(B, N, device=dev, generator=g)
+    mic = 0.5 * torch.roll(ref, 128, dims=1) + near + 1e-3 * torch.randn(B, N, device=dev, generator=g)
+    lens = torch.randint(N // 2, N + 1, (B,), generator=torch.Generator().manual_seed(7)).tolist()
+    lens[-1] = N
+    lens[0] = 300
+    erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
+    with torch.no_grad():
+        out, loss = nlms_net.forward_ragged(mic, ref, near, erb_t, lens)
+        torch.cuda.synchronize()
+        assert torch.isfinite(out).all()
+        for i in (0, 1, 2047, 3333, B - 1):
+            o1, l1 = nlms_net.forward_ragged(mic[i:i + 1], ref[i:i + 1], near[i:i + 1], erb_t, lens[i:i + 1])
+            ol = 256 * (lens[i] // 256)
+            assert torch.equal(out[i, :ol], o1[0, :ol]), i
+            assert not out[i, ol:].any()
+            assert abs(float(loss[i]) - float(l1[0])) <= 1e-6 * max(1.0, abs(float(l1[0]))), i
+    del mic, ref, near, out
+    torch.cuda.empty_cache()
