@@ -116,7 +116,7 @@ __device__ __forceinline__ void wave_fence() {
 //      group read 16 consecutive entries, conflict-free; a gather
 //      tw[(lb*k1) & 255] would be 2-4-way conflicted for k1 = 4, 8, 12).
 template <bool INV>
-__device__ __forceinline__ void fft256(float2 (&v)[16], int lb, float* scr, const float2* twT) {
+__device__ __forceinline__ void fft256_scalar(float2 (&v)[16], int lb, float* scr, const float2* twT) {
     dft16<INV>(v);
     float2* s2 = reinterpret_cast<float2*>(scr);
     // all 15 twiddle reads first: interleaved with the transpose writes (which
@@ -146,6 +146,123 @@ __device__ __forceinline__ void fft256(float2 (&v)[16], int lb, float* scr, cons
     }
     wave_fence();
     dft16<INV>(v);
+}
+
+// ---------------------------------------------------------------------------
+// Packed-FP32 FFT core (AEC_FFT_PK, default).  A complex value is one
+// 64-bit VGPR pair, so every complex add / sub is ONE v_pk_add_f32 and every
+// complex rotation is one v_pk_mul_f32 + one v_pk_fma_f32; the lane swaps and
+// sign flips of the radix-4 butterfly (t1 -/+ i t3) and of the twiddle
+// product ride on the VOP3P op_sel / neg modifiers instead of extra VALU.
+// fft256: 381 -> 231 VALU per call (gfx950 ISA count); the NLMS analysis
+// kernel 3531 -> 3045 static VALU, 1.5-2 % faster (the transforms share the
+// SIMDs with LDS-latency-bound work, so the issue savings only partly show).
+// The arithmetic is the scalar core's up to fma contraction (~1 ulp per stage).
+// ---------------------------------------------------------------------------
+typedef float pf2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ pf2 pswap(pf2 a) { return __builtin_shufflevector(a, a, 1, 0); }
+
+// t1 - i t3 = (t1.x + t3.y, t1.y - t3.x)
+__device__ __forceinline__ pf2 p_sub_i(pf2 t1, pf2 t3) {
+    pf2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(t1), "v"(t3));
+    return r;
+}
+// t1 + i t3 = (t1.x - t3.y, t1.y + t3.x)
+__device__ __forceinline__ pf2 p_add_i(pf2 t1, pf2 t3) {
+    pf2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(t1), "v"(t3));
+    return r;
+}
+// x * t (CONJ: x * conj(t)) for a twiddle t loaded as a pair
+template <bool CONJ>
+__device__ __forceinline__ pf2 p_cmul(pf2 x, pf2 t) {
+    pf2 m, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(m) : "v"(x), "v"(t));      // (x.x t.x, x.y t.x)
+    if (!CONJ)   // (x.x t.x - x.y t.y, x.y t.x + x.x t.y)
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[0,1,0]"
+            : "=v"(r) : "v"(x), "v"(t), "v"(m));
+    else         // (x.x t.x + x.y t.y, x.y t.x - x.x t.y)
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]"
+            : "=v"(r) : "v"(x), "v"(t), "v"(m));
+    return r;
+}
+// a * (c + i s), c and s compile-time
+__device__ __forceinline__ pf2 p_rot(pf2 a, float c, float sn) {
+    return __builtin_elementwise_fma(pswap(a), pf2{-sn, sn}, a * pf2{c, c});
+}
+
+template <bool INV>
+__device__ __forceinline__ void p_dft4(pf2& a0, pf2& a1, pf2& a2, pf2& a3) {
+    const pf2 t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3, t3 = a1 - a3;
+    a0 = t0 + t2;
+    a2 = t0 - t2;
+    if (!INV) { a1 = p_sub_i(t1, t3); a3 = p_add_i(t1, t3); }
+    else      { a1 = p_add_i(t1, t3); a3 = p_sub_i(t1, t3); }
+}
+
+template <bool INV>
+__device__ __forceinline__ void p_dft16(pf2 (&v)[16]) {
+    constexpr float C1 = 0.92387953251128674f;
+    constexpr float S1 = 0.38268343236508978f;
+    constexpr float R2 = 0.70710678118654752f;
+    constexpr float sg = INV ? 1.f : -1.f;
+#pragma unroll
+    for (int a0 = 0; a0 < 4; ++a0) p_dft4<INV>(v[a0], v[a0 + 4], v[a0 + 8], v[a0 + 12]);
+    v[1 + 4] = p_rot(v[1 + 4], C1, sg * S1);
+    v[1 + 8] = p_rot(v[1 + 8], R2, sg * R2);
+    v[1 + 12] = p_rot(v[1 + 12], S1, sg * C1);
+    v[2 + 4] = p_rot(v[2 + 4], R2, sg * R2);
+    v[2 + 8] = INV ? p_add_i(pf2{0.f, 0.f}, v[2 + 8]) : p_sub_i(pf2{0.f, 0.f}, v[2 + 8]);   // * (+-i)
+    v[2 + 12] = p_rot(v[2 + 12], -R2, sg * R2);
+    v[3 + 4] = p_rot(v[3 + 4], S1, sg * C1);
+    v[3 + 8] = p_rot(v[3 + 8], -R2, sg * R2);
+    v[3 + 12] = p_rot(v[3 + 12], -C1, -sg * S1);
+#pragma unroll
+    for (int k0 = 0; k0 < 4; ++k0) p_dft4<INV>(v[4 * k0], v[4 * k0 + 1], v[4 * k0 + 2], v[4 * k0 + 3]);
+}
+
+template <bool INV>
+__device__ __forceinline__ void fft256_packed(float2 (&v)[16], int lb, float* scr, const float2* twT) {
+    pf2 u[16];
+#pragma unroll
+    for (int a = 0; a < 16; ++a) u[a] = pf2{v[a].x, v[a].y};
+    p_dft16<INV>(u);
+    pf2* s2 = reinterpret_cast<pf2*>(scr);
+    const pf2* tw = reinterpret_cast<const pf2*>(twT);
+    pf2 w[15];
+    static_for<0, 15>([&](auto ii) {
+        constexpr int i = decltype(ii)::value;
+        w[i] = tw[(i + 1) * 16 + lb];
+    });
+    s2[lb] = u[kP(0)];
+    static_for<0, 15>([&](auto ii) {
+        constexpr int i = decltype(ii)::value;
+        s2[(i + 1) * 18 + lb] = p_cmul<INV>(u[kP(i + 1)], w[i]);
+    });
+    wave_fence();
+    const pf2* sr = reinterpret_cast<const pf2*>(scr) + lb * 18;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) u[q] = sr[q];
+    wave_fence();
+    p_dft16<INV>(u);
+#pragma unroll
+    for (int a = 0; a < 16; ++a) v[a] = make_float2(u[a].x, u[a].y);
+}
+
+#ifndef AEC_FFT_PK
+#define AEC_FFT_PK 1
+#endif
+template <bool INV>
+__device__ __forceinline__ void fft256(float2 (&v)[16], int lb, float* scr, const float2* twT) {
+    // forward transforms packed, inverse scalar: the packed inverse made the
+    // fused GRU + synthesis kernel 4 % slower (its recurrence wave shares the
+    // SIMDs with the synthesis waves), and every synthesis path must run the
+    // same inverse arithmetic (the fused / separate / streaming kernels are
+    // tested bit-identical)
+    if constexpr (AEC_FFT_PK && !INV) fft256_packed<INV>(v, lb, scr, twT);
+    else fft256_scalar<INV>(v, lb, scr, twT);
 }
 
 // Cross-lane partner within each 16-lane row: out[lb] = x[(16 - lb) & 15]
