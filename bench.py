@@ -194,6 +194,22 @@ def erle_check(run_gpu, run_ref, n, streams=2):
                 scene='far-end single talk (near = 0), 10 s, synthetic RIR echo')
 
 
+def _init_dist(torch, dist, world, local):
+    """One process per GPU over RCCL (backend "nccl").  AEC_BENCH_BACKEND=gloo
+    rehearses the multi-rank flow (barriers, max-over-ranks, rank-0 line) with
+    several ranks sharing the GPUs of a smaller box; never used for numbers."""
+    if world > 1:
+        backend = os.environ.get('AEC_BENCH_BACKEND', 'nccl')
+        if backend == 'gloo':
+            local = local % torch.cuda.device_count()
+        torch.cuda.set_device(local)
+        if backend == 'gloo':
+            dist.init_process_group('gloo')
+        else:
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    return local
+
+
 def main_crn(args):
     """BASELINE config 3: the DCCRN post-filter (bf16 MFMA), B streams x 10 s."""
     import numpy as np
@@ -202,9 +218,7 @@ def main_crn(args):
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    local = _init_dist(torch, dist, world, local)
     dev = torch.device('cuda', local)
     import aec_amd
     from aec_amd import shard, synth
@@ -317,9 +331,7 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    local = _init_dist(torch, dist, world, local)
     dev = torch.device('cuda', local)
     import aec_amd
     from aec_amd import shard, synth
