@@ -11,6 +11,6 @@ for v in base alt base alt; do
   python - "$v" "$R/gpurun_out/lib_ab_${PIPE}_$v.log" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
-print(sys.argv[1], 'ms/step', d['ms_per_step'], d.get('kernel_ms_per_step'))
+print(sys.argv[1], 'ms/step', d['ms_per_step'], d.get('kernel_ms_per_step') or d.get('stage_ms_per_step'))
 PY
 done
