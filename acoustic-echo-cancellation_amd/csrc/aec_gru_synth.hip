@@ -22,6 +22,9 @@
 // sample is the unfused path's (synth_frame, the same OLA expression), so
 // the result is bit-identical to gru_kernel + synthesis_kernel
 // (tests/test_gpu_parity.py::test_fused_synthesis_bit_exact).
+#ifndef AEC_OUT_NT
+#define AEC_OUT_NT 1   // waveform stores nt: written once, never re-read on the device (fused kernel -1 %)
+#endif
 #ifndef AEC_SPEC_LD_NT
 #define AEC_SPEC_LD_NT 0   // E-spectrum row loads nt (A/B builds only)
 #endif
@@ -284,7 +287,13 @@ __global__ __launch_bounds__(kFusedThreads, 1) void gru_synth_kernel(GruArgs p, 
                         o.y = (a.y + cv.y) * cf.y + 1e-9f;
                         o.z = (a.z + cv.z) * cf.z + 1e-9f;
                         o.w = (a.w + cv.w) * cf.w + 1e-9f;
+#if AEC_OUT_NT
+                        typedef float f4v __attribute__((ext_vector_type(4)));
+                        __builtin_nontemporal_store(f4v{o.x, o.y, o.z, o.w},
+                                                    reinterpret_cast<f4v*>(orow + (j0 + i) * kHop + r));
+#else
                         *reinterpret_cast<float4*>(orow + (j0 + i) * kHop + r) = o;
+#endif
                     }
                 } else {
                     for (int e = hh; e < kCH * kHop; e += kHeadLanes) {
