@@ -25,10 +25,13 @@ error: version-2/3 superblocks, v2 object headers, dense link storage and
 v4 chunk indexes. The writer emits the same structures, with chunked
 datasets by default as h5py's `chunks=True` does.
 
-Parity is unpinned against libhdf5, which is not in this image. The format
-constants and structure follow the specification. The reader is tested on
-files made by the writer, including multi-level group B-trees (over 256
-utterances) and multi-chunk datasets.
+libhdf5 itself is not in this image. The reader is checked against files
+libhdf5 wrote (tests/golden/foreign/, tests/test_h5lite.py): a MATLAB 7.3
+file with a 512-byte user block, checked value for value against scipy's
+reader of the same variable in MATLAB v5 format, and the HDF5 example files
+PyTables ships (chunked, big-endian, float16/32/64).  Files from its own
+writer cover multi-level group B-trees (over 256 utterances) and
+multi-chunk datasets.
 """
 from __future__ import annotations
 
@@ -104,6 +107,8 @@ class Dataset:
         rank = len(self.shape)
         cshape = cdims[:rank]
         out = np.zeros(self.shape if rank else (1,), dtype=np.uint8 if es == 1 else np.dtype(f'V{es}'))
+        if btree == UNDEF:                                 # no chunk written yet: all fill value (0)
+            return out.tobytes()
         for offs, size, mask, addr in self._f._chunk_records(btree, rank):
             raw = self._f._buf[addr:addr + size]
             raw = _unfilter(raw, self._filters, mask, es)
@@ -161,17 +166,26 @@ class File(Group):
         size = os.fstat(self._fh.fileno()).st_size
         if size == 0:
             raise H5Error(f'{path}: empty file')
-        self._buf = mmap.mmap(self._fh.fileno(), 0, access=mmap.ACCESS_READ)
+        self._map = mmap.mmap(self._fh.fileno(), 0, access=mmap.ACCESS_READ)
+        self._buf = memoryview(self._map)
         base = self._find_superblock()
-        self._parse_superblock(base)
+        # Every address in the file is relative to the base address, the
+        # superblock's own position (spec §II.A "Base Address"): a file with a
+        # user block (superblock at 512, 1024, ...) is read through a view that
+        # starts at the superblock
+        self._buf = self._buf[base:]
+        self._parse_superblock(0)
         root_links = self._group_links(self._root_addr)
         super().__init__(self, '/', root_links)
 
     # -- context manager / close
     def close(self):
         if getattr(self, '_buf', None) is not None:
-            self._buf.close()
+            self._buf.release()
             self._buf = None
+        if getattr(self, '_map', None) is not None:
+            self._map.close()
+            self._map = None
             self._fh.close()
 
     def __enter__(self):
@@ -193,7 +207,7 @@ class File(Group):
     def _find_superblock(self) -> int:
         off = 0
         while off + 8 <= len(self._buf):
-            if self._buf[off:off + 8] == SIGNATURE:
+            if bytes(self._buf[off:off + 8]) == SIGNATURE:
                 return off
             off = 512 if off == 0 else off * 2
         raise H5Error('not an HDF5 file (no superblock signature)')
@@ -208,8 +222,8 @@ class File(Group):
         if self._so != 8 or self._sl != 8:
             raise H5Error('only 8-byte offsets / lengths are supported')
         p = base + 24 + (4 if ver == 1 else 0)            # versions, sizes, K values, flags (+ v1 K)
-        if base != 0 or self._u(p, 8) != 0:
-            raise H5Error('files with a user block / non-zero base address are not supported')
+        # the stored base address is 0 (or the superblock's absolute offset, which
+        # the view already applies): either way addresses count from the superblock
         p += 8 * 4                                        # base, free-space, EOF, driver
         # root group symbol table entry: name offset, object header address, cache type, scratch
         self._root_addr = self._u(p + 8, 8)

@@ -153,9 +153,12 @@ class Little_net(nn.Module):
 
     def forward_ragged(self, mic, ref, near, erb, lengths):
         """Batched call with per-row true lengths (rows zero-padded to a common
-        width).  Returns out [B, 256*(max(lengths)//256)] (row b valid up to
-        256*(lengths[b]//256), zero beyond) and per-row losses [B] (None when
-        ``near`` is None)."""
+        width).  ``lengths`` is [B] (one length per row) or [B, 3] (mic, ref,
+        near lengths of each row: every signal normalised over and padded
+        beyond its own length, as test.py:139 feeds the reference; the three
+        must share the frame count N//256 + 1).  Returns out
+        [B, 256*(max(mic lengths)//256)] (row b valid up to 256*(n_mic//256),
+        zero beyond) and per-row losses [B] (None when ``near`` is None)."""
         if torch.is_grad_enabled() and (mic.requires_grad or any(p.requires_grad for p in self._params())
                                         and self.training):
             raise NotImplementedError('Little_net (gfx950) is inference-only: call it under torch.no_grad() '
@@ -175,12 +178,19 @@ class Little_net(nn.Module):
         near = near.contiguous().float() if near is not None else None
         B, L = mic.shape
         lengths = np.asarray(lengths, dtype=np.int64)
-        if lengths.shape != (B,) or (lengths < 1).any() or (lengths > L).any():
-            raise ValueError('lengths must be [B] with 1 <= length <= N')
+        if lengths.shape not in ((B,), (B, 3)) or (lengths < 1).any() or (lengths > L).any():
+            raise ValueError('lengths must be [B] or [B, 3] with 1 <= length <= N')
+        nmic = lengths if lengths.ndim == 1 else lengths[:, 0]
+        if lengths.ndim == 2:
+            cols = [0, 1, 2] if near is not None else [0, 1]
+            if (lengths[:, cols] // HOP != (nmic // HOP)[:, None]).any():
+                # ERB.py:287-290 / 318-323 combine the signals frame by frame
+                raise RuntimeError('mic, ref and near must have the same frame count N//256 + 1 '
+                                   '(the reference raises on the shape mismatch)')
         h, idx = self._handle(dev)
         self._sync_erb(h, idx, erb)
-        lout = HOP * (int(lengths.max()) // HOP)
-        out = torch.zeros(B, lout, device=dev, dtype=torch.float32) if (lengths != lengths.max()).any() \
+        lout = HOP * (int(nmic.max()) // HOP)
+        out = torch.zeros(B, lout, device=dev, dtype=torch.float32) if (nmic != nmic.max()).any() \
             else torch.empty(B, lout, device=dev, dtype=torch.float32)
         loss = torch.empty(B, device=dev, dtype=torch.float32) if near is not None else None
         stream = torch.cuda.current_stream(dev).cuda_stream

@@ -16,6 +16,7 @@ the CPU tests.
 from __future__ import annotations
 
 import heapq
+import os
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -49,9 +50,45 @@ def balanced_shards(lengths: Sequence[int], world: int) -> List[List[int]]:
     return [sorted(s) for s in shards]
 
 
+_BOUND: Optional[int] = None     # this rank's GPU, set by bind_device()
+
+
+def local_rank() -> int:
+    """This process's GPU index under torchrun (LOCAL_RANK), 0 otherwise."""
+    return int(os.environ.get('LOCAL_RANK', '0'))
+
+
+def bind_device(local: Optional[int] = None) -> int:
+    """Make GPU `local` (default LOCAL_RANK) this rank's current device and the
+    device of every collective below.  RCCL needs one GPU per rank: a rank
+    left on cuda:0 duplicates rank 0's GPU and the first collective fails or
+    hangs."""
+    global _BOUND
+    local = local_rank() if local is None else int(local)
+    torch.cuda.set_device(local)
+    _BOUND = local
+    return local
+
+
+def init_process_group(backend: Optional[str] = None) -> None:
+    """Join the torchrun process group, one GPU per rank: bind LOCAL_RANK's GPU
+    first and hand it to RCCL as the group's device (`device_id`), as
+    bench.py does; gloo (CPU) when no GPU is visible."""
+    if dist.is_initialized():
+        return
+    if backend is None:
+        backend = 'nccl' if torch.cuda.is_available() else 'gloo'
+    if backend == 'nccl':
+        local = bind_device()
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    else:
+        dist.init_process_group(backend)
+
+
 def _dev():
+    """Device of the collectives: the rank's bound GPU under RCCL, CPU under gloo."""
     if dist.get_backend() == 'nccl':
-        return torch.device('cuda', torch.cuda.current_device())
+        return torch.device('cuda', _BOUND if _BOUND is not None else local_rank())
     return torch.device('cpu')
 
 

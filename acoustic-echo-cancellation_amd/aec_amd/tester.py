@@ -28,7 +28,7 @@ writes every file.
 Extra flags (all optional):
 - `--nlms` puts the FD-NLMS stage in front of the post-filter;
 - `--streams` sets the utterances per GPU call;
-- `--device` picks the GPU;
+- `--device` picks the GPU (default: LOCAL_RANK, the rank's bound GPU);
 - `--gather` writes every file on rank 0 (waveforms gathered over RCCL).
 """
 from __future__ import annotations
@@ -46,8 +46,9 @@ import numpy as np
 from . import h5lite, shard, wavio
 from .configs import erb_conf, nlms_conf, speech_conf
 
-# enhance(mic, ref, near, lengths) -> list of 1-D float32 outputs, one per row
-Enhancer = Callable[[np.ndarray, np.ndarray, np.ndarray, Sequence[int]], List[np.ndarray]]
+# enhance(mic, ref, near, lengths[B][3] = (mic, ref, near) lengths) -> list of
+# 1-D float32 outputs, one per row, each 256*(n_mic//256) samples
+Enhancer = Callable[[np.ndarray, np.ndarray, np.ndarray, np.ndarray], List[np.ndarray]]
 
 
 def get_logger(name, log_file=False):
@@ -81,15 +82,13 @@ def build_parser():
 
 
 def _dist():
-    """(rank, world); joins the torchrun process group when one is configured."""
+    """(rank, world); joins the torchrun process group when one is configured,
+    with this rank bound to its LOCAL_RANK GPU (shard.init_process_group)."""
     world = int(os.environ.get('WORLD_SIZE', '1'))
     if world <= 1:
         return 0, 1
-    import torch
     import torch.distributed as dist
-    if not dist.is_initialized():
-        backend = 'nccl' if torch.cuda.is_available() else 'gloo'
-        dist.init_process_group(backend)
+    shard.init_process_group()
     return dist.get_rank(), dist.get_world_size()
 
 
@@ -113,7 +112,7 @@ class Tester(object):
         from .checkpoint import CheckPoint
         from .erb import EquivalentRectangularBandwidth
         from .little_net import Little_net
-        local = self.args.device if self.args.device is not None else int(os.environ.get('LOCAL_RANK', rank))
+        local = self.args.device if self.args.device is not None else shard.local_rank()
         device = torch.device('cuda', local)
         net = Little_net(speech_conf, erb_conf['total_erb_bands'], nlms=nlms_conf if self.args.nlms else None)
         logger.info('backbone summary:\n{}'.format(net))
@@ -129,11 +128,12 @@ class Tester(object):
         erb = torch.tensor(ERB.filters, dtype=torch.float32, device=device)
 
         def enhance(mic, ref, near, lengths):
+            lengths = np.asarray(lengths, np.int64).reshape(len(mic), 3)
             with torch.no_grad():
                 M, R, N = (torch.from_numpy(a).to(device, non_blocking=True) for a in (mic, ref, near))
-                out, _ = net.forward_ragged(M, R, N, erb, list(lengths))
+                out, _ = net.forward_ragged(M, R, N, erb, lengths)
                 out = out.cpu().numpy()
-            return [out[b, :256 * (int(n) // 256)] for b, n in enumerate(lengths)]
+            return [out[b, :256 * (int(n) // 256)] for b, n in enumerate(lengths[:, 0])]
 
         return enhance
 
@@ -162,21 +162,20 @@ class Tester(object):
             for s in range(0, len(mine), max(1, self.args.streams)):
                 ks = mine[s:s + self.args.streams]
                 egs = [self._load(reader, k) for k in ks]
-                L = max(e['n_samples'] for e in egs)
-                rows = {key: np.zeros((len(ks), L), np.float32) for key in ('nearend_mic', 'farend_speech',
-                                                                           'nearend_speech')}
+                sig = ('nearend_mic', 'farend_speech', 'nearend_speech')     # mic, ref, near (test.py:157)
+                lens = np.array([[len(e[key]) for key in sig] for e in egs], np.int64)
+                rows = {key: np.zeros((len(ks), int(lens.max())), np.float32) for key in sig}
                 for b, e in enumerate(egs):
-                    for key in rows:
-                        rows[key][b, :e['n_samples']] = e[key]
-                outs = enhance(rows['nearend_mic'], rows['farend_speech'], rows['nearend_speech'],
-                               [e['n_samples'] for e in egs])
+                    for key in sig:
+                        rows[key][b, :len(e[key])] = e[key]
+                outs = enhance(rows['nearend_mic'], rows['farend_speech'], rows['nearend_speech'], lens)
                 for k, e, out in zip(ks, egs, outs):
                     if gather:
                         local[k] = out
                     else:
                         futs.append(pool.submit(self._write, est_subdir, k, out, e))
                     n_utt += 1
-                    n_frames += e['n_samples'] // 256 + 1
+                    n_frames += len(e['nearend_mic']) // 256 + 1
             if gather:
                 merged = shard.gather_to_root(local)
                 local = {}
@@ -196,17 +195,11 @@ class Tester(object):
 
     @staticmethod
     def _load(reader, k):
-        """ValidateDataset.__getitem__ + collate_fn at batch 1 (test.py:25-67): every
-        signal is zero-padded to len(nearend_speech) (np.pad raises when longer)."""
-        e = h5lite.read_utterance(reader, k)
-        n = e['n_samples']
-        for key in h5lite.SIGNALS:
-            if len(e[key]) > n:
-                raise ValueError(f'utterance {k}: {key} is longer than nearend_speech '
-                                 '(the reference collate_fn cannot pad it either)')
-            if len(e[key]) < n:
-                e[key] = np.pad(e[key], (0, n - len(e[key])), 'constant')
-        return e
+        """ValidateDataset.__getitem__ (test.py:25-33) as the test loader delivers
+        it: DataLoader(batch_size=1) with the DEFAULT collate (test.py:139; the
+        padding collate_fn at :38-67 is not passed), so every signal keeps its
+        stored length, and so do the WAVs written from it (:165-169)."""
+        return h5lite.read_utterance(reader, k)
 
     def _write(self, est_subdir, k, out, e):
         sr = self.sample_rate

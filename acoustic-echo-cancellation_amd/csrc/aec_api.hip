@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/aec_hip.h"
+#include "aec_device.h"
 #include "aec_launch.h"
 #include "aec_tables.h"
 
@@ -202,12 +203,16 @@ struct aec_handle {
     int sub_max = 1;
     hipStream_t sst[kMaxSub] = {};
     hipEvent_t ev_start = nullptr, ev_ana[kMaxSub] = {}, ev_done[kMaxSub] = {};
-    int64_t* d_len = nullptr;    // [B]
+    int64_t* d_len = nullptr;    // [B] mic length: sets the frame count and output length
+    int32_t* d_slen = nullptr;   // [B][4] per-signal lengths (mic, ref, near, -): normaliser + zero padding
     float* d_feats = nullptr;    // [B][T][96]
     float* d_est = nullptr;      // [B][T][32]
     float* d_dbg = nullptr;      // [2][B][T][32]  (h, mask)
     float2* d_spec = nullptr;    // [B][T][256] NLMS error spectrum (nlms_taps > 0 only)
-    std::vector<int64_t> last_lens;
+    std::vector<int64_t> last_lens;                 // [B][3] of the last call (work lists rebuilt on change)
+    // host staging of the work lists (kept alive while their async copies run)
+    std::vector<WorkItem> h_items, h_sitems;
+    std::vector<int32_t> h_slen;
     int debug = 0;
     int gru_mode = 0;            // AEC_GRU_MODE (timing experiments; results invalid unless 0)
     int nlms_mode = 0;           // AEC_NLMS_MODE (timing experiments; results invalid unless 0)
@@ -256,6 +261,15 @@ static const size_t kWeights32 = 96 * 64 + 96 * 32 + 96 + 96 + 32 * 64 + 32 + 32
         }                                                                                \
     } while (0)
 
+// select the handle's device for the rest of the entry point; the caller's
+// current device is restored on return (aec_device.h)
+#define AEC_ON_DEVICE(h)                                                                  \
+    DeviceGuard dg_((h)->device);                                                         \
+    if (dg_.err != hipSuccess) {                                                          \
+        (h)->err = std::string("hipSetDevice: ") + hipGetErrorString(dg_.err);            \
+        return AEC_ERR_HIP;                                                               \
+    }
+
 static aec_status fail(aec_handle* h, aec_status s, const std::string& m) {
     if (h) h->err = m;
     return s;
@@ -292,7 +306,9 @@ const char* aec_last_error(const aec_handle* h) { return h ? h->err.c_str() : "n
 aec_status aec_set_weights(aec_handle* h, const float* w, size_t n) {
     if (!h) return AEC_ERR_INVALID_ARG;
     if (!w || n != kWeights32) return fail(h, AEC_ERR_INVALID_ARG, "weights blob must hold 12544 floats");
-    HIP_TRY(h, hipSetDevice(h->device));
+    AEC_ON_DEVICE(h);
+    // kernels launched on any stream may still be reading the old blob
+    HIP_TRY(h, hipDeviceSynchronize());
     HIP_TRY(h, hipMemcpy(h->d_w, w, n * sizeof(float), hipMemcpyHostToDevice));
     h->have_w = true;
     return AEC_OK;
@@ -303,7 +319,7 @@ aec_status aec_set_erb(aec_handle* h, const float* erb) {
     if (!erb) return fail(h, AEC_ERR_INVALID_ARG, "erb matrix is null");
     const ErbTables t = build_erb_tables(erb);
     if (!t.ok) return fail(h, AEC_ERR_UNSUPPORTED, std::string("erb matrix: ") + t.why);
-    HIP_TRY(h, hipSetDevice(h->device));
+    AEC_ON_DEVICE(h);
     HIP_TRY(h, hipDeviceSynchronize());   // the previous tables may still be in use
     if (h->d_sched) { HIP_TRY(h, hipFree(h->d_sched)); h->d_sched = nullptr; }
     if (h->d_bintab) { HIP_TRY(h, hipFree(h->d_bintab)); h->d_bintab = nullptr; }
@@ -344,7 +360,8 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
             h->num_cus = cus;
     }
     auto bail = [&](aec_status s) { aec_destroy(h); return s; };
-    if (hipSetDevice(device) != hipSuccess) return bail(AEC_ERR_HIP);
+    DeviceGuard dg(device);
+    if (dg.err != hipSuccess) return bail(AEC_ERR_HIP);
     for (int k = 0; k < aec_handle::kMaxSub; ++k) {
         if (hipStreamCreateWithFlags(&h->sst[k], hipStreamNonBlocking) != hipSuccess) return bail(AEC_ERR_HIP);
         if (hipEventCreateWithFlags(&h->ev_ana[k], hipEventDisableTiming) != hipSuccess) return bail(AEC_ERR_HIP);
@@ -373,14 +390,16 @@ static aec_status ensure_ws(aec_handle* h, int64_t B, int64_t T) {
     const int64_t nT = T > h->ws_T ? T : h->ws_T;
     HIP_TRY(h, hipDeviceSynchronize());
     (void)hipFree(h->d_mom); (void)hipFree(h->d_cvals); (void)hipFree(h->d_len); (void)hipFree(h->d_feats);
-    (void)hipFree(h->d_est); (void)hipFree(h->d_dbg); (void)hipFree(h->d_spec);
+    (void)hipFree(h->d_est); (void)hipFree(h->d_dbg); (void)hipFree(h->d_spec); (void)hipFree(h->d_slen);
     h->d_mom = nullptr; h->d_cvals = nullptr; h->d_len = nullptr; h->d_feats = h->d_est = h->d_dbg = nullptr;
+    h->d_slen = nullptr;
     h->d_spec = nullptr;
     h->ws_B = h->ws_T = 0;
     h->last_lens.clear();
     HIP_TRY(h, hipMalloc(&h->d_mom, nB * 3 * kMomChunks * sizeof(double2)));
     HIP_TRY(h, hipMalloc(&h->d_cvals, nB * 3 * sizeof(float)));
     HIP_TRY(h, hipMalloc(&h->d_len, nB * sizeof(int64_t)));
+    HIP_TRY(h, hipMalloc(&h->d_slen, nB * 4 * sizeof(int32_t)));
     HIP_TRY(h, hipMalloc(&h->d_feats, nB * nT * 96 * sizeof(float)));
     HIP_TRY(h, hipMalloc(&h->d_est, nB * nT * 32 * sizeof(float)));
     HIP_TRY(h, hipMalloc(&h->d_dbg, 2 * nB * nT * 32 * sizeof(float)));
@@ -400,46 +419,75 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
                        const int64_t* lengths, int32_t B, int64_t ld, float* out, int64_t ld_out,
                        float* loss, void* stream) {
     if (!h) return AEC_ERR_INVALID_ARG;
-    if (!h->have_w || !h->have_erb) return fail(h, AEC_ERR_INVALID_ARG, "weights / erb not set");
     if (B < 0 || !lengths) return fail(h, AEC_ERR_INVALID_ARG, "bad batch / lengths");
+    std::vector<int64_t> l3((size_t)B * 3);
+    for (int b = 0; b < B; ++b) l3[3 * b] = l3[3 * b + 1] = l3[3 * b + 2] = lengths[b];
+    return aec_process_siglens(h, mic, ref, near, l3.data(), B, ld, out, ld_out, loss, stream);
+}
+
+aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref, const float* near,
+                               const int64_t* lengths3, int32_t B, int64_t ld, float* out, int64_t ld_out,
+                               float* loss, void* stream) {
+    if (!h) return AEC_ERR_INVALID_ARG;
+    if (!h->have_w || !h->have_erb) return fail(h, AEC_ERR_INVALID_ARG, "weights / erb not set");
+    if (B < 0 || !lengths3) return fail(h, AEC_ERR_INVALID_ARG, "bad batch / lengths");
     if (B == 0) return AEC_OK;
     if (!mic || !ref) return fail(h, AEC_ERR_INVALID_ARG, "null mic / ref");
     if (loss && !near) return fail(h, AEC_ERR_INVALID_ARG, "loss requires near");
+    const int nsig_in = near ? 3 : 2;
     int64_t nmax = 0;
     for (int b = 0; b < B; ++b) {
-        if (lengths[b] < 1 || lengths[b] > ld) return fail(h, AEC_ERR_INVALID_ARG, "length out of [1, ld]");
-        if (lengths[b] > INT32_MAX - 4096) return fail(h, AEC_ERR_UNSUPPORTED, "stream longer than 2^31 - 4096 samples");
-        if (aec_out_len(lengths[b]) > ld_out) return fail(h, AEC_ERR_INVALID_ARG, "ld_out too small");
-        nmax = lengths[b] > nmax ? lengths[b] : nmax;
+        const int64_t n = lengths3[3 * b];
+        for (int s = 0; s < nsig_in; ++s) {
+            const int64_t ns = lengths3[3 * b + s];
+            if (ns < 1 || ns > ld) return fail(h, AEC_ERR_INVALID_ARG, "length out of [1, ld]");
+            if (ns > INT32_MAX - 4096) return fail(h, AEC_ERR_UNSUPPORTED, "stream longer than 2^31 - 4096 samples");
+            // Little_net.forward combines the three signals frame by frame
+            // (ERB.py:287-290, 318-323): the reference raises on a frame-count mismatch
+            if (ns / 256 != n / 256)
+                return fail(h, AEC_ERR_INVALID_ARG, "ref / near frame count differs from mic's (N//256 + 1)");
+        }
+        if (aec_out_len(n) > ld_out) return fail(h, AEC_ERR_INVALID_ARG, "ld_out too small");
+        nmax = n > nmax ? n : nmax;
     }
     if (!out && aec_out_len(nmax) > 0) return fail(h, AEC_ERR_INVALID_ARG, "null out");
     const int64_t Tmax = aec_num_frames(nmax);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    HIP_TRY(h, hipSetDevice(h->device));
+    AEC_ON_DEVICE(h);
     aec_status s = ensure_ws(h, B, Tmax);
     if (s != AEC_OK) return s;
-    if (h->last_lens.size() != (size_t)B || std::memcmp(h->last_lens.data(), lengths, B * sizeof(int64_t)) != 0) {
-        h->last_lens.assign(lengths, lengths + B);
+    if (h->last_lens.size() != (size_t)B * 3 ||
+        std::memcmp(h->last_lens.data(), lengths3, (size_t)B * 3 * sizeof(int64_t)) != 0) {
+        // kernels of an earlier call (on any stream) may still read the work lists
+        HIP_TRY(h, hipDeviceSynchronize());
+        h->last_lens.assign(lengths3, lengths3 + (size_t)B * 3);
+        h->h_slen.assign((size_t)B * 4, 0);
+        std::vector<int64_t> lens(B);
+        for (int b = 0; b < B; ++b) {
+            lens[b] = lengths3[3 * b];
+            for (int sg = 0; sg < 3; ++sg) h->h_slen[4 * b + sg] = (int32_t)(sg < nsig_in ? lengths3[3 * b + sg] : lens[b]);
+        }
         // analysis work list: 4-frame items of every stream, valid frames only
-        std::vector<WorkItem> items;
+        std::vector<WorkItem>& items = h->h_items;
+        items.clear();
         h->item_off.assign(B + 1, 0);
         for (int b = 0; b < B; ++b) {
             h->item_off[b] = (int64_t)items.size();
-            const int64_t T = aec_num_frames(lengths[b]);
-            for (int64_t wt = 0; wt < T; wt += 4) items.push_back({b, (int32_t)wt, lengths[b]});
+            const int64_t T = aec_num_frames(lens[b]);
+            for (int64_t wt = 0; wt < T; wt += 4) items.push_back({b, (int32_t)wt, lens[b]});
         }
         h->item_off[B] = (int64_t)items.size();
         // synthesis work list: 15 output hops per block item
-        std::vector<WorkItem> sitems;
+        std::vector<WorkItem>& sitems = h->h_sitems;
+        sitems.clear();
         h->sitem_off.assign(B + 1, 0);
         for (int b = 0; b < B; ++b) {
             h->sitem_off[b] = (int64_t)sitems.size();
-            const int64_t nhop = lengths[b] / 256;
-            for (int64_t h0 = 0; h0 < nhop; h0 += kHopsOut) sitems.push_back({b, (int32_t)h0, lengths[b]});
+            const int64_t nhop = lens[b] / 256;
+            for (int64_t h0 = 0; h0 < nhop; h0 += kHopsOut) sitems.push_back({b, (int32_t)h0, lens[b]});
         }
         h->sitem_off[B] = (int64_t)sitems.size();
         if ((int64_t)items.size() > h->items_cap || (int64_t)sitems.size() > h->sitems_cap) {
-            HIP_TRY(h, hipStreamSynchronize(st));
             if (h->d_items) HIP_TRY(h, hipFree(h->d_items));
             if (h->d_sitems) HIP_TRY(h, hipFree(h->d_sitems));
             h->d_items = h->d_sitems = nullptr;
@@ -453,9 +501,11 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
         if (!sitems.empty())
             HIP_TRY(h, hipMemcpyAsync(h->d_sitems, sitems.data(), sitems.size() * sizeof(WorkItem),
                                       hipMemcpyHostToDevice, st));
-        // pageable sources: staged synchronously by the runtime, safe to reuse on return
-        HIP_TRY(h, hipMemcpyAsync(h->d_len, h->last_lens.data(), B * sizeof(int64_t), hipMemcpyHostToDevice, st));
+        HIP_TRY(h, hipMemcpyAsync(h->d_len, lens.data(), B * sizeof(int64_t), hipMemcpyHostToDevice, st));
+        HIP_TRY(h, hipMemcpyAsync(h->d_slen, h->h_slen.data(), (size_t)B * 4 * sizeof(int32_t), hipMemcpyHostToDevice, st));
         HIP_TRY(h, hipMemcpyAsync(h->d_items, items.data(), items.size() * sizeof(WorkItem), hipMemcpyHostToDevice, st));
+        // `lens` is a local: make its (pageable, possibly staged) copy complete before it goes away
+        HIP_TRY(h, hipStreamSynchronize(st));
     }
     const int nsig = near ? 3 : 2;
     const int S = std::max(1, std::min(h->sub_max, B / 32));
@@ -468,8 +518,8 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
             if (k > 0) HIP_TRY(h, hipStreamWaitEvent(ks, h->ev_ana[k - 1], 0));
         }
         mark(h, ks);
-        HIP_TRY(h, launch_moments(mic, ref, near, ld, h->d_len, h->d_mom, b0, b1 - b0, nsig, ks));
-        HIP_TRY(h, launch_norm_finalize(h->d_mom, h->d_len, h->d_cvals, b0, b1, nsig, ks));
+        HIP_TRY(h, launch_moments(mic, ref, near, ld, h->d_slen, h->d_mom, b0, b1 - b0, nsig, ks));
+        HIP_TRY(h, launch_norm_finalize(h->d_mom, h->d_slen, h->d_cvals, b0, b1, nsig, ks));
 
         if (h->cfg.nlms_taps > 0 && B <= h->small_b && h->nlms_mode == 0) {
             // few streams: transforms frame-parallel (K2 + rows), recursion per stream, mic_erb frame-parallel
@@ -485,7 +535,7 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
             AnalysisArgs a{};
             a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
             a.ld = ld; a.items = h->d_items + h->item_off[b0]; a.nitems = h->item_off[b1] - h->item_off[b0];
-            a.num_cus = h->num_cus; a.cvals = h->d_cvals;
+            a.num_cus = h->num_cus; a.cvals = h->d_cvals; a.slen = h->d_slen;
             a.tables = reinterpret_cast<const float*>(h->d_tab);
             a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
             a.feats = h->d_feats; a.Tmax = Tmax; a.rows = h->d_rows;
@@ -501,7 +551,7 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
                 return fail(h, AEC_ERR_UNSUPPORTED, "erb schedule too long for the NLMS kernel's LDS budget");
             NlmsArgs a{};
             a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
-            a.ld = ld; a.lens = h->d_len; a.b0 = b0; a.cvals = h->d_cvals;
+            a.ld = ld; a.lens = h->d_len; a.slen = h->d_slen; a.b0 = b0; a.cvals = h->d_cvals;
             a.tables = reinterpret_cast<const float*>(h->d_tab);
             a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
             a.feats = h->d_feats; a.Tmax = Tmax; a.spec = h->d_spec;
@@ -515,7 +565,7 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
             AnalysisArgs a{};
             a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
             a.ld = ld; a.items = h->d_items + h->item_off[b0]; a.nitems = h->item_off[b1] - h->item_off[b0];
-            a.num_cus = h->num_cus; a.cvals = h->d_cvals;
+            a.num_cus = h->num_cus; a.cvals = h->d_cvals; a.slen = h->d_slen;
             a.tables = reinterpret_cast<const float*>(h->d_tab);
             a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
             a.feats = h->d_feats; a.Tmax = Tmax;
@@ -567,7 +617,7 @@ aec_status aec_debug_copy(aec_handle* h, int32_t what, float* dst, size_t n, voi
     const int64_t B = h->last_B, T = h->last_T;
     if (!dst || n < (size_t)(B * T * 32)) return fail(h, AEC_ERR_INVALID_ARG, "dst too small");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    HIP_TRY(h, hipSetDevice(h->device));
+    AEC_ON_DEVICE(h);
     if (what >= 0 && what <= 2) {
         HIP_TRY(h, hipMemcpy2DAsync(dst, 32 * sizeof(float), h->d_feats + 32 * what, 96 * sizeof(float),
                                     32 * sizeof(float), B * T, hipMemcpyDeviceToDevice, st));
@@ -645,7 +695,7 @@ aec_status aec_erb_tables_check(const float* erb, const float* mags, const float
 aec_status aec_stream_open(aec_handle* h, int32_t B) {
     if (!h) return AEC_ERR_INVALID_ARG;
     if (B < 1) return fail(h, AEC_ERR_INVALID_ARG, "stream count must be >= 1");
-    HIP_TRY(h, hipSetDevice(h->device));
+    AEC_ON_DEVICE(h);
     HIP_TRY(h, hipDeviceSynchronize());   // a previous state may still be in use
     if (h->d_state) { HIP_TRY(h, hipFree(h->d_state)); h->d_state = nullptr; }
     h->stream_B = 0;
@@ -661,7 +711,7 @@ aec_status aec_stream_reset(aec_handle* h, int32_t b, void* stream) {
     if (!h) return AEC_ERR_INVALID_ARG;
     if (!h->d_state) return fail(h, AEC_ERR_INVALID_ARG, "aec_stream_open first");
     if (b < -1 || b >= h->stream_B) return fail(h, AEC_ERR_INVALID_ARG, "stream index out of range");
-    HIP_TRY(h, hipSetDevice(h->device));
+    AEC_ON_DEVICE(h);
     const int64_t first = b < 0 ? 0 : b, count = b < 0 ? h->stream_B : 1;
     HIP_TRY(h, hipMemsetAsync(h->d_state + first * h->stream_stride, 0, (size_t)count * h->stream_stride * sizeof(float),
                               reinterpret_cast<hipStream_t>(stream)));
@@ -675,7 +725,7 @@ aec_status aec_stream_step(aec_handle* h, const float* mic, const float* ref, in
     if (!h->have_w || !h->have_erb) return fail(h, AEC_ERR_INVALID_ARG, "weights / erb not set");
     if (!mic || !ref || !out) return fail(h, AEC_ERR_INVALID_ARG, "null mic / ref / out");
     if (ld_in < 256 || ld_out < 256) return fail(h, AEC_ERR_INVALID_ARG, "ld_in / ld_out must be >= 256");
-    HIP_TRY(h, hipSetDevice(h->device));
+    AEC_ON_DEVICE(h);
     StreamStepArgs a{};
     a.mic = mic; a.ref = ref; a.ld_in = ld_in; a.out = out; a.ld_out = ld_out;
     a.state = h->d_state; a.state_stride = h->stream_stride;
@@ -695,11 +745,11 @@ void aec_destroy(aec_handle* h) {
         if (h->ev_done[k]) (void)hipEventDestroy(h->ev_done[k]);
     }
     if (h->ev_start) (void)hipEventDestroy(h->ev_start);
-    (void)hipSetDevice(h->device);
+    DeviceGuard dg(h->device);
     (void)hipFree(h->d_w); (void)hipFree(h->d_tab); (void)hipFree(h->d_sched); (void)hipFree(h->d_bintab);
     (void)hipFree(h->d_mom); (void)hipFree(h->d_cvals); (void)hipFree(h->d_items); (void)hipFree(h->d_sitems); (void)hipFree(h->d_len);
     (void)hipFree(h->d_feats); (void)hipFree(h->d_est); (void)hipFree(h->d_dbg); (void)hipFree(h->d_spec);
-    (void)hipFree(h->d_state); (void)hipFree(h->d_rows);
+    (void)hipFree(h->d_state); (void)hipFree(h->d_rows); (void)hipFree(h->d_slen);
     delete h;
 }
 

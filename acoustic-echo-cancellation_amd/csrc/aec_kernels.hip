@@ -49,12 +49,12 @@ template <int U, int NT, bool NTL>
 __global__ __launch_bounds__(NT) void moments_kernel(const float* __restrict__ mic,
                                                       const float* __restrict__ ref,
                                                       const float* __restrict__ near, int64_t ld,
-                                                      const int64_t* __restrict__ lens,
+                                                      const int32_t* __restrict__ slen,
                                                       double2* __restrict__ mom, int b0) {
     const int ch = blockIdx.x, s = blockIdx.y, b = b0 + blockIdx.z;
     const float* base = (s == 0 ? mic : (s == 1 ? ref : near));
     const float* x = base + (int64_t)b * ld;
-    const int64_t n = lens[b];
+    const int64_t n = slen[4 * b + s];
     // chunk start = a multiple of 1024 samples (float4-aligned); a vector pass
     // reads U float4 per thread (1024 U samples), then single float4s, then the
     // scalar tail
@@ -142,12 +142,12 @@ __device__ __forceinline__ float norm_scalar(const double2* __restrict__ mom, in
 
 // c for every (stream, signal): cvals[b*3 + s]
 __global__ __launch_bounds__(256) void norm_finalize_kernel(const double2* __restrict__ mom,
-                                                            const int64_t* __restrict__ lens,
+                                                            const int32_t* __restrict__ slen,
                                                             float* __restrict__ cvals, int b0, int b1, int nsig) {
     const int i = b0 * 3 + blockIdx.x * 256 + threadIdx.x;
     if (i >= b1 * 3) return;
     const int b = i / 3, s = i % 3;
-    cvals[i] = s < nsig ? norm_scalar(mom, b, s, lens[b]) : 0.f;
+    cvals[i] = s < nsig ? norm_scalar(mom, b, s, slen[4 * b + s]) : 0.f;
 }
 
 // --------------------------------------------------------------------------
@@ -214,9 +214,12 @@ __global__ __launch_bounds__(256, 3) void analysis_kernel(AnalysisArgs p) {
             // keep the LDS table reads inside the loop (hoisting the loop-invariant
             // schedule / twiddle / window reads would pin ~100 VGPRs)
             asm volatile("" ::: "memory");
-            wave_commit(wr, pf, p.cvals[it.b * 3 + s], (int)it.n, it.wt, lane);
+            // signal s's own length: its normaliser and zero padding (mic = it.n)
+            const int ns = s == 0 ? (int)it.n : p.slen[4 * it.b + s];
+            wave_commit(wr, pf, p.cvals[it.b * 3 + s], ns, it.wt, lane);
             if (s + 1 < p.nsig)
-                wave_prefetch(pf, p.sig[s + 1] + (int64_t)it.b * p.ld, (int)it.n, it.wt, lane, (al >> (s + 1)) & 1);
+                wave_prefetch(pf, p.sig[s + 1] + (int64_t)it.b * p.ld, p.slen[4 * it.b + s + 1], it.wt, lane,
+                              (al >> (s + 1)) & 1);
             else if (k2 < p.nitems)
                 wave_prefetch(pf, p.sig[0] + (int64_t)it2.b * p.ld, (int)it2.n, it2.wt, lane, al & 1);
             wave_fence();
@@ -294,11 +297,11 @@ constexpr int kERow = 512 + 48;        // floats per LDS error row: 256 float2, 
 // 4 frames at wt), prefetch the next task, window + rFFT -> xa / xb / x128.
 __device__ __forceinline__ void nlms_transform(float* wr, float* scr, float4 (&pf)[kWavePf], float cval, int n, int wt,
                                                int lane, int gg, int lb, const float* sHann, const float2* sTwT,
-                                               const float2* sTw512, const float* next_row, int next_wt,
+                                               const float2* sTw512, const float* next_row, int next_n, int next_wt,
                                                bool next_al, float2 (&xa)[8], float2 (&xb)[8], float2& x128) {
     asm volatile("" ::: "memory");
     wave_commit(wr, pf, cval, n, wt, lane);
-    if (next_row) wave_prefetch(pf, next_row, n, next_wt, lane, next_al);
+    if (next_row) wave_prefetch(pf, next_row, next_n, next_wt, lane, next_al);
     wave_fence();
     float2 v[16];
     load_frame(v, wr, sHann, gg, lb);
@@ -350,7 +353,8 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
     float* wr = sWave + (role < 2 ? wave : 0) * kWaveFloats;
     float* scr = wr + gg * kGroupFloats;
     const int b = p.b0 + blockIdx.x;
-    const int n = (int)p.lens[b];
+    const int n = (int)p.lens[b];                                   // mic: frame count
+    const int n_ref = p.slen[4 * b + 1], n_near = p.slen[4 * b + 2];
     const int64_t T = n / kHop + 1;
     const int nch = (int)((T + kFPB - 1) / kFPB);
     const bool have_near = p.nsig == 3;
@@ -439,10 +443,10 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
     // mic waves walk near(c), mic(c), near(c+1), ...; ref waves ref(c), ref(c+1), ...
     float4 pf[kWavePf];
     if (role == 0) {
-        if (have_near) wave_prefetch(pf, row_near, n, 4 * q, lane, al_near);
+        if (have_near) wave_prefetch(pf, row_near, n_near, 4 * q, lane, al_near);
         else wave_prefetch(pf, row_mic, n, 4 * q, lane, al_mic);
     } else {
-        wave_prefetch(pf, row_ref, n, 4 * q, lane, al_ref);
+        wave_prefetch(pf, row_ref, n_ref, 4 * q, lane, al_ref);
     }
     for (int c = 0; c < nch + 2; ++c) {
         const int wt = c * kFPB + 4 * q;
@@ -451,8 +455,8 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
         if (role == 0) {
             if (c < nch && !(p.mode & 8)) {
                 if (have_near) {
-                    nlms_transform(wr, scr, pf, p.cvals[b * 3 + 2], n, wt, lane, gg, lb, sHann, sTwT, sTw512,
-                                   row_mic, wt, al_mic, xa, xb, x128);
+                    nlms_transform(wr, scr, pf, p.cvals[b * 3 + 2], n_near, wt, lane, gg, lb, sHann, sTwT, sTw512,
+                                   row_mic, n, wt, al_mic, xa, xb, x128);
                     if (!(p.mode & 2)) {
                         mags_to_scr(scr, lb, sw, xa, xb, x128);
                         wave_fence();
@@ -461,15 +465,15 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
                 }
                 const bool more = c + 1 < nch;
                 nlms_transform(wr, scr, pf, p.cvals[b * 3 + 0], n, wt, lane, gg, lb, sHann, sTwT, sTw512,
-                               more ? (have_near ? row_near : row_mic) : nullptr, wt + kFPB,
+                               more ? (have_near ? row_near : row_mic) : nullptr, have_near ? n_near : n, wt + kFPB,
                                have_near ? al_near : al_mic, xa, xb, x128);
                 row_to_scr(scr, lb, xa, xb, x128);
             }
         } else {
             if (erb_role == 1 && c >= 2 && !(p.mode & 4)) mic_erb_pass(c - 2);
             if (c < nch && !(p.mode & 8)) {
-                nlms_transform(wr, scr, pf, p.cvals[b * 3 + 1], n, wt, lane, gg, lb, sHann, sTwT, sTw512,
-                               c + 1 < nch ? row_ref : nullptr, wt + kFPB, al_ref, xa, xb, x128);
+                nlms_transform(wr, scr, pf, p.cvals[b * 3 + 1], n_ref, wt, lane, gg, lb, sHann, sTwT, sTw512,
+                               c + 1 < nch ? row_ref : nullptr, n_ref, wt + kFPB, al_ref, xa, xb, x128);
                 mags_to_scr(scr, lb, sw, xa, xb, x128);
                 wave_fence();
                 erb_project(scr, sSched, sComb, L, lb, sw, t < T ? feats + t * 96 + 32 : nullptr);
@@ -699,7 +703,7 @@ hipError_t launch_mic_erb(const float2* spec, float* feats, const int64_t* lens,
 // host-side launchers (called by aec_api.hip)
 // --------------------------------------------------------------------------
 hipError_t launch_moments(const float* mic, const float* ref, const float* near, int64_t ld,
-                          const int64_t* lens, double2* mom, int b0, int nb, int nsig, hipStream_t st) {
+                          const int32_t* slen, double2* mom, int b0, int nb, int nsig, hipStream_t st) {
     if (nb <= 0) return hipSuccess;
     // 4 float4 in flight per thread, nontemporal loads (each sample is read once
     // here; the analysis pass re-reads it from HBM anyway).  256 x 10 s x 3
@@ -709,16 +713,16 @@ hipError_t launch_moments(const float* mic, const float* ref, const float* near,
     static const int cfg = [] { const char* e = std::getenv("AEC_MOM_CFG"); return e ? std::atoi(e) : 0; }();
     const dim3 g(kMomChunks, nsig, nb);
     if (cfg == 1)
-        hipLaunchKernelGGL((moments_kernel<4, 256, false>), g, dim3(256), 0, st, mic, ref, near, ld, lens, mom, b0);
+        hipLaunchKernelGGL((moments_kernel<4, 256, false>), g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0);
     else
-        hipLaunchKernelGGL((moments_kernel<4, 256, true>), g, dim3(256), 0, st, mic, ref, near, ld, lens, mom, b0);
+        hipLaunchKernelGGL((moments_kernel<4, 256, true>), g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0);
     return hipGetLastError();
 }
 
-hipError_t launch_norm_finalize(const double2* mom, const int64_t* lens, float* cvals, int b0, int b1, int nsig,
+hipError_t launch_norm_finalize(const double2* mom, const int32_t* slen, float* cvals, int b0, int b1, int nsig,
                                 hipStream_t st) {
     if (b1 <= b0) return hipSuccess;
-    hipLaunchKernelGGL(norm_finalize_kernel, dim3(((b1 - b0) * 3 + 255) / 256), dim3(256), 0, st, mom, lens, cvals,
+    hipLaunchKernelGGL(norm_finalize_kernel, dim3(((b1 - b0) * 3 + 255) / 256), dim3(256), 0, st, mom, slen, cvals,
                        b0, b1, nsig);
     return hipGetLastError();
 }

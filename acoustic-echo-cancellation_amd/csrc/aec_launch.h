@@ -28,6 +28,7 @@ struct AnalysisArgs {
     int64_t nitems;
     int num_cus;
     const float* cvals;      // [B][3] normaliser scalars
+    const int32_t* slen;     // [B][4] per-signal lengths (mic, ref, near, -); mic = the item's n
     const float* tables;     // DevTables
     const float* sched;      // ERB schedule: float4[L][16] then int2[32] (aec_tables.h)
     int sched_len;           // L (multiple of 4)
@@ -43,6 +44,7 @@ struct NlmsArgs {
     const float* sig[3];
     int64_t ld;
     const int64_t* lens;
+    const int32_t* slen;     // [B][4] per-signal lengths (mic, ref, near, -)
     int b0;                  // first stream of this launch (block i runs stream b0 + i)
     const float* cvals;
     const float* tables;
@@ -135,9 +137,10 @@ inline size_t synthesis_smem_bytes() {
     return 260 * 16 + (258 * 2 + 256 * 2 + 512 + 256 + kFPB * 33 + 4 + (size_t)kFPB * kGroupFloats) * 4;
 }
 
+// slen: [B][4] per-signal lengths (mic, ref, near, -)
 hipError_t launch_moments(const float* mic, const float* ref, const float* near, int64_t ld,
-                          const int64_t* lens, double2* mom, int b0, int nb, int nsig, hipStream_t st);
-hipError_t launch_norm_finalize(const double2* mom, const int64_t* lens, float* cvals, int b0, int b1, int nsig,
+                          const int32_t* slen, double2* mom, int b0, int nb, int nsig, hipStream_t st);
+hipError_t launch_norm_finalize(const double2* mom, const int32_t* slen, float* cvals, int b0, int b1, int nsig,
                                 hipStream_t st);
 hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t st);
 hipError_t launch_nlms_analysis(const NlmsArgs& a, int nb, hipStream_t st);

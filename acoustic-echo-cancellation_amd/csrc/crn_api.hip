@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/aec_crn.h"
+#include "aec_device.h"
 #include "aec_tables.h"
 #include "crn_launch.h"
 
@@ -801,7 +802,8 @@ aec_status aec_crn_create(const aec_crn_config* cfg, const float* params, size_t
         return s;
     };
     if (h->H % 32 || ilog2(h->Q) < 0) return bail(AEC_ERR_UNSUPPORTED);
-    if (hipSetDevice(device) != hipSuccess) return bail(AEC_ERR_HIP);
+    aec::DeviceGuard dg(device);
+    if (dg.err != hipSuccess) return bail(AEC_ERR_HIP);
     if (hipMalloc(&h->d_tab, sizeof(aec::DevTables)) != hipSuccess) return bail(AEC_ERR_OOM);
     aec::DevTables tab;
     aec::build_dev_tables(tab);
@@ -820,7 +822,8 @@ aec_status aec_crn_create(const aec_crn_config* cfg, const float* params, size_t
 
 aec_status aec_crn_set_params(aec_crn_handle* h, const float* params, size_t n) {
     if (!h || !params) return AEC_ERR_INVALID_ARG;
-    if (hipSetDevice(h->device) != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
+    aec::DeviceGuard dg(h->device);   // the caller's current device is restored on return
+    if (dg.err != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
     return load_params(h, params, n);
 }
 
@@ -853,7 +856,8 @@ aec_status aec_crn_process(aec_crn_handle* h, const float* mic, const float* far
     if (!h->have_params) return crn_fail(h, AEC_ERR_INVALID_ARG, "parameters not set");
     if (!mic || !far) return crn_fail(h, AEC_ERR_INVALID_ARG, "null signal");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (hipSetDevice(h->device) != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
+    aec::DeviceGuard dg(h->device);   // the caller's current device is restored on return
+    if (dg.err != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
     int64_t Tmax = 0;
     aec_status s = prepare(h, lengths, B, ld, &Tmax, st);
     if (s != AEC_OK) return s;
@@ -883,7 +887,8 @@ aec_status aec_crn_stft(aec_crn_handle* h, const float* x, const int64_t* length
                         void* stream) {
     if (!h || !x || !spec) return AEC_ERR_INVALID_ARG;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (hipSetDevice(h->device) != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
+    aec::DeviceGuard dg(h->device);   // the caller's current device is restored on return
+    if (dg.err != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
     int64_t Tmax = 0;
     aec_status s = prepare(h, lengths, B, ld, &Tmax, st);
     if (s != AEC_OK) return s;
@@ -896,7 +901,8 @@ aec_status aec_crn_stream_open(aec_crn_handle* h, int32_t B) {
     if (!h || B <= 0) return AEC_ERR_INVALID_ARG;
     if (!h->have_params) return crn_fail(h, AEC_ERR_INVALID_ARG, "parameters not set");
     if (h->nrnn > 8) return crn_fail(h, AEC_ERR_UNSUPPORTED, "too many LSTM layers for streaming");
-    if (hipSetDevice(h->device) != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
+    aec::DeviceGuard dg(h->device);   // the caller's current device is restored on return
+    if (dg.err != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
     stream_free(h);
     h->ss = new (std::nothrow) StreamState();
     if (!h->ss) return AEC_ERR_OOM;
@@ -963,7 +969,8 @@ aec_status aec_crn_stream_step(aec_crn_handle* h, const float* mic, const float*
     if (!mic || !far || !out || ld_in < 256 || ld_out < 256) return crn_fail(h, AEC_ERR_INVALID_ARG, "bad hop buffers");
     StreamState& ss = *h->ss;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (hipSetDevice(h->device) != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
+    aec::DeviceGuard dg(h->device);   // the caller's current device is restored on return
+    if (dg.err != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
     const int par = (int)(ss.k & 1);
     const int B = ss.B;
     CRN_TRY(h, hipMemcpy2DAsync(ss.hop + (size_t)(par * 2 + 0) * B * 256, 256 * sizeof(float), mic,
@@ -1027,7 +1034,7 @@ aec_status aec_crn_profile_read(aec_crn_handle* h, double* ms5, int64_t* calls) 
 
 void aec_crn_destroy(aec_crn_handle* h) {
     if (!h) return;
-    (void)hipSetDevice(h->device);
+    aec::DeviceGuard dg(h->device);
     stream_free(h);
     for (void* p : h->allocs) (void)hipFree(p);
     for (auto* v : {&h->enc, &h->dec, &h->lih, &h->lhh})

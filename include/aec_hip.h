@@ -95,6 +95,19 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
                        const int64_t* lengths, int32_t B, int64_t ld,
                        float* out, int64_t ld_out, float* loss, void* stream);
 
+/* aec_process with a length per signal, as scripts/test.py feeds the
+ * reference (test.py:139: default collate at batch 1, every signal at its
+ * stored length): each signal is normalised over, and zero-padded beyond, its
+ * own length (ERB.py:254-256, attention_ccrn.py:48).  The mic length sets the
+ * frame count and the output length; ref / near must have the same frame
+ * count N//256 + 1 (the reference's frame-wise concat / loss raise otherwise,
+ * ERB.py:287-290, 318-323) — AEC_ERR_INVALID_ARG here.
+ *   lengths3 : host [B][3] int64 (mic, ref, near); near's entry is ignored when
+ *              near is NULL */
+aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref, const float* near,
+                               const int64_t* lengths3, int32_t B, int64_t ld,
+                               float* out, int64_t ld_out, float* loss, void* stream);
+
 /* Streaming (serving): the reference's per-frame loop (Little_net.forward,
  * ERB.py:252-334) advanced by one 256-sample hop per stream per call, as ONE
  * fused kernel launch (frame -> rFFT -> [FD-NLMS] -> ERB -> GRU step -> head

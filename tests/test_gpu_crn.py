@@ -204,3 +204,48 @@ def test_streaming_equals_batch(dtype):
     got1 = torch.cat(outs[1:])
     no = 256 * (lens[0] // 256)
     assert rel(got1[:no].cpu(), ref_out[0, :no].cpu()) <= tol
+
+
+def test_bf16_batch256_embeds_goldens():
+    """BASELINE config 3's shape: bf16, 256 rows in one call.  The reference
+    golden utterances (full net_conf, v2 'E') sit in a 256-row ragged batch;
+    they match the reference within the bf16 tolerance, and EVERY row equals
+    its own single-utterance call bit for bit (no coupling across rows)."""
+    net, m, conf = build('v2E_16000', 'bf16')
+    from aec_amd import synth
+    gold = {5: 'v2E_16000', 200: 'v2E_2125', 77: 'v2E_255'}
+    for g in gold.values():
+        assert META[g]['version'] == 2 and META[g]['overrides'] == {} and META[g]['weight_seed'] == m['weight_seed']
+    rng = np.random.default_rng(256)
+    B = 256
+    rows = []
+    for b in range(B):
+        if b in gold:
+            d = np.load(os.path.join(GOLD, f'crn_{gold[b]}.npz'))
+            rows.append((d['mic'], d['far']))
+        else:
+            n = int(rng.integers(256, 4000))
+            mic, far, _ = synth.scene(n, 3000 + b)
+            rows.append((mic, far))
+    lens = [len(r[0]) for r in rows]
+    L = max(lens)
+    pad = lambda k: torch.tensor(np.stack([np.pad(r[k], (0, L - len(r[k]))) for r in rows]), device='cuda:0')
+    with torch.no_grad():
+        bout, _, bmask = net.forward_ragged(pad(0), pad(1), lens, want_spec=False, want_mask=True)
+    torch.cuda.synchronize()
+    for b, g in gold.items():
+        d = np.load(os.path.join(GOLD, f'crn_{g}.npz'))
+        no = META[g]['out_len']
+        o = bout[b, :no].cpu().numpy()
+        assert o.shape == d['out_wav'].shape and np.isfinite(o).all()
+        assert not bout[b, no:].any()
+        if no:
+            assert rel(o, d['out_wav']) <= BF16_WAV_TOL, g
+            tn = META[g]['n'] // 256 + 1
+            assert rel(bmask[b][..., :tn].cpu().numpy(), d['mask']) <= BF16_MASK_TOL, g
+    with torch.no_grad():
+        for b in range(B):
+            o1, _, _ = net.forward_ragged(T(rows[b][0]), T(rows[b][1]), [lens[b]], want_spec=False)
+            no = 256 * (lens[b] // 256)
+            assert torch.equal(bout[b, :no], o1[0, :no]), b
+    torch.cuda.synchronize()

@@ -249,3 +249,29 @@ def test_max_batch_4096_streams_matches_single_calls(nlms_net, golden_erb):
             assert abs(float(loss[i]) - float(l1[0])) <= 1e-6 * max(1.0, abs(float(l1[0]))), i
     del mic, ref, near, out
     torch.cuda.empty_cache()
+
+
+def test_nlms_10s_batch_vs_oracle(nlms_net, golden_weights, golden_erb):
+    """BASELINE C2 lengths: 10 s streams (626 dependent NLMS frames per bin)
+    through the batch path the bench runs (B > AEC_SMALLB: one K2n block per
+    stream), checked against the float64 oracle: waveform <= 1e-4 RMS, loss
+    <= 1e-4 relative; the same stream alone (the small-batch split path)
+    gives the same bits."""
+    from aec_amd import synth
+    n, B = 160000, 80
+    mic, ref, near = synth.batch(B, n, seed0=4400)
+    dev = 'cuda:0'
+    erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
+    M, R, N = (torch.from_numpy(a).to(dev) for a in (mic, ref, near))
+    with torch.no_grad():
+        out, loss = nlms_net.forward_ragged(M, R, N, erb_t, [n] * B)
+        out1, loss1 = nlms_net.forward_ragged(M[:1], R[:1], N[:1], erb_t, [n])
+    torch.cuda.synchronize()
+    out, loss = out.cpu().numpy(), loss.cpu().numpy()
+    for b in (0, 41, B - 1):
+        o, l = O.aec_forward(mic[b], ref[b], near[b], golden_erb.astype(np.float32), golden_weights, nlms_cfg=NLMS)
+        assert out[b].shape == o.shape == (n,)
+        assert _rms(out[b], o) <= WAVE_RMS_TOL, b
+        assert _loss_ok(float(loss[b]), l), b
+    assert np.array_equal(out1[0].cpu().numpy(), out[0])
+    assert float(loss1[0]) == pytest.approx(float(loss[0]), rel=1e-6)

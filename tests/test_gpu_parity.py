@@ -164,3 +164,45 @@ def test_erle_delta_vs_oracle(gpu_net, golden_weights, golden_erb):
     out, _ = _run(gpu_net, golden_erb, mic, ref, near)
     o, _ = O.little_net_forward(mic, ref, near, golden_erb.astype(np.float32), golden_weights)
     assert abs(O.erle_db(mic, out) - O.erle_db(mic, o)) <= 0.1
+
+
+def test_unequal_signal_lengths_vs_golden(gpu_net, golden_erb):
+    """aec_process_siglens: mic / ref / near at their own stored lengths
+    (test.py:139 default collate) against the reference's outputs, batched
+    in one ragged call; a frame-count mismatch raises like the reference."""
+    d = dict(np.load(os.path.join(GOLDEN, 'siglens.npz')))
+    meta = json.load(open(os.path.join(GOLDEN, 'siglens_meta.json')))
+    cases = meta['cases']
+    B = len(cases)
+    L = max(max(c['n_mic'], c['n_ref'], c['n_near']) for c in cases)
+    rows = {k: np.zeros((B, L), np.float32) for k in ('mic', 'ref', 'near')}
+    lens = np.zeros((B, 3), np.int64)
+    for i, c in enumerate(cases):
+        for j, k in enumerate(('mic', 'ref', 'near')):
+            x = d[f'{k}{i}']
+            rows[k][i, :len(x)] = x
+            lens[i, j] = len(x)
+    dev = 'cuda:0'
+    erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
+    T = lambda a: torch.from_numpy(a).to(dev)
+    with torch.no_grad():
+        out, loss = gpu_net.forward_ragged(T(rows['mic']), T(rows['ref']), T(rows['near']), erb_t, lens)
+    torch.cuda.synchronize()
+    out, loss = out.cpu().numpy(), loss.cpu().numpy()
+    for i, c in enumerate(cases):
+        exp = d[f'out{i}']
+        assert exp.shape == (c['out_len'],)
+        assert _rms(out[i, :c['out_len']], exp) <= WAVE_RMS_TOL
+        assert not out[i, c['out_len']:].any()
+        assert _loss_ok(float(loss[i]), float(d[f'loss{i}']))
+    bad = lens.copy()
+    bad[1, 1] = 256 * (lens[1, 0] // 256 + 1) + 40     # ref one frame longer than mic
+    assert bad[1, 1] <= L
+    with pytest.raises(RuntimeError):
+        gpu_net.forward_ragged(T(rows['mic']), T(rows['ref']), T(rows['near']), erb_t, bad)
+    h, _ = gpu_net._handle(torch.device(dev))          # the C ABI refuses it too (AEC_ERR_INVALID_ARG)
+    m, r, nn_ = T(rows['mic']), T(rows['ref']), T(rows['near'])
+    o = torch.empty(B, L, device=dev)
+    with pytest.raises(RuntimeError, match='frame count'):
+        h.process(m.data_ptr(), r.data_ptr(), nn_.data_ptr(), bad, B, L, o.data_ptr(), L, None,
+                  torch.cuda.current_stream().cuda_stream)

@@ -8,6 +8,7 @@ tests pin:
   multi-level group B-tree) and empty datasets;
 - the chunk size h5py's `chunks=True` picks.
 """
+import os
 import struct
 import zlib
 
@@ -97,3 +98,50 @@ def test_rejects_non_hdf5_and_latest(tmp_path):
     q.write_bytes(h5lite.SIGNATURE + bytes([2]) + b'\0' * 100)
     with pytest.raises(h5lite.H5Error, match='superblock version 2'):
         h5lite.File(str(q))
+
+
+# ---------------------------------------------------------- libhdf5-written files
+FOREIGN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'foreign')
+
+
+def test_reads_libhdf5_file_with_user_block():
+    """A MATLAB 7.3 file written by libhdf5 (superblock at 512 behind a user
+    block; addresses relative to it): the variable equals what scipy's MATLAB
+    v5 reader returns for the same variable saved by the same MATLAB."""
+    import scipy.io as sio
+    with open(os.path.join(FOREIGN, 'testhdf5_7.4_GLNX86.mat'), 'rb') as fh:
+        raw = fh.read()
+    assert raw[512:520] == h5lite.SIGNATURE and raw[:8] != h5lite.SIGNATURE
+    f = h5lite.File(os.path.join(FOREIGN, 'testhdf5_7.4_GLNX86.mat'))
+    try:
+        assert f.keys() == ['testdouble']
+        got = f['testdouble'].read()
+    finally:
+        f.close()
+    exp = sio.loadmat(os.path.join(FOREIGN, 'testdouble_7.4_GLNX86.mat'))['testdouble']
+    assert got.dtype == np.float64 and got.shape == exp.T.shape     # HDF5 MATLAB arrays are stored transposed
+    assert np.array_equal(got, exp.T)
+    assert np.array_equal(got[:, 0], np.linspace(0, 2 * np.pi, 9))
+
+
+def test_reads_hdf5_example_files():
+    """libhdf5-written example files (PyTables' test data): contiguous
+    float16/32/64, big-endian int32 (h5_write: data[i][j] = i + j) and a
+    chunked, extended dataset (h5_extend)."""
+    with h5lite.File(os.path.join(FOREIGN, 'float.h5')) as f:
+        ij = np.add.outer(np.arange(5), np.arange(6))
+        for k, dt in (('float16', np.float16), ('float32', np.float32), ('float64', np.float64)):
+            a = f[k].read()
+            assert a.dtype == dt and np.array_equal(a, ij.astype(dt))
+    with h5lite.File(os.path.join(FOREIGN, 'smpl_i32be.h5')) as f:
+        a = f['TestArray'].read()
+        assert a.dtype == np.int32 and np.array_equal(a, np.add.outer(np.arange(6), np.arange(5)))
+    with h5lite.File(os.path.join(FOREIGN, 'smpl_SDSextendible.h5')) as f:
+        ds = f['ExtendibleArray']
+        assert ds._layout[0] == 'chunked'
+        a = ds.read()
+    exp = np.zeros((10, 5), np.int32)
+    exp[:3, :3] = 1
+    exp[:2, 3:] = 3
+    exp[3:, 0] = 2
+    assert np.array_equal(a, exp)

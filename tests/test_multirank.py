@@ -115,3 +115,39 @@ def test_balanced_shards_properties():
     assert shard.balanced_shards([5, 5, 5], 8)[3:] == [[]] * 5
     with pytest.raises(ValueError):
         shard.balanced_shards([1], 0)
+
+
+def test_rank_binds_its_local_gpu_for_rccl(monkeypatch):
+    """Under torchrun every rank must run its collectives on ITS GPU
+    (LOCAL_RANK), not on cuda:0: the CLI's group init binds the device first
+    and hands it to RCCL, and the collectives' device follows (shard._dev).
+    torch.cuda / the process group are stubbed: no GPU here."""
+    from aec_amd import tester
+    calls = {}
+    monkeypatch.setenv('WORLD_SIZE', '2')
+    monkeypatch.setenv('RANK', '1')
+    monkeypatch.setenv('LOCAL_RANK', '1')
+    monkeypatch.setattr(shard, '_BOUND', None)
+    monkeypatch.setattr(torch.cuda, 'is_available', lambda: True)
+    monkeypatch.setattr(torch.cuda, 'set_device', lambda d: calls.setdefault('set_device', int(d)))
+    monkeypatch.setattr(torch.cuda, 'current_device', lambda: 0)   # what an unbound rank would see
+    state = {'init': False}
+
+    def fake_init(backend, **kw):
+        calls['backend'] = backend
+        calls['device_id'] = kw.get('device_id')
+        state['init'] = True
+
+    monkeypatch.setattr(dist, 'is_initialized', lambda: state['init'])
+    monkeypatch.setattr(dist, 'is_available', lambda: True)
+    monkeypatch.setattr(dist, 'init_process_group', fake_init)
+    monkeypatch.setattr(dist, 'get_rank', lambda: 1)
+    monkeypatch.setattr(dist, 'get_world_size', lambda: 2)
+    monkeypatch.setattr(dist, 'get_backend', lambda *a: 'nccl')
+    assert tester._dist() == (1, 2)
+    assert calls['set_device'] == 1
+    assert calls['backend'] == 'nccl' and calls['device_id'] == torch.device('cuda', 1)
+    assert shard._dev() == torch.device('cuda', 1)
+    # the device a collective tensor is built on: the bound GPU even with cuda:0 current
+    monkeypatch.setattr(shard, '_BOUND', None)
+    assert shard._dev() == torch.device('cuda', 1)              # LOCAL_RANK when not bound yet

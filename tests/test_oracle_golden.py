@@ -119,3 +119,21 @@ def test_torch_port_matches_golden(golden_weights, golden_erb):
         assert out.shape[1] == d['out'].shape[0]
         assert np.sqrt(np.mean((out[0].numpy() - d['out']) ** 2)) < 1e-5
         assert abs(float(loss[0]) - float(d['loss'])) < 1e-5 * abs(float(d['loss']))
+
+
+def test_oracle_vs_reference_unequal_signal_lengths(golden_weights, golden_erb):
+    """test.py:139 feeds each signal at its stored length (default collate):
+    the oracle's per-signal normaliser / framing reproduces the reference on
+    unequal lengths with equal frame counts (tests/golden/make_siglens_golden.py)."""
+    d = dict(np.load(os.path.join(GOLDEN, 'siglens.npz')))
+    meta = json.load(open(os.path.join(GOLDEN, 'siglens_meta.json')))
+    assert meta['mismatch'] == 'RuntimeError'                     # the reference raises on a frame mismatch
+    for i, c in enumerate(meta['cases']):
+        mic, ref, near = d[f'mic{i}'], d[f'ref{i}'], d[f'near{i}']
+        assert (len(mic), len(ref), len(near)) == (c['n_mic'], c['n_ref'], c['n_near'])
+        out, loss = O.little_net_forward(mic, ref, near, golden_erb.astype(np.float32), golden_weights)
+        assert out.shape == d[f'out{i}'].shape == (c['out_len'],)
+        assert np.sqrt(np.mean((out - d[f'out{i}']) ** 2)) < 5e-6
+        assert abs(loss - float(d[f'loss{i}'])) < 1e-5 * max(1, abs(loss))
+    with pytest.raises(ValueError):                               # numpy's shape error, as torch's RuntimeError
+        O.little_net_forward(mic[:3000], ref[:3300], near[:3000], golden_erb, golden_weights)
