@@ -220,6 +220,11 @@ struct aec_handle {
     int nlms_erb = 1;            // AEC_NLMS_ERB: role running the mic_erb pass (1 ref, 2 nlms)
     int fused = 1;               // AEC_FUSED_SYNTH: GRU + synthesis in one kernel (NLMS path)
     int fused_mode = 0;          // AEC_FUSED_MODE (timing experiments; results invalid unless 0)
+    int pipe = 0;                // AEC_PIPE: the fused per-stream pipeline (aec_pipe.hip) for B >= pipe_minb
+    int pipe_minb = 1;           // AEC_PIPE_MINB
+    int pipe_mode = 0;           // AEC_PIPE_MODE (timing experiments; results invalid unless 0)
+    float2* d_ring = nullptr;    // [B][kPipeRingRows][256] pipeline error-spectrum ring
+    int64_t ring_B = 0;
     int small_b = 64;            // AEC_SMALLB: NLMS batches up to this many streams take the split path
                                  // (per 10 s step: B = 1 0.477 -> 0.336 ms, B = 16 0.486 -> 0.354,
                                  // B = 64 0.504 -> 0.485; B = 128 slower)
@@ -353,6 +358,9 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
     if (const char* m = std::getenv("AEC_FUSED_SYNTH")) h->fused = std::atoi(m);
     if (const char* m = std::getenv("AEC_FUSED_MODE")) h->fused_mode = std::atoi(m);
     if (const char* m = std::getenv("AEC_SMALLB")) h->small_b = std::atoi(m);
+    if (const char* m = std::getenv("AEC_PIPE")) h->pipe = std::atoi(m);
+    if (const char* m = std::getenv("AEC_PIPE_MINB")) h->pipe_minb = std::atoi(m);
+    if (const char* m = std::getenv("AEC_PIPE_MODE")) h->pipe_mode = std::atoi(m);
     if (const char* m = std::getenv("AEC_SUBBATCH")) h->sub_max = std::max(1, std::min(aec_handle::kMaxSub, std::atoi(m)));
     {
         int cus = 0;
@@ -508,6 +516,42 @@ aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref
         HIP_TRY(h, hipStreamSynchronize(st));
     }
     const int nsig = near ? 3 : 2;
+    if (h->pipe && B >= h->pipe_minb && h->gru_mode == 0 && h->nlms_mode == 0) {
+        // K1 moments, then K6: every stream's whole chain in one block (aec_pipe.hip)
+        if (pipe_smem_bytes(h->sched_len) > 160 * 1024)
+            return fail(h, AEC_ERR_UNSUPPORTED, "erb schedule too long for the pipeline kernel's LDS budget");
+        if (B > h->ring_B) {
+            HIP_TRY(h, hipDeviceSynchronize());
+            if (h->d_ring) HIP_TRY(h, hipFree(h->d_ring));
+            h->d_ring = nullptr;
+            h->ring_B = 0;
+            HIP_TRY(h, hipMalloc(&h->d_ring, (size_t)B * kPipeRingRows * 256 * sizeof(float2)));
+            h->ring_B = B;
+        }
+        mark(h, st);
+        HIP_TRY(h, launch_moments(mic, ref, near, ld, h->d_slen, h->d_mom, 0, B, nsig, st));
+        mark(h, st);
+        PipeArgs a{};
+        a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
+        a.ld = ld; a.lens = h->d_len; a.slen = h->d_slen; a.b0 = 0; a.nsig = nsig;
+        a.mom = h->d_mom; a.tables = reinterpret_cast<const float*>(h->d_tab);
+        a.sched = h->d_sched; a.sched_len = h->sched_len; a.bintab = h->d_bintab; a.w = h->d_w;
+        a.ring = h->d_ring; a.out = out; a.ld_out = ld_out; a.loss = loss;
+        a.taps = h->cfg.nlms_taps; a.mu = h->cfg.nlms_mu; a.beta = h->cfg.nlms_beta; a.delta = h->cfg.nlms_delta;
+        if (h->debug) {
+            a.feats = h->d_feats; a.est = h->d_est;
+            a.dbg_h = h->d_dbg; a.dbg_mask = h->d_dbg + (size_t)B * Tmax * 32;
+        }
+        a.Tmax = Tmax;
+        a.mode = h->pipe_mode;
+        HIP_TRY(h, launch_pipe(a, B, st));
+        mark(h, st);
+        mark(h, st);
+        mark(h, st);
+        h->last_B = B;
+        h->last_T = Tmax;
+        return AEC_OK;
+    }
     const int S = std::max(1, std::min(h->sub_max, B / 32));
     if (S > 1) HIP_TRY(h, hipEventRecord(h->ev_start, st));
     for (int k = 0; k < S; ++k) {
@@ -749,7 +793,7 @@ void aec_destroy(aec_handle* h) {
     (void)hipFree(h->d_w); (void)hipFree(h->d_tab); (void)hipFree(h->d_sched); (void)hipFree(h->d_bintab);
     (void)hipFree(h->d_mom); (void)hipFree(h->d_cvals); (void)hipFree(h->d_items); (void)hipFree(h->d_sitems); (void)hipFree(h->d_len);
     (void)hipFree(h->d_feats); (void)hipFree(h->d_est); (void)hipFree(h->d_dbg); (void)hipFree(h->d_spec);
-    (void)hipFree(h->d_state); (void)hipFree(h->d_rows); (void)hipFree(h->d_slen);
+    (void)hipFree(h->d_state); (void)hipFree(h->d_rows); (void)hipFree(h->d_slen); (void)hipFree(h->d_ring);
     delete h;
 }
 

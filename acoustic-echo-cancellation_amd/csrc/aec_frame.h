@@ -216,6 +216,25 @@ __device__ __forceinline__ void synth_frame(const float2 (&xa)[8], const float2 
     }
 }
 
+// c = mean(x)/std(x, unbiased) from the partials (ERB.py:254-256).
+__device__ __forceinline__ float norm_scalar(const double2* __restrict__ mom, int b, int s, int64_t n) {
+    constexpr int kMomChunks = 8;   // aec_launch.h
+    const double2* m = mom + ((int64_t)b * 3 + s) * kMomChunks;
+    double S1 = 0.0, S2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < kMomChunks; ++i) {
+        const double2 v = m[i];
+        S1 += v.x;
+        S2 += v.y;
+    }
+    const double dn = (double)n;
+    const double mean = S1 / dn;
+    double num = S2 - S1 * mean;
+    if (num < 0.0) num = 0.0;                      // rounding on a constant signal
+    const double sd = sqrt(num / (dn - 1.0));      // n == 1 -> 0/0 = nan, as torch.std
+    return (float)(mean / sd);
+}
+
 // GRU gate nonlinearities (nn.GRU, ERB.py:213): fast exp / reciprocal.
 __device__ __forceinline__ float sigmoidf_(float x) {
     return __builtin_amdgcn_rcpf(1.f + __expf(-x));

@@ -122,24 +122,6 @@ __global__ __launch_bounds__(NT) void moments_kernel(const float* __restrict__ m
     }
 }
 
-// c = mean(x)/std(x, unbiased) from the partials (ERB.py:254-256).
-__device__ __forceinline__ float norm_scalar(const double2* __restrict__ mom, int b, int s, int64_t n) {
-    const double2* m = mom + ((int64_t)b * 3 + s) * kMomChunks;
-    double S1 = 0.0, S2 = 0.0;
-#pragma unroll
-    for (int i = 0; i < kMomChunks; ++i) {
-        const double2 v = m[i];
-        S1 += v.x;
-        S2 += v.y;
-    }
-    const double dn = (double)n;
-    const double mean = S1 / dn;
-    double num = S2 - S1 * mean;
-    if (num < 0.0) num = 0.0;                      // rounding on a constant signal
-    const double sd = sqrt(num / (dn - 1.0));      // n == 1 -> 0/0 = nan, as torch.std
-    return (float)(mean / sd);
-}
-
 // c for every (stream, signal): cvals[b*3 + s]
 __global__ __launch_bounds__(256) void norm_finalize_kernel(const double2* __restrict__ mom,
                                                             const int32_t* __restrict__ slen,
