@@ -150,8 +150,8 @@ struct PipeArgs {
     float* dbg_h;            // [B][Tmax][32]
     float* dbg_mask;         // [B][Tmax][32]
     int64_t Tmax;
-    int mode;                // timing experiments only (AEC_PIPE_MODE; results invalid unless 0): bit r skips
-                             // role r's work (1 GRU, 2 SY, 4 HD, 8 NL, 16 MIC, 32 REF + mic_erb, 64 gi)
+    int mode;                // timing experiments only (AEC_PIPE_MODE; results invalid unless 0): bits skip
+                             // a role's work: 1 GRU, 2 SY + OLA, 4 HD, 8 NL, 16 MIC + mic_erb, 32 REF, 64 gi, 128 NEAR
 };
 constexpr int kPipeFrames = 8;                       // frames per pipeline tick
 constexpr int kPipeRingRows = 4 * kPipeFrames;       // E rows kept per stream (4 chunks)

@@ -14,18 +14,22 @@
 // frames ("ticks"), so the transforms, the NLMS and the synthesis hide under
 // the recurrence, and E only crosses a 4-chunk ring that stays in the XCD's L2.
 //
-// 12 waves (168 VGPRs each, 3 per SIMD; waves w, w+4, w+8 share a SIMD), roles
-// by wave index; in tick c ("|" = the mid-tick barrier B1, every tick ends with B2):
-//   w0      GRU   recurrence of chunk c-3 (kGruSplit steps | the rest)
-//   w1, w2  SY    synthesis of chunk c-5 (gains, irFFT, window) | overlap-add +
-//                 WOLA -> out; E rows of chunk c-4 from the ring into registers
-//   w3      HD    head / mask / est_erb / loss of chunk c-4
-//   w4..w7  NL    NLMS recursion of chunk c-1 -> E rows (LDS + ring) | copy the
-//                 M / R rows of chunk c into registers (bin k = lane + 64 (w-4);
-//                 lane 0 also bin 256)
-//   w8, w9  MIC   near transform -> near_erb, mic transform -> M rows (chunk c) |
-//   w10,w11 REF   ref transform -> ref_erb, R rows (chunk c) | mic_erb = ERB(|E|) of chunk c-1
-//   (w8..w11 also: gi = W_ih x + b of chunk c-2 after B1)
+// 16 waves (128 VGPRs each, 4 per SIMD; waves w, w+4, w+8, w+12 share a SIMD),
+// roles by wave index; in tick c ("|" = the mid-tick barrier B1, every tick
+// ends with B2):
+//   w0       GRU   recurrence of chunk c-3 (kGruA steps | the rest)
+//   w1       HD    head / mask / est_erb / loss of chunk c-4 (4 frames | 4 frames)
+//   w2, w3   GI    gi = W_ih x + b of chunk c-2 | overlap-add + WOLA of chunk c-5 -> out
+//   w4..w7   NL    NLMS recursion of chunk c-1 -> E rows (LDS + ring) | copy the
+//                  M / R rows of chunk c into registers (bin k = lane + 64 (w-4);
+//                  lane 0 also bin 256)
+//   w8, w9   MIC   mic transform of chunk c -> M rows | mic_erb = ERB(|E|) of chunk c-1
+//   w10,w11  REF   ref transform of chunk c -> ref_erb, R rows |
+//   w12,w13  NEAR  near transform of chunk c -> near_erb (loss) |
+//   w14,w15  SY    synthesis of chunk c-5 (gains, irFFT, window) | E rows of chunk c-4
+//                  from the ring into LDS
+// Every wave that transforms does one 4-frame pass per tick, all of them
+// before B1, so the tick is one transform pass plus the mic_erb pass long.
 // B1 orders the M / R rows (written before it) against the NL copy and the E
 // rows against the mic_erb pass; B2 frees them for the next tick.  Hand-offs
 // more than one tick apart go through LDS rings indexed by chunk.
@@ -46,30 +50,27 @@
 #include "aec_tables.h"
 
 #ifndef PIPE_GRU_A
-#define PIPE_GRU_A 3          // GRU steps in phase A / B of a tick (the rest in phase C)
-#endif
-#ifndef PIPE_GRU_B
-#define PIPE_GRU_B 2
+#define PIPE_GRU_A 6          // GRU steps before the mid-tick barrier (the rest after it)
 #endif
 
 namespace aec {
 
 namespace {
 constexpr int kPF = kPipeFrames;          // 8 frames per tick
-constexpr int kWaves = 12;
+constexpr int kWaves = 16;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kERowP = 512 + 48;          // LDS error row: 256 float2 + ERB partials
 constexpr int kEstSP = 33;
 constexpr int kSchedMax = 32;             // ERB schedule entries per lane (erb_conf: 32)
-constexpr int kGruA = PIPE_GRU_A, kGruB = PIPE_GRU_B;
+constexpr int kGruA = PIPE_GRU_A;
 
-enum : int { W_GRU = 0, W_SY0 = 1, W_SY1 = 2, W_HD = 3, W_NL0 = 4, W_MIC0 = 8, W_REF0 = 10 };
+enum : int { W_GRU = 0, W_HD = 1, W_GI0 = 2, W_NL0 = 4, W_MIC0 = 8, W_REF0 = 10, W_NEAR0 = 12, W_SY0 = 14 };
 
 // LDS carve (floats).  Every offset is a compile-time constant: LDS addresses
 // become instruction immediates and cost no SGPR / VGPR.
 struct Carve {
-    int sched = 0, comb = 0, tw512 = 0, twT = 0, hann = 0, coff = 0, bin = 0, wT = 0, tf = 0, sy = 0, e = 0, gi = 0,
-        h = 0, hb = 0, micr = 0, refr = 0, nearr = 0, est = 0, o = 0, ec = 0, c = 0, sye = 0, total = 0;
+    int sched = 0, comb = 0, tw512 = 0, twT = 0, hann = 0, coff = 0, bin = 0, tf = 0, sy = 0, e = 0, gi = 0,
+        h = 0, hb = 0, micr = 0, refr = 0, nearr = 0, est = 0, o = 0, ec = 0, c = 0, w2t = 0, sye = 0, total = 0;
     constexpr Carve() {
         int o_ = 0;
         auto take = [&](int n) { const int r = o_; o_ += (n + 3) & ~3; return r; };
@@ -80,8 +81,7 @@ struct Carve {
         hann = take(512);
         coff = take(256);
         bin = take(260 * 4);
-        wT = take(64 * 96);                  // W_ih as float4 columns [16][96] (gi_row)
-        tf = take(4 * kWaveFloats);          // MIC0, MIC1, REF0, REF1
+        tf = take(6 * kWaveFloats);          // MIC0, MIC1, REF0, REF1, NEAR0, NEAR1
         sy = take(2 * kWaveFloats);
         e = take(kPF * kERowP);
         gi = take(2 * kPF * 96);
@@ -94,6 +94,7 @@ struct Carve {
         o = take(2 * 32);
         ec = take(2 * 256);                  // OLA tail: second half of a chunk's last frame
         c = take(4);
+        w2t = take(32 * 32);                 // linear2 weight transposed [k][j] (head wave)
         sye = take(kPF * 512);               // E rows of the chunk the SY waves synthesise next
         total = o_;
     }
@@ -138,30 +139,62 @@ __device__ __forceinline__ bool row_aligned(const float* base, int64_t ld) {
 }
 
 // gi = W_ih[row] . x + bias with x = [mic_erb, |mic_erb - ref_erb|] read from
-// the two feature rows (ERB.py:287-290) and W_ih from LDS as float4 columns
-// wq[q][row] = W_ih[row][4q .. 4q+3] (lane = row: conflict-free b128 reads):
-// gru_gi's exact operation order (aec_frame.h), so the same bits.  Processed
-// in 4 blocks of 4 q with a scheduling barrier between them, so at most 16
-// weights and 4 x vectors are in flight per lane.
-__device__ __forceinline__ float gi_row(const float4* wq, int row, const float* xm, const float* xr, float gbias) {
+// the two feature rows (ERB.py:287-290), W_ih[row] in registers: gru_gi's exact
+// operation order (aec_frame.h), so the same bits.  Partly unrolled: the fully
+// unrolled form hoists all 16 x vectors and spills at 128 VGPRs.
+__device__ __forceinline__ float gi_row(const float (&wih)[64], const float* xm, const float* xr, float gbias) {
     const float4* m4 = reinterpret_cast<const float4*>(xm);
     const float4* r4 = reinterpret_cast<const float4*>(xr);
     f2v a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
-#pragma unroll 4
-    for (int q = 0; q < 16; ++q) {
-        float4 xv;
-        if (q < 8) {
-            xv = m4[q];
-        } else {
-            const float4 a = m4[q - 8], r = r4[q - 8];
-            xv = make_float4(fabsf(a.x - r.x), fabsf(a.y - r.y), fabsf(a.z - r.z), fabsf(a.w - r.w));
-        }
-        const float4 w = wq[q * 96 + row];
-        a0 = __builtin_elementwise_fma(f2v{w.x, w.y}, f2v{xv.x, xv.y}, a0);
-        a1 = __builtin_elementwise_fma(f2v{w.z, w.w}, f2v{xv.z, xv.w}, a1);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const float4 xv = m4[q];
+        a0 = __builtin_elementwise_fma(f2v{wih[4 * q], wih[4 * q + 1]}, f2v{xv.x, xv.y}, a0);
+        a1 = __builtin_elementwise_fma(f2v{wih[4 * q + 2], wih[4 * q + 3]}, f2v{xv.z, xv.w}, a1);
+    }
+#pragma unroll
+    for (int q = 8; q < 16; ++q) {
+        const float4 a = m4[q - 8], r = r4[q - 8];
+        const float4 xv = make_float4(fabsf(a.x - r.x), fabsf(a.y - r.y), fabsf(a.z - r.z), fabsf(a.w - r.w));
+        a0 = __builtin_elementwise_fma(f2v{wih[4 * q], wih[4 * q + 1]}, f2v{xv.x, xv.y}, a0);
+        a1 = __builtin_elementwise_fma(f2v{wih[4 * q + 2], wih[4 * q + 3]}, f2v{xv.z, xv.w}, a1);
     }
     const f2v s2 = a0 + a1;
     return gbias + (s2.x + s2.y);
+}
+
+// head_mask (aec_frame.h) with linear2's weights read from LDS (w2t[k][j] =
+// W2[j][k]) instead of registers: the same operations in the same order.
+__device__ __forceinline__ float head_mask_w2lds(const float (&w1)[64], const float* w2t, float b1j, float b2j,
+                                                 const float* h, const float* mic, float* orow, int j) {
+    const float4* h4 = reinterpret_cast<const float4*>(h);
+    const float4* m4 = reinterpret_cast<const float4*>(mic);
+    f2v a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const float4 hv = h4[q];
+        const float4 mv = m4[q];
+        a0 = __builtin_elementwise_fma(f2v{w1[4 * q], w1[4 * q + 1]}, f2v{hv.x, hv.y}, a0);
+        a1 = __builtin_elementwise_fma(f2v{w1[4 * q + 2], w1[4 * q + 3]}, f2v{hv.z, hv.w}, a1);
+        a0 = __builtin_elementwise_fma(f2v{w1[32 + 4 * q], w1[32 + 4 * q + 1]}, f2v{mv.x, mv.y}, a0);
+        a1 = __builtin_elementwise_fma(f2v{w1[32 + 4 * q + 2], w1[32 + 4 * q + 3]}, f2v{mv.z, mv.w}, a1);
+    }
+    const f2v s1 = a0 + a1;
+    orow[j] = fmaxf(b1j + (s1.x + s1.y), 0.f);
+    wave_fence();
+    const float4* o4 = reinterpret_cast<const float4*>(orow);
+    f2v c0 = {0.f, 0.f}, c1 = {0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const float4 ov = o4[q];
+        const float w0 = w2t[(4 * q) * 32 + j], w1_ = w2t[(4 * q + 1) * 32 + j];
+        const float w2_ = w2t[(4 * q + 2) * 32 + j], w3 = w2t[(4 * q + 3) * 32 + j];
+        c0 = __builtin_elementwise_fma(f2v{w0, w1_}, f2v{ov.x, ov.y}, c0);
+        c1 = __builtin_elementwise_fma(f2v{w2_, w3}, f2v{ov.z, ov.w}, c1);
+    }
+    wave_fence();                                   // the row is reused by the group's next frame
+    const f2v s2 = c0 + c1;
+    return sigmoidf_(b2j + (s2.x + s2.y));
 }
 
 struct PipeStream {
@@ -169,24 +202,6 @@ struct PipeStream {
     bool have_near;
 };
 
-// gi of chunk cs (768 row x frame dots) by the 4 NL waves in phase C of a
-// tick: lane l of NL wave v (0..3) takes dots l + 64 v + 256 u
-__device__ __forceinline__ void gi_chunk(const PipeArgs& p, int cs, int v, int lane) {
-    const float4* sWT = reinterpret_cast<const float4*>(lds<kC.wT>());
-    const float* sMicR = lds<kC.micr>();
-    const float* sRefR = lds<kC.refr>();
-    float* sGi = lds<kC.gi>();
-    const float* b_ih = p.w + 96 * 64 + 96 * 32;
-    const float* b_hh = b_ih + 96;
-#pragma unroll 1
-    for (int u = 0; u < 3; ++u) {
-        const int d = lane + 64 * v + 256 * u;
-        const int row = d % 96, f = d / 96;
-        const float gbias = b_ih[row] + (row < 64 ? b_hh[row] : 0.f);
-        const int fr_ = (cs & 3) * kPF + f;
-        sGi[((cs & 1) * kPF + f) * 96 + row] = gi_row(sWT, row, sMicR + fr_ * 32, sRefR + fr_ * 32, gbias);
-    }
-}
 }  // namespace
 
 size_t pipe_smem_bytes(int sched_len) { return sched_len <= kSchedMax ? (size_t)kC.total * 4 : SIZE_MAX; }
@@ -236,44 +251,92 @@ __device__ __forceinline__ void role_gru(const PipeArgs& p, const PipeStream& s)
         };
         steps(0, min(kGruA, f_end));
         barrier_lds();
-        steps(kGruA, min(kGruA + kGruB, f_end));
-        barrier_lds();
-        steps(kGruA + kGruB, f_end);
+        steps(kGruA, f_end);
         barrier_lds();
     }
 }
 
-// ---------------------------------------------------------- synthesis ----
-__device__ __forceinline__ void role_sy(const PipeArgs& p, const PipeStream& s) {
+// ------------------------------------------------ head / mask / est / loss ----
+__device__ __forceinline__ void role_hd(const PipeArgs& p, const PipeStream& s) {
+    const int lane = threadIdx.x & 63;
+    const float* sH = lds<kC.h>();
+    const float* sMicR = lds<kC.micr>();
+    const float* sNearR = lds<kC.nearr>();
+    float* sEst = lds<kC.est>();
+    float* sO = lds<kC.o>();
+    const float* W1 = p.w + 96 * 64 + 96 * 32 + 96 + 96;
+    const float* b1 = W1 + 32 * 64;
+    const float* W2 = b1 + 32;
+    const float* b2 = W2 + 32 * 32;
+    const int g = lane >> 5, j = lane & 31;
+    float w1[64];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) w1[k] = W1[j * 64 + k];
+    const float* sW2T = lds<kC.w2t>();                        // W2[j][k] at [k][j]: conflict-free
+    const float b1j = b1[j], b2j = b2[j];
+    (void)W2;
+    float lacc = 0.f;
+    for (int c = 0; c < s.nticks; ++c) {
+        const int ch = c - 4;
+        const bool act = ch >= 0 && ch < s.nch && !(p.mode & 4);
+        auto frames = [&](int f0) {
+#pragma unroll 1
+            for (int f = f0 + g; f < f0 + 4; f += 2) {
+                const int t = ch * kPF + f;
+                float est = 0.f;
+                if (t < s.T) {                                    // uniform within the 32-lane group
+                    const float* hrow = sH + ((ch & 1) * kPF + f) * 32;
+                    const float* mrow = sMicR + ((ch & 3) * kPF + f) * 32;
+                    const float mask = head_mask_w2lds(w1, sW2T, b1j, b2j, hrow, mrow, sO + g * 32, j);
+                    est = mask * mrow[j];
+                    if (s.have_near) {
+                        const float d = sqrtf(sNearR[((ch & 7) * kPF + f) * 32 + j]) - sqrtf(est);
+                        lacc += d * d;
+                    }
+                    if (p.est) {
+                        const int64_t o_idx = ((int64_t)s.b * p.Tmax + t) * 32 + j;
+                        p.est[o_idx] = est;
+                        if (p.dbg_h) p.dbg_h[o_idx] = hrow[j];
+                        if (p.dbg_mask) p.dbg_mask[o_idx] = mask;
+                    }
+                }
+                sEst[((ch & 1) * kPF + f) * kEstSP + j] = est;    // frames past the end: gain 0
+            }
+        };
+        if (act) frames(0);
+        barrier_lds();
+        if (act) frames(4);
+        barrier_lds();
+    }
+    if (p.loss) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) lacc += __shfl_xor(lacc, o);
+        if (lane == 0) p.loss[s.b] = lacc / (float)(s.T * 32);
+    }
+}
+
+// ----------------------- input projection | overlap-add + WOLA ----------
+__device__ __forceinline__ void role_gi(const PipeArgs& p, const PipeStream& s) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int gg = lane >> 4, lb = lane & 15;
-    const int w = wave - W_SY0;
-    const int fi = 4 * w + gg;                                // frame of the chunk this group synthesises
-    float* sSY = lds<kC.sy>();
-    float* scr = sSY + w * kWaveFloats + gg * kGroupFloats;
-    const float* sEst = lds<kC.est>();
-    const float4* sBin = reinterpret_cast<const float4*>(lds<kC.bin>());
-    const float2* sTw512 = reinterpret_cast<const float2*>(lds<kC.tw512>());
-    const float2* sTwT = reinterpret_cast<const float2*>(lds<kC.twT>());
-    const float* sHann = lds<kC.hann>();
+    const int w = wave - W_GI0;
+    const float* sMicR = lds<kC.micr>();
+    const float* sRefR = lds<kC.refr>();
+    float* sGi = lds<kC.gi>();
+    const float* sSY = lds<kC.sy>();
     const float* sCoff = lds<kC.coff>();
     float* sEC = lds<kC.ec>();
-    const float2* ring = p.ring + (int64_t)s.b * kPipeRingRows * 256;
+    // gi: row = 64 w + lane (wave 1: lanes 0..31), all 8 frames of the chunk
+    const int grow = 64 * w + lane;
+    const bool has_row = grow < 96;
+    const int rr = has_row ? grow : 0;
+    float wih[64];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) wih[k] = p.w[rr * 64 + k];
+    const float* b_ih = p.w + 96 * 64 + 96 * 32;
+    const float* b_hh = b_ih + 96;
+    const float gbias = b_ih[rr] + (rr < 64 ? b_hh[rr] : 0.f);
     float* orow = p.out + (int64_t)s.b * p.ld_out;
     const bool oal = row_aligned(p.out, p.ld_out);
-    float* sSyE = lds<kC.sye>();
-    // E rows of chunk cl (this wave's 4 frames) -> sSyE, nt loads: written by the
-    // NL waves of this CU three ticks ago, served by the XCD's L2 (L1 bypassed)
-    auto load_rows = [&](int cl) {
-        typedef float f4t __attribute__((ext_vector_type(4)));
-        const f4t* src = reinterpret_cast<const f4t*>(ring + ((cl & 3) * kPF + 4 * w) * 256);
-        f4t* dst = reinterpret_cast<f4t*>(sSyE + 4 * w * 512);
-        f4t v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(src + lane + 64 * u);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) dst[lane + 64 * u] = v[u];
-    };
     // output hop j (256 samples) = second half of one frame + first half of the next
     auto ola = [&](const float* a_half, const float* c_half, int64_t j) {
         if (j < 0 || j >= s.nhop) return;
@@ -299,92 +362,71 @@ __device__ __forceinline__ void role_sy(const PipeArgs& p, const PipeStream& s) 
     };
     auto fr = [&](int f) { return sSY + (f >> 2) * kWaveFloats + (f & 3) * kGroupFloats; };
     for (int c = 0; c < s.nticks; ++c) {
+        const int cs = c - 2;
+        if (has_row && cs >= 0 && cs < s.nch && !(p.mode & 64)) {
+#pragma unroll 1
+            for (int f = 0; f < kPF; ++f) {
+                const int row = (cs & 3) * kPF + f;
+                sGi[((cs & 1) * kPF + f) * 96 + grow] = gi_row(wih, sMicR + row * 32, sRefR + row * 32, gbias);
+            }
+        }
+        barrier_lds();
+        const int co = c - 5;
+        if (co >= 0 && co < s.nch && !(p.mode & 2)) {
+            // hops j0 + f: wave 0 f = -1 (previous chunk's frame 7 + frame 0) .. 3, wave 1 f = 4 .. 6
+            const int64_t j0 = (int64_t)co * kPF;
+            const int f_lo = w == 0 ? -1 : 4, f_hi = w == 0 ? 4 : 7;
+#pragma unroll 1
+            for (int f = f_lo; f < f_hi; ++f)
+                ola(f < 0 ? sEC + ((co - 1) & 1) * 256 : fr(f) + 256, fr(f + 1), j0 + f);
+            if (w == 1)
+                for (int r = lane; r < 256; r += 64) sEC[(co & 1) * 256 + r] = fr(7)[256 + r];
+        }
+        barrier_lds();
+    }
+}
+
+// ---------------------------------------------------------- synthesis ----
+__device__ __forceinline__ void role_sy(const PipeArgs& p, const PipeStream& s) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int gg = lane >> 4, lb = lane & 15;
+    const int w = wave - W_SY0;
+    const int fi = 4 * w + gg;                                // frame of the chunk this group synthesises
+    float* scr = lds<kC.sy>() + w * kWaveFloats + gg * kGroupFloats;
+    const float* sEst = lds<kC.est>();
+    const float4* sBin = reinterpret_cast<const float4*>(lds<kC.bin>());
+    const float2* sTw512 = reinterpret_cast<const float2*>(lds<kC.tw512>());
+    const float2* sTwT = reinterpret_cast<const float2*>(lds<kC.twT>());
+    const float* sHann = lds<kC.hann>();
+    float* sSyE = lds<kC.sye>();
+    const float2* ring = p.ring + (int64_t)s.b * kPipeRingRows * 256;
+    for (int c = 0; c < s.nticks; ++c) {
         const int cs = c - 5;
-        const bool act = cs >= 0 && cs < s.nch && !(p.mode & 2);
-        if (act) {
+        if (cs >= 0 && cs < s.nch && !(p.mode & 2)) {
             float2 xa[8], xb[8], x128;
             row_to_pairs(reinterpret_cast<const float2*>(sSyE + fi * 512), lb, true, xa, xb, x128);
             synth_frame(xa, xb, x128, sEst + ((cs & 1) * kPF + fi) * kEstSP, sBin, sTw512, sTwT, sHann, scr, lb);
         }
         barrier_lds();
-        if (act) {
-            const int64_t j0 = (int64_t)cs * kPF;
-            // hops j0 + f: wave 0 f = -1 (previous chunk's frame 7 + frame 0) .. 3, wave 1 f = 4 .. 6
-            const int f_lo = w == 0 ? -1 : 4, f_hi = w == 0 ? 4 : 7;
-#pragma unroll 1
-            for (int f = f_lo; f < f_hi; ++f)
-                ola(f < 0 ? sEC + ((cs - 1) & 1) * 256 : fr(f) + 256, fr(f + 1), j0 + f);
-            if (w == 1)
-                for (int r = lane; r < 256; r += 64) sEC[(cs & 1) * 256 + r] = fr(7)[256 + r];
-        }
+        // E rows of chunk c-4 (this wave's 4 frames) -> sSyE, nt loads: written by the NL
+        // waves of this CU three ticks ago, served by the XCD's L2 (L1 bypassed)
         const int cl = c - 4;
-        if (cl >= 0 && cl < s.nch && !(p.mode & 2)) load_rows(cl);
+        if (cl >= 0 && cl < s.nch && !(p.mode & 2)) {
+            typedef float f4t __attribute__((ext_vector_type(4)));
+            const f4t* src = reinterpret_cast<const f4t*>(ring + ((cl & 3) * kPF + 4 * w) * 256);
+            f4t* dst = reinterpret_cast<f4t*>(sSyE + 4 * w * 512);
+            f4t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(src + lane + 64 * u);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) dst[lane + 64 * u] = v[u];
+        }
         wait_vm0();            // the ring slot read here is rewritten by the NL waves next tick
         barrier_lds();
-        barrier_lds();
     }
 }
 
-// ------------------------------------------------ head / mask / est / loss ----
-__device__ __forceinline__ void role_hd(const PipeArgs& p, const PipeStream& s) {
-    const int lane = threadIdx.x & 63;
-    const float* sH = lds<kC.h>();
-    const float* sMicR = lds<kC.micr>();
-    const float* sNearR = lds<kC.nearr>();
-    float* sEst = lds<kC.est>();
-    float* sO = lds<kC.o>();
-    const float* W1 = p.w + 96 * 64 + 96 * 32 + 96 + 96;
-    const float* b1 = W1 + 32 * 64;
-    const float* W2 = b1 + 32;
-    const float* b2 = W2 + 32 * 32;
-    const int g = lane >> 5, j = lane & 31;
-    float w1[64], w2[32];
-#pragma unroll
-    for (int k = 0; k < 64; ++k) w1[k] = W1[j * 64 + k];
-#pragma unroll
-    for (int k = 0; k < 32; ++k) w2[k] = W2[j * 32 + k];
-    const float b1j = b1[j], b2j = b2[j];
-    float lacc = 0.f;
-    for (int c = 0; c < s.nticks; ++c) {
-        const int ch = c - 4;
-        const bool act = ch >= 0 && ch < s.nch && !(p.mode & 4);
-        auto frames = [&](int f0) {
-            for (int f = f0 + g; f < f0 + 4; f += 2) {
-                const int t = ch * kPF + f;
-                float est = 0.f;
-                if (t < s.T) {                                    // uniform within the 32-lane group
-                    const float* hrow = sH + ((ch & 1) * kPF + f) * 32;
-                    const float* mrow = sMicR + ((ch & 3) * kPF + f) * 32;
-                    const float mask = head_mask(w1, w2, b1j, b2j, hrow, mrow, sO + g * 32, j);
-                    est = mask * mrow[j];
-                    if (s.have_near) {
-                        const float d = sqrtf(sNearR[((ch & 7) * kPF + f) * 32 + j]) - sqrtf(est);
-                        lacc += d * d;
-                    }
-                    if (p.est) {
-                        const int64_t o_idx = ((int64_t)s.b * p.Tmax + t) * 32 + j;
-                        p.est[o_idx] = est;
-                        if (p.dbg_h) p.dbg_h[o_idx] = hrow[j];
-                        if (p.dbg_mask) p.dbg_mask[o_idx] = mask;
-                    }
-                }
-                sEst[((ch & 1) * kPF + f) * kEstSP + j] = est;    // frames past the end: gain 0
-            }
-        };
-        if (act) frames(0);
-        barrier_lds();
-        barrier_lds();
-        if (act) frames(4);
-        barrier_lds();
-    }
-    if (p.loss) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) lacc += __shfl_xor(lacc, o);
-        if (lane == 0) p.loss[s.b] = lacc / (float)(s.T * 32);
-    }
-}
-
-// ------------------------------------------- NLMS recursion (+ gi) -------
+// --------------------------------------------------- NLMS recursion ------
 template <int TAPS>
 __device__ __forceinline__ void role_nl(const PipeArgs& p, const PipeStream& s) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -422,76 +464,19 @@ __device__ __forceinline__ void role_nl(const PipeArgs& p, const PipeStream& s) 
         }
         wait_vm0();            // this tick's E stores are in L2 before the SY waves read them
         barrier_lds();
-        const int cs = c - 2;
-        if (cs >= 0 && cs < s.nch && !(p.mode & 64)) gi_chunk(p, cs, q, lane);
-        barrier_lds();
     }
 }
 
-// --------------------------------- near + mic transforms | (nothing) ------
-__device__ __forceinline__ void role_mic(const PipeArgs& p, const PipeStream& s) {
+// ------------------------------------------------------- transforms ------
+// kind 0 (MIC): mic transform -> M rows | mic_erb = ERB(|E|) of chunk c-1
+// kind 1 (REF): ref transform -> ref_erb, R rows |
+// kind 2 (NEAR): near transform -> near_erb |
+template <int KIND>
+__device__ __forceinline__ void role_tf(const PipeArgs& p, const PipeStream& s) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int gg = lane >> 4, lb = lane & 15, sw = 16 * (gg & 1);
-    const int m = wave - W_MIC0;
-    float* wr = lds<kC.tf>() + m * kWaveFloats;
-    float* scr = wr + gg * kGroupFloats;
-    const float4* sSched = reinterpret_cast<const float4*>(lds<kC.sched>());
-    const int2* sComb = reinterpret_cast<const int2*>(lds<kC.comb>());
-    const float2* sTw512 = reinterpret_cast<const float2*>(lds<kC.tw512>());
-    const float2* sTwT = reinterpret_cast<const float2*>(lds<kC.twT>());
-    const float* sHann = lds<kC.hann>();
-    float* sNearR = lds<kC.nearr>();
-    const float* sC = lds<kC.c>();
-    const int L = p.sched_len;
-    const int n = s.n;
-    const float* row_mic = p.sig[0] + (int64_t)s.b * p.ld;
-    const float* row_near = s.have_near ? p.sig[2] + (int64_t)s.b * p.ld : nullptr;
-    const bool al_mic = row_aligned(p.sig[0], p.ld);
-    const bool al_near = s.have_near && row_aligned(p.sig[2], p.ld);
-    const int n_near = p.slen[4 * s.b + 2];
-    const float cm = sC[0], cn = sC[2];
-    float* feats = p.feats ? p.feats + (int64_t)s.b * p.Tmax * 96 : nullptr;
-    const bool tf = !(p.mode & 16);
-    float4 pf[kWavePf];
-    wave_prefetch(pf, row_mic, n, 4 * m, lane, al_mic);
-    for (int c = 0; c < s.nticks; ++c) {
-        const int wt = c * kPF + 4 * m;
-        const int t = wt + gg;
-        // A: mic transform -> M row of frame t (read by the NL waves in B); prefetch near
-        if (c < s.nch && tf) {
-            float2 xa[8], xb[8], x128;
-            const bool more = s.have_near || c + 1 < s.nch;
-            transform4(wr, scr, pf, cm, n, wt, lane, gg, lb, sHann, sTwT, sTw512,
-                       more ? (s.have_near ? row_near : row_mic) : nullptr, s.have_near ? n_near : n,
-                       s.have_near ? wt : wt + kPF, s.have_near ? al_near : al_mic, xa, xb, x128);
-            row_to_scr(scr, lb, xa, xb, x128);
-        }
-        barrier_lds();
-        barrier_lds();
-        // C: the M rows are consumed; near transform -> near_erb (loss only); prefetch the next mic
-        if (c < s.nch && tf && s.have_near) {
-            float2 xa[8], xb[8], x128;
-            transform4(wr, scr, pf, cn, n_near, wt, lane, gg, lb, sHann, sTwT, sTw512,
-                       c + 1 < s.nch ? row_mic : nullptr, n, wt + kPF, al_mic, xa, xb, x128);
-            mags_to_scr(scr, lb, sw, xa, xb, x128);
-            wave_fence();
-            float* fo = sNearR + ((c & 7) * kPF + 4 * m + gg) * 32;
-            erb_project(scr, sSched, sComb, L, lb, sw, fo);
-            if (feats && t < s.T) {
-                feats[(int64_t)t * 96 + 64 + lb] = fo[lb];
-                feats[(int64_t)t * 96 + 64 + lb + 16] = fo[lb + 16];
-            }
-        }
-        barrier_lds();
-    }
-}
-
-// ----------------------------- ref transform | mic_erb = ERB(|E|) ---------
-__device__ __forceinline__ void role_ref(const PipeArgs& p, const PipeStream& s) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int gg = lane >> 4, lb = lane & 15, sw = 16 * (gg & 1);
-    const int r = wave - W_REF0;
-    float* wr = lds<kC.tf>() + (2 + r) * kWaveFloats;
+    const int m = wave - (KIND == 0 ? W_MIC0 : (KIND == 1 ? W_REF0 : W_NEAR0));
+    float* wr = lds<kC.tf>() + (2 * KIND + m) * kWaveFloats;
     float* scr = wr + gg * kGroupFloats;
     const float4* sSched = reinterpret_cast<const float4*>(lds<kC.sched>());
     const int2* sComb = reinterpret_cast<const int2*>(lds<kC.comb>());
@@ -499,39 +484,42 @@ __device__ __forceinline__ void role_ref(const PipeArgs& p, const PipeStream& s)
     const float2* sTwT = reinterpret_cast<const float2*>(lds<kC.twT>());
     const float* sHann = lds<kC.hann>();
     float* sE = lds<kC.e>();
-    float* sMicR = lds<kC.micr>();
-    float* sRefR = lds<kC.refr>();
-    const float* sC = lds<kC.c>();
+    float* ring_erb = KIND == 0 ? lds<kC.micr>() : (KIND == 1 ? lds<kC.refr>() : lds<kC.nearr>());
     const int L = p.sched_len;
-    const float* row_ref = p.sig[1] + (int64_t)s.b * p.ld;
-    const bool al = row_aligned(p.sig[1], p.ld);
-    const int n_ref = p.slen[4 * s.b + 1];
-    const float cr = sC[1];
+    const bool on = KIND != 2 || s.have_near;
+    const float* row = on ? p.sig[KIND == 0 ? 0 : (KIND == 1 ? 1 : 2)] + (int64_t)s.b * p.ld : nullptr;
+    const bool al = on && row_aligned(p.sig[KIND == 0 ? 0 : (KIND == 1 ? 1 : 2)], p.ld);
+    const int n = KIND == 0 ? s.n : p.slen[4 * s.b + KIND];
+    const float cval = lds<kC.c>()[KIND];
     float* feats = p.feats ? p.feats + (int64_t)s.b * p.Tmax * 96 : nullptr;
+    const int foff = KIND == 0 ? 0 : (KIND == 1 ? 32 : 64);
+    const bool tf = on && !(p.mode & (KIND == 0 ? 16 : (KIND == 1 ? 32 : 128)));
     float4 pf[kWavePf];
-    wave_prefetch(pf, row_ref, n_ref, 4 * r, lane, al);
+    if (on) wave_prefetch(pf, row, n, 4 * m, lane, al);
     for (int c = 0; c < s.nticks; ++c) {
-        if (c < s.nch && !(p.mode & 32)) {
-            const int wt = c * kPF + 4 * r;
+        if (c < s.nch && tf) {
+            const int wt = c * kPF + 4 * m;
             const int t = wt + gg;
             float2 xa[8], xb[8], x128;
-            transform4(wr, scr, pf, cr, n_ref, wt, lane, gg, lb, sHann, sTwT, sTw512,
-                       c + 1 < s.nch ? row_ref : nullptr, n_ref, wt + kPF, al, xa, xb, x128);
-            mags_to_scr(scr, lb, sw, xa, xb, x128);
-            wave_fence();
-            float* fo = sRefR + ((c & 3) * kPF + 4 * r + gg) * 32;
-            erb_project(scr, sSched, sComb, L, lb, sw, fo);
-            if (feats && t < s.T) {
-                feats[(int64_t)t * 96 + 32 + lb] = fo[lb];
-                feats[(int64_t)t * 96 + 32 + lb + 16] = fo[lb + 16];
+            transform4(wr, scr, pf, cval, n, wt, lane, gg, lb, sHann, sTwT, sTw512, c + 1 < s.nch ? row : nullptr, n,
+                       wt + kPF, al, xa, xb, x128);
+            if (KIND != 0) {
+                mags_to_scr(scr, lb, sw, xa, xb, x128);
+                wave_fence();
+                float* fo = ring_erb + (((KIND == 1 ? (c & 3) : (c & 7))) * kPF + 4 * m + gg) * 32;
+                erb_project(scr, sSched, sComb, L, lb, sw, fo);
+                if (feats && t < s.T) {
+                    feats[(int64_t)t * 96 + foff + lb] = fo[lb];
+                    feats[(int64_t)t * 96 + foff + lb + 16] = fo[lb + 16];
+                }
             }
-            row_to_scr(scr, lb, xa, xb, x128);               // R row, for the NL waves
+            if (KIND != 2) row_to_scr(scr, lb, xa, xb, x128);   // M / R row of frame t, for the NL waves
         }
         barrier_lds();
         const int c1 = c - 1;
-        if (c1 >= 0 && c1 < s.nch && !(p.mode & 32)) {
+        if (KIND == 0 && c1 >= 0 && c1 < s.nch && !(p.mode & 16)) {
             // mic_erb of chunk c-1 from its E rows (complete since B1)
-            const int fi = 4 * r + gg;
+            const int fi = 4 * m + gg;
             const int t = c1 * kPF + fi;
             float* er = sE + fi * kERowP;
             float2 xa[8], xb[8], x128;
@@ -539,14 +527,13 @@ __device__ __forceinline__ void role_ref(const PipeArgs& p, const PipeStream& s)
             wave_fence();
             mags_to_scr(er, lb, sw, xa, xb, x128);
             wave_fence();
-            float* fo = sMicR + ((c1 & 3) * kPF + fi) * 32;
+            float* fo = ring_erb + ((c1 & 3) * kPF + fi) * 32;
             erb_project(er, sSched, sComb, L, lb, sw, fo);
             if (feats && t < s.T) {
                 feats[(int64_t)t * 96 + lb] = fo[lb];
                 feats[(int64_t)t * 96 + lb + 16] = fo[lb + 16];
             }
         }
-        barrier_lds();
         barrier_lds();
     }
 }
@@ -580,23 +567,25 @@ __global__ __launch_bounds__(kThreads, 1) void pipe_kernel(PipeArgs p) {
             lds<kC.hann>()[tid] = tb->hann[tid];
             lds<kC.ec>()[tid] = 0.f;
         }
-        for (int i = tid; i < 96 * 64; i += kThreads) {           // W_ih [96][64] -> float4 columns [16][96]
-            const int row = i / 64, col = i % 64;
-            lds<kC.wT>()[((col >> 2) * 96 + row) * 4 + (col & 3)] = p.w[i];
+        {
+            const float* W2 = p.w + 96 * 64 + 96 * 32 + 96 + 96 + 32 * 64 + 32;
+            for (int i = tid; i < 32 * 32; i += kThreads) lds<kC.w2t>()[(i & 31) * 32 + (i >> 5)] = W2[i];
         }
         if (tid < 3) lds<kC.c>()[tid] = tid < p.nsig ? norm_scalar(p.mom, s.b, tid, p.slen[4 * s.b + tid]) : 0.f;
     }
     __syncthreads();
 #ifndef PIPE_ROLES
-#define PIPE_ROLES 0x3F        // build experiments only: bit r compiles role r (GRU SY HD NL MIC REF)
+#define PIPE_ROLES 0xFF        // build experiments only: bit r compiles role r (GRU HD GI NL MIC REF NEAR SY)
 #endif
-    auto idle = [&]() { for (int c = 0; c < s.nticks; ++c) { barrier_lds(); barrier_lds(); barrier_lds(); } };
+    auto idle = [&]() { for (int c = 0; c < s.nticks; ++c) { barrier_lds(); barrier_lds(); } };
     if (wave == W_GRU) { if constexpr (PIPE_ROLES & 1) role_gru(p, s); else idle(); }
-    else if (wave == W_SY0 || wave == W_SY1) { if constexpr (PIPE_ROLES & 2) role_sy(p, s); else idle(); }
-    else if (wave == W_HD) { if constexpr (PIPE_ROLES & 4) role_hd(p, s); else idle(); }
+    else if (wave == W_HD) { if constexpr (PIPE_ROLES & 2) role_hd(p, s); else idle(); }
+    else if (wave < W_NL0) { if constexpr (PIPE_ROLES & 4) role_gi(p, s); else idle(); }
     else if (wave < W_MIC0) { if constexpr (PIPE_ROLES & 8) role_nl<TAPS>(p, s); else idle(); }
-    else if (wave < W_REF0) { if constexpr (PIPE_ROLES & 16) role_mic(p, s); else idle(); }
-    else { if constexpr (PIPE_ROLES & 32) role_ref(p, s); else idle(); }
+    else if (wave < W_REF0) { if constexpr (PIPE_ROLES & 16) role_tf<0>(p, s); else idle(); }
+    else if (wave < W_NEAR0) { if constexpr (PIPE_ROLES & 32) role_tf<1>(p, s); else idle(); }
+    else if (wave < W_SY0) { if constexpr (PIPE_ROLES & 64) role_tf<2>(p, s); else idle(); }
+    else { if constexpr (PIPE_ROLES & 128) role_sy(p, s); else idle(); }
 }
 
 template <int TAPS>
