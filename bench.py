@@ -57,6 +57,12 @@ WORKLOAD = {
 # the NLMS path runs K3 + K4 as one kernel (aec_gru_synth.hip) unless AEC_FUSED_SYNTH=0
 ALG['full']['gru_synthesis'] = {k: GRU[k] + ALG['full']['synthesis'][k] for k in ('bytes', 'flops')}
 PIPE = dict(bytes=4096, flops=82000)      # whole path, per frame
+SURVEY_NLMS_FLOPS = 257 * (16 * 4 + 10)    # FD-NLMS adds 257 (16 L + 10) FLOP/frame, L = 4 taps
+
+
+def path_flops(pipeline):
+    """SURVEY.md §8(d) algorithmic FLOP per frame of the whole path."""
+    return PIPE['flops'] + (SURVEY_NLMS_FLOPS if pipeline == 'full' else 0)
 
 
 def parse():
@@ -77,32 +83,46 @@ def parse():
     ap.add_argument('--crn-version', type=int, choices=[1, 2], default=2, help='1 = dccrn.py, 2 = dccrn2.py')
     ap.add_argument('--no-rtf', action='store_true', help='skip the batch-1 latency probe (profiling runs)')
     ap.add_argument('--sweep', action='store_true', help='also report a batch sweep')
+    ap.add_argument('--no-c3', action='store_true', help='skip the BASELINE config 3 (DCCRN bf16) figure')
+    ap.add_argument('--c3-steps', type=int, default=10, help='timed steps of the config 3 figure')
     return ap.parse_args()
 
 
 def roofline(pipeline, kernel, ms_per_launch, frames_per_launch, pmc):
-    a = ALG[pipeline][kernel]
+    """Dominant kernel vs the MI355X roofline.  `achieved` = SURVEY.md §8(d)'s
+    per-frame algorithmic figure for the whole path (4,096 B; 82 kFLOP + the
+    NLMS's 19 kFLOP) x the frames one launch processes / the launch's time
+    (HIP events); the governing bound is the larger of the HBM and FP32 times.
+    The kernel's own algorithmic share (the part of the path it implements,
+    DESIGN.md §5) is reported beside it as `kernel_share`."""
     t = ms_per_launch * 1e-3
-    gbs = a['bytes'] * frames_per_launch / t / 1e9
-    tfl = a['flops'] * frames_per_launch / t / 1e12
-    t_hbm = a['bytes'] / (HBM_PEAK_GBS * 1e9)
-    t_fl = a['flops'] / (FP32_PEAK_TFLOPS * 1e12)
+    fl = path_flops(pipeline)
+    t_hbm = PIPE['bytes'] / (HBM_PEAK_GBS * 1e9)
+    t_fl = fl / (FP32_PEAK_TFLOPS * 1e12)
     traffic = None
     kname = {'analysis': 'nlms_analysis', 'gru_synthesis': 'gru_synth'}.get(kernel, kernel) \
         if pipeline == 'full' else kernel
     if pmc and pmc.get('pipeline') == pipeline and kname in pmc.get('kernels', {}):
         traffic = pmc['kernels'][kname].get('hbm_bytes_per_launch')
+    a = ALG[pipeline].get(kernel, dict(bytes=PIPE['bytes'], flops=fl))
+    share = dict(alg_bytes_per_frame=a['bytes'], alg_flops_per_frame=a['flops'],
+                 achieved_gbs=round(a['bytes'] * frames_per_launch / t / 1e9, 1),
+                 achieved_tflops=round(a['flops'] * frames_per_launch / t / 1e12, 3))
+    share['frac'] = round(max(share['achieved_gbs'] / HBM_PEAK_GBS, share['achieved_tflops'] / FP32_PEAK_TFLOPS), 4)
     if t_hbm >= t_fl:
+        gbs = PIPE['bytes'] * frames_per_launch / t / 1e9
         return dict(bound='hbm', achieved=round(gbs, 1), peak=HBM_PEAK_GBS, unit='GB/s',
                     frac=round(gbs / HBM_PEAK_GBS, 4), traffic=traffic, kernel=kernel,
-                    alg_bytes_per_frame=a['bytes'], frames_per_launch=frames_per_launch)
+                    alg_bytes_per_frame=PIPE['bytes'], frames_per_launch=frames_per_launch, kernel_share=share)
+    tfl = fl * frames_per_launch / t / 1e12
     return dict(bound='valu_fp32', achieved=round(tfl, 3), peak=FP32_PEAK_TFLOPS, unit='TFLOP/s',
                 frac=round(tfl / FP32_PEAK_TFLOPS, 4), traffic=traffic, kernel=kernel,
-                alg_flops_per_frame=a['flops'], frames_per_launch=frames_per_launch)
+                alg_flops_per_frame=fl, frames_per_launch=frames_per_launch, kernel_share=share)
 
 
-def cpu_baseline(seconds, B=16, n=160000):
-    """The reference op mix on host cores (oracle/torch_port.py), bounded sample."""
+def cpu_baseline(seconds, B=256, n=160000):
+    """The reference op mix on host cores (oracle/torch_port.py), bounded
+    sample: B = 256 x 10 s streams, then a few batch-1 calls."""
     import numpy as np
     import torch
     sys.path.insert(0, os.path.join(REPO, 'oracle'))
@@ -113,7 +133,7 @@ def cpu_baseline(seconds, B=16, n=160000):
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     mic, ref, near = (torch.from_numpy(a) for a in synth.batch(B, n, seed0=5000))
-    port(mic[:2], ref[:2], near[:2])               # warm-up
+    port(mic[:2, :16000], ref[:2, :16000], near[:2, :16000])      # warm-up
     frames = 0
     t0 = time.perf_counter()
     reps = 0
@@ -124,9 +144,17 @@ def cpu_baseline(seconds, B=16, n=160000):
         el = time.perf_counter() - t0
         if el >= seconds and reps >= 2:
             break
+    lat = []
+    for i in range(3):
+        t1 = time.perf_counter()
+        port(mic[i:i + 1], ref[i:i + 1], near[i:i + 1])
+        lat.append(time.perf_counter() - t1)
+    b1 = float(np.median(lat))
     return dict(value=round(frames / el, 1), unit='frames/s', cores=threads, kind='port',
                 sample=f'{reps} x [{B} streams x {n} samples] through oracle/torch_port.py '
-                       f'(reference op mix: conv1d DFT, nn.GRU, conv_transpose1d), {el:.1f} s wall')
+                       f'(reference op mix: conv1d DFT, nn.GRU, conv_transpose1d), {el:.1f} s wall; '
+                       f'batch 1: median of 3 single 10 s streams',
+                batch1_frames_per_s=round((n // 256 + 1) / b1, 1), rtf_batch1=round(b1 / (n / 16000), 6))
 
 
 BF16_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
@@ -210,25 +238,19 @@ def _init_dist(torch, dist, world, local):
     return local
 
 
-def main_crn(args):
-    """BASELINE config 3: the DCCRN post-filter (bf16 MFMA), B streams x 10 s."""
+def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu):
+    """BASELINE config 3: the DCCRN post-filter (dccrn2.py, configs.net_conf) on
+    B streams x n samples; returns the measurements (timing = max over ranks)."""
     import numpy as np
     import torch
     import torch.distributed as dist
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    local = _init_dist(torch, dist, world, local)
-    dev = torch.device('cuda', local)
     import aec_amd
     from aec_amd import shard, synth
     conf = dict(aec_amd.net_conf)
-    B = args.streams
-    n = int(round(args.seconds * 16000))
     T = n // 256 + 1
     torch.manual_seed(0)                         # the reference's own init (random weights, no checkpoint ships)
     mod = aec_amd.dccrn if args.crn_version == 1 else aec_amd.dccrn2
-    net = mod.DCCRN(conf, dtype=args.crn_dtype).eval().to(dev)
+    net = mod.DCCRN(conf, dtype=dtype).eval().to(dev)
     mic, far, _ = (torch.from_numpy(a).to(dev) for a in synth.batch(B, n, seed0=1000 * rank))
     lens = [n] * B
 
@@ -236,7 +258,7 @@ def main_crn(args):
         return net.forward_ragged(mic, far, lens, want_spec=False)
 
     with torch.no_grad():
-        for _ in range(args.warmup):
+        for _ in range(warmup):
             step()
         torch.cuda.synchronize(dev)
         h = net._handle(dev)
@@ -246,7 +268,7 @@ def main_crn(args):
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(steps):
             step()
         torch.cuda.synchronize(dev)
         if world > 1:
@@ -262,23 +284,29 @@ def main_crn(args):
             net.forward_ragged(mic[:1], far[:1], [n], want_spec=False)
             torch.cuda.synchronize(dev)
             lat.append(time.perf_counter() - t1)
-        rtf1 = float(np.median(lat)) / args.seconds if lat else None
-    frames_total = world * B * T * args.steps
-    value = frames_total / el
-    ms_step = el / args.steps * 1e3
+        rtf1 = float(np.median(lat)) / (n / 16000) if lat else None
+    value = world * B * T * steps / el
+    ms_step = el / steps * 1e3
     stage_ms = {k: sms[i] / max(calls, 1) for i, k in enumerate(CRN_STAGES)}
     fl = crn_flops_per_frame(conf, args.crn_version)
     # fp8 runs only the LSTM input projections on the scaled fp8 MFMA; everything else is bf16,
     # so it is priced against the bf16 peak (conservative for the input-GEMM half of the LSTM stage)
-    peak = FP32_PEAK_TFLOPS if args.crn_dtype == 'f32' else BF16_PEAK_TFLOPS
+    peak = FP32_PEAK_TFLOPS if dtype == 'f32' else BF16_PEAK_TFLOPS
     dom = max(stage_ms, key=stage_ms.get)
     dom_fl = fl.get(dom, 0)
     ach = dom_fl * B * T / (stage_ms[dom] * 1e-3) / 1e12 if dom_fl else 0.0
-    whole = fl['total'] * B * T / (ms_step * 1e-3 / 1) / 1e12
-    cpu = None
-    erle = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline_crn(args.cpu_seconds, conf, args.crn_version, n=n)
+    whole = fl['total'] * B * T / (ms_step * 1e-3) / 1e12
+    res = dict(value=round(value, 1), value_per_gpu=round(value / world, 1), ms_per_step=round(ms_step, 3),
+               rtf_batch1=rtf1, stage_ms_per_step={k: round(v, 3) for k, v in stage_ms.items()},
+               roofline={'bound': 'mfma', 'achieved': round(ach, 1), 'peak': peak, 'unit': 'TFLOP/s',
+                         'frac': round(ach / peak, 4), 'traffic': None,
+                         'kernel': f'{dom} stage ({"input GEMM + per-frame recurrence steps + combine per layer" if dom == "lstm" else "GEMM launches"})',
+                         'alg_flops_per_frame': dom_fl, 'frames_per_launch': B * T},
+               pipeline_roofline={'alg_flops_per_frame': fl['total'], 'achieved_tflops': round(whole, 1),
+                                  'mfma_frac': round(whole / peak, 4)},
+               erle=None, cpu_baseline=None)
+    if with_cpu and rank == 0 and world == 1:
+        res['cpu_baseline'] = cpu_baseline_crn(args.cpu_seconds, conf, args.crn_version, n=n)
         sys.path.insert(0, os.path.join(REPO, 'oracle'))
         from torch_crn_port import TorchCrnPort
         wref = {k: v.detach().cpu().numpy() for k, v in net.state_dict().items()}
@@ -290,32 +318,45 @@ def main_crn(args):
                                              [len(m_)], want_spec=False)
             return o[0].cpu().numpy()
 
-        erle = erle_check(gpu1, lambda m_, f_, _n: port(torch.from_numpy(m_)[None], torch.from_numpy(f_)[None])[0].numpy(), n)
+        res['erle'] = erle_check(gpu1, lambda m_, f_, _n: port(torch.from_numpy(m_)[None],
+                                                               torch.from_numpy(f_)[None])[0].numpy(), n)
+    del net
+    torch.cuda.empty_cache()
+    return res
+
+
+def crn_workload(args, dtype, B):
+    return (f'C3 (BASELINE configs[2]): DCCRN v{args.crn_version} '
+            f'({"dccrn2.py" if args.crn_version == 2 else "dccrn.py"}, configs.net_conf, {dtype} MFMA) on {B} '
+            'concurrent 10 s 16 kHz streams per GPU, reference init (torch.manual_seed(0))')
+
+
+def main_crn(args):
+    """--pipeline crn: BASELINE config 3 as the headline line."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = _init_dist(torch, dist, world, int(os.environ.get('LOCAL_RANK', '0')))
+    dev = torch.device('cuda', local)
+    B = args.streams
+    n = int(round(args.seconds * 16000))
+    r = run_crn(args, dev, rank, world, args.crn_dtype, args.steps, args.warmup, B, n, not args.no_cpu)
     if rank == 0:
         line = {
             'metric': '16kHz frames/sec/GPU (batched AEC) + RTF@batch=1; ERLE delta vs reference',
-            'value': round(value, 1), 'unit': 'frames/s', 'n_gpus': world, 'steps': args.steps,
-            'warmup': args.warmup, 'ms_per_step': round(ms_step, 3), 'higher_is_better': True,
+            'value': r['value'], 'unit': 'frames/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': r['ms_per_step'], 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': args.crn_dtype, 'data': 'synthetic',
-            'config': {'workload': f'C3 (BASELINE configs[2]): DCCRN v{args.crn_version} '
-                                   f'({"dccrn2.py" if args.crn_version == 2 else "dccrn.py"}, configs.net_conf, '
-                                   f'{args.crn_dtype} MFMA) on {B} concurrent 10 s 16 kHz streams per GPU, '
-                                   'reference init (torch.manual_seed(0))',
-                       'streams_per_gpu': B, 'samples_per_stream': n, 'frames_per_stream': T,
+            'config': {'workload': crn_workload(args, args.crn_dtype, B),
+                       'streams_per_gpu': B, 'samples_per_stream': n, 'frames_per_stream': n // 256 + 1,
                        'frame': '256-sample hop', 'pipeline': 'crn',
                        'parallelism': f'streams sharded, {world} rank(s)'},
-            'xRT': round(value * 256 / 16000, 1),
-            'rtf_batch1': rtf1,
-            'stage_ms_per_step': {k: round(v, 3) for k, v in stage_ms.items()},
-            'roofline': {'bound': 'mfma', 'achieved': round(ach, 1), 'peak': peak, 'unit': 'TFLOP/s',
-                         'frac': round(ach / peak, 4), 'traffic': None,
-                         'kernel': f'{dom} stage ({"input GEMM + per-frame recurrence steps + combine per layer" if dom == "lstm" else "GEMM launches"})',
-                         'alg_flops_per_frame': dom_fl, 'frames_per_launch': B * T},
-            'pipeline_roofline': {'alg_flops_per_frame': fl['total'], 'achieved_tflops': round(whole, 1),
-                                  'mfma_frac': round(whole / peak, 4)},
-            'erle': erle,
-            'cpu_baseline': cpu,
+            'value_per_gpu': r['value_per_gpu'],
+            'xRT': round(r['value'] * 256 / 16000, 1),
         }
+        line.update({k: r[k] for k in ('rtf_batch1', 'stage_ms_per_step', 'roofline', 'pipeline_roofline',
+                                       'erle', 'cpu_baseline')})
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -402,26 +443,45 @@ def main():
     frames_total = world * B * T * args.steps
     value = frames_total / el
     ms_step = el / args.steps * 1e3
-    # `calls` counts kernel launches (aec_process splits a batch into sub-batches,
-    # one launch of each kernel per sub-batch); per-step = per-call sum
-    launches_per_step = max(calls, 1) / args.steps
+    # `calls` counts aec_process calls (profile marks per call; one launch of each
+    # kernel per call here: 256 streams, no sub-batching)
+    calls_per_step = max(calls, 1) / args.steps
     per_kernel_ms = {k: kms[i] / args.steps for i, k in enumerate(KERNELS)}
     per_launch_ms = {k: kms[i] / max(calls, 1) for i, k in enumerate(KERNELS)}
-    if args.pipeline == 'full' and os.environ.get('AEC_FUSED_SYNTH', '1') != '0':
+    pipe = os.environ.get('AEC_PIPE', '0') not in ('', '0')
+    if pipe:
+        # K1 moments + K6 (aec_pipe.hip): the whole chain in one launch, timed in the 'analysis' slot
+        kernels_per_call = ['moments_kernel', 'pipe_kernel']
+        for d in (per_kernel_ms, per_launch_ms):
+            d['pipe'] = d.pop('analysis') + d.pop('gru') + d.pop('synthesis')
+    elif args.pipeline == 'full' and os.environ.get('AEC_FUSED_SYNTH', '1') != '0':
         # one fused launch: its time is in the 'gru' slot, the 'synthesis' slot is an empty interval
+        kernels_per_call = ['moments_kernel', 'norm_finalize_kernel', 'nlms_analysis_kernel', 'gru_synth_kernel']
         for d in (per_kernel_ms, per_launch_ms):
             d['gru_synthesis'] = d.pop('gru') + d.pop('synthesis')
+    else:
+        kernels_per_call = ['moments_kernel', 'norm_finalize_kernel', 'analysis_kernel', 'gru_kernel',
+                            'synthesis_kernel']
+    launches_per_step = calls_per_step * len(kernels_per_call)
     dom = max(per_kernel_ms, key=per_kernel_ms.get)
     pmc = None
     pmc_path = os.path.join(REPO, 'profiles', f'pmc_latest_{args.pipeline}.json')
     if os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path))
-    roof = roofline(args.pipeline, dom, per_launch_ms[dom], int(round(B * T / launches_per_step)), pmc)
-    pipe_t = ms_step * 1e-3 / world
+    roof = roofline(args.pipeline, dom, per_launch_ms[dom], int(round(B * T / calls_per_step)), pmc)
+    pipe_t = ms_step * 1e-3
     pipe_gbs = PIPE['bytes'] * B * T / pipe_t / 1e9
-    pipe_tfl = PIPE['flops'] * B * T / pipe_t / 1e12
+    pipe_tfl = path_flops(args.pipeline) * B * T / pipe_t / 1e12
     cpu = None
     erle = None
+    c3 = None
+    if world == 1 and not args.no_c3:
+        # BASELINE config 3 (DCCRN bf16, 256 x 10 s) in the same driver-timed run
+        c3 = run_crn(args, dev, rank, world, 'bf16', args.c3_steps, 2, 256, 160000, False)
+        c3 = dict(workload=crn_workload(args, 'bf16', 256), dtype='bf16', steps=args.c3_steps,
+                  frames_per_s=c3['value'], ms_per_step=c3['ms_per_step'], rtf_batch1=c3['rtf_batch1'],
+                  stage_ms_per_step=c3['stage_ms_per_step'], roofline=c3['roofline'],
+                  pipeline_roofline=c3['pipeline_roofline'])
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_seconds)
         sys.path.insert(0, os.path.join(REPO, 'oracle'))
@@ -444,16 +504,20 @@ def main():
                        'streams_per_gpu': B, 'samples_per_stream': n, 'frames_per_stream': T,
                        'frame': '256-sample hop', 'pipeline': args.pipeline,
                        'parallelism': f'streams sharded, {world} rank(s)'},
+            'value_per_gpu': round(value / world, 1),
             'xRT': round(value * 256 / 16000, 1),
             'rtf_batch1': rtf1,
             'kernel_ms_per_step': {k: round(v, 4) for k, v in per_kernel_ms.items()},
+            'kernels_per_step': kernels_per_call,
             'launches_per_step': launches_per_step,
             'roofline': roof,
-            'pipeline_roofline': {'alg_bytes_per_frame': PIPE['bytes'], 'alg_flops_per_frame': PIPE['flops'],
+            'pipeline_roofline': {'alg_bytes_per_frame': PIPE['bytes'],
+                                  'alg_flops_per_frame': path_flops(args.pipeline),
                                   'hbm_frac': round(pipe_gbs / HBM_PEAK_GBS, 4),
                                   'fp32_frac': round(pipe_tfl / FP32_PEAK_TFLOPS, 4)},
             'erle': erle,
             'cpu_baseline': cpu,
+            'c3_crn_bf16': c3,
         }
         if sweep:
             line['batch_sweep_frames_per_s'] = sweep

@@ -7,7 +7,7 @@ ALT=$1; PIPE=${2:-full}
 mkdir -p $R/gpurun_out
 for v in base alt base alt; do
   if [ $v = alt ]; then export AEC_HIP_LIB=$ALT; else unset AEC_HIP_LIB; fi
-  timeout -k 10 120 python $R/bench.py --pipeline $PIPE --no-cpu --no-rtf --steps 50 > $R/gpurun_out/lib_ab_${PIPE}_$v.log 2>&1 || exit 1
+  timeout -k 10 120 python $R/bench.py --pipeline $PIPE --no-cpu --no-c3 --no-rtf --steps 50 > $R/gpurun_out/lib_ab_${PIPE}_$v.log 2>&1 || exit 1
   python - "$v" "$R/gpurun_out/lib_ab_${PIPE}_$v.log" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])

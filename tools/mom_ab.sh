@@ -4,7 +4,7 @@ set -uo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out
 for c in ${CFGS:-0 1 2 3 4 5 0}; do
-  AEC_MOM_CFG=$c timeout -k 10 120 python $R/bench.py --no-cpu --no-rtf --steps 50 > $R/gpurun_out/mom_ab_$c.log 2>&1 || exit 1
+  AEC_MOM_CFG=$c timeout -k 10 120 python $R/bench.py --no-cpu --no-c3 --no-rtf --steps 50 > $R/gpurun_out/mom_ab_$c.log 2>&1 || exit 1
   python - "$c" "$R/gpurun_out/mom_ab_$c.log" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])

@@ -13,6 +13,6 @@ for set in "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS
            "SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_WAIT_INST_ANY" \
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --pmc $set --output-format csv -d "$OUT/p$i" -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu > "$OUT/p$i.log" 2>&1 || exit 1
+  timeout -k 10 240 rocprofv3 --pmc $set --output-format csv -d "$OUT/p$i" -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu --no-c3 > "$OUT/p$i.log" 2>&1 || exit 1
 done
 echo done
