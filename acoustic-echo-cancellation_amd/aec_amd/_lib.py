@@ -30,6 +30,7 @@ EXPORTS = ('aec_weights_count', 'aec_create', 'aec_set_weights', 'aec_set_erb', 
 
 # every symbol include/aec_crn.h declares
 CRN_EXPORTS = ('aec_crn_param_count', 'aec_crn_create', 'aec_crn_set_params', 'aec_crn_process', 'aec_crn_stft',
+               'aec_crn_error_spec',
                'aec_crn_stream_open', 'aec_crn_stream_reset', 'aec_crn_stream_step',
                'aec_crn_profile_enable', 'aec_crn_profile_read', 'aec_crn_last_error', 'aec_crn_destroy')
 
@@ -39,7 +40,9 @@ class CrnConfig(ctypes.Structure):
     _fields_ = [('version', ctypes.c_int32), ('n_layers', ctypes.c_int32),
                 ('conv_channels', ctypes.c_int32 * 9), ('hidden_dim', ctypes.c_int32),
                 ('rnn_layers', ctypes.c_int32), ('use_cbn', ctypes.c_int32),
-                ('masking_mode', ctypes.c_int32), ('dtype', ctypes.c_int32)]
+                ('masking_mode', ctypes.c_int32), ('dtype', ctypes.c_int32),
+                ('nlms_taps', ctypes.c_int32), ('nlms_mu', ctypes.c_float), ('nlms_beta', ctypes.c_float),
+                ('nlms_delta', ctypes.c_float)]
 
 
 class AecConfig(ctypes.Structure):
@@ -112,6 +115,8 @@ def load():
     lib.aec_crn_process.restype = ctypes.c_int
     lib.aec_crn_stft.argtypes = [P, P, P, ctypes.c_int32, ctypes.c_int64, P, P]
     lib.aec_crn_stft.restype = ctypes.c_int
+    lib.aec_crn_error_spec.argtypes = [P, P, P]
+    lib.aec_crn_error_spec.restype = ctypes.c_int
     lib.aec_crn_stream_open.argtypes = [P, ctypes.c_int32]
     lib.aec_crn_stream_open.restype = ctypes.c_int
     lib.aec_crn_stream_reset.argtypes = [P, ctypes.c_int32, P]
@@ -226,8 +231,10 @@ class Handle:
             pass
 
 
-def crn_config(version, conf, dtype):
-    """aec_crn_config from a reference config dict (configs.net_conf, configs.py:29-46)."""
+def crn_config(version, conf, dtype, nlms=None):
+    """aec_crn_config from a reference config dict (configs.net_conf, configs.py:29-46);
+    nlms: None (the reference network) or dict(taps, mu, beta, delta) for the
+    build-defined FD-NLMS front end (include/aec_crn.h)."""
     ch = list(conf['conv_channels'])
     if len(ch) > 9:
         raise NotImplementedError('at most 8 encoder layers')
@@ -241,6 +248,11 @@ def crn_config(version, conf, dtype):
     c.use_cbn = int(bool(conf.get('use_cbn', False)))
     c.masking_mode = ord(conf.get('masking_mode', 'C')[0]) if version == 2 else ord('C')
     c.dtype = {'f32': 0, 'float32': 0, 'bf16': 1, 'bfloat16': 1, 'fp8': 2, 'mxfp8': 2}[dtype]
+    if nlms:
+        c.nlms_taps = int(nlms.get('taps', 4))
+        c.nlms_mu = float(nlms.get('mu', 0.3))
+        c.nlms_beta = float(nlms.get('beta', 0.5))
+        c.nlms_delta = float(nlms.get('delta', 1e-4))
     return c
 
 
@@ -252,9 +264,9 @@ def crn_param_count(version, conf, dtype='f32'):
 class CrnHandle:
     """Owns one aec_crn_handle (include/aec_crn.h), one per device."""
 
-    def __init__(self, version, conf, dtype, device: int):
+    def __init__(self, version, conf, dtype, device: int, nlms=None):
         self.lib = load()
-        self.cfg = crn_config(version, conf, dtype)
+        self.cfg = crn_config(version, conf, dtype, nlms)
         h = ctypes.c_void_p()
         check(self.lib.aec_crn_create(ctypes.byref(self.cfg), None, 0, int(device), ctypes.byref(h)), None,
               'aec_crn_create (unsupported config?)')
@@ -277,6 +289,9 @@ class CrnHandle:
         lens = np.ascontiguousarray(lengths, dtype=np.int64)
         check(self.lib.aec_crn_stft(self.h, x_ptr, lens.ctypes.data, int(B), int(ld), spec_ptr, stream), self.h,
               'aec_crn_stft', True)
+
+    def error_spec(self, spec_ptr, stream):
+        check(self.lib.aec_crn_error_spec(self.h, spec_ptr, stream), self.h, 'aec_crn_error_spec', True)
 
     def stream_open(self, B):
         check(self.lib.aec_crn_stream_open(self.h, int(B)), self.h, 'aec_crn_stream_open', True)

@@ -109,12 +109,14 @@ class NavieComplexLSTM(nn.Module):
 class _DCCRNBase(nn.Module):
     VERSION = 0
 
-    def __init__(self, config, dtype='f32'):
+    def __init__(self, config, dtype='f32', nlms=None):
         super().__init__()
         self.config = config
         self.dtype_name = dtype
+        self.nlms = dict(nlms) if nlms else None   # build-defined FD-NLMS front end (include/aec_crn.h)
         self._handles = {}
         self._p_key = {}
+        self._last_shape = {}                      # device index -> (B, Tmax) of the last forward
 
     # ---- parameter blob (include/aec_crn.h order) ---------------------------
     def _norm_names(self, prefix, cbn):
@@ -152,7 +154,7 @@ class _DCCRNBase(nn.Module):
         idx = device.index if device.index is not None else torch.cuda.current_device()
         h = self._handles.get(idx)
         if h is None:
-            h = _lib.CrnHandle(self.VERSION, self.config, self.dtype_name, idx)
+            h = _lib.CrnHandle(self.VERSION, self.config, self.dtype_name, idx, self.nlms)
             self._handles[idx] = h
         sd = self.state_dict(keep_vars=True)
         key = tuple((sd[n].data_ptr(), sd[n]._version) for n in self.param_names())
@@ -188,6 +190,19 @@ class _DCCRNBase(nn.Module):
         x = x.contiguous().float()
         with torch.cuda.device(x.device):
             h.stft(x.data_ptr(), lengths, B, N, spec.data_ptr(), torch.cuda.current_stream(x.device).cuda_stream)
+        return torch.cat([spec[..., 0], spec[..., 1]], dim=2).transpose(1, 2)
+
+    def error_spectra(self, device):
+        """NLMS networks: the FD-NLMS error spectrum E of the last forward on
+        ``device`` (the spectrum the mask was applied to) -> [B, 514, T]."""
+        if not self.nlms:
+            raise RuntimeError('error_spectra needs a network built with nlms=...')
+        dev = torch.device(device)
+        h = self._handle(dev)
+        B, T = self._last_shape[dev.index if dev.index is not None else torch.cuda.current_device()]
+        spec = torch.empty(B, T, 257, 2, device=dev, dtype=torch.float32)
+        with torch.cuda.device(dev):
+            h.error_spec(spec.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
         return torch.cat([spec[..., 0], spec[..., 1]], dim=2).transpose(1, 2)
 
     # ---- streaming (include/aec_crn.h aec_crn_stream_*) ------------------------
@@ -244,6 +259,7 @@ class _DCCRNBase(nn.Module):
             h.process(mic.data_ptr(), far.data_ptr(), lengths, B, N, out.data_ptr() if lout > 0 else None,
                       max(lout, 1), spec.data_ptr() if spec is not None else None,
                       mask.data_ptr() if mask is not None else None, torch.cuda.current_stream(dev).cuda_stream)
+        self._last_shape[dev.index if dev.index is not None else torch.cuda.current_device()] = (B, T)
         out_spec = torch.cat([spec[..., 0], spec[..., 1]], dim=2).transpose(1, 2) if spec is not None else None
         mk = mask.permute(0, 3, 2, 1) if mask is not None else None
         return out, out_spec, mk

@@ -16,8 +16,8 @@ from .crn import (ComplexConvTranspose2d, _check_fixed, _ConviSTFTBuffers, _Conv
 class DCCRN(_DCCRNBase):
     VERSION = 1
 
-    def __init__(self, config, dtype='f32'):
-        super().__init__(config, dtype)
+    def __init__(self, config, dtype='f32', nlms=None):
+        super().__init__(config, dtype, nlms)
         _check_fixed(config)
         ch = config['conv_channels']
         self.encoder = nn.ModuleList()
@@ -52,7 +52,9 @@ class DCCRN(_DCCRNBase):
         out_wav, out_spec, mask = self.forward_ragged(mic, far, [N] * B, want_spec=True, want_mask=True)
         near_specs = self.spectra(near)
         # training loss (dccrn.py:556-581) from the GPU spectra and mask (elementwise)
-        ms, es = self.spectra(mic), self.spectra(echo)
+        # (an NLMS network masks the error spectrum E, so E is the cRM reference)
+        ms = self.error_spectra(mic.device) if self.nlms else self.spectra(mic)
+        es = self.spectra(echo)
         K = 257
         mr, mi = ms[:, :K], ms[:, K:]
         nr, ni = near_specs[:, :K], near_specs[:, K:]

@@ -17,8 +17,8 @@ from .crn import (ComplexBatchNorm, ComplexConvTranspose2d, NavieComplexLSTM, _c
 class DCCRN(_DCCRNBase):
     VERSION = 2
 
-    def __init__(self, config, dtype='f32'):
-        super().__init__(config, dtype)
+    def __init__(self, config, dtype='f32', nlms=None):
+        super().__init__(config, dtype, nlms)
         _check_fixed(config)
         if not config['use_clstm']:
             raise NotImplementedError('dccrn2.DCCRN needs use_clstm=True (dccrn2.py:114-116)')

@@ -17,6 +17,7 @@
 
 #include "../../include/aec_crn.h"
 #include "aec_device.h"
+#include "aec_launch.h"
 #include "aec_tables.h"
 #include "crn_launch.h"
 
@@ -90,8 +91,14 @@ struct aec_crn_handle {
     uint8_t* as = nullptr;
     float* cst = nullptr;
     float* mask = nullptr;
+    float2* nrows = nullptr;                       // NLMS: packed mic / far rows [B][T][2][256]
+    float2* espec = nullptr;                       //       error rows E [B][T][256]
+    float2* ndummy = nullptr;                      //       [B][256] sink for frames past a stream's end
     int64_t* d_len = nullptr;
     std::vector<int64_t> last_lens;                // host copy of what d_len holds
+    int32_t last_B = 0;                            // shape of the last aec_crn_process call (aec_crn_error_spec)
+    int64_t last_T = 0;
+    std::vector<int64_t> proc_lens;                //   and its lengths
     std::vector<void*> allocs;
     StreamState* ss = nullptr;                     // aec_crn_stream_* state
     // profiling
@@ -132,6 +139,10 @@ static std::string check_cfg(const aec_crn_config& c) {
         if (c.rnn_layers < 1 || c.rnn_layers > 8) return "rnn_layers out of range";
         if (c.masking_mode != 'E' && c.masking_mode != 'C' && c.masking_mode != 'R') return "masking_mode must be E, C or R";
     }
+    if (c.nlms_taps < 0 || c.nlms_taps > 8) return "nlms_taps must be 0..8";
+    if (c.nlms_taps > 0 && !(c.nlms_mu >= 0.f && c.nlms_mu < 2.f && c.nlms_beta >= 0.f && c.nlms_beta < 1.f &&
+                             c.nlms_delta > 0.f))
+        return "NLMS needs mu in [0, 2), beta in [0, 1), delta > 0";
     return "";
 }
 
@@ -473,6 +484,7 @@ static aec_status ensure_ws(aec_crn_handle* h, int64_t B, int64_t T) {
     for (void* p : h->allocs) (void)hipFree(p);
     h->allocs.clear();
     h->last_lens.clear();                          // d_len is reallocated below
+    h->last_B = 0;                                 // and the NLMS rows with it
     const int64_t nB = std::max<int64_t>(B, h->ws_B), nT = std::max<int64_t>(T, h->ws_T);
     const int64_t BT = nB * nT;
     const size_t es = h->es;
@@ -495,6 +507,11 @@ static aec_status ensure_ws(aec_crn_handle* h, int64_t B, int64_t T) {
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->cst), (size_t)nB * h->CELLS * h->S * h->H * sizeof(float)));
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->mask), (size_t)BT * 256 * 2 * sizeof(float)));
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->d_len), (size_t)nB * sizeof(int64_t)));
+    if (h->cfg.nlms_taps > 0) {
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->nrows), (size_t)BT * 512 * sizeof(float2)));
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->espec), (size_t)BT * 256 * sizeof(float2)));
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->ndummy), (size_t)nB * 256 * sizeof(float2)));
+    }
     h->ws_B = nB;
     h->ws_T = nT;
     return AEC_OK;
@@ -666,8 +683,16 @@ static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int
     const int H = h->H, S = h->S, C = h->CELLS;
     mark(h, st);
     // front: X0 [Tmax][B][256][8]
+    const aec_crn_config& c = h->cfg;
     crn::FrontArgs fa{mic, far, ld, h->d_len, Tmax, h->d_tab, h->x0, nullptr};
+    if (c.nlms_taps > 0) fa.rows = h->nrows;
     CRN_TRY(h, crn::launch_front<T>(fa, B, st));
+    if (c.nlms_taps > 0) {   // FD-NLMS: rows -> E rows (one block per stream) -> X0
+        CRN_TRY(h, aec::launch_nlms_recursion(h->nrows, h->espec, h->d_len, Tmax, c.nlms_taps, c.nlms_mu, c.nlms_beta,
+                                              c.nlms_delta, 0, B, h->ndummy, st));
+        crn::RowsX0Args xa{h->nrows, h->espec, h->d_len, Tmax, h->x0, B};
+        CRN_TRY(h, crn::launch_rows_x0<T>(xa, st));
+    }
     mark(h, st);
     aec_status s = run_encoder<T>(h, bf, BT, st);
     if (s != AEC_OK) return s;
@@ -692,6 +717,7 @@ static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int
     if (out || spec) {
         crn::BackArgs ba{mic, ld, h->d_len, Tmax, h->d_tab, reinterpret_cast<const float2*>(h->mask), out, ld_out,
                          reinterpret_cast<float2*>(spec)};
+        if (c.nlms_taps > 0) ba.espec = h->espec;
         CRN_TRY(h, crn::launch_back(ba, B, mask_mode(h), st));
     }
     if (mask_out)   // internal frames are t-major ([Tmax][B]); the ABI's mask is [B][Tmax]
@@ -722,6 +748,9 @@ struct StreamState {
     float* hop = nullptr;                // [2 parity][2 signal][B][256] input hop ring (mic, far)
     float* tail = nullptr;               // [B][256] overlap-add tail
     float* out = nullptr;                // [B][256] output hop
+    float2* nrows = nullptr;             // NLMS: packed rows [B][2][256]
+    float2* nstate = nullptr;            //       recursion state [B][2*taps][256]
+    float2* espec = nullptr;             //       E rows [B][256]
     hipGraphExec_t graph[2] = {nullptr, nullptr};
     hipStream_t cap = nullptr;           // capture stream
 };
@@ -745,8 +774,14 @@ static aec_status stream_launches(aec_crn_handle* h, int par, hipStream_t st) {
     const float* cur_far = ss.hop + (size_t)(par * 2 + 1) * B * 256;
     const float* prev_mic = ss.hop + (size_t)((1 - par) * 2 + 0) * B * 256;
     const float* prev_far = ss.hop + (size_t)((1 - par) * 2 + 1) * B * 256;
+    const aec_crn_config& c = h->cfg;
     crn::StreamFrontArgs fa{prev_mic, cur_mic, prev_far, cur_far, h->d_tab, ss.x0, B};
+    if (c.nlms_taps > 0) fa.rows = ss.nrows;
     CRN_TRY(h, crn::launch_stream_front<T>(fa, st));
+    if (c.nlms_taps > 0) {
+        crn::StreamNlmsArgs na{ss.nrows, ss.nstate, ss.espec, ss.x0, B, c.nlms_mu, c.nlms_beta, c.nlms_delta};
+        CRN_TRY(h, crn::launch_stream_nlms<T>(na, c.nlms_taps, st));
+    }
     aec_status s = run_encoder<T>(h, bf, B, st);
     if (s != AEC_OK) return s;
     for (int l = 0; l < h->nrnn; ++l) {
@@ -760,6 +795,7 @@ static aec_status stream_launches(aec_crn_handle* h, int par, hipStream_t st) {
     s = run_decoder<T>(h, bf, B, st);
     if (s != AEC_OK) return s;
     crn::StreamBackArgs ba{prev_mic, cur_mic, h->d_tab, reinterpret_cast<const float2*>(ss.mask), ss.tail, ss.out, B};
+    if (c.nlms_taps > 0) ba.espec = ss.espec;
     CRN_TRY(h, crn::launch_stream_back(ba, mask_mode(h), st));
     return AEC_OK;
 }
@@ -871,6 +907,9 @@ aec_status aec_crn_process(aec_crn_handle* h, const float* mic, const float* far
     s = h->es == 4 ? run<float>(h, mic, far, B, ld, Tmax, out, ld_out, spec, mask, st)
                    : run<bf16_t>(h, mic, far, B, ld, Tmax, out, ld_out, spec, mask, st);
     if (s != AEC_OK) return s;
+    h->last_B = B;
+    h->last_T = Tmax;
+    h->proc_lens = h->last_lens;
     if (h->profile && h->ev_used == 6) {
         CRN_TRY(h, hipEventSynchronize(h->ev[5]));
         for (int k = 0; k < 5; ++k) {
@@ -894,6 +933,22 @@ aec_status aec_crn_stft(aec_crn_handle* h, const float* x, const int64_t* length
     if (s != AEC_OK) return s;
     crn::FrontArgs fa{x, x, ld, h->d_len, Tmax, h->d_tab, nullptr, reinterpret_cast<float2*>(spec)};
     CRN_TRY(h, crn::launch_front<float>(fa, B, st));
+    return AEC_OK;
+}
+
+aec_status aec_crn_error_spec(aec_crn_handle* h, float* spec, void* stream) {
+    if (!h || !spec) return AEC_ERR_INVALID_ARG;
+    if (h->cfg.nlms_taps <= 0) return crn_fail(h, AEC_ERR_INVALID_ARG, "the handle has no NLMS front end");
+    if (h->last_B <= 0) return crn_fail(h, AEC_ERR_INVALID_ARG, "no aec_crn_process call yet");
+    aec::DeviceGuard dg(h->device);   // the caller's current device is restored on return
+    if (dg.err != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (h->last_lens != h->proc_lens) {   // an aec_crn_stft since then uploaded other lengths
+        h->last_lens = h->proc_lens;
+        CRN_TRY(h, hipMemcpyAsync(h->d_len, h->last_lens.data(), h->last_lens.size() * sizeof(int64_t),
+                                  hipMemcpyHostToDevice, st));
+    }
+    CRN_TRY(h, crn::launch_unpack_rows(h->espec, h->d_len, h->last_B, h->last_T, reinterpret_cast<float2*>(spec), st));
     return AEC_OK;
 }
 
@@ -937,6 +992,11 @@ aec_status aec_crn_stream_open(aec_crn_handle* h, int32_t B) {
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.hop), (size_t)4 * B * 256 * sizeof(float)));
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.tail), (size_t)B * 256 * sizeof(float)));
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.out), (size_t)B * 256 * sizeof(float)));
+    if (h->cfg.nlms_taps > 0) {
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.nrows), (size_t)B * 512 * sizeof(float2)));
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.nstate), (size_t)B * 2 * h->cfg.nlms_taps * 256 * sizeof(float2)));
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.espec), (size_t)B * 256 * sizeof(float2)));
+    }
     CRN_TRY(h, hipStreamCreateWithFlags(&ss.cap, hipStreamNonBlocking));
     CRN_TRY(h, hipDeviceSynchronize());
     ss.k = 0;
@@ -959,6 +1019,10 @@ aec_status aec_crn_stream_reset(aec_crn_handle* h, int32_t b, void* stream) {
     for (int q = 0; q < 4; ++q)
         CRN_TRY(h, hipMemsetAsync(ss.hop + ((size_t)q * ss.B + b0) * 256, 0, (size_t)nb * 256 * sizeof(float), st));
     CRN_TRY(h, hipMemsetAsync(ss.tail + (size_t)b0 * 256, 0, (size_t)nb * 256 * sizeof(float), st));
+    if (ss.nstate) {   // NLMS: W, history, P = 0 (a fresh recursion)
+        const size_t srow = (size_t)2 * h->cfg.nlms_taps * 256;
+        CRN_TRY(h, hipMemsetAsync(ss.nstate + b0 * srow, 0, nb * srow * sizeof(float2), st));
+    }
     if (b < 0) ss.k = 0;
     return AEC_OK;
 }

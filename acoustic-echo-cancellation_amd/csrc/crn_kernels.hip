@@ -25,6 +25,7 @@
 #include <stdlib.h>
 
 #include "aec_fft.h"
+#include "aec_frame.h"
 #include "aec_stft.h"
 #include "aec_tables.h"
 #include "crn_gemm.h"
@@ -57,6 +58,25 @@ __device__ __forceinline__ void put_bin<bf16_t>(bf16_t* row, int k, float2 m, fl
     v[2] = 0u;
     v[3] = 0u;
     *reinterpret_cast<u32x4*>(row + (int64_t)(k - 1) * 8) = v;
+}
+
+// One frame's packed spectrum row (256 float2, slot 0 = (X[0], X[256])) from
+// the unpacked pairs of its 16-lane group: the row layout of
+// aec::row_to_scr, read by the NLMS recursion (aec_kernels.hip).
+__device__ __forceinline__ void put_row(float2* row, int lb, bool live, const float2 (&xa)[8], const float2 (&xb)[8],
+                                        float2 x128) {
+    const float2 z = make_float2(0.f, 0.f);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const int kk = lb + 16 * m;
+        if (kk == 0) {
+            row[0] = live ? make_float2(xa[0].x, xb[0].x) : z;
+        } else {
+            row[kk] = live ? xa[m] : z;
+            row[256 - kk] = live ? xb[m] : z;
+        }
+    }
+    if (lb == 0) row[128] = live ? x128 : z;
 }
 
 template <typename T, bool kSpec>
@@ -108,6 +128,12 @@ __global__ __launch_bounds__(256) void crn_front_kernel(FrontArgs p) {
     if (t >= p.Tmax) return;
     const bool live = t < Tn;
     const float2 z = make_float2(0.f, 0.f);
+    if (!kSpec && p.rows) {   // NLMS: packed mic / far rows [B][Tmax][2][256]; X0 comes from E later
+        float2* r0 = p.rows + ((int64_t)b * p.Tmax + t) * 512;
+        put_row(r0, lb, live, ma, mb, m128);
+        put_row(r0 + 256, lb, live, fa, fb, f128);
+        return;
+    }
     if (kSpec) {   // complex spectrum [B][Tmax][257] of `mic` (ConvSTFT output, dccrn.py:45-52)
         float2* srow = p.spec + ((int64_t)b * p.Tmax + t) * 257;
 #pragma unroll
@@ -180,21 +206,25 @@ __global__ __launch_bounds__(256) void crn_back_kernel(BackArgs p) {
     float* scr = wr + gg * kGroupFloats;
     const bool aligned = ((p.ld & 3) == 0) && ((reinterpret_cast<uintptr_t>(p.mic) & 15) == 0);
     const int tw0 = (int)(h0 + kWaveFrames * wave);
-    float4 pf[kWavePf];
-    aec::wave_prefetch(pf, p.mic + (int64_t)b * p.ld, (int)n, tw0, lane, aligned);
-    aec::wave_fence();
-    aec::wave_commit(wr, pf, 0.f, (int)n, tw0, lane);
-    aec::wave_fence();
-    float2 v[16];
-    float2 xa[8], xb[8], x128;
-    aec::load_frame(v, wr, sHann, gg, lb);
-    aec::wave_fence();
-    aec::fft256<false>(v, lb, scr, sTwT);
-    aec::rfft_unpack(v, lb, sTw512, xa, xb, x128);
-
-    // mask row of frame t (bins 1..256 -> index bin-1); DC has mask 0 (F.pad, dccrn.py:577-578)
     const int64_t t = h0 + g;
     const bool live = t <= nhop && t < p.Tmax;
+    float2 v[16];
+    float2 xa[8], xb[8], x128;
+    if (p.espec) {   // NLMS: the error rows (frames past the stream end read as zeros)
+        aec::row_to_pairs(p.espec + ((int64_t)b * p.Tmax + (live ? t : 0)) * 256, lb, live, xa, xb, x128);
+    } else {
+        float4 pf[kWavePf];
+        aec::wave_prefetch(pf, p.mic + (int64_t)b * p.ld, (int)n, tw0, lane, aligned);
+        aec::wave_fence();
+        aec::wave_commit(wr, pf, 0.f, (int)n, tw0, lane);
+        aec::wave_fence();
+        aec::load_frame(v, wr, sHann, gg, lb);
+        aec::wave_fence();
+        aec::fft256<false>(v, lb, scr, sTwT);
+        aec::rfft_unpack(v, lb, sTw512, xa, xb, x128);
+    }
+
+    // mask row of frame t (bins 1..256 -> index bin-1); DC has mask 0 (F.pad, dccrn.py:577-578)
     const float2* mrow = p.mask + ((int64_t)(live ? t : 0) * gridDim.y + b) * 256;   // frame f = t*B + b
     const float2 z = make_float2(0.f, 0.f);
     auto mk = [&](int bin) { return (live && bin > 0) ? mrow[bin - 1] : z; };
@@ -311,6 +341,11 @@ __global__ __launch_bounds__(256) void crn_stream_front_kernel(StreamFrontArgs p
         aec::wave_fence();
     }
     if (b >= p.B) return;
+    if (p.rows) {   // NLMS: packed rows [B][2][256]; crn_stream_nlms_kernel writes X0
+        put_row(p.rows + (int64_t)b * 512, lb, true, ma, mb, m128);
+        put_row(p.rows + (int64_t)b * 512 + 256, lb, true, fa, fb, f128);
+        return;
+    }
     T* row = reinterpret_cast<T*>(p.x0) + (int64_t)b * 256 * 8;
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
@@ -341,14 +376,18 @@ __global__ __launch_bounds__(256) void crn_stream_back_kernel(StreamBackArgs p) 
     const int b = blockIdx.x * 16 + g;
     const int bb = b < p.B ? b : p.B - 1;
     float* reg = sGrp + g * kGroupFloats;
-    stage_frame(reg, p.prev_mic + (int64_t)bb * 256, p.cur_mic + (int64_t)bb * 256, lb);
-    aec::wave_fence();
     float2 v[16];
     float2 xa[8], xb[8], x128;
-    aec::load_frame(v, reg, sHann, 0, lb);
-    aec::wave_fence();
-    aec::fft256<false>(v, lb, reg, sTwT);
-    aec::rfft_unpack(v, lb, sTw512, xa, xb, x128);
+    if (p.espec) {   // NLMS: this frame's error row
+        aec::row_to_pairs(p.espec + (int64_t)bb * 256, lb, true, xa, xb, x128);
+    } else {
+        stage_frame(reg, p.prev_mic + (int64_t)bb * 256, p.cur_mic + (int64_t)bb * 256, lb);
+        aec::wave_fence();
+        aec::load_frame(v, reg, sHann, 0, lb);
+        aec::wave_fence();
+        aec::fft256<false>(v, lb, reg, sTwT);
+        aec::rfft_unpack(v, lb, sTw512, xa, xb, x128);
+    }
     const float2* mrow = p.mask + (int64_t)bb * 256;
     const float2 z = make_float2(0.f, 0.f);
     auto mk = [&](int bin) { return bin > 0 ? mrow[bin - 1] : z; };
@@ -399,6 +438,138 @@ __global__ __launch_bounds__(256) void crn_stream_back_kernel(StreamBackArgs p) 
         tail[r] = reg[256 + r];
     }
 }
+
+// --------------------------------------------------------------------------
+// FD-NLMS front end (aec_crn_config.nlms_taps > 0): the encoder's mic
+// channels and the masked spectrum are the NLMS error E (aec_hip.h recursion;
+// the per-bin arithmetic is aec::NlmsBin, shared with the Little_net path).
+// Batch: crn_front_kernel writes packed rows, aec::nlms_recursion_kernel
+// turns them into E rows, crn_rows_x0_kernel builds X0.  Streaming:
+// crn_stream_nlms_kernel advances every stream's recursion by one frame.
+// --------------------------------------------------------------------------
+// X0 bin k (k = 1..256) of one frame from its packed E / far rows
+template <typename T>
+__device__ __forceinline__ void x0_bin(T* row, int k, const float2* e, const float2* f) {
+    if (k < 256)
+        put_bin<T>(row, k, e[k], f[k]);
+    else   // Nyquist: the real half of slot 0
+        put_bin<T>(row, 256, make_float2(e[0].y, 0.f), make_float2(f[0].y, 0.f));
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void crn_rows_x0_kernel(RowsX0Args p) {
+    const int64_t f = blockIdx.x;                 // frame f = t*B + b
+    const int b = (int)(f % p.B);
+    const int64_t t = f / p.B;
+    const int k = threadIdx.x + 1;
+    T* row = reinterpret_cast<T*>(p.x0) + f * 256 * 8;
+    if (t >= p.lens[b] / kHop + 1) {
+        put_bin<T>(row, k, make_float2(0.f, 0.f), make_float2(0.f, 0.f));
+        return;
+    }
+    const float2* e = p.espec + ((int64_t)b * p.Tmax + t) * 256;
+    const float2* fr = p.rows + ((int64_t)b * p.Tmax + t) * 512 + 256;
+    x0_bin<T>(row, k, e, fr);
+}
+
+template <typename T, int TAPS>
+__global__ __launch_bounds__(256) void crn_stream_nlms_kernel(StreamNlmsArgs p) {
+    using aec::v2f;
+    const int b = blockIdx.x, k = threadIdx.x;
+    float2* nst = p.state + (int64_t)b * (2 * TAPS) * 256;
+    // restore (aec_stream.hip's layout: taps, raw far history, power); the
+    // history operands are re-derived with step()'s own expressions
+    aec::NlmsBin<TAPS> nb;
+    nb.reset(k == 0);
+    float2 rh[TAPS > 1 ? TAPS - 1 : 1];
+#pragma unroll
+    for (int l = 0; l < TAPS; ++l) {
+        const float2 w = nst[l * 256 + k];
+        nb.w[l] = v2f{w.x, w.y};
+    }
+#pragma unroll
+    for (int l = 0; l + 1 < TAPS; ++l) {
+        const float2 r2 = nst[(TAPS + l) * 256 + k];
+        rh[l] = r2;
+        const v2f r{r2.x, r2.y};
+        nb.a[l] = r * nb.ma;
+        nb.bq[l] = aec::vfma(v2f{r.y, r.x}, nb.mb, r * nb.mc);
+        nb.qq[l] = aec::vfma(nb.a[l], nb.a[l], nb.bq[l] * nb.bq[l]);
+    }
+    const float2 pp = nst[(2 * TAPS - 1) * 256 + k];
+    nb.p = v2f{pp.x, pp.y};
+    const float2* rows = p.rows + (int64_t)b * 512;
+    const float2 r = rows[256 + k];
+    const float2 e = nb.step(rows[k], r, p.mu, p.beta, p.delta);
+#pragma unroll
+    for (int l = 0; l < TAPS; ++l) nst[l * 256 + k] = make_float2(nb.w[l].x, nb.w[l].y);
+    if constexpr (TAPS > 1) {
+        nst[TAPS * 256 + k] = r;
+#pragma unroll
+        for (int l = 1; l + 1 < TAPS; ++l) nst[(TAPS + l) * 256 + k] = rh[l - 1];
+    }
+    nst[(2 * TAPS - 1) * 256 + k] = make_float2(nb.p.x, nb.p.y);
+    float2* erow = p.espec + (int64_t)b * 256;
+    erow[k] = e;
+    // X0 bin k (k >= 1) or, on lane 0, the Nyquist bin: from this lane's own
+    // values (slot k of E and far), so no exchange is needed
+    T* row = reinterpret_cast<T*>(p.x0) + (int64_t)b * 256 * 8;
+    if (k > 0)
+        put_bin<T>(row, k, e, r);
+    else
+        put_bin<T>(row, 256, make_float2(e.y, 0.f), make_float2(r.y, 0.f));
+}
+
+// E rows [B][Tmax][256] (packed) -> complex spectrum [B][Tmax][257]; frames t >= T_b zero
+__global__ __launch_bounds__(256) void crn_unpack_rows_kernel(const float2* __restrict__ espec,
+                                                              const int64_t* __restrict__ lens, int64_t Tmax,
+                                                              float2* __restrict__ spec) {
+    const int64_t f = blockIdx.x;                 // f = b*Tmax + t
+    const int b = (int)(f / Tmax);
+    const int64_t t = f - (int64_t)b * Tmax;
+    const int k = threadIdx.x;
+    const bool live = t < lens[b] / kHop + 1;
+    const float2 e = live ? espec[f * 256 + k] : make_float2(0.f, 0.f);
+    float2* row = spec + f * 257;
+    if (k == 0) {
+        row[0] = make_float2(e.x, 0.f);
+        row[256] = make_float2(e.y, 0.f);
+    } else {
+        row[k] = e;
+    }
+}
+
+hipError_t launch_unpack_rows(const float2* espec, const int64_t* lens, int B, int64_t Tmax, float2* spec,
+                              hipStream_t st) {
+    if (B <= 0 || Tmax <= 0) return hipSuccess;
+    hipLaunchKernelGGL(crn_unpack_rows_kernel, dim3((unsigned)(B * Tmax)), dim3(256), 0, st, espec, lens, Tmax, spec);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_rows_x0(const RowsX0Args& a, hipStream_t st) {
+    if (a.B <= 0 || a.Tmax <= 0) return hipSuccess;
+    hipLaunchKernelGGL((crn_rows_x0_kernel<T>), dim3((unsigned)(a.B * a.Tmax)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+template hipError_t launch_rows_x0<float>(const RowsX0Args&, hipStream_t);
+template hipError_t launch_rows_x0<bf16_t>(const RowsX0Args&, hipStream_t);
+
+template <typename T>
+hipError_t launch_stream_nlms(const StreamNlmsArgs& a, int taps, hipStream_t st) {
+    if (a.B <= 0) return hipSuccess;
+    switch (taps) {
+#define CRN_NLMS_CASE(N) \
+        case N: hipLaunchKernelGGL((crn_stream_nlms_kernel<T, N>), dim3((unsigned)a.B), dim3(256), 0, st, a); break;
+        CRN_NLMS_CASE(1) CRN_NLMS_CASE(2) CRN_NLMS_CASE(3) CRN_NLMS_CASE(4)
+        CRN_NLMS_CASE(5) CRN_NLMS_CASE(6) CRN_NLMS_CASE(7) CRN_NLMS_CASE(8)
+#undef CRN_NLMS_CASE
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+template hipError_t launch_stream_nlms<float>(const StreamNlmsArgs&, int, hipStream_t);
+template hipError_t launch_stream_nlms<bf16_t>(const StreamNlmsArgs&, int, hipStream_t);
 
 template <typename T>
 hipError_t launch_stream_front(const StreamFrontArgs& a, hipStream_t st) {

@@ -20,6 +20,20 @@ struct FrontArgs {
     const aec::DevTables* tab;
     void* x0;
     float2* spec;               // non-null: write the complex spectrum [B][Tmax][257] of `mic` instead of X0
+    float2* rows = nullptr;     // non-null (NLMS): write the packed mic / far rows [B][Tmax][2][256]
+                                // (slot 0 = (X[0], X[256]), the layout aec::nlms_recursion_kernel reads)
+                                // instead of X0
+};
+
+// NLMS: X0 from the error rows E [B][Tmax][256] (mic channels) and the far
+// half of the packed rows (far channels); frames t >= T_b zero.
+struct RowsX0Args {
+    const float2* rows;         // [B][Tmax][2][256]
+    const float2* espec;        // [B][Tmax][256]
+    const int64_t* lens;
+    int64_t Tmax;
+    void* x0;                   // [Tmax][B][256][8]
+    int32_t B;
 };
 
 // Back: mask [Tmax][B][256] float2 (bins 1..256) applied to the re-derived
@@ -36,6 +50,7 @@ struct BackArgs {
     float* out;
     int64_t ld_out;
     float2* spec;               // nullable
+    const float2* espec = nullptr;   // non-null (NLMS): mask the error rows E [B][Tmax][256] (packed) instead
 };
 
 // Row-GEMM epilogue: out[(m >> oshift)*o_hi + (m & mask)*o_lo + o_add + n] =
@@ -75,6 +90,18 @@ struct StreamFrontArgs {
     const aec::DevTables* tab;
     void* x0;                   // [B][256][8]
     int32_t B;
+    float2* rows = nullptr;     // non-null (NLMS): write the packed rows [B][2][256] instead of X0
+};
+// NLMS streaming step: one block per stream, bin slot per lane; state
+// [B][2*TAPS][256] float2 (taps, far history r[t-1..t-TAPS+1], power — the
+// aec_stream.hip layout) -> E rows [B][256] and X0.
+struct StreamNlmsArgs {
+    const float2* rows;         // [B][2][256]
+    float2* state;
+    float2* espec;              // [B][256]
+    void* x0;                   // [B][256][8]
+    int32_t B;
+    float mu, beta, delta;
 };
 struct StreamBackArgs {
     const float* prev_mic;
@@ -84,11 +111,18 @@ struct StreamBackArgs {
     float* tail;                // [B][256] overlap-add state (in / out)
     float* out;                 // [B][256] output hop (the previous hop of the stream)
     int32_t B;
+    const float2* espec = nullptr;   // non-null (NLMS): mask the E rows [B][256] instead of the mic frame
 };
 
 template <typename T>
 hipError_t launch_stream_front(const StreamFrontArgs& a, hipStream_t st);
 hipError_t launch_stream_back(const StreamBackArgs& a, int mode, hipStream_t st);
+template <typename T>
+hipError_t launch_stream_nlms(const StreamNlmsArgs& a, int taps, hipStream_t st);
+template <typename T>
+hipError_t launch_rows_x0(const RowsX0Args& a, hipStream_t st);
+hipError_t launch_unpack_rows(const float2* espec, const int64_t* lens, int B, int64_t Tmax, float2* spec,
+                              hipStream_t st);
 
 template <typename T, typename OutT>
 hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstages, const RowEpi& e, int npad,

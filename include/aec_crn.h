@@ -57,6 +57,18 @@ typedef struct {
                                    2 = bfloat16 with MX-fp8 LSTM input projections (OCP e4m3
                                    weights and activations, E8M0 scale per 32 k; needs
                                    H % 128 == 0 and H / (256 >> n_layers) % 32 == 0)       */
+    /* Build-defined FD-NLMS front end (no reference counterpart; SURVEY.md §8
+     * a13 + a14, the Stage-2 "NLMS -> CRN" composition).  nlms_taps = 0 is the
+     * reference-parity network.  With nlms_taps > 0 every frame's mic spectrum
+     * X_mic is replaced by the a-priori error E of the per-bin complex NLMS of
+     * aec_hip.h (same recursion, same parameter meaning) driven by the far
+     * spectrum; E feeds the encoder's mic channels AND is the spectrum the
+     * decoder's mask is applied to (out_spec / out_wav).  The far channels
+     * stay X_far.  Streaming carries the NLMS state per stream. */
+    int32_t nlms_taps;          /* 0 = off; 1..8 */
+    float   nlms_mu;            /* [0, 2)  */
+    float   nlms_beta;          /* [0, 1)  */
+    float   nlms_delta;         /* > 0     */
 } aec_crn_config;
 
 /* Number of floats in the parameter blob: the reference state_dict entries
@@ -91,6 +103,12 @@ aec_status aec_crn_set_params(aec_crn_handle* h, const float* params, size_t n_p
  *              for bins 1..256 (mask_real, mask_imag before F.pad) */
 aec_status aec_crn_process(aec_crn_handle* h, const float* mic, const float* far, const int64_t* lengths, int32_t B,
                            int64_t ld, float* out, int64_t ld_out, float* spec, float* mask, void* stream);
+
+/* NLMS handles (nlms_taps > 0): the FD-NLMS error spectrum E of the last
+ * aec_crn_process call -> device [B, Tmax, 257] float2 (frames t >= T_b zero),
+ * the spectrum the mask was applied to (the v1 loss's cRM reference,
+ * dccrn.py:556-566, when the network is fed E). */
+aec_status aec_crn_error_spec(aec_crn_handle* h, float* spec, void* stream);
 
 /* ConvSTFT of B signals -> device [B, Tmax, 257] float2 (frames t >= T_b zero). */
 aec_status aec_crn_stft(aec_crn_handle* h, const float* x, const int64_t* lengths, int32_t B, int64_t ld,

@@ -277,15 +277,29 @@ def apply_mask(mode, mr, mi, xr, xi):
     raise ValueError(mode)
 
 
-def forward(w, conf, version, mic, far, near=None, echo=None, capture=None):
+def forward(w, conf, version, mic, far, near=None, echo=None, capture=None, nlms=None):
     """One utterance through DCCRN (version 1: dccrn.py, 2: dccrn2.py), eval.
 
+    nlms: None (the reference network) or dict(taps, mu, beta, delta): the
+    build-defined FD-NLMS front end (include/aec_crn.h) — the mic spectrum is
+    replaced everywhere below (encoder input, masking, the v1 loss's cRM
+    reference) by the a-priori error of aec_oracle.nlms driven by the far
+    spectrum.
+
     Returns dict(out_wav [256*(N//256)], out_spec [514, T], near_spec
-    [514, T] or None, mask [2, 256, T], loss (version 1 with near and echo)).
+    [514, T] or None, mask [2, 256, T], loss (version 1 with near and echo),
+    err_spec [514, T] with nlms).
     """
     n = len(mic)
     mr_, mi_ = _specs(mic)
     fr_, fi_ = _specs(far)
+    err_spec = None
+    if nlms:
+        from aec_oracle import nlms as _nlms
+        E = _nlms((mr_ + 1j * mi_).T, (fr_ + 1j * fi_).T, taps=nlms.get('taps', 4), mu=nlms.get('mu', 0.3),
+                  beta=nlms.get('beta', 0.5), delta=nlms.get('delta', 1e-4)).T
+        mr_, mi_ = E.real.copy(), E.imag.copy()
+        err_spec = np.concatenate([mr_, mi_], axis=0)
     cs = np.stack([mr_, fr_, mi_, fi_], axis=0)[:, 1:, :]   # [4, 256, T] (dccrn.py:560-561)
     enc, skips = _encode(w, conf, version, cs)
     C, D, T = enc.shape
@@ -310,7 +324,7 @@ def forward(w, conf, version, mic, far, near=None, echo=None, capture=None):
     er, ei = apply_mask(mode, dec[0], dec[1], mr_, mi_)
     out_spec = np.concatenate([er, ei], axis=0)
     out_wav = istft((er + 1j * ei).T, n)
-    res = dict(out_wav=out_wav, out_spec=out_spec, mask=dec, near_spec=None, loss=None)
+    res = dict(out_wav=out_wav, out_spec=out_spec, mask=dec, near_spec=None, loss=None, err_spec=err_spec)
     if near is not None:
         nr, ni = _specs(near)
         res['near_spec'] = np.concatenate([nr, ni], axis=0)

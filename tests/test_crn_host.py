@@ -49,6 +49,39 @@ def test_unsupported_configs_rejected():
     assert _lib.crn_param_count(2, bad) == 0
 
 
+def test_nlms_config_validated_and_laid_out():
+    import ctypes
+    # aec_crn_config: 16 int32 fields then nlms_taps / mu / beta / delta (include/aec_crn.h)
+    assert ctypes.sizeof(_lib.CrnConfig) == 20 * 4
+    assert _lib.CrnConfig.nlms_taps.offset == 16 * 4
+    lib = _lib.load()
+    conf = aec_amd.net_conf
+    good = _lib.crn_config(2, conf, 'f32', dict(taps=4, mu=0.3, beta=0.5, delta=1e-4))
+    assert lib.aec_crn_param_count(ctypes.byref(good)) == _lib.crn_param_count(2, conf)   # same blob
+    for bad in (dict(taps=9), dict(taps=4, mu=2.0), dict(taps=4, beta=1.0), dict(taps=4, delta=0.0)):
+        c = _lib.crn_config(2, conf, 'f32', dict(dict(taps=4, mu=0.3, beta=0.5, delta=1e-4), **bad))
+        assert lib.aec_crn_param_count(ctypes.byref(c)) == 0, bad
+
+
+def test_oracle_nlms_front_end():
+    """crn_oracle.forward(nlms=...) replaces the mic spectrum by aec_oracle.nlms's
+    error: mu = 0 leaves E = X_mic (the plain network, bit for bit), and E is
+    exactly the recursion applied to the two ConvSTFT spectra."""
+    import aec_oracle as A
+    from aec_amd import synth
+    conf = copy.deepcopy(aec_amd.net_conf)
+    conf['conv_channels'] = [4, 8, 8, 8, 8, 8, 8]
+    w = C.make_weights(conf, 2, 3)
+    mic, far, _ = synth.scene(3000, 5)
+    plain = C.forward(w, conf, 2, mic, far)
+    mu0 = C.forward(w, conf, 2, mic, far, nlms=dict(taps=4, mu=0.0, beta=0.5, delta=1e-4))
+    assert np.array_equal(plain['out_wav'], mu0['out_wav'])
+    r = C.forward(w, conf, 2, mic, far, nlms=dict(taps=2, mu=0.5, beta=0.9, delta=1e-3))
+    E = A.nlms(A.stft(mic), A.stft(far), taps=2, mu=0.5, beta=0.9, delta=1e-3)
+    assert np.array_equal(r['err_spec'], np.concatenate([E.real.T, E.imag.T], axis=0))
+    assert not np.allclose(r['out_wav'], plain['out_wav'])
+
+
 def test_fixture_weights_load_strictly_by_reference_names():
     for version, mod in ((1, aec_amd.dccrn), (2, aec_amd.dccrn2)):
         net = mod.DCCRN(aec_amd.net_conf)
