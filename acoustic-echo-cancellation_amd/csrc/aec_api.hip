@@ -218,6 +218,7 @@ struct aec_handle {
     int nlms_mode = 0;           // AEC_NLMS_MODE (timing experiments; results invalid unless 0)
     int nlms_prio = 0;           // AEC_NLMS_PRIO: wave priorities mic|ref|nlms digits (0: all equal, fastest measured)
     int nlms_erb = 1;            // AEC_NLMS_ERB: role running the mic_erb pass (1 ref, 2 nlms)
+    int nlms16 = 0;              // AEC_NLMS16: 16-wave NLMS analysis (aec_nlms16.hip, taps <= 4; measured slower)
     int fused = 1;               // AEC_FUSED_SYNTH: GRU + synthesis in one kernel (NLMS path)
     int fused_mode = 0;          // AEC_FUSED_MODE (timing experiments; results invalid unless 0)
     int pipe = 0;                // AEC_PIPE: the fused per-stream pipeline (aec_pipe.hip) for B >= pipe_minb
@@ -355,6 +356,7 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
     if (const char* m = std::getenv("AEC_NLMS_MODE")) h->nlms_mode = std::atoi(m);
     if (const char* m = std::getenv("AEC_NLMS_PRIO")) h->nlms_prio = std::atoi(m);
     if (const char* m = std::getenv("AEC_NLMS_ERB")) h->nlms_erb = std::atoi(m);
+    if (const char* m = std::getenv("AEC_NLMS16")) h->nlms16 = std::atoi(m);
     if (const char* m = std::getenv("AEC_FUSED_SYNTH")) h->fused = std::atoi(m);
     if (const char* m = std::getenv("AEC_FUSED_MODE")) h->fused_mode = std::atoi(m);
     if (const char* m = std::getenv("AEC_SMALLB")) h->small_b = std::atoi(m);
@@ -604,7 +606,10 @@ aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref
             a.prio = h->nlms_prio;
             a.erb_role = h->nlms_erb;
             mark(h, ks);
-            HIP_TRY(h, launch_nlms_analysis(a, b1 - b0, ks));
+            if (h->nlms16 && nlms16_supported(a.taps, a.sched_len))
+                HIP_TRY(h, launch_nlms16(a, b1 - b0, ks));
+            else
+                HIP_TRY(h, launch_nlms_analysis(a, b1 - b0, ks));
         } else {
             AnalysisArgs a{};
             a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;

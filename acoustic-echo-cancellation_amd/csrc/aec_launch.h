@@ -179,6 +179,10 @@ hipError_t launch_norm_finalize(const double2* mom, const int32_t* slen, float* 
                                 hipStream_t st);
 hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t st);
 hipError_t launch_nlms_analysis(const NlmsArgs& a, int nb, hipStream_t st);
+// the 16-wave form (aec_nlms16.hip): one transform and one ERB pass per
+// transform wave and tick; taps 1..4, schedule length <= 48
+bool nlms16_supported(int taps, int sched_len);
+hipError_t launch_nlms16(const NlmsArgs& a, int nb, hipStream_t st);
 // small-batch NLMS path (few streams: the per-stream K2n block would leave the
 // chip idle): K2 with spectrum rows, then the recursion per (stream, bin) and
 // the mic_erb pass over all frames

@@ -81,6 +81,8 @@ def parse():
     ap.add_argument('--crn-dtype', choices=['bf16', 'f32', 'fp8'], default='bf16',
                     help='--pipeline crn compute type (fp8 = bf16 with MX-fp8 LSTM input projections)')
     ap.add_argument('--crn-version', type=int, choices=[1, 2], default=2, help='1 = dccrn.py, 2 = dccrn2.py')
+    ap.add_argument('--crn-nlms', action='store_true',
+                    help='--pipeline crn: feed the DCCRN the FD-NLMS error spectrum (C5, include/aec_crn.h)')
     ap.add_argument('--no-rtf', action='store_true', help='skip the batch-1 latency probe (profiling runs)')
     ap.add_argument('--sweep', action='store_true', help='also report a batch sweep')
     ap.add_argument('--no-c3', action='store_true', help='skip the BASELINE config 3 (DCCRN bf16) figure')
@@ -238,9 +240,11 @@ def _init_dist(torch, dist, world, local):
     return local
 
 
-def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu):
+def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu, nlms=None):
     """BASELINE config 3: the DCCRN post-filter (dccrn2.py, configs.net_conf) on
-    B streams x n samples; returns the measurements (timing = max over ranks)."""
+    B streams x n samples; returns the measurements (timing = max over ranks).
+    nlms: the FD-NLMS front end (C5: NLMS -> CRN, include/aec_crn.h), timed
+    in the 'front' stage."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -250,7 +254,7 @@ def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu):
     T = n // 256 + 1
     torch.manual_seed(0)                         # the reference's own init (random weights, no checkpoint ships)
     mod = aec_amd.dccrn if args.crn_version == 1 else aec_amd.dccrn2
-    net = mod.DCCRN(conf, dtype=dtype).eval().to(dev)
+    net = mod.DCCRN(conf, dtype=dtype, nlms=nlms).eval().to(dev)
     mic, far, _ = (torch.from_numpy(a).to(dev) for a in synth.batch(B, n, seed0=1000 * rank))
     lens = [n] * B
 
@@ -305,7 +309,7 @@ def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu):
                pipeline_roofline={'alg_flops_per_frame': fl['total'], 'achieved_tflops': round(whole, 1),
                                   'mfma_frac': round(whole / peak, 4)},
                erle=None, cpu_baseline=None)
-    if with_cpu and rank == 0 and world == 1:
+    if with_cpu and rank == 0 and world == 1 and not nlms:
         res['cpu_baseline'] = cpu_baseline_crn(args.cpu_seconds, conf, args.crn_version, n=n)
         sys.path.insert(0, os.path.join(REPO, 'oracle'))
         from torch_crn_port import TorchCrnPort
@@ -341,14 +345,17 @@ def main_crn(args):
     dev = torch.device('cuda', local)
     B = args.streams
     n = int(round(args.seconds * 16000))
-    r = run_crn(args, dev, rank, world, args.crn_dtype, args.steps, args.warmup, B, n, not args.no_cpu)
+    import aec_amd
+    nl = aec_amd.nlms_conf if args.crn_nlms else None
+    r = run_crn(args, dev, rank, world, args.crn_dtype, args.steps, args.warmup, B, n, not args.no_cpu, nl)
     if rank == 0:
         line = {
             'metric': '16kHz frames/sec/GPU (batched AEC) + RTF@batch=1; ERLE delta vs reference',
             'value': r['value'], 'unit': 'frames/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': r['ms_per_step'], 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': args.crn_dtype, 'data': 'synthetic',
-            'config': {'workload': crn_workload(args, args.crn_dtype, B),
+            'config': {'workload': crn_workload(args, args.crn_dtype, B) + (' fed by the FD-NLMS error spectrum (C5)'
+                                                                            if nl else ''),
                        'streams_per_gpu': B, 'samples_per_stream': n, 'frames_per_stream': n // 256 + 1,
                        'frame': '256-sample hop', 'pipeline': 'crn',
                        'parallelism': f'streams sharded, {world} rank(s)'},
@@ -482,6 +489,13 @@ def main():
                   frames_per_s=c3['value'], ms_per_step=c3['ms_per_step'], rtf_batch1=c3['rtf_batch1'],
                   stage_ms_per_step=c3['stage_ms_per_step'], roofline=c3['roofline'],
                   pipeline_roofline=c3['pipeline_roofline'])
+    c5 = None
+    if world == 1 and not args.no_c3:
+        # C5: the same network fed by the FD-NLMS error spectrum (NLMS -> CRN composition)
+        c5 = run_crn(args, dev, rank, world, 'bf16', args.c3_steps, 2, 256, 160000, False, aec_amd.nlms_conf)
+        c5 = dict(workload=crn_workload(args, 'bf16', 256) + ' fed by the FD-NLMS error spectrum (taps 4)',
+                  dtype='bf16', steps=args.c3_steps, frames_per_s=c5['value'], ms_per_step=c5['ms_per_step'],
+                  stage_ms_per_step=c5['stage_ms_per_step'])
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_seconds)
         sys.path.insert(0, os.path.join(REPO, 'oracle'))
@@ -518,6 +532,7 @@ def main():
             'erle': erle,
             'cpu_baseline': cpu,
             'c3_crn_bf16': c3,
+            'c5_nlms_crn_bf16': c5,
         }
         if sweep:
             line['batch_sweep_frames_per_s'] = sweep

@@ -329,3 +329,47 @@ def test_pipeline_kernel_bit_exact_bypass(golden_weights, golden_erb, monkeypatc
     """K6 with the NLMS bypassed (Little_net's own path, E = M) against
     analysis_kernel + gru_kernel + synthesis_kernel, with per-signal lengths."""
     _pipe_vs_kernels(golden_weights, golden_erb, monkeypatch, None, 950, siglens=True)
+
+
+@pytest.mark.parametrize('taps,siglens', [(4, False), (4, True), (1, False), (2, True), (3, False)])
+def test_nlms16_kernel_bit_exact(golden_weights, golden_erb, monkeypatch, taps, siglens):
+    """The 16-wave NLMS analysis (aec_nlms16.hip, AEC_NLMS16=1; off by default:
+    measured 0.358 vs 0.335 ms) against the 12-wave nlms_analysis_kernel: the
+    same per-frame functions in the same order, so the features, the waveform
+    (through the E spectrum) and est_erb are bit-identical.  Per-block path
+    forced (AEC_SMALLB=0); ragged lengths cover partial chunks, a stream
+    shorter than one chunk and a 10 s stream; siglens: ref / near shorter."""
+    from aec_amd import synth
+    lens = [33333, 4097, 255, 16000, 256, 2100, 160000]
+    L = max(lens)
+    rows = [synth.scene(n, 1200 + 10 * taps + i) for i, n in enumerate(lens)]
+    mic, ref, near = (np.zeros((len(lens), L), np.float32) for _ in range(3))
+    l3 = np.zeros((len(lens), 3), np.int64)
+    for i, (m, r, nn_) in enumerate(rows):
+        n = lens[i]
+        d = min(13, n % 256) if siglens else 0
+        mic[i, :n], ref[i, :n - d], near[i, :n - d // 2] = m, r[:n - d], nn_[:n - d // 2]
+        l3[i] = (n, n - d, n - d // 2)
+    dev = 'cuda:0'
+    erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
+    M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
+    T = L // 256 + 1
+    res = {}
+    monkeypatch.setenv('AEC_PIPE', '0')
+    monkeypatch.setenv('AEC_SMALLB', '0')
+    for k16 in ('0', '1'):
+        monkeypatch.setenv('AEC_NLMS16', k16)                   # read when the handle is created
+        net = _net(golden_weights, dict(NLMS, taps=taps))
+        net.set_debug(True)
+        with torch.no_grad():
+            out, loss = net.forward_ragged(M, R, N, erb_t, l3 if siglens else lens)
+        feats = {k: net.debug_intermediate(k, len(lens), T).cpu().numpy()
+                 for k in ('mic_erb', 'ref_erb', 'near_erb', 'est_erb')}
+        torch.cuda.synchronize()
+        res[k16] = (out.cpu().numpy(), loss.cpu().numpy(), feats)
+    (o0, l0, f0), (o1, l1, f1) = res['0'], res['1']
+    assert np.array_equal(o0, o1)
+    assert np.array_equal(l0, l1, equal_nan=True)
+    for k in f0:
+        for i, n in enumerate(lens):
+            assert np.array_equal(f0[k][i, :n // 256 + 1], f1[k][i, :n // 256 + 1], equal_nan=True), (k, i)
