@@ -85,6 +85,8 @@ def parse():
                     help='--pipeline crn: feed the DCCRN the FD-NLMS error spectrum (C5, include/aec_crn.h)')
     ap.add_argument('--no-rtf', action='store_true', help='skip the batch-1 latency probe (profiling runs)')
     ap.add_argument('--sweep', action='store_true', help='also report a batch sweep')
+    ap.add_argument('--inflight', type=int, default=2,
+                    help='batches in flight (HIP streams, one handle each; 1 = strictly sequential)')
     ap.add_argument('--no-c3', action='store_true', help='skip the BASELINE config 3 (DCCRN bf16) figure')
     ap.add_argument('--c3-steps', type=int, default=10, help='timed steps of the config 3 figure')
     return ap.parse_args()
@@ -258,16 +260,35 @@ def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu, nlms=N
     mic, far, _ = (torch.from_numpy(a).to(dev) for a in synth.batch(B, n, seed0=1000 * rank))
     lens = [n] * B
 
+    inflight = max(1, args.inflight)
+    nets = [net]
+    for _ in range(inflight - 1):
+        extra = mod.DCCRN(conf, dtype=dtype, nlms=nlms).eval()
+        extra.load_state_dict(net.state_dict())
+        nets.append(extra.to(dev))
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
+    kstep = [0]
+
     def step():
-        return net.forward_ragged(mic, far, lens, want_spec=False)
+        k = kstep[0] % inflight
+        kstep[0] += 1
+        with torch.cuda.stream(streams[k]):
+            return nets[k].forward_ragged(mic, far, lens, want_spec=False)
 
     with torch.no_grad():
-        for _ in range(warmup):
+        for _ in range(max(warmup, inflight)):
             step()
         torch.cuda.synchronize(dev)
+        # stage times: HIP events over a sequential pass (one batch in flight)
         h = net._handle(dev)
+        prof_steps = max(1, min(steps, 5))
         h.profile_enable(True)
         h.profile_read()
+        for _ in range(prof_steps):
+            net.forward_ragged(mic, far, lens, want_spec=False)
+        torch.cuda.synchronize(dev)
+        sms, calls = h.profile_read()
+        h.profile_enable(False)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
@@ -278,8 +299,6 @@ def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu, nlms=N
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
-        sms, calls = h.profile_read()
-        h.profile_enable(False)
         el = shard.max_over_ranks(el)
         lat = []
         for _ in range(0 if args.no_rtf else 3):
@@ -301,6 +320,7 @@ def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu, nlms=N
     ach = dom_fl * B * T / (stage_ms[dom] * 1e-3) / 1e12 if dom_fl else 0.0
     whole = fl['total'] * B * T / (ms_step * 1e-3) / 1e12
     res = dict(value=round(value, 1), value_per_gpu=round(value / world, 1), ms_per_step=round(ms_step, 3),
+               batches_in_flight=inflight,
                rtf_batch1=rtf1, stage_ms_per_step={k: round(v, 3) for k, v in stage_ms.items()},
                roofline={'bound': 'mfma', 'achieved': round(ach, 1), 'peak': peak, 'unit': 'TFLOP/s',
                          'frac': round(ach / peak, 4), 'traffic': None,
@@ -324,7 +344,7 @@ def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu, nlms=N
 
         res['erle'] = erle_check(gpu1, lambda m_, f_, _n: port(torch.from_numpy(m_)[None],
                                                                torch.from_numpy(f_)[None])[0].numpy(), n)
-    del net
+    del net, nets
     torch.cuda.empty_cache()
     return res
 
@@ -357,7 +377,7 @@ def main_crn(args):
             'config': {'workload': crn_workload(args, args.crn_dtype, B) + (' fed by the FD-NLMS error spectrum (C5)'
                                                                             if nl else ''),
                        'streams_per_gpu': B, 'samples_per_stream': n, 'frames_per_stream': n // 256 + 1,
-                       'frame': '256-sample hop', 'pipeline': 'crn',
+                       'frame': '256-sample hop', 'pipeline': 'crn', 'batches_in_flight': r['batches_in_flight'],
                        'parallelism': f'streams sharded, {world} rank(s)'},
             'value_per_gpu': r['value_per_gpu'],
             'xRT': round(r['value'] * 256 / 16000, 1),
@@ -400,15 +420,42 @@ def main():
     mic, ref, near = (torch.from_numpy(a).to(dev) for a in synth.batch(B, n, seed0=1000 * rank))
     lens = [n] * B
 
+    # batches in flight: step k runs on HIP stream k % inflight with its own handle
+    # (each aec_handle owns its workspace), so one batch's latency-bound GRU +
+    # synthesis kernel overlaps the next batch's moments pass; every batch is
+    # processed whole
+    inflight = max(1, args.inflight)
+    nets = [net]
+    for _ in range(inflight - 1):
+        extra = aec_amd.Little_net(aec_amd.speech_conf, 32, nlms=nlms).eval()
+        extra.load_state_dict(net.state_dict())
+        nets.append(extra.to(dev))
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
+    kstep = [0]
+
     def step():
-        return net.forward_ragged(mic, ref, near, erb, lens)
+        k = kstep[0] % inflight
+        kstep[0] += 1
+        with torch.cuda.stream(streams[k]):
+            return nets[k].forward_ragged(mic, ref, near, erb, lens)
 
     with torch.no_grad():
-        for _ in range(args.warmup):
+        for _ in range(max(args.warmup, inflight)):
             step()
         torch.cuda.synchronize(dev)
-        h, _ = net._handle(dev)
-        h.profile_enable(True)
+        # per-kernel times (roofline): HIP events around each kernel over a
+        # sequential pass (one batch in flight, so no event interval contains
+        # another batch's kernels)
+        h0 = nets[0]._handle(dev)[0]
+        prof_steps = max(1, min(args.steps, 10))
+        h0.profile_enable(True)
+        torch.cuda.synchronize(dev)
+        for _ in range(prof_steps):
+            nets[0].forward_ragged(mic, ref, near, erb, lens)
+        torch.cuda.synchronize(dev)
+        kms, calls = h0.profile_read()
+        h0.profile_enable(False)
+        # the timed region: K steps, `inflight` batches in flight
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
@@ -419,8 +466,6 @@ def main():
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
-        kms, calls = h.profile_read()
-        h.profile_enable(False)
         el = shard.max_over_ranks(el)              # all_reduce(MAX) of one scalar, outside the timed region
         # RTF at batch 1: one 10 s utterance, synchronous latency (median of 7)
         lat = []
@@ -452,8 +497,8 @@ def main():
     ms_step = el / args.steps * 1e3
     # `calls` counts aec_process calls (profile marks per call; one launch of each
     # kernel per call here: 256 streams, no sub-batching)
-    calls_per_step = max(calls, 1) / args.steps
-    per_kernel_ms = {k: kms[i] / args.steps for i, k in enumerate(KERNELS)}
+    calls_per_step = max(calls, 1) / prof_steps
+    per_kernel_ms = {k: kms[i] / prof_steps for i, k in enumerate(KERNELS)}
     per_launch_ms = {k: kms[i] / max(calls, 1) for i, k in enumerate(KERNELS)}
     pipe = os.environ.get('AEC_PIPE', '0') not in ('', '0')
     if pipe:
@@ -486,6 +531,7 @@ def main():
         # BASELINE config 3 (DCCRN bf16, 256 x 10 s) in the same driver-timed run
         c3 = run_crn(args, dev, rank, world, 'bf16', args.c3_steps, 2, 256, 160000, False)
         c3 = dict(workload=crn_workload(args, 'bf16', 256), dtype='bf16', steps=args.c3_steps,
+                  batches_in_flight=c3['batches_in_flight'],
                   frames_per_s=c3['value'], ms_per_step=c3['ms_per_step'], rtf_batch1=c3['rtf_batch1'],
                   stage_ms_per_step=c3['stage_ms_per_step'], roofline=c3['roofline'],
                   pipeline_roofline=c3['pipeline_roofline'])
@@ -494,7 +540,8 @@ def main():
         # C5: the same network fed by the FD-NLMS error spectrum (NLMS -> CRN composition)
         c5 = run_crn(args, dev, rank, world, 'bf16', args.c3_steps, 2, 256, 160000, False, aec_amd.nlms_conf)
         c5 = dict(workload=crn_workload(args, 'bf16', 256) + ' fed by the FD-NLMS error spectrum (taps 4)',
-                  dtype='bf16', steps=args.c3_steps, frames_per_s=c5['value'], ms_per_step=c5['ms_per_step'],
+                  dtype='bf16', steps=args.c3_steps, batches_in_flight=c5['batches_in_flight'],
+                  frames_per_s=c5['value'], ms_per_step=c5['ms_per_step'],
                   stage_ms_per_step=c5['stage_ms_per_step'])
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_seconds)
@@ -516,12 +563,13 @@ def main():
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
             'config': {'workload': WORKLOAD[args.pipeline],
                        'streams_per_gpu': B, 'samples_per_stream': n, 'frames_per_stream': T,
-                       'frame': '256-sample hop', 'pipeline': args.pipeline,
+                       'frame': '256-sample hop', 'pipeline': args.pipeline, 'batches_in_flight': inflight,
                        'parallelism': f'streams sharded, {world} rank(s)'},
             'value_per_gpu': round(value / world, 1),
             'xRT': round(value * 256 / 16000, 1),
             'rtf_batch1': rtf1,
             'kernel_ms_per_step': {k: round(v, 4) for k, v in per_kernel_ms.items()},
+            'kernel_timing': f'HIP events around each kernel, sequential pass of {prof_steps} steps (1 batch in flight)',
             'kernels_per_step': kernels_per_call,
             'launches_per_step': launches_per_step,
             'roofline': roof,
