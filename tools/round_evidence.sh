@@ -9,6 +9,8 @@ timeout -k 10 300 python $R/bench.py > $R/gpurun_out/bench_${TAG}_full.log 2>&1 
 echo "bench full done"
 timeout -k 10 300 python $R/bench.py --pipeline postfilter > $R/gpurun_out/bench_${TAG}_postfilter.log 2>&1 || exit 1
 echo "bench postfilter done"
-bash $R/tools/profile.sh ${TAG}_full --pipeline full || exit 1
-bash $R/tools/profile.sh ${TAG}_postfilter --pipeline postfilter || exit 1
+# traces with one batch in flight: kernel durations without a concurrent batch,
+# the configuration of bench.py's own per-kernel timing pass
+bash $R/tools/profile.sh ${TAG}_full --pipeline full --inflight 1 || exit 1
+bash $R/tools/profile.sh ${TAG}_postfilter --pipeline postfilter --inflight 1 || exit 1
 echo "profiles done"
