@@ -245,7 +245,8 @@ struct aec_handle {
 static hipEvent_t next_event(aec_handle* h) {
     if (h->ev_used == h->ev_pool.size()) {
         hipEvent_t e;
-        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        // timing marks without the system-scope release fence a default event adds
+        if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
         h->ev_pool.push_back(e);
     }
     return h->ev_pool[h->ev_used++];

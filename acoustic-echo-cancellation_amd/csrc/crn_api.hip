@@ -521,7 +521,8 @@ static void mark(aec_crn_handle* h, hipStream_t st) {
     if (!h->profile) return;
     if (h->ev_used == h->ev.size()) {
         hipEvent_t e;
-        if (hipEventCreate(&e) != hipSuccess) return;
+        // timing marks without the system-scope release fence a default event adds
+        if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return;
         h->ev.push_back(e);
     }
     (void)hipEventRecord(h->ev[h->ev_used++], st);
