@@ -349,6 +349,37 @@ def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu, nlms=N
     return res
 
 
+def run_c5_stream(dev, B=256, hops=200, dtype='fp8'):
+    """BASELINE config 5's per-GPU unit: the hipGraph-captured per-hop step of
+    the DCCRN (MX-fp8 LSTM input projections) fed by the FD-NLMS, B concurrent
+    streams, one 256-sample hop per stream per step (aec_crn_stream_step)."""
+    import torch
+    import aec_amd
+    torch.manual_seed(0)
+    net = aec_amd.dccrn2.DCCRN(dict(aec_amd.net_conf), dtype=dtype, nlms=aec_amd.nlms_conf).eval().to(dev)
+    net.stream_open(B, device=dev)
+    g = torch.Generator(device=dev).manual_seed(5)
+    mic = 0.1 * torch.randn(B, 256, device=dev, generator=g)
+    far = 0.1 * torch.randn(B, 256, device=dev, generator=g)
+    out = torch.empty(B, 256, device=dev)
+    with torch.no_grad():
+        for _ in range(10):
+            net.stream_step(mic, far, out)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(hops):
+            net.stream_step(mic, far, out)
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t0) / hops
+    del net
+    torch.cuda.empty_cache()
+    return dict(workload=f'C5 (BASELINE configs[4]) per GPU: {B} concurrent streams, one 256-sample hop per '
+                         f'stream per step through the hipGraph-captured STFT -> FD-NLMS (4 taps) -> DCCRN v2 '
+                         f'(net_conf, {dtype}: bf16 + MX-fp8 LSTM input projections) -> iSTFT step',
+                dtype=dtype, streams=B, hops=hops, ms_per_hop=round(dt * 1e3, 4), frames_per_s=round(B / dt, 1),
+                rtf=round(dt / 0.016, 5))
+
+
 def crn_workload(args, dtype, B):
     return (f'C3 (BASELINE configs[2]): DCCRN v{args.crn_version} '
             f'({"dccrn2.py" if args.crn_version == 2 else "dccrn.py"}, configs.net_conf, {dtype} MFMA) on {B} '
@@ -543,6 +574,9 @@ def main():
                   dtype='bf16', steps=args.c3_steps, batches_in_flight=c5['batches_in_flight'],
                   frames_per_s=c5['value'], ms_per_step=c5['ms_per_step'],
                   stage_ms_per_step=c5['stage_ms_per_step'])
+    c5s = None
+    if world == 1 and not args.no_c3:
+        c5s = run_c5_stream(dev)
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_seconds)
         sys.path.insert(0, os.path.join(REPO, 'oracle'))
@@ -581,6 +615,7 @@ def main():
             'cpu_baseline': cpu,
             'c3_crn_bf16': c3,
             'c5_nlms_crn_bf16': c5,
+            'c5_stream_fp8': c5s,
         }
         if sweep:
             line['batch_sweep_frames_per_s'] = sweep
