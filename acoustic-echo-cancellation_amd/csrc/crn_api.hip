@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -101,6 +102,11 @@ struct aec_crn_handle {
     std::vector<int64_t> proc_lens;                //   and its lengths
     std::vector<void*> allocs;
     StreamState* ss = nullptr;                     // aec_crn_stream_* state
+    // persistent LSTM recurrence (crn_persist.hip; AEC_CRN_PERSIST=0: one launch per frame)
+    int persist = 1;
+    int num_cus = 0;
+    int* psync = nullptr;                          // arrival counters + error word
+    int* perr_host = nullptr;                      // pinned copy of the error word
     // profiling
     int profile = 0;
     std::vector<hipEvent_t> ev;
@@ -676,12 +682,51 @@ static int mask_mode(const aec_crn_handle* h) {
     return h->cfg.version == 1 ? 1 : (h->cfg.masking_mode == 'E' ? 0 : h->cfg.masking_mode == 'C' ? 1 : 2);
 }
 
+// Device-wide order of persistent launches: a persistent grid needs every CU,
+// so two of them co-resident (two handles / streams) could starve each other.
+// Each launch waits for the previous one on this device.
+static std::mutex g_persist_mu;
+static hipEvent_t g_persist_ev[64] = {};
+
+static aec_status run_persist(aec_crn_handle* h, int l, int32_t B, int64_t Tmax, hipStream_t st) {
+    if (h->perr_host && *h->perr_host) {
+        h->persist = 0;
+        return crn_fail(h, AEC_ERR_HIP, "persistent LSTM recurrence timed out waiting for its team (disabled)");
+    }
+    std::lock_guard<std::mutex> lk(g_persist_mu);
+    hipEvent_t& ev = g_persist_ev[h->device & 63];
+    if (!ev) CRN_TRY(h, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    CRN_TRY(h, hipStreamWaitEvent(st, ev, 0));
+    for (int32_t b0 = 0; b0 < B; b0 += 256) {
+        const int nb = std::min<int32_t>(256, B - b0);
+        crn::PersistArgs a{};
+        a.whh = reinterpret_cast<const bf16_t*>(h->lhh[l].w);
+        a.gx = reinterpret_cast<const bf16_t*>(h->gx);
+        a.y = reinterpret_cast<bf16_t*>(h->y);
+        a.sync = h->psync;
+        a.B = B;
+        a.b0 = b0;
+        a.nb = nb;
+        a.T = (int)Tmax;
+        a.G = (nb + 63) / 64;
+        a.spin_limit = 1 << 22;
+        static const int pmode = [] { const char* v = getenv("CRN_PERSIST_MODE"); return v ? atoi(v) : 0; }();
+        a.mode = pmode;
+        CRN_TRY(h, hipMemsetAsync(h->psync, 0, (8 * 16 + 16) * sizeof(int), st));
+        CRN_TRY(h, crn::launch_lstm_persist(a, st));
+        CRN_TRY(h, hipMemcpyAsync(h->perr_host, h->psync + 8 * 16, sizeof(int), hipMemcpyDeviceToHost, st));
+    }
+    CRN_TRY(h, hipEventRecord(ev, st));
+    return AEC_OK;
+}
+
 template <typename T>
 static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int32_t B, int64_t ld, int64_t Tmax,
                       float* out, int64_t ld_out, float* spec, float* mask_out, hipStream_t st) {
     const int64_t BT = (int64_t)B * Tmax;
     const Bufs bf{h->x0, h->cat.data(), h->gx, h->xn, h->mask, h->aq, h->as};
     const int H = h->H, S = h->S, C = h->CELLS;
+    const bool persist = sizeof(T) == 2 && h->persist && h->psync && crn::persist_supported(H, C, S, h->num_cus);
     mark(h, st);
     // front: X0 [Tmax][B][256][8]
     const aec_crn_config& c = h->cfg;
@@ -702,6 +747,13 @@ static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int
         s = run_lstm_input<T>(h, bf, l, BT, st);
         if (s != AEC_OK) return s;
         const int64_t ystride = (int64_t)B * C * S * H, gstride = (int64_t)B * S * C * 4 * H;   // per frame
+        if (persist) {   // all Tmax frames of the layer in one launch per 256 streams
+            s = run_persist(h, l, B, Tmax, st);
+            if (s != AEC_OK) return s;
+            s = run_lstm_combine<T>(h, bf, l, h->y, BT, st);
+            if (s != AEC_OK) return s;
+            continue;
+        }
         for (int64_t t = 0; t < Tmax; ++t) {
             crn::StepArgs sa{h->lhh[l].w, reinterpret_cast<const T*>(h->gx) + t * gstride,
                              reinterpret_cast<const T*>(h->y) + (t > 0 ? t - 1 : 0) * ystride,
@@ -845,6 +897,15 @@ aec_status aec_crn_create(const aec_crn_config* cfg, const float* params, size_t
     aec::DevTables tab;
     aec::build_dev_tables(tab);
     if (hipMemcpy(h->d_tab, &tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess) return bail(AEC_ERR_HIP);
+    if (const char* v = getenv("AEC_CRN_PERSIST")) h->persist = atoi(v);
+    if (hipDeviceGetAttribute(&h->num_cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) h->num_cus = 0;
+    if (h->es == 2 && crn::persist_supported(h->H, h->CELLS, h->S, h->num_cus)) {
+        // team arrival counters + error word, and a pinned copy of the error word
+        if (hipMalloc(reinterpret_cast<void**>(&h->psync), (8 * 16 + 16) * sizeof(int)) != hipSuccess)
+            return bail(AEC_ERR_OOM);
+        if (hipHostMalloc(reinterpret_cast<void**>(&h->perr_host), sizeof(int)) != hipSuccess) return bail(AEC_ERR_OOM);
+        *h->perr_host = 0;
+    }
     h->enc.assign(h->L, Packed{});
     h->dec.assign(2 * h->L, Packed{});
     h->lih.assign(h->nrnn, Packed{});
@@ -1110,6 +1171,8 @@ void aec_crn_destroy(aec_crn_handle* h) {
             if (pk.wsc) (void)hipFree(pk.wsc);
         }
     if (h->d_tab) (void)hipFree(h->d_tab);
+    if (h->psync) (void)hipFree(h->psync);
+    if (h->perr_host) (void)hipHostFree(h->perr_host);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     delete h;
 }

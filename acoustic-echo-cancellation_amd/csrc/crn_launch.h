@@ -142,6 +142,26 @@ template <typename T>
 hipError_t launch_lstm_combine(const T* y, T* dst, int64_t nframes, int H, int cells, int seqs, int dshift,
                                int64_t ldf, int64_t ldd, hipStream_t st);
 
+// Persistent LSTM recurrence (crn_persist.hip): all T frames of one layer in
+// one launch for up to 256 streams (64 G blocks, G = ceil(nb / 64) row
+// groups), W_hh in AGPRs, h handed over per team through y with arrival counters.
+struct PersistArgs {
+    const bf16_t* whh;          // packed W_hh [CELLS*4H][H]
+    const bf16_t* gx;           // [T][B][S][CELLS*4H] (frame f = t*B + b)
+    bf16_t* y;                  // [T][B][CELLS][S][H]: the layer output and the h hand-off
+    int* sync;                  // [8 teams x 16] arrival counters + [16] error word, zeroed per launch
+    int32_t B;                  // streams of the batch (frame row stride)
+    int32_t b0, nb;             // this launch's streams b0 .. b0 + nb - 1 (nb <= 256)
+    int32_t T;
+    int32_t G;                  // row groups (1..4)
+    int32_t spin_limit;         // polls before a block gives up (error word set)
+    int32_t mode = 0;           // timing experiments only (CRN_PERSIST_MODE; results invalid unless 0):
+                                // bit0 h loads out of range (zeros), bit1 no MFMA phase, bit2 no team wait
+};
+size_t persist_lds_bytes();
+bool persist_supported(int H, int cells, int seqs, int num_cus);
+hipError_t launch_lstm_persist(const PersistArgs& a, hipStream_t st);
+
 // tile width the host must pad the weight rows (N) to for a GEMM of N columns
 inline int gemm_bn(int N) { return N <= 16 ? 16 : N <= 32 ? 32 : N <= 64 ? 64 : 128; }
 

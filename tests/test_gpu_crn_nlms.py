@@ -183,3 +183,35 @@ def test_error_spec_needs_nlms_handle():
     net, _, _, _ = build('v2E_2125', 'f32', nlms=None)
     with pytest.raises(RuntimeError):
         net.error_spectra('cuda:0')
+
+
+FP8_WAV_TOL = 1e-1
+
+
+def test_fp8_nlms_stream_step_close_to_oracle():
+    """BASELINE config 5's unit: the hipGraph-captured per-hop step with the
+    FD-NLMS in front and MX-fp8 LSTM input projections (dtype 'fp8'), against
+    the float64 oracle (crn_oracle + aec_oracle.nlms) within the fp8 bar of
+    tests/test_gpu_crn.py (relative RMS <= 1e-1), and against the fp8 batch
+    forward of the same network (<= 2e-2: the step kernels are the batch
+    kernels; the streaming front / back restate the batch transforms)."""
+    net, m, conf, w = build('v2E_2125', 'fp8')
+    n = 16000
+    mic, far, _, _ = synth.scene(n, 93, return_echo=True)
+    nh = n // 256 + 1
+    M = torch.zeros(1, 256 * (nh + 1), device='cuda:0')
+    F = torch.zeros_like(M)
+    M[0, :n] = torch.from_numpy(mic).cuda()
+    F[0, :n] = torch.from_numpy(far).cuda()
+    net.stream_open(1)
+    outs = []
+    with torch.no_grad():
+        for k in range(nh):
+            outs.append(net.stream_step(M[:, 256 * k:256 * (k + 1)], F[:, 256 * k:256 * (k + 1)]).clone())
+        ref_out, _, _ = net.forward_ragged(T(mic), T(far), [n], want_spec=False)
+    torch.cuda.synchronize()
+    got = torch.cat(outs[1:], dim=1)[0, :256 * (n // 256)].cpu().numpy()
+    r = C.forward(w, conf, 2, mic, far, nlms=NLMS)
+    assert np.isfinite(got).all()
+    assert rel(got, r['out_wav']) <= FP8_WAV_TOL
+    assert rel(got, ref_out[0].cpu().numpy()) <= 2e-2
