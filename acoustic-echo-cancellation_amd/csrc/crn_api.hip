@@ -697,8 +697,10 @@ static aec_status run_persist(aec_crn_handle* h, int l, int32_t B, int64_t Tmax,
     hipEvent_t& ev = g_persist_ev[h->device & 63];
     if (!ev) CRN_TRY(h, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     CRN_TRY(h, hipStreamWaitEvent(st, ev, 0));
-    for (int32_t b0 = 0; b0 < B; b0 += 256) {
-        const int nb = std::min<int32_t>(256, B - b0);
+    // one block per CU: 64 streams (two teams of 32 blocks) per 64 CUs, at most 256 streams per launch
+    const int32_t chunk = 64 * std::min(4, h->num_cus / 64);
+    for (int32_t b0 = 0; b0 < B; b0 += chunk) {
+        const int nb = std::min<int32_t>(chunk, B - b0);
         crn::PersistArgs a{};
         a.whh = reinterpret_cast<const bf16_t*>(h->lhh[l].w);
         a.gx = reinterpret_cast<const bf16_t*>(h->gx);

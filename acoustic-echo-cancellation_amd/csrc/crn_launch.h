@@ -156,7 +156,8 @@ struct PersistArgs {
     int32_t G;                  // row groups (1..4)
     int32_t spin_limit;         // polls before a block gives up (error word set)
     int32_t mode = 0;           // timing experiments only (CRN_PERSIST_MODE; results invalid unless 0):
-                                // bit0 h loads out of range (zeros), bit1 no MFMA phase, bit2 no team wait
+                                // bit0 h loads out of range (zeros), bit1 no MFMA phase, bit2 no team wait,
+                                // bit3 no h stores, bit4 Gx loads out of range, bit5 no cell update
 };
 size_t persist_lds_bytes();
 bool persist_supported(int H, int cells, int seqs, int num_cus);

@@ -39,7 +39,8 @@
 //   * Every spin is bounded: a block whose team stalls past the bound sets the
 //     error word and leaves; its team-mates time out the same way, so the grid
 //     always drains.  The host serialises persistent launches per device
-//     (a second one co-resident with the first could starve it of CUs).
+//     (a second one co-resident with the first could starve it of CUs) and
+//     sizes the grid to at most one block per CU.
 //
 // Numerics: bf16 h / W, f32 accumulation and cell state, the step kernel's
 // cell arithmetic; the K halves are summed separately (not bit-identical to
@@ -47,6 +48,7 @@
 // the same code).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -83,7 +85,8 @@ __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" :
 
 __global__ __launch_bounds__(kPThreads, 1) void lstm_persist_kernel(PersistArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: LDS-DMA targets go to M0
     const int ug = wave & 1, kh = wave >> 1;
     const int nteams = 2 * p.G;
     const int team = blockIdx.x % nteams, slice = blockIdx.x / nteams;
@@ -132,7 +135,7 @@ __global__ __launch_bounds__(kPThreads, 1) void lstm_persist_kernel(PersistArgs 
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const int row = 4 * (8 * wave + i) + (lane >> 4);
-                const uint32_t vo = row < nrows ? (uint32_t)((lane >> 4) * 16384 + (lane & 15) * 16) : kOOB;
+                const uint32_t vo = (row < nrows && !(p.mode & 16)) ? (uint32_t)((lane >> 4) * 16384 + (lane & 15) * 16) : kOOB;
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
                     rgx, (__attribute__((address_space(3))) void*)(smem + oA + (8 * wave + i) * 1024), 16, vo,
                     (int)(gu + (uint32_t)(4 * (8 * wave + i)) * 16384u), 0, 0);
@@ -200,33 +203,40 @@ __global__ __launch_bounds__(kPThreads, 1) void lstm_persist_kernel(PersistArgs 
                 if (j + kNBuf - 1 < 8) issue(j + kNBuf - 1);   // into the buffer read at iteration j - 1
                 if (j == 5) issue_gx();                        // buffer 0 (chunk 4) is free
                 const char* base = smem + oA + ((j % kNBuf) * 2 + kh) * kABuf;
+                // A fragment of step n = (ks2, rt) = (n / 8, n % 8); the MFMA asm is volatile, so the
+                // compiler keeps every LDS read where it is written: read two steps ahead (a ring of
+                // 3 fragments) so the read latency hides behind the previous steps' MFMAs
+                auto read_af = [&](int n) {
+                    const int r = 16 * (n & 7) + fr;
+                    return *reinterpret_cast<const u32x4*>(base + r * 128 + swz_slot<128>(r, (n >> 3) * 4 + fq) * 16);
+                };
+                u32x4 afr[3];
+                afr[0] = read_af(0);
+                afr[1] = read_af(1);
 #pragma unroll
-                for (int ks2 = 0; ks2 < 2; ++ks2) {
-#pragma unroll
-                    for (int rt = 0; rt < 8; ++rt) {
-                        const int r = 16 * rt + fr;
-                        const u32x4 af =
-                            *reinterpret_cast<const u32x4*>(base + r * 128 + swz_slot<128>(r, ks2 * 4 + fq) * 16);
-                        // MFMA as inline asm so W_hh stays in AGPRs (operand "a"): with the builtin
-                        // the allocator keeps W in arch VGPRs and spills it (256 W + 128 acc)
+                for (int n = 0; n < 16; ++n) {
+                    const int ks2 = n >> 3, rt = n & 7;
+                    if (n + 2 < 16) afr[(n + 2) % 3] = read_af(n + 2);
+                    const u32x4 af = afr[n % 3];
+                    // MFMA as inline asm so W_hh stays in AGPRs (operand "a"): with the builtin
+                    // the allocator keeps W in arch VGPRs and spills it (256 W + 128 acc)
 #ifndef CRN_PERSIST_ASM
 #define CRN_PERSIST_ASM 1
 #endif
 #if !CRN_PERSIST_ASM
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) mma_chunk(acc[rt][q], af, wreg[q][2 * j + ks2], bf16_t{});
+                    for (int q = 0; q < 4; ++q) mma_chunk(acc[rt][q], af, wreg[q][2 * j + ks2], bf16_t{});
 #else
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            if (j == 0 && ks2 == 0)
-                                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0"
-                                             : "=v"(acc[rt][q]) : "v"(af), "a"(wreg[q][2 * j + ks2]));
-                            else
-                                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
-                                             : "+v"(acc[rt][q]) : "v"(af), "a"(wreg[q][2 * j + ks2]));
-                        }
-#endif
+                    for (int q = 0; q < 4; ++q) {
+                        if (j == 0 && ks2 == 0)
+                            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0"
+                                         : "=v"(acc[rt][q]) : "v"(af), "a"(wreg[q][2 * j + ks2]));
+                        else
+                            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+                                         : "+v"(acc[rt][q]) : "v"(af), "a"(wreg[q][2 * j + ks2]));
                     }
+#endif
                 }
             }
             // the accumulators were written by inline-asm MFMAs, which the compiler's hazard
@@ -284,8 +294,10 @@ __global__ __launch_bounds__(kPThreads, 1) void lstm_persist_kernel(PersistArgs 
                 }
             }
         };
-        if (kh == 0) finish(std::integral_constant<int, 0>{});
-        else finish(std::integral_constant<int, 1>{});
+        if (!(p.mode & 32)) {
+            if (kh == 0) finish(std::integral_constant<int, 0>{});
+            else finish(std::integral_constant<int, 1>{});
+        }
         __syncthreads();
         // ---- publish h_t: y of frame t, sc1 (write-through) 16-B stores, 64 B per row
         {
@@ -294,7 +306,7 @@ __global__ __launch_bounds__(kPThreads, 1) void lstm_persist_kernel(PersistArgs 
             for (int i = 0; i < 2; ++i) {
                 const int piece = tid + kPThreads * i;        // 512 pieces: row r, 16-B quarter
                 const int r = piece >> 2, qq = piece & 3;
-                if (r < nrows) {
+                if (r < nrows && !(p.mode & 8)) {
                     const u32x4 v = *reinterpret_cast<const u32x4*>(smem + oH + r * kPU * 2 + qq * 16);
                     const uint32_t off = yrow0 + (uint32_t)((r >> 1) * 8192 + (r & 1) * 2048 + u0 * 2 + qq * 16);
                     __builtin_amdgcn_raw_buffer_store_b128(v, ry, off, 0, 16);   // sc1
@@ -319,9 +331,22 @@ hipError_t launch_lstm_persist(const PersistArgs& a, hipStream_t st) {
     static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_persist_kernel),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPLds);
     if (attr != hipSuccess) return attr;
+    // Co-residency: one block per CU (LDS and registers), grid <= CUs (the caller chunks the
+    // streams by the CU count).  A plain launch: hipLaunchCooperativeKernel gives the same
+    // guarantee but its queue crashes rocprofv3 at process exit (AEC_CRN_PERSIST_COOP=1 selects it).
+    static const int per_cu = [] {
+        int n = 0;
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(lstm_persist_kernel),
+                                                            kPThreads, kPLds) == hipSuccess ? n : 0;
+    }();
+    if (per_cu < 1) return hipErrorCooperativeLaunchTooLarge;
+    static const int coop = [] { const char* v = getenv("AEC_CRN_PERSIST_COOP"); return v ? atoi(v) : 0; }();
+    if (!coop) {
+        lstm_persist_kernel<<<dim3(64 * a.G), dim3(kPThreads), kPLds, st>>>(a);
+        return hipGetLastError();
+    }
     PersistArgs args = a;
     void* kargs[] = {&args};
-    // cooperative: the runtime rejects a grid that cannot be co-resident
     return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(lstm_persist_kernel), dim3(64 * a.G),
                                       dim3(kPThreads), kargs, kPLds, st);
 }
