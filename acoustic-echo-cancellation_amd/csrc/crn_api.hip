@@ -14,6 +14,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <cstdio>
 #include <vector>
 
 #include "../../include/aec_crn.h"
@@ -102,8 +103,8 @@ struct aec_crn_handle {
     std::vector<int64_t> proc_lens;                //   and its lengths
     std::vector<void*> allocs;
     StreamState* ss = nullptr;                     // aec_crn_stream_* state
-    // persistent LSTM recurrence (crn_persist.hip; AEC_CRN_PERSIST=0: one launch per frame)
-    int persist = 1;
+    // persistent LSTM recurrence (crn_persist.hip; AEC_CRN_PERSIST=0: one launch per frame, 1 / 2: kernel version)
+    int persist = 2;
     int num_cus = 0;
     int* psync = nullptr;                          // arrival counters + error word
     int* perr_host = nullptr;                      // pinned copy of the error word
@@ -714,9 +715,36 @@ static aec_status run_persist(aec_crn_handle* h, int l, int32_t B, int64_t Tmax,
         a.spin_limit = 1 << 22;
         static const int pmode = [] { const char* v = getenv("CRN_PERSIST_MODE"); return v ? atoi(v) : 0; }();
         a.mode = pmode;
-        CRN_TRY(h, hipMemsetAsync(h->psync, 0, (8 * 16 + 16) * sizeof(int), st));
-        CRN_TRY(h, crn::launch_lstm_persist(a, st));
-        CRN_TRY(h, hipMemcpyAsync(h->perr_host, h->psync + 8 * 16, sizeof(int), hipMemcpyDeviceToHost, st));
+        CRN_TRY(h, hipMemsetAsync(h->psync, 0, crn::kPersistSyncInts * sizeof(int), st));
+        static const bool dbg = getenv("CRN_PERSIST_DBG") != nullptr;
+        long long* dd = nullptr;
+        if (dbg && Tmax > 301) {
+            CRN_TRY(h, hipMalloc(reinterpret_cast<void**>(&dd), 256 * 4 * 2 * 24 * sizeof(long long)));
+            CRN_TRY(h, hipMemsetAsync(dd, 0, 256 * 4 * 2 * 24 * sizeof(long long), st));
+            a.dbg = dd;
+        }
+        CRN_TRY(h, crn::launch_lstm_persist(a, h->persist, st));
+        if (dd) {   // per event: mean ticks since the phase start over blocks and waves
+            std::vector<long long> v(256 * 4 * 2 * 24);
+            CRN_TRY(h, hipMemcpyAsync(v.data(), dd, v.size() * sizeof(long long), hipMemcpyDeviceToHost, st));
+            CRN_TRY(h, hipStreamSynchronize(st));
+            (void)hipFree(dd);
+            for (int hm = 0; hm < 2; ++hm) {
+                double sum[24] = {};
+                int n = 0;
+                for (int b = 0; b < 64 * a.G; ++b)
+                    for (int w = 0; w < 4; ++w) {
+                        const long long* e = &v[((b * 4 + w) * 2 + hm) * 24];
+                        if (!e[0] || !e[18]) continue;
+                        for (int k = 1; k < 19; ++k) sum[k] += (double)(e[k] - e[0]);
+                        ++n;
+                    }
+                fprintf(stderr, "persist2 dbg H%d n=%d poll %.0f", hm, n, sum[1] / n);
+                for (int k = 0; k < 8; ++k) fprintf(stderr, " | c%d %.0f %.0f", k, sum[2 + 2 * k] / n, sum[3 + 2 * k] / n);
+                fprintf(stderr, " | end %.0f\n", sum[18] / n);
+            }
+        }
+        CRN_TRY(h, hipMemcpyAsync(h->perr_host, h->psync + crn::kPersistErr, sizeof(int), hipMemcpyDeviceToHost, st));
     }
     CRN_TRY(h, hipEventRecord(ev, st));
     return AEC_OK;
@@ -903,7 +931,7 @@ aec_status aec_crn_create(const aec_crn_config* cfg, const float* params, size_t
     if (hipDeviceGetAttribute(&h->num_cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) h->num_cus = 0;
     if (h->es == 2 && crn::persist_supported(h->H, h->CELLS, h->S, h->num_cus)) {
         // team arrival counters + error word, and a pinned copy of the error word
-        if (hipMalloc(reinterpret_cast<void**>(&h->psync), (8 * 16 + 16) * sizeof(int)) != hipSuccess)
+        if (hipMalloc(reinterpret_cast<void**>(&h->psync), crn::kPersistSyncInts * sizeof(int)) != hipSuccess)
             return bail(AEC_ERR_OOM);
         if (hipHostMalloc(reinterpret_cast<void**>(&h->perr_host), sizeof(int)) != hipSuccess) return bail(AEC_ERR_OOM);
         *h->perr_host = 0;

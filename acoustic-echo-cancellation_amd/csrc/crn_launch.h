@@ -149,7 +149,8 @@ struct PersistArgs {
     const bf16_t* whh;          // packed W_hh [CELLS*4H][H]
     const bf16_t* gx;           // [T][B][S][CELLS*4H] (frame f = t*B + b)
     bf16_t* y;                  // [T][B][CELLS][S][H]: the layer output and the h hand-off
-    int* sync;                  // [8 teams x 16] arrival counters + [16] error word, zeroed per launch
+    int* sync;                  // kPersistSyncInts ints zeroed per launch: arrival counters (one 64-B
+                                // line each: [team] in v1, [team][half] in v2), error word at kPersistErr
     int32_t B;                  // streams of the batch (frame row stride)
     int32_t b0, nb;             // this launch's streams b0 .. b0 + nb - 1 (nb <= 256)
     int32_t T;
@@ -158,10 +159,15 @@ struct PersistArgs {
     int32_t mode = 0;           // timing experiments only (CRN_PERSIST_MODE; results invalid unless 0):
                                 // bit0 h loads out of range (zeros), bit1 no MFMA phase, bit2 no team wait,
                                 // bit3 no h stores, bit4 Gx loads out of range, bit5 no cell update
+    long long* dbg = nullptr;   // version 2 timing probe (CRN_PERSIST_DBG): [block][wave][2 phases][24 events]
 };
-size_t persist_lds_bytes();
+constexpr int kPersistErr = 8 * 2 * 16;          // error word (after 8 teams x 2 halves of counters)
+constexpr int kPersistSyncInts = kPersistErr + 16;
 bool persist_supported(int H, int cells, int seqs, int num_cus);
-hipError_t launch_lstm_persist(const PersistArgs& a, hipStream_t st);
+// version 1: one phase per frame (gates GEMM, then cell update and hand-off);
+// version 2: the team's rows in two halves whose phases alternate, so each
+// half's cell update and hand-off run under the other half's MFMAs
+hipError_t launch_lstm_persist(const PersistArgs& a, int version, hipStream_t st);
 
 // tile width the host must pad the weight rows (N) to for a GEMM of N columns
 inline int gemm_bn(int N) { return N <= 16 ? 16 : N <= 32 ? 32 : N <= 64 ? 64 : 128; }

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 for m in ${MODES:-0 1 2 4 6 7}; do
-  CRN_PERSIST_MODE=$m AEC_CRN_PERSIST=1 timeout -k 10 300 python bench.py --pipeline crn --steps 3 --warmup 1 --no-cpu --no-rtf --inflight 1 > gpurun_out/pm_$m.json 2> gpurun_out/pm_$m.err || exit 1
+  CRN_PERSIST_MODE=$m AEC_CRN_PERSIST=${PV:-1} timeout -k 10 300 python bench.py --pipeline crn --steps 3 --warmup 1 --no-cpu --no-rtf --inflight 1 > gpurun_out/pm_$m.json 2> gpurun_out/pm_$m.err || exit 1
   python - "$m" <<'PY'
 import json, sys
 d = json.loads(open(f'gpurun_out/pm_{sys.argv[1]}.json').read().strip().splitlines()[-1])
