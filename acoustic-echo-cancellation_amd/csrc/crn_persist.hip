@@ -50,6 +50,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "crn_gemm.h"
@@ -460,10 +461,6 @@ __global__ __launch_bounds__(kPThreads, 1) void lstm_persist2_kernel(PersistArgs
                                                      16, vo, (int)(so + (uint32_t)i * 32768u), 0, CRN_PERSIST_AUX);
         }
     };
-    // arrivals: one per block per half and frame (the wave whose LDS count completes the block's
-    // four signals for all of them: 32 atomics per counter and frame instead of 128)
-    __shared__ int sArr[2];
-    if (tid < 2) sArr[tid] = 0;
     auto poll = [&](int hm, int target) {
         if (stalled) return;
         int bad = 0;
@@ -481,12 +478,11 @@ __global__ __launch_bounds__(kPThreads, 1) void lstm_persist2_kernel(PersistArgs
         }
         stalled = __builtin_amdgcn_readfirstlane(bad) != 0;
     };
-    auto arrive = [&](int hf) {                              // after this wave's h stores completed
-        if (lane == 0) {
-            const int old = __hip_atomic_fetch_add(&sArr[hf], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if ((old & 3) == 3)
-                __hip_atomic_fetch_add(p.sync + (team * 2 + hf) * 16, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+    // one arrival per block per half and frame (32 atomics per counter and frame, not 128): called
+    // behind a workgroup barrier that follows every wave's wait completing its h store
+    auto arrive = [&](int hf) {
+        if (wave == 0 && lane == 0)
+            __hip_atomic_fetch_add(p.sync + (team * 2 + hf) * 16, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
 
     f32x4 acc[2][4][4];                                     // [half][slot][gate]
@@ -589,9 +585,9 @@ __global__ __launch_bounds__(kPThreads, 1) void lstm_persist2_kernel(PersistArgs
             static_for<kStages>([&](auto S) { stage(std::integral_constant<int, HF>{}, S); });
             publish(HF, tf);
             wait_vm<0>();
+            __syncthreads();                                 // every wave's store done; reads of X done before it is rewritten
             arrive(HF);
             load_gx(std::integral_constant<int, HF>{}, tf + 1, tf + 1 < T);
-            __syncthreads();                                 // every wave's reads of X done before it is rewritten
         }
         if (zero_hm) {
 #pragma unroll
@@ -626,9 +622,10 @@ __global__ __launch_bounds__(kPThreads, 1) void lstm_persist2_kernel(PersistArgs
         const int rsw = ((fr >> 1) & 7);                     // swizzle key of every A row the lane reads
         static_for<8>([&](auto Jc) {
                 constexpr int j = decltype(Jc)::value;
-                // issue order (vmcnt is in order): C0 C1 C2 | C3 | C4 | C5 | C6 S | C7 G | A: 4 DMAs per
-                // chunk, the h store S, 8 Gx loads G, the arrival atomic A.  j = 5 also completes S.
-                constexpr int kWait[8] = {8, 8, 8, 8, 9, 12, 13, 9};
+                // issue order (vmcnt is in order): C0 C1 C2 | C3 | C4 | C5 | C6 S | C7 G: 4 DMAs per chunk,
+                // the h store S, 8 Gx loads G.  j = 5 also completes S.  Wave 0 adds the arrival atomic
+                // after the j = 5 barrier: counted as absent, which only makes its later waits stricter.
+                constexpr int kWait[8] = {8, 8, 8, 8, 9, 12, 13, 8};
                 mark(HM, tm, 2 + 2 * j);                     // before the wait of chunk j
                 wait_vm<kWait[j]>();
                 mark(HM, tm, 3 + 2 * j);                     // chunk j landed (this wave's view)
