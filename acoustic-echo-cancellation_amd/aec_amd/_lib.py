@@ -25,7 +25,9 @@ _STATUS = {0: 'AEC_OK', 1: 'AEC_ERR_INVALID_ARG', 2: 'AEC_ERR_OOM', 3: 'AEC_ERR_
 EXPORTS = ('aec_weights_count', 'aec_create', 'aec_set_weights', 'aec_set_erb', 'aec_process', 'aec_process_siglens',
            'aec_stream_open', 'aec_stream_reset', 'aec_stream_step',
            'aec_set_debug', 'aec_debug_copy', 'aec_profile_enable', 'aec_profile_read',
-           'aec_erb_tables_check', 'aec_num_frames', 'aec_out_len', 'aec_last_error', 'aec_destroy')
+           'aec_erb_tables_check', 'aec_num_frames', 'aec_out_len', 'aec_last_error', 'aec_destroy',
+           'aec_set_weights_device', 'aec_train_forward', 'aec_train_backward', 'aec_train_generation',
+           'aec_adam_step')
 
 
 # every symbol include/aec_crn.h declares
@@ -104,6 +106,18 @@ def load():
     lib.aec_last_error.restype = ctypes.c_char_p
     lib.aec_destroy.argtypes = [P]
     lib.aec_destroy.restype = None
+    lib.aec_set_weights_device.argtypes = [P, P, ctypes.c_size_t, P]
+    lib.aec_set_weights_device.restype = ctypes.c_int
+    lib.aec_train_forward.argtypes = [P, P, P, P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, P, ctypes.c_int64,
+                                      P, P]
+    lib.aec_train_forward.restype = ctypes.c_int
+    lib.aec_train_backward.argtypes = [P, P, P, P]
+    lib.aec_train_backward.restype = ctypes.c_int
+    lib.aec_train_generation.argtypes = [P]
+    lib.aec_train_generation.restype = ctypes.c_int64
+    F = ctypes.c_float
+    lib.aec_adam_step.argtypes = [P, P, P, P, P, ctypes.c_size_t, ctypes.c_int64, F, F, F, F, F, P]
+    lib.aec_adam_step.restype = ctypes.c_int
     # DCCRN (include/aec_crn.h)
     lib.aec_crn_param_count.argtypes = [ctypes.POINTER(CrnConfig)]
     lib.aec_crn_param_count.restype = ctypes.c_size_t
@@ -222,6 +236,24 @@ class Handle:
         check(self.lib.aec_profile_read(self.h, ms, ctypes.byref(calls)), self.h, 'aec_profile_read')
         return list(ms), int(calls.value)
 
+    # --- training (include/aec_hip.h aec_train_*) --------------------------------
+    def set_weights_device(self, ptr, n, stream):
+        check(self.lib.aec_set_weights_device(self.h, ptr, int(n), stream), self.h, 'aec_set_weights_device')
+
+    def train_forward(self, mic_ptr, ref_ptr, near_ptr, n, B, ld, out_ptr, ld_out, loss_ptr, stream):
+        check(self.lib.aec_train_forward(self.h, mic_ptr, ref_ptr, near_ptr, int(n), int(B), int(ld), out_ptr,
+                                         int(ld_out), loss_ptr, stream), self.h, 'aec_train_forward')
+
+    def train_backward(self, grad_loss_ptr, grad_ptr, stream):
+        check(self.lib.aec_train_backward(self.h, grad_loss_ptr, grad_ptr, stream), self.h, 'aec_train_backward')
+
+    def train_generation(self):
+        return int(self.lib.aec_train_generation(self.h))
+
+    def adam_step(self, p_ptr, g_ptr, m_ptr, v_ptr, n, step, lr, beta1, beta2, eps, weight_decay, stream):
+        check(self.lib.aec_adam_step(self.h, p_ptr, g_ptr, m_ptr, v_ptr, int(n), int(step), float(lr), float(beta1),
+                                     float(beta2), float(eps), float(weight_decay), stream), self.h, 'aec_adam_step')
+
     def __del__(self):
         try:
             if getattr(self, 'h', None):
@@ -320,3 +352,4 @@ class CrnHandle:
                 self.h = None
         except Exception:
             pass
+

@@ -592,6 +592,20 @@ def default_chunk(n: int, itemsize: int = 4) -> int:
     return c
 
 
+def _write_file(path: str, w: '_Writer', sb: int, root_items) -> None:
+    root, root_bt, root_heap = _write_group(w, root_items)
+    eof = len(w.buf)
+    sbody = SIGNATURE + struct.pack('<8B', 0, 0, 0, 0, 0, 8, 8, 0) + struct.pack('<HHI', 4, 16, 0)
+    sbody += struct.pack('<QQQQ', 0, UNDEF, eof, UNDEF)
+    sbody += struct.pack('<QQII', 0, root, 1, 0) + struct.pack('<QQ', root_bt, root_heap)
+    assert len(sbody) == 96
+    w.put(sb, sbody)
+    tmp = path + '.tmp'
+    with open(tmp, 'wb') as fh:
+        fh.write(w.buf)
+    os.replace(tmp, path)
+
+
 def write_utterances(path: str, utterances: List[Dict[str, np.ndarray]], chunks: bool = True) -> None:
     """Write the reference's test-set layout: groups "0".."n-1", each with the
     four float32 signals (generate_h5files/test_wav2h5.py:44-48)."""
@@ -605,17 +619,20 @@ def write_utterances(path: str, utterances: List[Dict[str, np.ndarray]], chunks:
             kids.append((key, _write_dataset(w, a, default_chunk(a.size) if chunks else None)))
         gaddr, _, _ = _write_group(w, kids)
         groups.append((str(i), gaddr))
-    root, root_bt, root_heap = _write_group(w, groups)
-    eof = len(w.buf)
-    sbody = SIGNATURE + struct.pack('<8B', 0, 0, 0, 0, 0, 8, 8, 0) + struct.pack('<HHI', 4, 16, 0)
-    sbody += struct.pack('<QQQQ', 0, UNDEF, eof, UNDEF)
-    sbody += struct.pack('<QQII', 0, root, 1, 0) + struct.pack('<QQ', root_bt, root_heap)
-    assert len(sbody) == 96
-    w.put(sb, sbody)
-    tmp = path + '.tmp'
-    with open(tmp, 'wb') as fh:
-        fh.write(w.buf)
-    os.replace(tmp, path)
+    _write_file(path, w, sb, groups)
+
+
+def write_signals(path: str, utt: Dict[str, np.ndarray], chunks: bool = True) -> None:
+    """Write the reference's training-file layout: one utterance per file, the
+    four float32 signals at the root (generate_h5files/train_wav2h5.py:38-42,
+    read by scripts/train1.py:33-40)."""
+    w = _Writer()
+    sb = w.alloc(96)
+    kids = []
+    for key in SIGNALS:
+        a = np.asarray(utt[key], np.float32).reshape(-1)
+        kids.append((key, _write_dataset(w, a, default_chunk(a.size) if chunks else None)))
+    _write_file(path, w, sb, kids)
 
 
 def read_utterance(f: File, k: int) -> Dict[str, np.ndarray]:

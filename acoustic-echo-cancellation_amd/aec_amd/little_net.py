@@ -15,8 +15,16 @@ as the reference processes a batch of one (its normaliser uses the row's own
 mean/std, ERB.py:254-256 at batch=1 — SURVEY.md §0.5).  ``loss`` is the sum of
 the per-row losses, which equals the reference's value at B = 1.
 
-Inference only: the reference trains through autograd (scripts/train1.py:207-218);
-this module raises if asked for gradients.
+Training (scripts/train1.py:191-218): in ``train()`` mode with gradients
+enabled, ``forward`` follows the reference's training semantics on the padded
+batch (one normaliser scalar per signal over the whole [B, N] tensor,
+ERB.py:254-256; the batch-summed loss) through ``aec_train_forward``, and
+``loss.backward()`` runs ``aec_train_backward`` (head + BPTT through the GRU
+on the device) into the parameters' ``.grad`` — so the reference's loop
+(``loss.backward(); optimizer.step()`` with ``torch.optim.Adam``) runs
+unchanged.  ``aec_amd.train.Adam`` is the same optimizer as one HIP kernel.
+The gradient flows through ``loss`` only (the reference never differentiates
+``out_wav``); the inputs get no gradient.
 """
 from __future__ import annotations
 
@@ -63,6 +71,54 @@ class _ConviSTFTBuffers(nn.Module):
         self.register_buffer('weight', weight)
         self.register_buffer('window', window)
         self.register_buffer('enframe', torch.eye(WIN)[:, None, :])
+
+
+class _TrainStep(torch.autograd.Function):
+    """forward: aec_train_forward; backward: aec_train_backward (include/aec_hip.h)."""
+
+    @staticmethod
+    def forward(ctx, net, mic, ref, near, erb, *params):
+        ctx.set_materialize_grads(False)
+        dev = mic.device
+        h, idx = net._handle(dev, upload=False)
+        net._sync_erb(h, idx, erb)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        blob = torch.cat([p.detach().reshape(-1).float() for p in params])
+        B, N = mic.shape
+        lout = HOP * (N // HOP)
+        out = torch.empty(B, lout, device=dev, dtype=torch.float32)
+        loss = torch.empty((), device=dev, dtype=torch.float32)
+        with torch.cuda.device(dev):
+            h.set_weights_device(blob.data_ptr(), blob.numel(), stream)
+            h.train_forward(mic.data_ptr(), ref.data_ptr(), near.data_ptr(), N, B, N,
+                            out.data_ptr() if lout > 0 else None, max(lout, 1), loss.data_ptr(), stream)
+        net._w_key.pop(idx, None)        # the device blob no longer matches any host upload
+        ctx.h, ctx.dev, ctx.gen = h, dev, h.train_generation()
+        ctx.shapes = [p.shape for p in params]
+        ctx.keep = (blob, mic, ref, near)   # the forward's buffers stay alive until the backward
+        return out, loss
+
+    @staticmethod
+    def backward(ctx, g_out, g_loss):
+        if g_out is not None:
+            raise NotImplementedError('Little_net (gfx950) differentiates the loss only; the reference trains '
+                                      'on loss (scripts/train1.py:207-212), not on out_wav')
+        h, dev = ctx.h, ctx.dev
+        if h.train_generation() != ctx.gen:
+            raise RuntimeError('Little_net (gfx950): backward of an older forward (another training forward '
+                               'ran in between); call backward before the next training forward')
+        grad = torch.empty(sum(int(np.prod(s)) for s in ctx.shapes), device=dev, dtype=torch.float32)
+        gl = g_loss.detach().float().contiguous() if g_loss is not None else None
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        with torch.cuda.device(dev):
+            h.train_backward(gl.data_ptr() if gl is not None else None, grad.data_ptr(), stream)
+        grads, o = [], 0
+        for s in ctx.shapes:
+            k = int(np.prod(s))
+            grads.append(grad[o:o + k].view(s))
+            o += k
+        ctx.keep = None
+        return (None, None, None, None, None, *grads)
 
 
 class Little_net(nn.Module):
@@ -117,7 +173,7 @@ class Little_net(nn.Module):
         """The 12,544-float blob in state_dict order (include/aec_hip.h)."""
         return torch.cat([p.detach().reshape(-1).float().cpu() for p in self._params()]).numpy()
 
-    def _handle(self, device):
+    def _handle(self, device, upload=True):
         idx = device.index if device.index is not None else torch.cuda.current_device()
         h = self._handles.get(idx)
         if h is None:
@@ -125,6 +181,8 @@ class Little_net(nn.Module):
             h = _lib.Handle(idx, nlms_taps=nl.get('taps', 0), nlms_mu=nl.get('mu', 0.5),
                             nlms_beta=nl.get('beta', 0.9), nlms_delta=nl.get('delta', 1e-4))
             self._handles[idx] = h
+        if not upload:
+            return h, idx
         wkey = tuple((p.data_ptr(), p._version) for p in self._params())
         if self._w_key.get(idx) != wkey:
             h.set_weights(self.weights_blob())
@@ -147,9 +205,36 @@ class Little_net(nn.Module):
         """(ERB.py:252-334) mic/ref/near [B, N] (or [N]) float32 on a HIP device."""
         if mic.dim() == 1:
             mic, ref, near = mic[None], ref[None], near[None] if near is not None else None
+        if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self._params()):
+            return self._train_forward(mic, ref, near, erb)
         B, N = mic.shape
         out, loss = self.forward_ragged(mic, ref, near, erb, [N] * B)
         return out, (loss.sum() if loss is not None else None)
+
+    def _train_forward(self, mic, ref, near, erb):
+        """Training semantics of the reference (scripts/train1.py:207-208): the
+        padded [B, N] batch as ONE tensor (batch-global normaliser), the
+        batch-summed loss; differentiable w.r.t. the 8 parameters."""
+        if self.nlms:
+            raise NotImplementedError('training covers the reference network (no FD-NLMS stage)')
+        if near is None:
+            raise ValueError('training needs near (the loss target)')
+        dev = mic.device
+        if dev.type != 'cuda':
+            raise RuntimeError(f'Little_net (gfx950) needs its inputs on a HIP device, got {dev}; '
+                               'there is no CPU path')
+        if mic.requires_grad or ref.requires_grad or near.requires_grad:
+            raise NotImplementedError('Little_net (gfx950) gives no gradient to its inputs')
+        for t in (ref, near):
+            if t.shape != mic.shape or t.device != dev:
+                raise ValueError('mic, ref and near must share shape and device')
+        if erb.shape != (257, 32):
+            raise ValueError(f'erb must be [257, 32], got {tuple(erb.shape)}')
+        params = self._params()
+        if any(p.device != dev for p in params):
+            raise RuntimeError('parameters and inputs must be on the same device (net.to(device))')
+        mic, ref, near = (t.detach().contiguous().float() for t in (mic, ref, near))
+        return _TrainStep.apply(self, mic, ref, near, erb, *params)
 
     def forward_ragged(self, mic, ref, near, erb, lengths):
         """Batched call with per-row true lengths (rows zero-padded to a common
@@ -161,8 +246,9 @@ class Little_net(nn.Module):
         zero beyond) and per-row losses [B] (None when ``near`` is None)."""
         if torch.is_grad_enabled() and (mic.requires_grad or any(p.requires_grad for p in self._params())
                                         and self.training):
-            raise NotImplementedError('Little_net (gfx950) is inference-only: call it under torch.no_grad() '
-                                      'and net.eval(), as scripts/test.py:134,156 does')
+            raise NotImplementedError('forward_ragged is the inference path (batch=1 semantics per row): call it '
+                                      'under torch.no_grad() and net.eval(), as scripts/test.py:134,156 does; '
+                                      'training goes through forward() in train() mode')
         dev = mic.device
         if dev.type != 'cuda':
             raise RuntimeError(f'Little_net (gfx950) needs its inputs on a HIP device, got {dev}; '
@@ -206,7 +292,7 @@ class Little_net(nn.Module):
         """Open B concurrent streams (state zeroed) on ``device``: afterwards
         ``stream_step`` advances every stream by one 256-sample hop."""
         if torch.is_grad_enabled() and self.training:
-            raise NotImplementedError('Little_net (gfx950) is inference-only: use net.eval() and torch.no_grad()')
+            raise NotImplementedError('streaming is inference-only: use net.eval() and torch.no_grad()')
         device = torch.device(device or 'cuda')
         if device.type != 'cuda':
             raise RuntimeError(f'Little_net (gfx950) streams live on a HIP device, got {device}')

@@ -240,6 +240,17 @@ struct aec_handle {
     float* d_state = nullptr;
     int32_t stream_B = 0;
     int64_t stream_stride = 0;
+    // training (aec_train_*): state of the last aec_train_forward, read by aec_train_backward
+    float* d_th = nullptr;       // [B][T][32] GRU outputs
+    float* d_tloss = nullptr;    // [B] per-row loss
+    float* d_rec = nullptr;      // [B*T][8][32]
+    float* d_dg = nullptr;       // [B*T][4][32]
+    float* d_part = nullptr;     // [nblk][12544]
+    int64_t train_cap = 0;       // frames the training buffers hold
+    int32_t train_rows = 0;      // rows d_tloss holds
+    int32_t part_cap = 0;        // blocks d_part holds
+    int32_t train_B = 0, train_T = 0;
+    int64_t train_gen = 0;       // incremented by every aec_train_forward
 };
 
 static hipEvent_t next_event(aec_handle* h) {
@@ -420,53 +431,10 @@ static aec_status ensure_ws(aec_handle* h, int64_t B, int64_t T) {
     return AEC_OK;
 }
 
-aec_status aec_set_debug(aec_handle* h, int32_t enable) {
-    if (!h) return AEC_ERR_INVALID_ARG;
-    h->debug = enable != 0;
-    return AEC_OK;
-}
-
-aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const float* near,
-                       const int64_t* lengths, int32_t B, int64_t ld, float* out, int64_t ld_out,
-                       float* loss, void* stream) {
-    if (!h) return AEC_ERR_INVALID_ARG;
-    if (B < 0 || !lengths) return fail(h, AEC_ERR_INVALID_ARG, "bad batch / lengths");
-    std::vector<int64_t> l3((size_t)B * 3);
-    for (int b = 0; b < B; ++b) l3[3 * b] = l3[3 * b + 1] = l3[3 * b + 2] = lengths[b];
-    return aec_process_siglens(h, mic, ref, near, l3.data(), B, ld, out, ld_out, loss, stream);
-}
-
-aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref, const float* near,
-                               const int64_t* lengths3, int32_t B, int64_t ld, float* out, int64_t ld_out,
-                               float* loss, void* stream) {
-    if (!h) return AEC_ERR_INVALID_ARG;
-    if (!h->have_w || !h->have_erb) return fail(h, AEC_ERR_INVALID_ARG, "weights / erb not set");
-    if (B < 0 || !lengths3) return fail(h, AEC_ERR_INVALID_ARG, "bad batch / lengths");
-    if (B == 0) return AEC_OK;
-    if (!mic || !ref) return fail(h, AEC_ERR_INVALID_ARG, "null mic / ref");
-    if (loss && !near) return fail(h, AEC_ERR_INVALID_ARG, "loss requires near");
-    const int nsig_in = near ? 3 : 2;
-    int64_t nmax = 0;
-    for (int b = 0; b < B; ++b) {
-        const int64_t n = lengths3[3 * b];
-        for (int s = 0; s < nsig_in; ++s) {
-            const int64_t ns = lengths3[3 * b + s];
-            if (ns < 1 || ns > ld) return fail(h, AEC_ERR_INVALID_ARG, "length out of [1, ld]");
-            if (ns > INT32_MAX - 4096) return fail(h, AEC_ERR_UNSUPPORTED, "stream longer than 2^31 - 4096 samples");
-            // Little_net.forward combines the three signals frame by frame
-            // (ERB.py:287-290, 318-323): the reference raises on a frame-count mismatch
-            if (ns / 256 != n / 256)
-                return fail(h, AEC_ERR_INVALID_ARG, "ref / near frame count differs from mic's (N//256 + 1)");
-        }
-        if (aec_out_len(n) > ld_out) return fail(h, AEC_ERR_INVALID_ARG, "ld_out too small");
-        nmax = n > nmax ? n : nmax;
-    }
-    if (!out && aec_out_len(nmax) > 0) return fail(h, AEC_ERR_INVALID_ARG, "null out");
-    const int64_t Tmax = aec_num_frames(nmax);
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    AEC_ON_DEVICE(h);
-    aec_status s = ensure_ws(h, B, Tmax);
-    if (s != AEC_OK) return s;
+// Host-built work lists of a batch (analysis items of 4 frames, synthesis
+// items of 15 hops) and the per-stream lengths; rebuilt only when the
+// lengths change.
+static aec_status prepare_lists(aec_handle* h, const int64_t* lengths3, int32_t B, int nsig_in, hipStream_t st) {
     if (h->last_lens.size() != (size_t)B * 3 ||
         std::memcmp(h->last_lens.data(), lengths3, (size_t)B * 3 * sizeof(int64_t)) != 0) {
         // kernels of an earlier call (on any stream) may still read the work lists
@@ -518,6 +486,58 @@ aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref
         // `lens` is a local: make its (pageable, possibly staged) copy complete before it goes away
         HIP_TRY(h, hipStreamSynchronize(st));
     }
+    return AEC_OK;
+}
+
+aec_status aec_set_debug(aec_handle* h, int32_t enable) {
+    if (!h) return AEC_ERR_INVALID_ARG;
+    h->debug = enable != 0;
+    return AEC_OK;
+}
+
+aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const float* near,
+                       const int64_t* lengths, int32_t B, int64_t ld, float* out, int64_t ld_out,
+                       float* loss, void* stream) {
+    if (!h) return AEC_ERR_INVALID_ARG;
+    if (B < 0 || !lengths) return fail(h, AEC_ERR_INVALID_ARG, "bad batch / lengths");
+    std::vector<int64_t> l3((size_t)B * 3);
+    for (int b = 0; b < B; ++b) l3[3 * b] = l3[3 * b + 1] = l3[3 * b + 2] = lengths[b];
+    return aec_process_siglens(h, mic, ref, near, l3.data(), B, ld, out, ld_out, loss, stream);
+}
+
+aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref, const float* near,
+                               const int64_t* lengths3, int32_t B, int64_t ld, float* out, int64_t ld_out,
+                               float* loss, void* stream) {
+    if (!h) return AEC_ERR_INVALID_ARG;
+    if (!h->have_w || !h->have_erb) return fail(h, AEC_ERR_INVALID_ARG, "weights / erb not set");
+    if (B < 0 || !lengths3) return fail(h, AEC_ERR_INVALID_ARG, "bad batch / lengths");
+    if (B == 0) return AEC_OK;
+    if (!mic || !ref) return fail(h, AEC_ERR_INVALID_ARG, "null mic / ref");
+    if (loss && !near) return fail(h, AEC_ERR_INVALID_ARG, "loss requires near");
+    const int nsig_in = near ? 3 : 2;
+    int64_t nmax = 0;
+    for (int b = 0; b < B; ++b) {
+        const int64_t n = lengths3[3 * b];
+        for (int s = 0; s < nsig_in; ++s) {
+            const int64_t ns = lengths3[3 * b + s];
+            if (ns < 1 || ns > ld) return fail(h, AEC_ERR_INVALID_ARG, "length out of [1, ld]");
+            if (ns > INT32_MAX - 4096) return fail(h, AEC_ERR_UNSUPPORTED, "stream longer than 2^31 - 4096 samples");
+            // Little_net.forward combines the three signals frame by frame
+            // (ERB.py:287-290, 318-323): the reference raises on a frame-count mismatch
+            if (ns / 256 != n / 256)
+                return fail(h, AEC_ERR_INVALID_ARG, "ref / near frame count differs from mic's (N//256 + 1)");
+        }
+        if (aec_out_len(n) > ld_out) return fail(h, AEC_ERR_INVALID_ARG, "ld_out too small");
+        nmax = n > nmax ? n : nmax;
+    }
+    if (!out && aec_out_len(nmax) > 0) return fail(h, AEC_ERR_INVALID_ARG, "null out");
+    const int64_t Tmax = aec_num_frames(nmax);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    AEC_ON_DEVICE(h);
+    aec_status s = ensure_ws(h, B, Tmax);
+    if (s != AEC_OK) return s;
+    s = prepare_lists(h, lengths3, B, nsig_in, st);
+    if (s != AEC_OK) return s;
     const int nsig = near ? 3 : 2;
     if (h->pipe && B >= h->pipe_minb && h->gru_mode == 0 && h->nlms_mode == 0) {
         // K1 moments, then K6: every stream's whole chain in one block (aec_pipe.hip)
@@ -786,6 +806,126 @@ aec_status aec_stream_step(aec_handle* h, const float* mic, const float* ref, in
     return AEC_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Training step (scripts/train1.py:191-218; kernels in aec_train.hip)
+// ---------------------------------------------------------------------------
+aec_status aec_set_weights_device(aec_handle* h, const float* w, size_t n, void* stream) {
+    if (!h) return AEC_ERR_INVALID_ARG;
+    if (!w || n != kWeights32) return fail(h, AEC_ERR_INVALID_ARG, "weights blob must hold 12544 floats");
+    AEC_ON_DEVICE(h);
+    HIP_TRY(h, hipMemcpyAsync(h->d_w, w, n * sizeof(float), hipMemcpyDeviceToDevice,
+                              reinterpret_cast<hipStream_t>(stream)));
+    h->have_w = true;
+    return AEC_OK;
+}
+
+aec_status aec_train_forward(aec_handle* h, const float* mic, const float* ref, const float* near, int64_t n,
+                             int32_t B, int64_t ld, float* out, int64_t ld_out, float* loss, void* stream) {
+    if (!h) return AEC_ERR_INVALID_ARG;
+    if (!h->have_w || !h->have_erb) return fail(h, AEC_ERR_INVALID_ARG, "weights / erb not set");
+    if (h->cfg.nlms_taps != 0)
+        return fail(h, AEC_ERR_UNSUPPORTED, "training is the reference network's (nlms_taps = 0)");
+    if (B < 1 || n < 1 || n > ld) return fail(h, AEC_ERR_INVALID_ARG, "need B >= 1 and 1 <= n <= ld");
+    if (n > INT32_MAX - 4096) return fail(h, AEC_ERR_UNSUPPORTED, "stream longer than 2^31 - 4096 samples");
+    if (!mic || !ref || !near || !loss) return fail(h, AEC_ERR_INVALID_ARG, "mic, ref, near and loss are required");
+    if (out && aec_out_len(n) > ld_out) return fail(h, AEC_ERR_INVALID_ARG, "ld_out too small");
+    const int64_t T = aec_num_frames(n);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    AEC_ON_DEVICE(h);
+    aec_status s = ensure_ws(h, B, T);
+    if (s != AEC_OK) return s;
+    const int64_t frames = (int64_t)B * T;
+    const int nblk = train_wgrad_blocks(B, (int)T, h->num_cus);
+    if (frames > h->train_cap || B > h->train_rows || nblk > h->part_cap) {
+        HIP_TRY(h, hipDeviceSynchronize());
+        (void)hipFree(h->d_th); (void)hipFree(h->d_tloss); (void)hipFree(h->d_rec); (void)hipFree(h->d_dg);
+        (void)hipFree(h->d_part);
+        h->d_th = h->d_tloss = h->d_rec = h->d_dg = h->d_part = nullptr;
+        h->train_cap = 0; h->train_rows = 0; h->part_cap = 0;
+        const int64_t fc = std::max(frames, h->ws_B * h->ws_T);
+        HIP_TRY(h, hipMalloc(&h->d_th, (size_t)h->ws_B * h->ws_T * 32 * sizeof(float)));
+        HIP_TRY(h, hipMalloc(&h->d_tloss, (size_t)h->ws_B * sizeof(float)));
+        HIP_TRY(h, hipMalloc(&h->d_rec, (size_t)fc * 256 * sizeof(float)));
+        HIP_TRY(h, hipMalloc(&h->d_dg, (size_t)fc * 128 * sizeof(float)));
+        const int pc = std::max(nblk, 2 * h->num_cus);
+        HIP_TRY(h, hipMalloc(&h->d_part, (size_t)pc * kWeights * sizeof(float)));
+        h->train_cap = fc; h->train_rows = (int32_t)h->ws_B; h->part_cap = pc;
+    }
+    // collate_fn (train1.py:43-74) pads every row to n: one length for all
+    std::vector<int64_t> l3((size_t)B * 3, n);
+    s = prepare_lists(h, l3.data(), B, 3, st);
+    if (s != AEC_OK) return s;
+    const int64_t Tmax = T;
+    HIP_TRY(h, launch_moments(mic, ref, near, ld, h->d_slen, h->d_mom, 0, B, 3, st));
+    HIP_TRY(h, launch_norm_global(h->d_mom, B, n, h->d_cvals, st));
+    AnalysisArgs a{};
+    a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
+    a.ld = ld; a.items = h->d_items; a.nitems = h->item_off[B];
+    a.num_cus = h->num_cus; a.cvals = h->d_cvals; a.slen = h->d_slen;
+    a.tables = reinterpret_cast<const float*>(h->d_tab);
+    a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = 3;
+    a.feats = h->d_feats; a.Tmax = Tmax;
+    HIP_TRY(h, launch_analysis(a, st));
+    GruArgs g{};
+    g.feats = h->d_feats; g.Tmax = Tmax; g.lens = h->d_len; g.w = h->d_w;
+    g.est = h->d_est; g.loss = h->d_tloss; g.has_near = 1;
+    g.dbg_h = h->d_th;
+    g.mode = 0;
+    g.b0 = 0;
+    HIP_TRY(h, launch_gru(g, B, st));
+    if (out) {
+        SynthArgs y{};
+        y.mic = mic; y.ld = ld; y.items = h->d_sitems; y.nitems = h->sitem_off[B]; y.num_cus = h->num_cus;
+        y.cvals = h->d_cvals;
+        y.tables = reinterpret_cast<const float*>(h->d_tab);
+        y.bintab = h->d_bintab; y.est = h->d_est; y.Tmax = Tmax;
+        y.out = out; y.ld_out = ld_out;
+        HIP_TRY(h, launch_synthesis(y, st));
+    }
+    HIP_TRY(h, launch_loss_sum(h->d_tloss, B, loss, st));
+    h->last_B = B;
+    h->last_T = Tmax;
+    h->train_B = B;
+    h->train_T = (int32_t)T;
+    ++h->train_gen;
+    return AEC_OK;
+}
+
+int64_t aec_train_generation(const aec_handle* h) { return h ? h->train_gen : -1; }
+
+aec_status aec_train_backward(aec_handle* h, const float* grad_loss, float* grad, void* stream) {
+    if (!h) return AEC_ERR_INVALID_ARG;
+    if (h->train_B < 1) return fail(h, AEC_ERR_INVALID_ARG, "aec_train_backward before aec_train_forward");
+    if (!grad) return fail(h, AEC_ERR_INVALID_ARG, "null grad");
+    AEC_ON_DEVICE(h);
+    TrainArgs t{};
+    t.feats = h->d_feats; t.h = h->d_th; t.w = h->d_w;
+    t.rec = h->d_rec; t.dg = h->d_dg; t.part = h->d_part;
+    t.B = h->train_B; t.T = h->train_T; t.Tmax = h->train_T;
+    const int nblk = train_wgrad_blocks(t.B, t.T, h->num_cus);
+    if (nblk > h->part_cap) return fail(h, AEC_ERR_INVALID_ARG, "training workspace changed since the forward");
+    HIP_TRY(h, launch_train_backward(t, nblk, grad_loss, grad, reinterpret_cast<hipStream_t>(stream)));
+    return AEC_OK;
+}
+
+aec_status aec_adam_step(aec_handle* h, float* params, const float* grad, float* exp_avg, float* exp_avg_sq,
+                         size_t n, int64_t step, float lr, float beta1, float beta2, float eps, float weight_decay,
+                         void* stream) {
+    if (!h) return AEC_ERR_INVALID_ARG;
+    if (!params || !grad || !exp_avg || !exp_avg_sq) return fail(h, AEC_ERR_INVALID_ARG, "null buffer");
+    if (step < 1) return fail(h, AEC_ERR_INVALID_ARG, "step counts from 1");
+    if (!(lr >= 0.f) || !(beta1 >= 0.f && beta1 < 1.f) || !(beta2 >= 0.f && beta2 < 1.f) || !(eps >= 0.f) ||
+        !(weight_decay >= 0.f))
+        return fail(h, AEC_ERR_INVALID_ARG, "Adam hyper-parameters out of range");
+    AEC_ON_DEVICE(h);
+    // torch/optim/adam.py computes the bias corrections in double on the host
+    const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+    const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+    HIP_TRY(h, launch_adam(params, grad, exp_avg, exp_avg_sq, (int64_t)n, beta1, beta2, eps, weight_decay,
+                           (float)(lr / bc1), (float)std::sqrt(bc2), reinterpret_cast<hipStream_t>(stream)));
+    return AEC_OK;
+}
+
 void aec_destroy(aec_handle* h) {
     if (!h) return;
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
@@ -800,6 +940,8 @@ void aec_destroy(aec_handle* h) {
     (void)hipFree(h->d_mom); (void)hipFree(h->d_cvals); (void)hipFree(h->d_items); (void)hipFree(h->d_sitems); (void)hipFree(h->d_len);
     (void)hipFree(h->d_feats); (void)hipFree(h->d_est); (void)hipFree(h->d_dbg); (void)hipFree(h->d_spec);
     (void)hipFree(h->d_state); (void)hipFree(h->d_rows); (void)hipFree(h->d_slen); (void)hipFree(h->d_ring);
+    (void)hipFree(h->d_th); (void)hipFree(h->d_tloss); (void)hipFree(h->d_rec); (void)hipFree(h->d_dg);
+    (void)hipFree(h->d_part);
     delete h;
 }
 

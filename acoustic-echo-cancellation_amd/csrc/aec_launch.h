@@ -13,6 +13,7 @@ constexpr int kCH = 16;             // frames per chunk in the GRU pipeline
 constexpr int kMomChunks = 8;       // moment partials per (stream, signal)
 
 constexpr int kAnalysisBlocksPerCU = 3;
+constexpr int kWeights = 12544;     // Little_net parameter blob (state_dict order, include/aec_hip.h)
 
 // One analysis work item: 4 consecutive frames [wt, wt+4) of stream b (length n).
 struct WorkItem {
@@ -196,5 +197,24 @@ hipError_t launch_stream_step(const StreamStepArgs& a, int B, int taps, hipStrea
 // K3+K4 fused (aec_gru_synth.hip): GRU + head + synthesis of the NLMS error spectrum
 hipError_t launch_gru_synth(const GruArgs& g, const SynthArgs& y, int B, hipStream_t st);
 size_t gru_synth_smem_bytes();
+
+// Training step (aec_train.hip): the backward of Little_net's loss through the
+// head and the GRU for a padded batch of B rows of T frames each.
+struct TrainArgs {
+    const float* feats;      // [B][Tmax][96] mic_erb | ref_erb | near_erb (forward)
+    const float* h;          // [B][Tmax][32] GRU outputs (forward)
+    const float* w;          // weights blob
+    float* rec;              // [B*T][8][32] per-frame record (T1)
+    float* dg;               // [B*T][4][32] gate gradients (T2)
+    float* part;             // [nblk][kWeights] weight-gradient partials (T3)
+    int B, T;
+    int64_t Tmax;
+};
+hipError_t launch_norm_global(const double2* mom, int B, int64_t n, float* cvals, hipStream_t st);
+int train_wgrad_blocks(int B, int T, int num_cus);
+hipError_t launch_train_backward(const TrainArgs& a, int nblk, const float* grad_loss, float* grad, hipStream_t st);
+hipError_t launch_loss_sum(const float* per_stream, int B, float* loss, hipStream_t st);
+hipError_t launch_adam(float* prm, const float* grad, float* m, float* v, int64_t n, float beta1, float beta2,
+                       float eps, float wd, float step_size, float bc2_sqrt, hipStream_t st);
 
 }  // namespace aec

@@ -1,0 +1,462 @@
+// aec_train.hip — the training step of the Stage-2 post-filter on gfx950
+// (SURVEY.md §8(f) row 4).
+//
+// Reference: scripts/train1.py:191-218 — a zero-padded batch (collate_fn,
+// train1.py:43-74) through Little_net.forward with the batch-GLOBAL
+// normaliser (ERB.py:254-256 over the whole [B, N] tensor), loss.backward(),
+// Adam.step() (train1.py:153).  The loss (ERB.py:318-323) reaches the
+// parameters only through est_erb = mask * mic_erb, so the backward is the
+// head (linear1 / relu / linear2 / sigmoid) and BPTT through nn.GRU(64, 32);
+// the STFT / ERB features are parameter-free (fixed buffers).
+//
+// Forward = the inference kernels (K1 moments, norm_global_kernel here, K2
+// analysis, K3 gru_kernel writing h [B][Tmax][32], K4 synthesis).  Backward:
+//   T1 train_head_kernel   frame-parallel: the gates r, z, n, W_hn h + b_hn of
+//                          every frame recomputed from (x_t, h_{t-1}) — no
+//                          sequential dependency once h is known — and the
+//                          head forward + backward -> per-frame record
+//                          rec [B*T][8][32] = dh_head, r, z, n, ghn, dz1, dz2, o
+//   T2 train_bptt_kernel   one wave per stream, t = T-1 .. 0: the gate
+//                          gradients and dh_{t-1} = dh z + W_hh^T dg (W_hh^T in
+//                          registers, split over the wave halves as the
+//                          forward step is) -> dg [B*T][4][32] = dar, daz, dan, dghn
+//   T3 train_wgrad_kernel  every parameter gradient is a sum over frames of an
+//                          outer product of two per-frame vectors (or of one
+//                          vector, for the biases): blocks stage frame records
+//                          in LDS and each thread accumulates ~25 of the 12,544
+//                          blob entries -> part [nblk][12544] (no atomics)
+//   T4 train_reduce_kernel grad = grad_loss * sum over blocks (fixed order, f64)
+//   adam_kernel            torch.optim.Adam's update, one thread per element
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "aec_fft.h"
+#include "aec_frame.h"
+#include "aec_launch.h"
+
+namespace aec {
+
+namespace {
+constexpr int kRec = 8 * 32;           // per-frame record floats (T1 -> T2, T3)
+constexpr int kDg = 4 * 32;            // per-frame gate gradients (T2 -> T3)
+constexpr int kWgF = 32;               // frames per T3 LDS stage
+constexpr int kWgRow = 452;            // T3 LDS frame row (see train_wgrad_kernel)
+constexpr int kWgThreads = 512;
+constexpr int kWgPer = (kWeights + kWgThreads - 1) / kWgThreads;   // 25 outputs per thread
+
+__device__ __forceinline__ float sig_acc(float x) { return 1.f / (1.f + expf(-x)); }
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Batch-global normaliser: c_s = mean / std (unbiased) over all B rows of
+// signal s (each row contributes its kMomChunks partials over n samples), the
+// same scalar for every row (ERB.py:254-256 on the padded [B, N] batch).
+// grid = 3 (signal), block = 256; fixed-order sums (deterministic).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void norm_global_kernel(const double2* __restrict__ mom, int B, int64_t n,
+                                                          float* __restrict__ cvals) {
+    const int s = blockIdx.x, tid = threadIdx.x;
+    double s1 = 0.0, s2 = 0.0;
+    for (int i = tid; i < B * kMomChunks; i += 256) {
+        const int b = i / kMomChunks, c = i % kMomChunks;
+        const double2 v = mom[((int64_t)b * 3 + s) * kMomChunks + c];
+        s1 += v.x;
+        s2 += v.y;
+    }
+    __shared__ double r1[256], r2[256];
+    r1[tid] = s1;
+    r2[tid] = s2;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if (tid < st) {
+            r1[tid] += r1[tid + st];
+            r2[tid] += r2[tid + st];
+        }
+        __syncthreads();
+    }
+    const double dn = (double)B * (double)n;
+    const double mean = r1[0] / dn;
+    double num = r2[0] - r1[0] * mean;
+    if (num < 0.0) num = 0.0;
+    const float c = (float)(mean / sqrt(num / (dn - 1.0)));
+    for (int b = tid; b < B; b += 256) cvals[b * 3 + s] = c;
+}
+
+// ---------------------------------------------------------------------------
+// T1: per-frame gates + head forward / backward.  One half-wave (32 lanes,
+// lane j = unit / band j) per frame, grid-strided over the B*T frames.  The
+// matrices sit in LDS transposed where a lane walks a row (lane j reads
+// W^T[k][j]: consecutive lanes, consecutive banks) and as stored where a lane
+// walks a column (do = W2^T dz2, dh = W1[:, :32]^T dz1).
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int oWihT = 0;                       // [64][96]
+constexpr int oWhhT = oWihT + 64 * 96;         // [32][96]
+constexpr int oW1T = oWhhT + 32 * 96;          // [64][32]
+constexpr int oW2T = oW1T + 64 * 32;           // [32][32]
+constexpr int oW1 = oW2T + 32 * 32;            // [32][64]
+constexpr int oW2 = oW1 + 32 * 64;             // [32][32]
+constexpr int oBih = oW2 + 32 * 32;            // [96]
+constexpr int oBhh = oBih + 96;                // [96]
+constexpr int oB1 = oBhh + 96;                 // [32]
+constexpr int oB2 = oB1 + 32;                  // [32]
+constexpr int oScr = oB2 + 32;                 // 8 half-waves x kScr
+constexpr int kScr = 256;                      // x 64 | hp 32 | hc 64 | o 32 | dz2 32 | dz1 32
+constexpr int kHeadFloats = oScr + 8 * kScr;
+}  // namespace
+
+size_t train_head_smem_bytes() { return (size_t)kHeadFloats * 4; }
+
+__global__ __launch_bounds__(256) void train_head_kernel(TrainArgs p) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x;
+    const float* W_ih = p.w;                  // [96][64]   (blob order, aec_hip.h)
+    const float* W_hh = W_ih + 96 * 64;       // [96][32]
+    const float* b_ih = W_hh + 96 * 32;
+    const float* b_hh = b_ih + 96;
+    const float* W1 = b_hh + 96;              // [32][64]
+    const float* b1 = W1 + 32 * 64;
+    const float* W2 = b1 + 32;                // [32][32]
+    const float* b2 = W2 + 32 * 32;
+    for (int i = tid; i < 96 * 64; i += 256) smem[oWihT + (i % 64) * 96 + i / 64] = W_ih[i];
+    for (int i = tid; i < 96 * 32; i += 256) smem[oWhhT + (i % 32) * 96 + i / 32] = W_hh[i];
+    for (int i = tid; i < 32 * 64; i += 256) {
+        smem[oW1T + (i % 64) * 32 + i / 64] = W1[i];
+        smem[oW1 + i] = W1[i];
+    }
+    for (int i = tid; i < 32 * 32; i += 256) {
+        smem[oW2T + (i % 32) * 32 + i / 32] = W2[i];
+        smem[oW2 + i] = W2[i];
+    }
+    if (tid < 96) {
+        smem[oBih + tid] = b_ih[tid];
+        smem[oBhh + tid] = b_hh[tid];
+    }
+    if (tid < 32) {
+        smem[oB1 + tid] = b1[tid];
+        smem[oB2 + tid] = b2[tid];
+    }
+    __syncthreads();
+    const float* sWihT = smem + oWihT;
+    const float* sWhhT = smem + oWhhT;
+    const float* sW1T = smem + oW1T;
+    const float* sW2T = smem + oW2T;
+    const float* sW1 = smem + oW1;
+    const float* sW2 = smem + oW2;
+    const int hw = tid >> 5, j = tid & 31;
+    float* sx = smem + oScr + hw * kScr;      // x [64]
+    float* shp = sx + 64;                     // h_{t-1} [32]
+    float* shc = shp + 32;                    // [h_t, mic_erb] [64]
+    float* so = shc + 64;                     // relu(linear1) [32]
+    float* sdz2 = so + 32;
+    float* sdz1 = sdz2 + 32;
+    const int T = p.T;
+    const int64_t nf = (int64_t)p.B * T;
+    const float inv_tf = 1.f / (float)(T * 32);
+    for (int64_t g = (int64_t)blockIdx.x * 8 + hw; g < nf; g += (int64_t)gridDim.x * 8) {
+        const int b = (int)(g / T), t = (int)(g % T);
+        const int64_t row = (int64_t)b * p.Tmax + t;
+        const float* fr = p.feats + row * 96;
+        const float me = fr[j], re = fr[32 + j], ne = fr[64 + j];
+        const float ht = p.h[row * 32 + j];
+        const float hp = t > 0 ? p.h[(row - 1) * 32 + j] : 0.f;
+        sx[j] = me;
+        sx[32 + j] = fabsf(me - re);
+        shp[j] = hp;
+        shc[j] = ht;
+        shc[32 + j] = me;
+        wave_fence();
+        // gates (nn.GRU: r, z, n), recomputed from x_t and h_{t-1}
+        float gir = smem[oBih + j], giz = smem[oBih + 32 + j], gin = smem[oBih + 64 + j];
+#pragma unroll 8
+        for (int k = 0; k < 64; ++k) {
+            const float xv = sx[k];
+            gir = fmaf(sWihT[k * 96 + j], xv, gir);
+            giz = fmaf(sWihT[k * 96 + 32 + j], xv, giz);
+            gin = fmaf(sWihT[k * 96 + 64 + j], xv, gin);
+        }
+        float ghr = smem[oBhh + j], ghz = smem[oBhh + 32 + j], ghn = smem[oBhh + 64 + j];
+#pragma unroll 8
+        for (int k = 0; k < 32; ++k) {
+            const float hv = shp[k];
+            ghr = fmaf(sWhhT[k * 96 + j], hv, ghr);
+            ghz = fmaf(sWhhT[k * 96 + 32 + j], hv, ghz);
+            ghn = fmaf(sWhhT[k * 96 + 64 + j], hv, ghn);
+        }
+        const float r = sig_acc(gir + ghr);
+        const float z = sig_acc(giz + ghz);
+        const float n = tanhf(gin + r * ghn);
+        // head forward (ERB.py:295-304)
+        float z1 = smem[oB1 + j];
+#pragma unroll 8
+        for (int k = 0; k < 64; ++k) z1 = fmaf(sW1T[k * 32 + j], shc[k], z1);
+        const float o = fmaxf(z1, 0.f);
+        so[j] = o;
+        wave_fence();
+        float z2 = smem[oB2 + j];
+#pragma unroll 8
+        for (int k = 0; k < 32; ++k) z2 = fmaf(sW2T[k * 32 + j], so[k], z2);
+        const float mask = sig_acc(z2);
+        const float est = mask * me;
+        // loss (ERB.py:318-323) backward with d loss = 1; grad_loss scales T4
+        const float u = sqrtf(ne) - sqrtf(est);
+        const float dest = -(2.f * u * inv_tf) * (0.5f / sqrtf(est));
+        const float dz2 = dest * me * mask * (1.f - mask);
+        sdz2[j] = dz2;
+        wave_fence();
+        float dov = 0.f;
+#pragma unroll 8
+        for (int k = 0; k < 32; ++k) dov = fmaf(sW2[k * 32 + j], sdz2[k], dov);
+        const float dz1 = o > 0.f ? dov : 0.f;
+        sdz1[j] = dz1;
+        wave_fence();
+        float dhh = 0.f;
+#pragma unroll 8
+        for (int k = 0; k < 32; ++k) dhh = fmaf(sW1[k * 64 + j], sdz1[k], dhh);
+        float* rec = p.rec + g * kRec;
+        rec[j] = dhh;
+        rec[32 + j] = r;
+        rec[64 + j] = z;
+        rec[96 + j] = n;
+        rec[128 + j] = ghn;
+        rec[160 + j] = dz1;
+        rec[192 + j] = dz2;
+        rec[224 + j] = o;
+        wave_fence();                           // scratch reused by the next frame
+    }
+}
+
+// ---------------------------------------------------------------------------
+// T2: BPTT, one wave per stream.  Lane l: unit j = l & 31, half kh = l >> 5.
+// The lane holds W_hh[g][j] for the 48 gate rows g = 32 i + 16 kh + q
+// (i = r, z, n; q < 16): dh_{t-1}[j] = dh[j] z[j] + sum_g W_hh[g][j] dgh[g],
+// the two halves' partial sums combined with v_permlane32_swap (fixed order:
+// half 0 + half 1, identical in both halves).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void train_bptt_kernel(TrainArgs p) {
+    __shared__ __attribute__((aligned(16))) float sG[96];
+    const int lane = threadIdx.x, j = lane & 31, kh = lane >> 5;
+    const int b = blockIdx.x;
+    const float* W_hh = p.w + 96 * 64;
+    float wT[48];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) wT[16 * i + q] = W_hh[(32 * i + 16 * kh + q) * 32 + j];
+    const int T = p.T;
+    const float* rec0 = p.rec + (int64_t)b * T * kRec;
+    float* dg0 = p.dg + (int64_t)b * T * kDg;
+    const float* h0 = p.h + (int64_t)b * p.Tmax * 32;
+    auto ld = [&](int t, float& dhh, float& r, float& z, float& n, float& ghn, float& hp) {
+        const float* rc = rec0 + (int64_t)t * kRec;
+        dhh = rc[j]; r = rc[32 + j]; z = rc[64 + j]; n = rc[96 + j]; ghn = rc[128 + j];
+        hp = t > 0 ? h0[(int64_t)(t - 1) * 32 + j] : 0.f;
+    };
+    float dhh, r, z, n, ghn, hp;
+    ld(T - 1, dhh, r, z, n, ghn, hp);
+    float carry = 0.f;
+    for (int t = T - 1; t >= 0; --t) {
+        float ndhh = 0.f, nr = 0.f, nz = 0.f, nn_ = 0.f, nghn = 0.f, nhp = 0.f;
+        if (t > 0) ld(t - 1, ndhh, nr, nz, nn_, nghn, nhp);       // next step's inputs, off the chain
+        const float dh = dhh + carry;
+        const float dn = dh * (1.f - z);
+        const float dzz = dh * (hp - n);
+        const float dan = dn * (1.f - n * n);
+        const float dar = dan * ghn * r * (1.f - r);
+        const float daz = dzz * z * (1.f - z);
+        const float dghn = dan * r;
+        if (kh == 0) {
+            float* d = dg0 + (int64_t)t * kDg;
+            d[j] = dar;
+            d[32 + j] = daz;
+            d[64 + j] = dan;
+            d[96 + j] = dghn;
+            sG[j] = dar;
+            sG[32 + j] = daz;
+            sG[64 + j] = dghn;
+        }
+        wave_fence();
+        float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const float4* g4 = reinterpret_cast<const float4*>(sG + 32 * i + 16 * kh);
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const float4 v = g4[q4];
+                acc0 = fmaf(wT[16 * i + 4 * q4], v.x, acc0);
+                acc1 = fmaf(wT[16 * i + 4 * q4 + 1], v.y, acc1);
+                acc0 = fmaf(wT[16 * i + 4 * q4 + 2], v.z, acc0);
+                acc1 = fmaf(wT[16 * i + 4 * q4 + 3], v.w, acc1);
+            }
+        }
+        const float part = acc0 + acc1;
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(part), __float_as_uint(part), false, false);
+        const float other = __uint_as_float(kh ? sw[0] : sw[1]);
+        const float sum = kh ? (other + part) : (part + other);
+        carry = fmaf(dh, z, sum);
+        wave_fence();                           // sG reads done before the next step's writes
+        dhh = ndhh; r = nr; z = nz; n = nn_; ghn = nghn; hp = nhp;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// T3: weight-gradient partials.  LDS frame row (floats):
+//   [0, 96)   dgi = (dar, daz, dan)          [96, 192) dgh = (dar, daz, dghn)
+//   [192,256) x = (mic_erb, |mic - ref|)      [256,288) h_{t-1}
+//   [288,320) dz1   [320,384) (h_t, mic_erb)  [384,416) dz2   [416,448) o
+//   [448]     1.0 (bias columns)
+// Blob entry e (state_dict order) = sum over frames of row[A(e)] * row[B(e)].
+// Block k owns the frames [k * per, (k + 1) * per) of the flattened B*T.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wg_pair(int e) {
+    int a, c;
+    if (e < 6144) { a = e / 64; c = 192 + e % 64; }                          // W_ih
+    else if (e < 9216) { e -= 6144; a = 96 + e / 32; c = 256 + e % 32; }    // W_hh
+    else if (e < 9312) { a = e - 9216; c = 448; }                           // b_ih
+    else if (e < 9408) { a = 96 + e - 9312; c = 448; }                      // b_hh
+    else if (e < 11456) { e -= 9408; a = 288 + e / 64; c = 320 + e % 64; }  // linear1.weight
+    else if (e < 11488) { a = 288 + e - 11456; c = 448; }                   // linear1.bias
+    else if (e < 12512) { e -= 11488; a = 384 + e / 32; c = 416 + e % 32; } // linear2.weight
+    else { a = 384 + e - 12512; c = 448; }                                  // linear2.bias
+    return (uint32_t)a | ((uint32_t)c << 16);
+}
+
+__global__ __launch_bounds__(kWgThreads) void train_wgrad_kernel(TrainArgs p, int64_t per) {
+    __shared__ __attribute__((aligned(16))) float sR[kWgF * kWgRow];
+    const int tid = threadIdx.x;
+    uint32_t pr[kWgPer];
+    float acc[kWgPer];
+#pragma unroll
+    for (int i = 0; i < kWgPer; ++i) {
+        const int e = tid + i * kWgThreads;
+        pr[i] = e < kWeights ? wg_pair(e) : (448u | (448u << 16));
+        acc[i] = 0.f;
+    }
+    const int T = p.T;
+    const int64_t nf = (int64_t)p.B * T;
+    const int64_t g0 = (int64_t)blockIdx.x * per, g1 = min(nf, g0 + per);
+    for (int64_t gs = g0; gs < g1; gs += kWgF) {
+        const int nfr = (int)min((int64_t)kWgF, g1 - gs);
+        __syncthreads();                                  // previous stage consumed
+        for (int e = tid; e < kWgF * 32; e += kWgThreads) {
+            const int f = e >> 5, j = e & 31;
+            float* row = sR + f * kWgRow;
+            if (f < nfr) {
+                const int64_t g = gs + f;
+                const int b = (int)(g / T), t = (int)(g % T);
+                const int64_t fi = (int64_t)b * p.Tmax + t;
+                const float* d = p.dg + g * kDg;
+                const float* rc = p.rec + g * kRec;
+                const float dar = d[j], daz = d[32 + j], dan = d[64 + j], dghn = d[96 + j];
+                const float me = p.feats[fi * 96 + j], re = p.feats[fi * 96 + 32 + j];
+                row[j] = dar; row[32 + j] = daz; row[64 + j] = dan;
+                row[96 + j] = dar; row[128 + j] = daz; row[160 + j] = dghn;
+                row[192 + j] = me; row[224 + j] = fabsf(me - re);
+                row[256 + j] = t > 0 ? p.h[(fi - 1) * 32 + j] : 0.f;
+                row[288 + j] = rc[160 + j];
+                row[320 + j] = p.h[fi * 32 + j];
+                row[352 + j] = me;
+                row[384 + j] = rc[192 + j];
+                row[416 + j] = rc[224 + j];
+                if (j == 0) row[448] = 1.f;
+            } else {
+                for (int c = j; c < kWgRow; c += 32) row[c] = 0.f;
+            }
+        }
+        __syncthreads();
+        for (int f = 0; f < nfr; ++f) {
+            const float* row = sR + f * kWgRow;
+#pragma unroll
+            for (int i = 0; i < kWgPer; ++i) acc[i] = fmaf(row[pr[i] & 0xffff], row[pr[i] >> 16], acc[i]);
+        }
+    }
+    float* part = p.part + (int64_t)blockIdx.x * kWeights;
+#pragma unroll
+    for (int i = 0; i < kWgPer; ++i) {
+        const int e = tid + i * kWgThreads;
+        if (e < kWeights) part[e] = acc[i];
+    }
+}
+
+// T4: grad[e] = grad_loss * sum_k part[k][e]; the batch loss = sum_b loss_b.
+__global__ __launch_bounds__(256) void train_reduce_kernel(TrainArgs p, int nblk, const float* __restrict__ grad_loss,
+                                                           float* __restrict__ grad) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= kWeights) return;
+    double s = 0.0;
+    for (int k = 0; k < nblk; ++k) s += (double)p.part[(int64_t)k * kWeights + e];
+    const float gl = grad_loss ? *grad_loss : 1.f;
+    grad[e] = (float)s * gl;
+}
+
+__global__ void loss_sum_kernel(const float* __restrict__ per_stream, int B, float* __restrict__ loss) {
+    if (threadIdx.x != 0) return;
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += per_stream[b];
+    *loss = s;
+}
+
+// torch.optim.Adam (amsgrad = False, maximize = False; torch/optim/adam.py):
+//   g += wd p;  m = lerp(m, g, 1 - beta1);  v = beta2 v + (1 - beta2) g^2
+//   p -= step_size * m / (sqrt(v) / bc2_sqrt + eps),  step_size = lr / (1 - beta1^step)
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ prm, const float* __restrict__ grad,
+                                                   float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                   float beta1, float beta2, float eps, float wd, float step_size,
+                                                   float bc2_sqrt) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float g = grad[i];
+    const float pv = prm[i];
+    if (wd != 0.f) g = fmaf(wd, pv, g);
+    const float mv = m[i];
+    const float mn = fmaf(1.f - beta1, g - mv, mv);
+    const float vn = fmaf(beta2, v[i], (1.f - beta2) * g * g);
+    m[i] = mn;
+    v[i] = vn;
+    const float denom = sqrtf(vn) / bc2_sqrt + eps;
+    prm[i] = pv - step_size * (mn / denom);
+}
+
+hipError_t launch_norm_global(const double2* mom, int B, int64_t n, float* cvals, hipStream_t st) {
+    hipLaunchKernelGGL(norm_global_kernel, dim3(3), dim3(256), 0, st, mom, B, n, cvals);
+    return hipGetLastError();
+}
+
+int train_wgrad_blocks(int B, int T, int num_cus) {
+    const int64_t nf = (int64_t)B * T;
+    const int64_t stages = (nf + kWgF - 1) / kWgF;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(stages, 2 * (int64_t)num_cus));
+}
+
+hipError_t launch_train_backward(const TrainArgs& a, int nblk, const float* grad_loss, float* grad, hipStream_t st) {
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(train_head_kernel),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)train_head_smem_bytes());
+    if (attr != hipSuccess) return attr;
+    const int64_t nf = (int64_t)a.B * a.T;
+    const int hblocks = (int)std::min<int64_t>((nf + 7) / 8, 4096);
+    hipLaunchKernelGGL(train_head_kernel, dim3(hblocks), dim3(256), train_head_smem_bytes(), st, a);
+    hipLaunchKernelGGL(train_bptt_kernel, dim3(a.B), dim3(64), 0, st, a);
+    const int64_t stages = (nf + kWgF - 1) / kWgF;
+    const int64_t per = ((stages + nblk - 1) / nblk) * kWgF;
+    hipLaunchKernelGGL(train_wgrad_kernel, dim3(nblk), dim3(kWgThreads), 0, st, a, per);
+    hipLaunchKernelGGL(train_reduce_kernel, dim3((kWeights + 255) / 256), dim3(256), 0, st, a, nblk, grad_loss, grad);
+    return hipGetLastError();
+}
+
+hipError_t launch_loss_sum(const float* per_stream, int B, float* loss, hipStream_t st) {
+    hipLaunchKernelGGL(loss_sum_kernel, dim3(1), dim3(64), 0, st, per_stream, B, loss);
+    return hipGetLastError();
+}
+
+hipError_t launch_adam(float* prm, const float* grad, float* m, float* v, int64_t n, float beta1, float beta2,
+                       float eps, float wd, float step_size, float bc2_sqrt, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, prm, grad, m, v, n, beta1,
+                       beta2, eps, wd, step_size, bc2_sqrt);
+    return hipGetLastError();
+}
+
+}  // namespace aec

@@ -155,6 +155,41 @@ aec_status aec_profile_read(aec_handle* h, double* ms4, int64_t* calls);
 aec_status aec_erb_tables_check(const float* erb_257xbands, const float* mags, const float* est,
                                 float* bands, float* gains, int32_t* sched_len, int32_t* conflicts);
 
+/* Training step: replaces one iteration of
+ * Trainer.train (scripts/train1.py:191-218) — net(mic, far, near, erb) on a
+ * collate_fn-padded batch (train1.py:43-74), loss.backward(), Adam.step()
+ * (train1.py:153).
+ *   aec_set_weights_device(h, w, n, st)
+ *        the 12,544-float blob from DEVICE memory, copied on `stream` (the
+ *        parameters of a training loop stay on the device).
+ *   aec_train_forward(h, mic, ref, near, n, B, ld, out, ld_out, loss, st)
+ *        Little_net.forward (ERB.py:252-334) in training semantics: B rows of
+ *        n samples each (already zero-padded, as collate_fn pads), ONE
+ *        normaliser scalar per signal over the whole [B, n] batch
+ *        (ERB.py:254-256), *loss (device, 1 float) = the reference's batch
+ *        loss (ERB.py:318-323, summed over rows).  out (nullable) receives the
+ *        [B, 256*(n//256)] enhanced waveforms.  Keeps what the backward needs
+ *        in the handle (nlms_taps must be 0: the reference network).
+ *   aec_train_backward(h, grad_loss, grad, st)
+ *        loss.backward() for the last aec_train_forward: grad (device, 12,544
+ *        floats, blob order) = grad_loss * d loss / d params; grad_loss is a
+ *        device scalar (NULL = 1).
+ *   aec_train_generation(h)
+ *        count of aec_train_forward calls (an autograd binding checks that
+ *        its backward belongs to the latest forward).
+ *   aec_adam_step(h, params, grad, exp_avg, exp_avg_sq, n, step, lr, beta1,
+ *                 beta2, eps, weight_decay, st)
+ *        torch.optim.Adam (amsgrad = False) over n device floats at 1-based
+ *        `step` (train1.py:153 builds Adam(lr = train_conf['lr'])). */
+aec_status aec_set_weights_device(aec_handle* h, const float* weights_dev, size_t n_weights, void* stream);
+aec_status aec_train_forward(aec_handle* h, const float* mic, const float* ref, const float* near, int64_t n,
+                             int32_t B, int64_t ld, float* out, int64_t ld_out, float* loss, void* stream);
+aec_status aec_train_backward(aec_handle* h, const float* grad_loss, float* grad, void* stream);
+int64_t aec_train_generation(const aec_handle* h);
+aec_status aec_adam_step(aec_handle* h, float* params, const float* grad, float* exp_avg, float* exp_avg_sq,
+                         size_t n, int64_t step, float lr, float beta1, float beta2, float eps, float weight_decay,
+                         void* stream);
+
 /* Frame / output-length integers (bit-exact framing contract). */
 int64_t aec_num_frames(int64_t n_samples);   /* n//256 + 1 */
 int64_t aec_out_len(int64_t n_samples);      /* 256*(n//256) */

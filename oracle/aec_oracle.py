@@ -260,3 +260,116 @@ def erle_db(mic, out, skip=8000):
     m = np.asarray(mic[:L], np.float64)[skip:]
     o = np.asarray(out, np.float64)[skip:]
     return 10.0 * np.log10(np.sum(m * m) / max(np.sum(o * o), 1e-30))
+
+
+# --------------------------------------------------------------------------
+# Training step (SURVEY §8(f) row 4) — scripts/train1.py:191-218:
+#   padded batch (collate_fn, train1.py:43-74) -> Little_net.forward with the
+#   batch-GLOBAL normaliser (ERB.py:254-256 over the whole [B, N] tensor) ->
+#   loss.backward() -> Adam.step().  The loss (ERB.py:318-323) depends on the
+#   parameters only through est_erb = mask * mic_erb, so the gradient flows
+#   through the head (linear1 / relu / linear2 / sigmoid) and the GRU (BPTT);
+#   the STFT / ERB features carry no parameters (fixed buffers, fix=True).
+# Pinned by tests/golden/train.npz (the reference's own autograd + Adam,
+# tests/golden/make_train_golden.py).
+# --------------------------------------------------------------------------
+def train_features(mic_b, ref_b, near_b, erb):
+    """[B, N] padded batch -> (mic_erb, ref_erb, near_erb) [B, T, 32], with one
+    normaliser scalar per signal over the whole batch (ERB.py:254-256)."""
+    erb = np.asarray(erb, np.float64)
+    feats = []
+    for X in (mic_b, ref_b, near_b):
+        X = np.asarray(X, np.float64)
+        c = X.mean() / X.std(ddof=1)
+        feats.append(np.stack([magnitude(stft(x - c)) @ erb for x in X]))
+    return feats
+
+
+def gru_with_gates(x, w_ih, w_hh, b_ih, b_hh):
+    """gru() that also returns what BPTT needs: h [T,32] and r, z, n,
+    ghn = W_hn h_{t-1} + b_hn [T,32] each (nn.GRU gate order r, z, n)."""
+    x = np.asarray(x, np.float64)
+    w_ih, w_hh = np.asarray(w_ih, np.float64), np.asarray(w_hh, np.float64)
+    b_ih, b_hh = np.asarray(b_ih, np.float64), np.asarray(b_hh, np.float64)
+    H = w_hh.shape[1]
+    T = x.shape[0]
+    gi = x @ w_ih.T + b_ih
+    h = np.zeros(H)
+    hs, rs, zs, ns, ghns = (np.zeros((T, H)) for _ in range(5))
+    for t in range(T):
+        gh = w_hh @ h + b_hh
+        r = _sig(gi[t, :H] + gh[:H])
+        z = _sig(gi[t, H:2 * H] + gh[H:2 * H])
+        n_ = np.tanh(gi[t, 2 * H:] + r * gh[2 * H:])
+        h = (1.0 - z) * n_ + z * h
+        hs[t], rs[t], zs[t], ns[t], ghns[t] = h, r, z, n_, gh[2 * H:]
+    return hs, rs, zs, ns, ghns
+
+
+def train_loss_and_grads(mic_b, ref_b, near_b, erb, w):
+    """Loss (ERB.py:318-323, summed over the batch) and d loss / d param for
+    the 8 parameters (state_dict names), float64 manual backward."""
+    W = {k: np.asarray(v, np.float64) for k, v in w.items()}
+    mic_erb, ref_erb, near_erb = train_features(mic_b, ref_b, near_b, erb)
+    B, T, F = mic_erb.shape
+    g = {k: np.zeros_like(W[k]) for k in W if k.startswith(('gru1.', 'linear'))}
+    loss = 0.0
+    W1, W2 = W['linear1.weight'], W['linear2.weight']
+    Whh = W['gru1.weight_hh_l0']
+    H = Whh.shape[1]
+    for b in range(B):
+        me = mic_erb[b]
+        x = np.concatenate([me, np.abs(me - ref_erb[b])], axis=1)
+        h, r, z, n_, ghn = gru_with_gates(x, W['gru1.weight_ih_l0'], Whh,
+                                          W['gru1.bias_ih_l0'], W['gru1.bias_hh_l0'])
+        hc = np.concatenate([h, me], axis=1)
+        z1 = hc @ W1.T + W['linear1.bias']
+        o = np.maximum(z1, 0.0)
+        mask = _sig(o @ W2.T + W['linear2.bias'])
+        est = mask * me
+        u = near_erb[b] ** 0.5 - est ** 0.5
+        loss += np.sum(u * u) / (T * F)
+        # backward of the head (torch: pow, sigmoid, threshold (relu), addmm)
+        dest = -(2.0 * u / (T * F)) * 0.5 * est ** -0.5
+        dz2 = dest * me * mask * (1.0 - mask)
+        g['linear2.weight'] += dz2.T @ o
+        g['linear2.bias'] += dz2.sum(0)
+        dz1 = (dz2 @ W2) * (z1 > 0)
+        g['linear1.weight'] += dz1.T @ hc
+        g['linear1.bias'] += dz1.sum(0)
+        dh_head = dz1 @ W1[:, :H]
+        # BPTT through nn.GRU (gate order r, z, n; n = tanh(gi_n + r * ghn))
+        hprev = np.vstack([np.zeros((1, H)), h[:-1]])
+        dgi = np.zeros((T, 3 * H))
+        dgh = np.zeros((T, 3 * H))
+        carry = np.zeros(H)
+        for t in range(T - 1, -1, -1):
+            dh = dh_head[t] + carry
+            dn = dh * (1.0 - z[t])
+            dz = dh * (hprev[t] - n_[t])
+            dan = dn * (1.0 - n_[t] ** 2)
+            dar = dan * ghn[t] * r[t] * (1.0 - r[t])
+            daz = dz * z[t] * (1.0 - z[t])
+            dgi[t] = np.concatenate([dar, daz, dan])
+            dgh[t] = np.concatenate([dar, daz, dan * r[t]])
+            carry = dh * z[t] + dgh[t] @ Whh
+        g['gru1.weight_ih_l0'] += dgi.T @ x
+        g['gru1.weight_hh_l0'] += dgh.T @ hprev
+        g['gru1.bias_ih_l0'] += dgi.sum(0)
+        g['gru1.bias_hh_l0'] += dgh.sum(0)
+    return loss, g
+
+
+def adam_step(p, grad, exp_avg, exp_avg_sq, step, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8,
+              weight_decay=0.0):
+    """torch.optim.Adam (amsgrad=False, maximize=False) for one tensor at
+    1-based ``step`` — the algorithm of torch 2.10's torch/optim/adam.py
+    (_single_tensor_adam), the optimizer scripts/train1.py:153 builds.
+    Works in the dtype of its inputs; returns (p, exp_avg, exp_avg_sq)."""
+    g = grad + weight_decay * p if weight_decay else grad
+    exp_avg = exp_avg + (g - exp_avg) * (1.0 - beta1)              # lerp_(grad, 1 - beta1)
+    exp_avg_sq = exp_avg_sq * beta2 + (1.0 - beta2) * g * g
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
+    denom = np.sqrt(exp_avg_sq) / np.sqrt(bc2) + eps
+    return p - (lr / bc1) * exp_avg / denom, exp_avg, exp_avg_sq
