@@ -901,7 +901,7 @@ aec_status aec_train_backward(aec_handle* h, const float* grad_loss, float* grad
     TrainArgs t{};
     t.feats = h->d_feats; t.h = h->d_th; t.w = h->d_w;
     t.rec = h->d_rec; t.dg = h->d_dg; t.part = h->d_part;
-    t.B = h->train_B; t.T = h->train_T; t.Tmax = h->train_T;
+    t.B = h->train_B; t.T = h->train_T; t.Tmax = h->train_T; t.num_cus = h->num_cus;
     const int nblk = train_wgrad_blocks(t.B, t.T, h->num_cus);
     if (nblk > h->part_cap) return fail(h, AEC_ERR_INVALID_ARG, "training workspace changed since the forward");
     HIP_TRY(h, launch_train_backward(t, nblk, grad_loss, grad, reinterpret_cast<hipStream_t>(stream)));

@@ -209,6 +209,7 @@ struct TrainArgs {
     float* part;             // [nblk][kWeights] weight-gradient partials (T3)
     int B, T;
     int64_t Tmax;
+    int num_cus;
 };
 hipError_t launch_norm_global(const double2* mom, int B, int64_t n, float* cvals, hipStream_t st);
 int train_wgrad_blocks(int B, int T, int num_cus);

@@ -249,55 +249,70 @@ __global__ __launch_bounds__(64) void train_bptt_kernel(TrainArgs p) {
     const float* rec0 = p.rec + (int64_t)b * T * kRec;
     float* dg0 = p.dg + (int64_t)b * T * kDg;
     const float* h0 = p.h + (int64_t)b * p.Tmax * 32;
-    auto ld = [&](int t, float& dhh, float& r, float& z, float& n, float& ghn, float& hp) {
-        const float* rc = rec0 + (int64_t)t * kRec;
-        dhh = rc[j]; r = rc[32 + j]; z = rc[64 + j]; n = rc[96 + j]; ghn = rc[128 + j];
-        hp = t > 0 ? h0[(int64_t)(t - 1) * 32 + j] : 0.f;
+    // inputs of kP steps are loaded one chunk ahead (HBM latency spans
+    // several steps of the chain)
+    constexpr int kP = 8;
+    float cur[kP][6], nxt[kP][6];
+    auto ld = [&](float (&v)[kP][6], int tc) {
+#pragma unroll
+        for (int i = 0; i < kP; ++i) {
+            const int t = tc - i;
+            const float* rc = rec0 + (int64_t)max(t, 0) * kRec;
+            v[i][0] = rc[j]; v[i][1] = rc[32 + j]; v[i][2] = rc[64 + j]; v[i][3] = rc[96 + j]; v[i][4] = rc[128 + j];
+            v[i][5] = t > 0 ? h0[(int64_t)(t - 1) * 32 + j] : 0.f;
+        }
     };
-    float dhh, r, z, n, ghn, hp;
-    ld(T - 1, dhh, r, z, n, ghn, hp);
+    ld(cur, T - 1);
     float carry = 0.f;
-    for (int t = T - 1; t >= 0; --t) {
-        float ndhh = 0.f, nr = 0.f, nz = 0.f, nn_ = 0.f, nghn = 0.f, nhp = 0.f;
-        if (t > 0) ld(t - 1, ndhh, nr, nz, nn_, nghn, nhp);       // next step's inputs, off the chain
-        const float dh = dhh + carry;
-        const float dn = dh * (1.f - z);
-        const float dzz = dh * (hp - n);
-        const float dan = dn * (1.f - n * n);
-        const float dar = dan * ghn * r * (1.f - r);
-        const float daz = dzz * z * (1.f - z);
-        const float dghn = dan * r;
-        if (kh == 0) {
-            float* d = dg0 + (int64_t)t * kDg;
-            d[j] = dar;
-            d[32 + j] = daz;
-            d[64 + j] = dan;
-            d[96 + j] = dghn;
-            sG[j] = dar;
-            sG[32 + j] = daz;
-            sG[64 + j] = dghn;
-        }
-        wave_fence();
-        float acc0 = 0.f, acc1 = 0.f;
+    for (int tc = T - 1; tc >= 0; tc -= kP) {
+        if (tc - kP >= 0) ld(nxt, tc - kP);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const float4* g4 = reinterpret_cast<const float4*>(sG + 32 * i + 16 * kh);
-#pragma unroll
-            for (int q4 = 0; q4 < 4; ++q4) {
-                const float4 v = g4[q4];
-                acc0 = fmaf(wT[16 * i + 4 * q4], v.x, acc0);
-                acc1 = fmaf(wT[16 * i + 4 * q4 + 1], v.y, acc1);
-                acc0 = fmaf(wT[16 * i + 4 * q4 + 2], v.z, acc0);
-                acc1 = fmaf(wT[16 * i + 4 * q4 + 3], v.w, acc1);
+        for (int i = 0; i < kP; ++i) {
+            const int t = tc - i;
+            if (t < 0) break;
+            const float dhh = cur[i][0], r = cur[i][1], z = cur[i][2], n = cur[i][3], ghn = cur[i][4], hp = cur[i][5];
+            const float dh = dhh + carry;
+            const float dn = dh * (1.f - z);
+            const float dzz = dh * (hp - n);
+            const float dan = dn * (1.f - n * n);
+            const float dar = dan * ghn * r * (1.f - r);
+            const float daz = dzz * z * (1.f - z);
+            const float dghn = dan * r;
+            if (kh == 0) {
+                float* d = dg0 + (int64_t)t * kDg;
+                d[j] = dar;
+                d[32 + j] = daz;
+                d[64 + j] = dan;
+                d[96 + j] = dghn;
+                sG[j] = dar;
+                sG[32 + j] = daz;
+                sG[64 + j] = dghn;
             }
+            wave_fence();
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int g = 0; g < 3; ++g) {
+                const float4* g4 = reinterpret_cast<const float4*>(sG + 32 * g + 16 * kh);
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                    const float4 v = g4[q4];
+                    acc[0] = fmaf(wT[16 * g + 4 * q4], v.x, acc[0]);
+                    acc[1] = fmaf(wT[16 * g + 4 * q4 + 1], v.y, acc[1]);
+                    acc[2] = fmaf(wT[16 * g + 4 * q4 + 2], v.z, acc[2]);
+                    acc[3] = fmaf(wT[16 * g + 4 * q4 + 3], v.w, acc[3]);
+                }
+            }
+            const float part = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(part), __float_as_uint(part), false, false);
+            const float other = __uint_as_float(kh ? sw[0] : sw[1]);
+            const float sum = kh ? (other + part) : (part + other);
+            carry = fmaf(dh, z, sum);
+            wave_fence();                       // sG reads done before the next step's writes
         }
-        const float part = acc0 + acc1;
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(part), __float_as_uint(part), false, false);
-        const float other = __uint_as_float(kh ? sw[0] : sw[1]);
-        const float sum = kh ? (other + part) : (part + other);
-        carry = fmaf(dh, z, sum);
-        wave_fence();                           // sG reads done before the next step's writes
-        dhh = ndhh; r = nr; z = nz; n = nn_; ghn = nghn; hp = nhp;
+#pragma unroll
+        for (int i = 0; i < kP; ++i)
+#pragma unroll
+            for (int q = 0; q < 6; ++q) cur[i][q] = nxt[i][q];
     }
 }
 
@@ -380,15 +395,32 @@ __global__ __launch_bounds__(kWgThreads) void train_wgrad_kernel(TrainArgs p, in
     }
 }
 
-// T4: grad[e] = grad_loss * sum_k part[k][e]; the batch loss = sum_b loss_b.
+// T4: grad[e] = grad_loss * sum_k part[k][e]: block = 64 entries x 4 waves,
+// wave q sums blocks k = q, q + 4, ... (8 loads in flight), then a fixed-order
+// combine (deterministic).
 __global__ __launch_bounds__(256) void train_reduce_kernel(TrainArgs p, int nblk, const float* __restrict__ grad_loss,
                                                            float* __restrict__ grad) {
-    const int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= kWeights) return;
+    __shared__ double sp[4][64];
+    const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int e = blockIdx.x * 64 + lane;
     double s = 0.0;
-    for (int k = 0; k < nblk; ++k) s += (double)p.part[(int64_t)k * kWeights + e];
-    const float gl = grad_loss ? *grad_loss : 1.f;
-    grad[e] = (float)s * gl;
+    if (e < kWeights) {
+        int k = q;
+        for (; k + 28 < nblk; k += 32) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = p.part[(int64_t)(k + 4 * u) * kWeights + e];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += (double)v[u];
+        }
+        for (; k < nblk; k += 4) s += (double)p.part[(int64_t)k * kWeights + e];
+    }
+    sp[q][lane] = s;
+    __syncthreads();
+    if (q == 0 && e < kWeights) {
+        const float gl = grad_loss ? *grad_loss : 1.f;
+        grad[e] = (float)((sp[0][lane] + sp[1][lane]) + (sp[2][lane] + sp[3][lane])) * gl;
+    }
 }
 
 __global__ void loss_sum_kernel(const float* __restrict__ per_stream, int B, float* __restrict__ loss) {
@@ -436,13 +468,13 @@ hipError_t launch_train_backward(const TrainArgs& a, int nblk, const float* grad
                                                        (int)train_head_smem_bytes());
     if (attr != hipSuccess) return attr;
     const int64_t nf = (int64_t)a.B * a.T;
-    const int hblocks = (int)std::min<int64_t>((nf + 7) / 8, 4096);
+    const int hblocks = (int)std::min<int64_t>((nf + 7) / 8, 2 * (int64_t)a.num_cus);
     hipLaunchKernelGGL(train_head_kernel, dim3(hblocks), dim3(256), train_head_smem_bytes(), st, a);
     hipLaunchKernelGGL(train_bptt_kernel, dim3(a.B), dim3(64), 0, st, a);
     const int64_t stages = (nf + kWgF - 1) / kWgF;
     const int64_t per = ((stages + nblk - 1) / nblk) * kWgF;
     hipLaunchKernelGGL(train_wgrad_kernel, dim3(nblk), dim3(kWgThreads), 0, st, a, per);
-    hipLaunchKernelGGL(train_reduce_kernel, dim3((kWeights + 255) / 256), dim3(256), 0, st, a, nblk, grad_loss, grad);
+    hipLaunchKernelGGL(train_reduce_kernel, dim3((kWeights + 63) / 64), dim3(256), 0, st, a, nblk, grad_loss, grad);
     return hipGetLastError();
 }
 

@@ -89,6 +89,8 @@ def parse():
                     help='batches in flight (HIP streams, one handle each; 1 = strictly sequential)')
     ap.add_argument('--no-c3', action='store_true', help='skip the BASELINE config 3 (DCCRN bf16) figure')
     ap.add_argument('--c3-steps', type=int, default=10, help='timed steps of the config 3 figure')
+    ap.add_argument('--no-train', action='store_true', help='skip the training-step figure')
+    ap.add_argument('--train-steps', type=int, default=10, help='timed steps of the training-step figure')
     return ap.parse_args()
 
 
@@ -380,6 +382,97 @@ def run_c5_stream(dev, B=256, hops=200, dtype='fp8'):
                 rtf=round(dt / 0.016, 5))
 
 
+def cpu_baseline_train(seconds, B=16, n=160000):
+    """Training iteration (train1.py:199-218) with the reference's CPU op mix
+    and autograd (oracle/torch_port.py TorchTrainPort), bounded sample."""
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.join(REPO, 'oracle'))
+    from torch_port import TorchTrainPort
+    from aec_amd import synth, erb_matrix
+    w = dict(np.load(os.path.join(REPO, 'tests', 'golden', 'weights.npz')))
+    port = TorchTrainPort(w, erb_matrix())
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    mic, ref, near = (torch.from_numpy(a) for a in synth.batch(B, n, seed0=6000))
+    port.step(mic[:2, :16000], ref[:2, :16000], near[:2, :16000])
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        port.step(mic, ref, near)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or reps >= 20:
+            break
+    return dict(value=round(reps * B * (n // 256 + 1) / el, 1), unit='frames/s', cores=threads, kind='port',
+                ms_per_step=round(el / reps * 1e3, 1),
+                sample=f'{reps} training iterations on [{B} x {n}] through oracle/torch_port.py TorchTrainPort '
+                       f'(reference op mix + autograd + torch Adam), {el:.1f} s wall')
+
+
+def run_train(dev, B=16, n=160000, steps=10, warmup=2, with_cpu=False):
+    """Training iteration of scripts/train1.py:199-218 on the drop-in:
+    Little_net.train() forward on the padded [B, n] batch, loss.backward()
+    (aec_train_backward), Adam.step() (aec_adam_step); inputs resident."""
+    import numpy as np
+    import torch
+    import aec_amd
+    from aec_amd import synth
+    from aec_amd.train import Adam
+    w = dict(np.load(os.path.join(REPO, 'tests', 'golden', 'weights.npz')))
+    net = aec_amd.Little_net(aec_amd.speech_conf, 32)
+    sd = net.state_dict()
+    for k in ['gru1.weight_ih_l0', 'gru1.weight_hh_l0', 'gru1.bias_ih_l0', 'gru1.bias_hh_l0',
+              'linear1.weight', 'linear1.bias', 'linear2.weight', 'linear2.bias']:
+        sd[k] = torch.from_numpy(w[k])
+    net.load_state_dict(sd)
+    net = net.to(dev).train()
+    erb = torch.tensor(aec_amd.erb_matrix(), dtype=torch.float32, device=dev)
+    mic, ref, near = (torch.from_numpy(a).to(dev) for a in synth.batch(B, n, seed0=7000))
+    opt = Adam(net.parameters(), lr=aec_amd.train_conf['lr'])
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    stage = np.zeros(3)
+
+    def one(timed=False):
+        opt.zero_grad()
+        if timed:
+            ev[0].record()
+        _, loss = net(mic, ref, near, erb)
+        if timed:
+            ev[1].record()
+        loss.backward()
+        if timed:
+            ev[2].record()
+        opt.step()
+        if timed:
+            ev[3].record()
+        return loss
+
+    for _ in range(warmup):
+        one()
+    torch.cuda.synchronize(dev)
+    for _ in range(3):                        # stage split: a separate, event-bracketed pass
+        one(True)
+        torch.cuda.synchronize(dev)
+        stage += [ev[i].elapsed_time(ev[i + 1]) for i in range(3)]
+    stage /= 3
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = one()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    T = n // 256 + 1
+    res = dict(workload=f'one training iteration (train1.py:199-218): Little_net forward on a padded [{B} x {n}] '
+                        'batch (batch-global normaliser), loss.backward() (head + BPTT on the device), Adam.step()',
+               batch=B, steps=steps, ms_per_step=round(el / steps * 1e3, 3),
+               frames_per_s=round(B * T * steps / el, 1),
+               stage_ms={'forward': round(stage[0], 3), 'backward': round(stage[1], 3), 'adam': round(stage[2], 3)},
+               loss=round(float(loss), 5))
+    if with_cpu:
+        res['cpu_baseline'] = cpu_baseline_train(10.0, B, n)
+    return res
+
+
 def crn_workload(args, dtype, B):
     return (f'C3 (BASELINE configs[2]): DCCRN v{args.crn_version} '
             f'({"dccrn2.py" if args.crn_version == 2 else "dccrn.py"}, configs.net_conf, {dtype} MFMA) on {B} '
@@ -577,6 +670,11 @@ def main():
     c5s = None
     if world == 1 and not args.no_c3:
         c5s = run_c5_stream(dev)
+    tr = None
+    if world == 1 and not args.no_train:
+        tr = run_train(dev, 16, 160000, args.train_steps, with_cpu=not args.no_cpu)
+        tr['batch256'] = {k: v for k, v in run_train(dev, 256, 160000, max(2, args.train_steps // 2)).items()
+                          if k in ('ms_per_step', 'frames_per_s', 'stage_ms')}
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_seconds)
         sys.path.insert(0, os.path.join(REPO, 'oracle'))
@@ -616,6 +714,7 @@ def main():
             'c3_crn_bf16': c3,
             'c5_nlms_crn_bf16': c5,
             'c5_stream_fp8': c5s,
+            'train_step': tr,
         }
         if sweep:
             line['batch_sweep_frames_per_s'] = sweep

@@ -71,3 +71,42 @@ class TorchPort:
         out = y[:, 0] + 1e-9
         loss = ((near_erb ** 0.5 - est ** 0.5) ** 2).sum((1, 2)) / (T * self.erb.shape[1])
         return out, loss
+
+
+class TorchTrainPort(TorchPort):
+    """One training iteration of scripts/train1.py:199-218 with the reference's
+    CPU op mix and autograd: batch-GLOBAL normaliser (ERB.py:254-256 over the
+    padded [B, N] batch), batch-summed loss, loss.backward(), torch Adam.
+    Baseline / test only (bench.py's training CPU figure)."""
+
+    def __init__(self, weights: dict, erb: np.ndarray, lr=1e-5):
+        super().__init__(weights, erb)
+        for t in (self.w1, self.b1, self.w2, self.b2):
+            t.requires_grad_(True)
+        self.params = [self.gru.weight_ih_l0, self.gru.weight_hh_l0, self.gru.bias_ih_l0, self.gru.bias_hh_l0,
+                       self.w1, self.b1, self.w2, self.b2]
+        self.opt = torch.optim.Adam(self.params, lr=lr)
+
+    def loss(self, mic, ref, near):
+        norm = lambda x: x - (x.mean() / x.std())
+        mic, ref, near = norm(mic), norm(ref), norm(near)
+        K = WIN // 2 + 1
+        S = [self._stft(x) for x in (mic, ref, near)]
+        mag = [torch.sqrt(s[:, :K] ** 2 + s[:, K:] ** 2 + 1e-9).transpose(1, 2) for s in S]
+        mic_erb, ref_erb, near_erb = (m @ self.erb for m in mag)
+        h, _ = self.gru(torch.cat([mic_erb, (mic_erb - ref_erb).abs()], 2))
+        o = torch.relu(torch.cat([h, mic_erb], 2) @ self.w1.T + self.b1)
+        est = torch.sigmoid(o @ self.w2.T + self.b2) * mic_erb
+        gain = (est @ self.erb.T).transpose(1, 2)
+        spec = torch.cat([gain * S[0][:, :K], gain * S[0][:, K:]], 1)
+        T = spec.shape[-1]
+        F.conv_transpose1d(spec, self.inv, stride=HOP)          # out_wav, computed (and unused) as in train1.py
+        return ((near_erb ** 0.5 - est ** 0.5) ** 2).sum() / (T * self.erb.shape[1])
+
+    def step(self, mic, ref, near):
+        self.opt.zero_grad()
+        with torch.enable_grad():
+            loss = self.loss(mic, ref, near)
+        loss.backward()
+        self.opt.step()
+        return float(loss)

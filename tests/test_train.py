@@ -264,3 +264,16 @@ def test_backward_of_stale_forward_raises(tg, golden_weights, golden_erb):
         out, l3 = net(mic, ref, near, erb_t)
     with pytest.raises(NotImplementedError):
         out.sum().backward()
+
+
+def test_torch_train_port_matches_reference(tg, golden_weights, golden_erb):
+    """The CPU baseline of the training figure (oracle/torch_port.py) follows
+    the reference's autograd + Adam."""
+    import torch
+    from torch_port import TorchTrainPort
+    port = TorchTrainPort(golden_weights, golden_erb.astype(np.float32), lr=LR)
+    for it in range(2):
+        loss = port.step(*(torch.from_numpy(tg[f'{s}{it}']) for s in ('mic', 'ref', 'near')))
+        assert abs(loss - float(tg[f'loss{it}'])) <= 1e-5 * float(tg[f'loss{it}'])
+        for k, p in zip(PARAM_KEYS, port.params):
+            assert _rel(p.grad.numpy(), tg[f'grad{it}/{k}']) <= 1e-4, (it, k)
