@@ -63,8 +63,9 @@ struct Packed {
     int npad = 0, kpad = 0, N = 0, K = 0;
     float alpha = 0.f;
     int act = 0;
-    uint8_t* wq = nullptr;      // dtype 2 (LSTM input projections): e4m3 [npad][kpad]
-    uint8_t* wsc = nullptr;     //   and E8M0 scales [npad][kpad / 32]
+    uint8_t* wq = nullptr;      // dtype 2 (LSTM input projections, qualifying conv layers): e4m3 [npad8][kpad]
+    uint8_t* wsc = nullptr;     //   and E8M0 scales [npad8][kpad / 32]
+    int npad8 = 0;              // rows of wq (a multiple of the MX GEMM's 256-column tile)
 };
 
 }  // namespace
@@ -321,8 +322,9 @@ static uint8_t host_e4m3(double x) {
 // dtype 2: the packed weight rows [npad][kpad] as MX-fp8 (E8M0 scale per 32 k:
 // 2^(floor(log2 amax) - 8), the same rule as the device's activation quantizer)
 static aec_status upload_mx8(aec_crn_handle* h, Packed& pk, const std::vector<double>& w) {
-    const size_t n = (size_t)pk.npad * pk.kpad, kb = (size_t)pk.kpad / 32;
-    std::vector<uint8_t> q(n, 0), sc((size_t)pk.npad * kb, 0);
+    pk.npad8 = (pk.N + 255) / 256 * 256;
+    const size_t n = (size_t)pk.npad8 * pk.kpad, kb = (size_t)pk.kpad / 32;
+    std::vector<uint8_t> q(n, 0), sc((size_t)pk.npad8 * kb, 0);
     for (int r = 0; r < pk.N; ++r)
         for (size_t b = 0; b < kb; ++b) {
             const double* x = &w[(size_t)r * pk.kpad + b * 32];
@@ -347,6 +349,15 @@ static aec_status upload_mx8(aec_crn_handle* h, Packed& pk, const std::vector<do
     return AEC_OK;
 }
 
+// dtype 2 also runs a conv layer on the MX-fp8 GEMM when its implicit rows
+// split into 32-k blocks inside one tap (2^kshift % 32 == 0), K is a whole
+// number of 128-k stages and the layer is wide enough (N >= 128) for the
+// 256-column MX tile: encoder layers 4-5 and decoder levels 5-6 of net_conf,
+// about 75 % of the conv FLOPs.
+static bool conv_mx8(const aec_crn_handle* h, const Packed& pk, int kshift_ch) {
+    return h->mx8 && pk.K % 128 == 0 && pk.kpad == pk.K && kshift_ch % 32 == 0 && pk.N >= 128;
+}
+
 static int kpad_for(int K, size_t es) {
     const int per = (int)(crn::kStageBytes / es);
     return (K + per - 1) / per * per;
@@ -365,7 +376,9 @@ static aec_status pack_encoder(aec_crn_handle* h, Packed& pk, const RealConv& r,
         for (int k = 0; k < 5; ++k)
             for (int q = 0; q < std::min(cin_buf, r.Ci); ++q)
                 w[(size_t)o * pk.kpad + k * cin_buf + q] = r.w[((size_t)o * r.Ci + q) * 5 + k];
-    return upload_packed(h, pk, w, r.b);
+    aec_status s = upload_packed(h, pk, w, r.b);
+    if (s == AEC_OK && conv_mx8(h, pk, cin_buf)) s = upload_mx8(h, pk, w);
+    return s;
 }
 
 // decoder level: input buffer channels [dec_r, dec_i, enc_r, enc_i] (C each
@@ -395,7 +408,9 @@ static aec_status pack_decoder(aec_crn_handle* h, Packed& pk, const RealConv& r,
             for (int q = 0; q < Cin; ++q)
                 w[(size_t)o * pk.kpad + j * Cin + q] = r.w[((size_t)o * Cin + ref(q)) * 5 + tap];
         }
-    return upload_packed(h, pk, w, r.b);
+    aec_status s = upload_packed(h, pk, w, r.b);
+    if (s == AEC_OK && act == 1 && conv_mx8(h, pk, Cin)) s = upload_mx8(h, pk, w);
+    return s;
 }
 
 // LSTM cell(s): unit order u' = d*Q + c <-> reference u = c*D + d; W_hh gate
@@ -486,6 +501,18 @@ static aec_status load_params(aec_crn_handle* h, const float* params, size_t n) 
     return AEC_OK;
 }
 
+// dtype 2: bytes per frame of the largest quantized row block (LSTM input
+// rows, or the implicit rows of an MX-fp8 conv layer)
+static size_t mx8_row_bytes(const aec_crn_handle* h) {
+    size_t m = (size_t)h->S * h->H;
+    for (int i = 0; i < h->L; ++i)
+        if (h->enc[i].wq) m = std::max(m, (size_t)(128 >> i) * h->enc[i].K);
+    for (int d = 0; d < h->L; ++d)
+        for (int par = 0; par < 2; ++par)
+            if (h->dec[2 * d + par].wq) m = std::max(m, (size_t)(256 >> (h->L - d)) * h->dec[2 * d + par].K);
+    return m;
+}
+
 static aec_status ensure_ws(aec_crn_handle* h, int64_t B, int64_t T) {
     if (B <= h->ws_B && T <= h->ws_T) return AEC_OK;
     for (void* p : h->allocs) (void)hipFree(p);
@@ -508,8 +535,9 @@ static aec_status ensure_ws(aec_crn_handle* h, int64_t B, int64_t T) {
     CRN_TRY(h, alloc(&h->y, (size_t)BT * h->CELLS * h->S * h->H * es));
     if (h->nrnn > 1) CRN_TRY(h, alloc(&h->xn, (size_t)BT * h->S * h->H * es));
     if (h->mx8) {
-        CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->aq), (size_t)BT * h->S * h->H));
-        CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->as), (size_t)BT * h->S * h->H / 32));
+        const size_t qb = (size_t)BT * mx8_row_bytes(h);
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->aq), qb));
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->as), qb / 32));
     }
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->cst), (size_t)nB * h->CELLS * h->S * h->H * sizeof(float)));
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->mask), (size_t)BT * 256 * 2 * sizeof(float)));
@@ -573,6 +601,11 @@ static aec_status run_encoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipS
         a.src_elems = F * Fin * ld_in;
         const int64_t ldo = 2 * ch[i + 1];
         RowEpi e{bf.cat[i + 1], a.M, pk.N, a.rshift, Fo * ldo, ldo, ch[i + 1], pk.bias, pk.alpha, pk.act};
+        if (pk.wq) {                       // dtype 2: e4m3 rows + E8M0 scales, scaled-MFMA GEMM
+            CRN_TRY(h, crn::launch_mx8_quant(a, bf.aq, bf.as, st));
+            CRN_TRY(h, crn::launch_gemm_mx8<T>(bf.aq, bf.as, pk.wq, pk.wsc, pk.kpad, e, pk.npad8, st));
+            continue;
+        }
         CRN_TRY(h, (crn::launch_gemm_rows<T, T>(a, reinterpret_cast<const T*>(pk.w), pk.kpad,
                                                  (int)(pk.kpad * sizeof(T) / crn::kStageBytes), e, pk.npad, st)));
     }
@@ -665,6 +698,11 @@ static aec_status run_decoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipS
             if (cl != 1) {
                 const int64_t ldo = 2 * ch[cl - 1];
                 RowEpi e{bf.cat[cl - 1], a.M, pk.N, a.rshift, Fo * ldo, 2 * ldo, par * ldo, pk.bias, pk.alpha, pk.act};
+                if (pk.wq) {               // dtype 2 (see conv_mx8)
+                    CRN_TRY(h, crn::launch_mx8_quant(a, bf.aq, bf.as, st));
+                    CRN_TRY(h, crn::launch_gemm_mx8<T>(bf.aq, bf.as, pk.wq, pk.wsc, pk.kpad, e, pk.npad8, st));
+                    continue;
+                }
                 CRN_TRY(h, (crn::launch_gemm_rows<T, T>(a, reinterpret_cast<const T*>(pk.w), pk.kpad,
                                                          (int)(pk.kpad * sizeof(T) / crn::kStageBytes), e, pk.npad,
                                                          st)));
@@ -1072,8 +1110,9 @@ aec_status aec_crn_stream_open(aec_crn_handle* h, int32_t B) {
     CRN_TRY(h, alloc(&ss.gx, (size_t)B * S * C * 4 * H * es));
     if (h->nrnn > 1) CRN_TRY(h, alloc(&ss.xn, (size_t)B * S * H * es));
     if (h->mx8) {
-        CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.aq), (size_t)B * S * H));
-        CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.as), (size_t)B * S * H / 32));
+        const size_t qb = (size_t)B * mx8_row_bytes(h);
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.aq), qb));
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.as), qb / 32));
     }
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.mask), (size_t)B * 256 * 2 * sizeof(float)));
     for (int l = 0; l < h->nrnn; ++l) {

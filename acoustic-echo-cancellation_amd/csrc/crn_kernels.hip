@@ -870,7 +870,9 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
 // to +-448, round to nearest even by v_cvt_pk_fp8_f32).
 // mx8_quant_kernel: one thread per (row, 32-k block) of a RowSrc (the block
 // lies inside one tap: 2^kshift % 32 == 0, checked by the host), reading 64
-// contiguous bytes of bf16 -> q [M][K] bytes, s [M][K/32] E8M0 codes.
+// contiguous bytes of bf16 -> q [M][K] bytes, s [M][K/32] E8M0 codes.  A
+// block whose tap falls in a conv's frequency padding (RowSrc validity,
+// pmul != 0) is zeros with scale code 0.
 // --------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void mx8_quant_kernel(RowSrc a, uint8_t* __restrict__ q, uint8_t* __restrict__ s) {
     const int KB = a.K / 32;
@@ -880,12 +882,16 @@ __global__ __launch_bounds__(256) void mx8_quant_kernel(RowSrc a, uint8_t* __res
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
         const int64_t m = t / KB;
         const int k0 = (int)(t - m * KB) * 32;
-        const int64_t off = (m >> a.rshift) * a.rs_hi + (m & lomask) * a.rs_lo + (int64_t)(k0 >> a.kshift) * a.ks +
-                            (k0 & kmask) + a.base_off;
-        const u32x4* src = reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(a.src) + off);
-        u32x4 raw[4];
+        const int64_t lo = m & lomask;
+        const int pos = (int)lo * a.pmul + (k0 >> a.kshift) + a.padd;
+        u32x4 raw[4] = {};
+        if (pos >= 0 && pos < a.plim) {
+            const int64_t off = (m >> a.rshift) * a.rs_hi + lo * a.rs_lo + (int64_t)(k0 >> a.kshift) * a.ks +
+                                (k0 & kmask) + a.base_off;
+            const u32x4* src = reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(a.src) + off);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) raw[i] = src[i];
+            for (int i = 0; i < 4; ++i) raw[i] = src[i];
+        }
         float v[32];
         float amax = 0.f;
 #pragma unroll
@@ -916,7 +922,7 @@ __global__ __launch_bounds__(256) void mx8_quant_kernel(RowSrc a, uint8_t* __res
 
 hipError_t launch_mx8_quant(const RowSrc& a, uint8_t* q, uint8_t* s, hipStream_t st) {
     if (a.M <= 0) return hipSuccess;
-    if (a.K % 128 || ((1 << a.kshift) % 32) || a.pmul != 0) return hipErrorInvalidValue;
+    if (a.K % 128 || ((1 << a.kshift) % 32)) return hipErrorInvalidValue;
     const int64_t total = a.M * (a.K / 32);
     const unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 256 * 64);
     hipLaunchKernelGGL(mx8_quant_kernel, dim3(grid), dim3(256), 0, st, a, q, s);
@@ -970,12 +976,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mx8_kernel(const uint8_t* _
                                         smem + wave * (PF * 16 * FN * 16 * (int)sizeof(OutT)));
 }
 
-template <typename OutT>
-hipError_t launch_gemm_mx8(const uint8_t* aq, const uint8_t* as, const uint8_t* bq, const uint8_t* bs, int K,
-                           const RowEpi& e, int npad, hipStream_t st) {
-    if (e.M <= 0) return hipSuccess;
-    // 256 x 256 tiles, 8 waves (2 x 4, 128 x 64 per wave), 2 stage buffers of 132 B per row
-    constexpr int WM = 2, WN = 4, FM = 8, FN = 4, NBUF = 2;
+template <typename OutT, int WM, int WN, int FM, int FN, int NBUF>
+static hipError_t launch_mx8_cfg(const uint8_t* aq, const uint8_t* as, const uint8_t* bq, const uint8_t* bs, int K,
+                                 const RowEpi& e, int npad, hipStream_t st) {
     constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
     if (K % 128 || npad % BN || e.N > npad) return hipErrorInvalidValue;
     auto kern = gemm_mx8_kernel<OutT, WM, WN, FM, FN, NBUF>;
@@ -987,6 +990,19 @@ hipError_t launch_gemm_mx8(const uint8_t* aq, const uint8_t* as, const uint8_t* 
     const unsigned grid = (unsigned)((e.M + BM - 1) / BM) * (unsigned)(npad / BN);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WM * WN), lds, st, aq, as, bq, bs, K, e);
     return hipGetLastError();
+}
+
+// 256 x 256 tiles (8 waves, 128 x 64 per wave) for the batch GEMMs; 64 x 64
+// tiles (2 waves) when the 256-tile grid would not cover the CUs (the
+// per-hop streaming step: M = streams x bins)
+template <typename OutT>
+hipError_t launch_gemm_mx8(const uint8_t* aq, const uint8_t* as, const uint8_t* bq, const uint8_t* bs, int K,
+                           const RowEpi& e, int npad, hipStream_t st) {
+    if (e.M <= 0) return hipSuccess;
+    const int64_t big_tiles = (e.M + 255) / 256 * ((npad + 255) / 256);
+    if (big_tiles < 256 && npad % 64 == 0)
+        return launch_mx8_cfg<OutT, 2, 1, 2, 4, 2>(aq, as, bq, bs, K, e, npad, st);
+    return launch_mx8_cfg<OutT, 2, 4, 8, 4, 2>(aq, as, bq, bs, K, e, npad, st);
 }
 template hipError_t launch_gemm_mx8<bf16_t>(const uint8_t*, const uint8_t*, const uint8_t*, const uint8_t*, int,
                                             const RowEpi&, int, hipStream_t);

@@ -79,7 +79,7 @@ def parse():
                          'postfilter = the reference Little_net path alone (NLMS bypass); '
                          'crn = BASELINE config 3: the DCCRN (dccrn2.py, configs.net_conf) post-filter')
     ap.add_argument('--crn-dtype', choices=['bf16', 'f32', 'fp8'], default='bf16',
-                    help='--pipeline crn compute type (fp8 = bf16 with MX-fp8 LSTM input projections)')
+                    help='--pipeline crn compute type (fp8 = bf16 with MX-fp8 LSTM input projections and wide conv layers)')
     ap.add_argument('--crn-version', type=int, choices=[1, 2], default=2, help='1 = dccrn.py, 2 = dccrn2.py')
     ap.add_argument('--crn-nlms', action='store_true',
                     help='--pipeline crn: feed the DCCRN the FD-NLMS error spectrum (C5, include/aec_crn.h)')
@@ -353,7 +353,7 @@ def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu, nlms=N
 
 def run_c5_stream(dev, B=256, hops=200, dtype='fp8'):
     """BASELINE config 5's per-GPU unit: the hipGraph-captured per-hop step of
-    the DCCRN (MX-fp8 LSTM input projections) fed by the FD-NLMS, B concurrent
+    the DCCRN (MX-fp8 LSTM input projections and wide conv layers) fed by the FD-NLMS, B concurrent
     streams, one 256-sample hop per stream per step (aec_crn_stream_step)."""
     import torch
     import aec_amd
@@ -377,7 +377,8 @@ def run_c5_stream(dev, B=256, hops=200, dtype='fp8'):
     torch.cuda.empty_cache()
     return dict(workload=f'C5 (BASELINE configs[4]) per GPU: {B} concurrent streams, one 256-sample hop per '
                          f'stream per step through the hipGraph-captured STFT -> FD-NLMS (4 taps) -> DCCRN v2 '
-                         f'(net_conf, {dtype}: bf16 + MX-fp8 LSTM input projections) -> iSTFT step',
+                         f'(net_conf, {dtype}' + (': bf16 + MX-fp8 LSTM input projections and encoder 4-5 / decoder 5-6 convs'
+                         if dtype == 'fp8' else '') + ') -> iSTFT step',
                 dtype=dtype, streams=B, hops=hops, ms_per_hop=round(dt * 1e3, 4), frames_per_s=round(B / dt, 1),
                 rtf=round(dt / 0.016, 5))
 

@@ -54,9 +54,13 @@ typedef struct {
     int32_t use_cbn;            /* v2: ComplexBatchNorm (1) or BatchNorm2d (0)               */
     int32_t masking_mode;       /* v2: 'E', 'C' or 'R' (character code); v1 uses 'C'         */
     int32_t dtype;              /* compute / storage type: 0 = float32, 1 = bfloat16,
-                                   2 = bfloat16 with MX-fp8 LSTM input projections (OCP e4m3
-                                   weights and activations, E8M0 scale per 32 k; needs
-                                   H % 128 == 0 and H / (256 >> n_layers) % 32 == 0)       */
+                                   2 = bfloat16 with MX-fp8 GEMMs (OCP e4m3 weights and
+                                   activations, E8M0 scale per 32 k) for the LSTM input
+                                   projections and every conv layer whose implicit rows
+                                   allow it (input channels % 32 == 0, K % 128 == 0,
+                                   output channels >= 128: encoder 4-5 and decoder levels
+                                   5-6 of net_conf); needs H % 128 == 0 and
+                                   H / (256 >> n_layers) % 32 == 0                         */
     /* Build-defined FD-NLMS front end (no reference counterpart; SURVEY.md §8
      * a13 + a14, the Stage-2 "NLMS -> CRN" composition).  nlms_taps = 0 is the
      * reference-parity network.  With nlms_taps > 0 every frame's mic spectrum

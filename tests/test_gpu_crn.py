@@ -7,10 +7,12 @@ Tolerances (relative RMS, written here):
   (observed float32-reference vs float64-oracle: ~6e-7);
 * bf16 path (bf16 storage / MFMA, f32 accumulate): out_wav <= BF16_WAV_TOL,
   mask <= BF16_MASK_TOL (reduced precision; the f32 path is the parity gate);
-* fp8 path (bf16 + MX-fp8 LSTM input projections: e4m3 weights and
+* fp8 path (bf16 + MX-fp8 GEMMs for the LSTM input projections and the
+  wide conv layers, encoder 4-5 / decoder levels 5-6: e4m3 weights and
   activations, E8M0 scale per 32 k): out_wav <= FP8_WAV_TOL, mask <=
   FP8_MASK_TOL against the reference, and within FP8_VS_BF16_TOL of the bf16
-  path (the only change is the input projection's operand rounding);
+  path (the only change is those GEMMs' operand rounding; observed out_wav
+  relative RMS vs the reference 0.0035-0.0045 against bf16's 0.0024-0.0034);
 * integer framing (T, output length) bit-exact; batch composition (ragged
   rows in one call vs one call per row) bit-exact on every path.
 """
