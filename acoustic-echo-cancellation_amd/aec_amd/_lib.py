@@ -27,7 +27,7 @@ EXPORTS = ('aec_weights_count', 'aec_create', 'aec_set_weights', 'aec_set_erb', 
            'aec_set_debug', 'aec_debug_copy', 'aec_profile_enable', 'aec_profile_read',
            'aec_erb_tables_check', 'aec_num_frames', 'aec_out_len', 'aec_last_error', 'aec_destroy',
            'aec_set_weights_device', 'aec_train_forward', 'aec_train_backward', 'aec_train_generation',
-           'aec_adam_step')
+           'aec_adam_step', 'aec_adam_step_multi')
 
 
 # every symbol include/aec_crn.h declares
@@ -118,6 +118,8 @@ def load():
     F = ctypes.c_float
     lib.aec_adam_step.argtypes = [P, P, P, P, P, ctypes.c_size_t, ctypes.c_int64, F, F, F, F, F, P]
     lib.aec_adam_step.restype = ctypes.c_int
+    lib.aec_adam_step_multi.argtypes = [P, P, P, P, P, P, P, ctypes.c_int32, F, F, F, F, F, P]
+    lib.aec_adam_step_multi.restype = ctypes.c_int
     # DCCRN (include/aec_crn.h)
     lib.aec_crn_param_count.argtypes = [ctypes.POINTER(CrnConfig)]
     lib.aec_crn_param_count.restype = ctypes.c_size_t
@@ -253,6 +255,15 @@ class Handle:
     def adam_step(self, p_ptr, g_ptr, m_ptr, v_ptr, n, step, lr, beta1, beta2, eps, weight_decay, stream):
         check(self.lib.aec_adam_step(self.h, p_ptr, g_ptr, m_ptr, v_ptr, int(n), int(step), float(lr), float(beta1),
                                      float(beta2), float(eps), float(weight_decay), stream), self.h, 'aec_adam_step')
+
+    def adam_step_multi(self, p_ptrs, g_ptrs, m_ptrs, v_ptrs, sizes, steps, lr, beta1, beta2, eps, weight_decay,
+                        stream):
+        n = len(p_ptrs)
+        arr = lambda xs: (ctypes.c_void_p * max(n, 1))(*xs)
+        i64 = lambda xs: (ctypes.c_int64 * max(n, 1))(*[int(x) for x in xs])
+        check(self.lib.aec_adam_step_multi(self.h, arr(p_ptrs), arr(g_ptrs), arr(m_ptrs), arr(v_ptrs), i64(sizes),
+                                           i64(steps), n, float(lr), float(beta1), float(beta2), float(eps),
+                                           float(weight_decay), stream), self.h, 'aec_adam_step_multi')
 
     def __del__(self):
         try:

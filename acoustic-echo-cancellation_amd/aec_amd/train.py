@@ -4,8 +4,8 @@
   file per utterance (root datasets ``nearend_speech``, ``nearend_mic``,
   ``farend_speech``, ``echo``), read with ``h5lite`` (h5py is absent); the
   batch zero-padded to the longest ``nearend_speech``.
-* ``Adam`` — ``torch.optim.Adam`` (train1.py:153) with the update in one HIP
-  kernel per parameter (``aec_adam_step``, include/aec_hip.h).  Same
+* ``Adam`` — ``torch.optim.Adam`` (train1.py:153) with the update of a param
+  group in one HIP launch (``aec_adam_step_multi``, include/aec_hip.h).  Same
   constructor, same ``state`` keys (``step``, ``exp_avg``, ``exp_avg_sq``), so
   its ``state_dict`` is interchangeable with torch's (the reference's
   ``CheckPoint`` stores ``optimizer.state_dict()``, train1.py:244-246).
@@ -65,7 +65,7 @@ def _adam_handle(dev):
 
 class Adam(torch.optim.Optimizer):
     """torch.optim.Adam (amsgrad = False, maximize = False) on the device:
-    one ``aec_adam_step`` launch per parameter tensor."""
+    one ``aec_adam_step_multi`` launch per param group (and device)."""
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, amsgrad=False):
         if amsgrad:
@@ -86,6 +86,7 @@ class Adam(torch.optim.Optimizer):
                 loss = closure()
         for group in self.param_groups:
             b1, b2 = group['betas']
+            per_dev = {}
             for p in group['params']:
                 if p.grad is None:
                     continue
@@ -99,12 +100,17 @@ class Adam(torch.optim.Optimizer):
                     st['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st['step'] += 1
-                g = p.grad.contiguous()
-                h = _adam_handle(p.device)
-                with torch.cuda.device(p.device):
-                    h.adam_step(p.data_ptr(), g.data_ptr(), st['exp_avg'].data_ptr(), st['exp_avg_sq'].data_ptr(),
-                                p.numel(), int(st['step'].item()), group['lr'], b1, b2, group['eps'],
-                                group['weight_decay'], torch.cuda.current_stream(p.device).cuda_stream)
+                per_dev.setdefault(p.device, []).append((p, p.grad.contiguous(), st))
+            for dev, items in per_dev.items():
+                h = _adam_handle(dev)
+                with torch.cuda.device(dev):
+                    # one launch for the group's tensors on this device (aec_adam_step_multi)
+                    h.adam_step_multi([p.data_ptr() for p, _, _ in items], [g.data_ptr() for _, g, _ in items],
+                                      [st['exp_avg'].data_ptr() for _, _, st in items],
+                                      [st['exp_avg_sq'].data_ptr() for _, _, st in items],
+                                      [p.numel() for p, _, _ in items], [int(st['step'].item()) for _, _, st in items],
+                                      group['lr'], b1, b2, group['eps'], group['weight_decay'],
+                                      torch.cuda.current_stream(dev).cuda_stream)
         return loss
 
 

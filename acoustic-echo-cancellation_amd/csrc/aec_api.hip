@@ -246,6 +246,9 @@ struct aec_handle {
     float* d_rec = nullptr;      // [B*T][8][32]
     float* d_dg = nullptr;       // [B*T][4][32]
     float* d_part = nullptr;     // [nblk][12544]
+    float* d_scan = nullptr;     // chunked-scan BPTT: [B][chunks][32][32 + 2]
+    int64_t scan_cap = 0;        // floats d_scan holds
+    int bptt_serial = 0;         // AEC_BPTT_SERIAL=1: the one-wave-per-stream BPTT (A/B)
     int64_t train_cap = 0;       // frames the training buffers hold
     int32_t train_rows = 0;      // rows d_tloss holds
     int32_t part_cap = 0;        // blocks d_part holds
@@ -375,6 +378,7 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
     if (const char* m = std::getenv("AEC_PIPE")) h->pipe = std::atoi(m);
     if (const char* m = std::getenv("AEC_PIPE_MINB")) h->pipe_minb = std::atoi(m);
     if (const char* m = std::getenv("AEC_PIPE_MODE")) h->pipe_mode = std::atoi(m);
+    if (const char* m = std::getenv("AEC_BPTT_SERIAL")) h->bptt_serial = std::atoi(m);
     if (const char* m = std::getenv("AEC_SUBBATCH")) h->sub_max = std::max(1, std::min(aec_handle::kMaxSub, std::atoi(m)));
     {
         int cus = 0;
@@ -904,6 +908,21 @@ aec_status aec_train_backward(aec_handle* h, const float* grad_loss, float* grad
     t.B = h->train_B; t.T = h->train_T; t.Tmax = h->train_T; t.num_cus = h->num_cus;
     const int nblk = train_wgrad_blocks(t.B, t.T, h->num_cus);
     if (nblk > h->part_cap) return fail(h, AEC_ERR_INVALID_ARG, "training workspace changed since the forward");
+    if (!h->bptt_serial) {
+        const int64_t nc = train_scan_chunks(t.T);
+        const int64_t need = (int64_t)t.B * nc * (1024 + 64);
+        if (need > h->scan_cap) {
+            HIP_TRY(h, hipDeviceSynchronize());
+            (void)hipFree(h->d_scan);
+            h->d_scan = nullptr;
+            h->scan_cap = 0;
+            HIP_TRY(h, hipMalloc(&h->d_scan, (size_t)need * sizeof(float)));
+            h->scan_cap = need;
+        }
+        t.scan_p = h->d_scan;
+        t.scan_q = h->d_scan + (size_t)t.B * nc * 1024;
+        t.scan_g = t.scan_q + (size_t)t.B * nc * 32;
+    }
     HIP_TRY(h, launch_train_backward(t, nblk, grad_loss, grad, reinterpret_cast<hipStream_t>(stream)));
     return AEC_OK;
 }
@@ -926,6 +945,36 @@ aec_status aec_adam_step(aec_handle* h, float* params, const float* grad, float*
     return AEC_OK;
 }
 
+aec_status aec_adam_step_multi(aec_handle* h, float* const* params, const float* const* grads, float* const* exp_avg,
+                               float* const* exp_avg_sq, const int64_t* sizes, const int64_t* steps, int32_t count,
+                               float lr, float beta1, float beta2, float eps, float weight_decay, void* stream) {
+    if (!h) return AEC_ERR_INVALID_ARG;
+    if (count < 0 || (count > 0 && (!params || !grads || !exp_avg || !exp_avg_sq || !sizes || !steps)))
+        return fail(h, AEC_ERR_INVALID_ARG, "null tensor list");
+    if (!(lr >= 0.f) || !(beta1 >= 0.f && beta1 < 1.f) || !(beta2 >= 0.f && beta2 < 1.f) || !(eps >= 0.f) ||
+        !(weight_decay >= 0.f))
+        return fail(h, AEC_ERR_INVALID_ARG, "Adam hyper-parameters out of range");
+    AEC_ON_DEVICE(h);
+    for (int32_t c0 = 0; c0 < count; c0 += kAdamMax) {
+        AdamList L{};
+        L.n = std::min<int32_t>(kAdamMax, count - c0);
+        L.off[0] = 0;
+        for (int k = 0; k < L.n; ++k) {
+            const int i = c0 + k;
+            if (!params[i] || !grads[i] || !exp_avg[i] || !exp_avg_sq[i] || sizes[i] < 0 || steps[i] < 1)
+                return fail(h, AEC_ERR_INVALID_ARG, "bad tensor in the list");
+            L.p[k] = params[i]; L.g[k] = grads[i]; L.m[k] = exp_avg[i]; L.v[k] = exp_avg_sq[i];
+            const double bc1 = 1.0 - std::pow((double)beta1, (double)steps[i]);
+            const double bc2 = 1.0 - std::pow((double)beta2, (double)steps[i]);
+            L.step_size[k] = (float)(lr / bc1);
+            L.bc2_sqrt[k] = (float)std::sqrt(bc2);
+            L.off[k + 1] = L.off[k] + sizes[i];
+        }
+        HIP_TRY(h, launch_adam_multi(L, beta1, beta2, eps, weight_decay, reinterpret_cast<hipStream_t>(stream)));
+    }
+    return AEC_OK;
+}
+
 void aec_destroy(aec_handle* h) {
     if (!h) return;
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
@@ -941,7 +990,7 @@ void aec_destroy(aec_handle* h) {
     (void)hipFree(h->d_feats); (void)hipFree(h->d_est); (void)hipFree(h->d_dbg); (void)hipFree(h->d_spec);
     (void)hipFree(h->d_state); (void)hipFree(h->d_rows); (void)hipFree(h->d_slen); (void)hipFree(h->d_ring);
     (void)hipFree(h->d_th); (void)hipFree(h->d_tloss); (void)hipFree(h->d_rec); (void)hipFree(h->d_dg);
-    (void)hipFree(h->d_part);
+    (void)hipFree(h->d_part); (void)hipFree(h->d_scan);
     delete h;
 }
 

@@ -210,11 +210,27 @@ struct TrainArgs {
     int B, T;
     int64_t Tmax;
     int num_cus;
+    float* scan_p;           // chunked-scan BPTT (null: the serial kernel): [B][chunks][32][32] chunk maps,
+    float* scan_q;           //   [B][chunks][32] offsets,
+    float* scan_g;           //   [B][chunks][32] g at each chunk's first step
 };
+int train_scan_chunks(int T);
 hipError_t launch_norm_global(const double2* mom, int B, int64_t n, float* cvals, hipStream_t st);
 int train_wgrad_blocks(int B, int T, int num_cus);
 hipError_t launch_train_backward(const TrainArgs& a, int nblk, const float* grad_loss, float* grad, hipStream_t st);
 hipError_t launch_loss_sum(const float* per_stream, int B, float* loss, hipStream_t st);
+constexpr int kAdamMax = 16;
+struct AdamList {                // up to kAdamMax tensors of one param group
+    float* p[kAdamMax];
+    const float* g[kAdamMax];
+    float* m[kAdamMax];
+    float* v[kAdamMax];
+    float step_size[kAdamMax];   // lr / (1 - beta1^step)
+    float bc2_sqrt[kAdamMax];    // sqrt(1 - beta2^step)
+    int64_t off[kAdamMax + 1];   // element offsets (off[0] = 0)
+    int n;
+};
+hipError_t launch_adam_multi(const AdamList& L, float beta1, float beta2, float eps, float wd, hipStream_t st);
 hipError_t launch_adam(float* prm, const float* grad, float* m, float* v, int64_t n, float beta1, float beta2,
                        float eps, float wd, float step_size, float bc2_sqrt, hipStream_t st);
 

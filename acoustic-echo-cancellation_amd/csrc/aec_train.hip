@@ -316,6 +316,275 @@ __global__ __launch_bounds__(64) void train_bptt_kernel(TrainArgs p) {
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// T2 as a chunked scan.  With the forward values fixed, BPTT is an AFFINE
+// recurrence in g_t = dL/dh_t:
+//   g_{t-1} = dh_head[t-1] + M_t g_t,
+//   M_t = diag(z_t) + W_r^T diag(a_r) + W_z^T diag(a_z) + W_n^T diag(a_n),
+//   a_r = (1-z)(1-n^2) ghn r(1-r),  a_z = (h_{t-1} - n) z(1-z),  a_n = (1-z)(1-n^2) r
+// so the 626-step chain splits into chunks of kL steps:
+//   T2a (B x chunks blocks, parallel): each chunk's map g_{t0} = P g_{t1} + q
+//       composed over its steps (32x32 P, 1,536 FMAs per lane and step);
+//   T2b (one wave per stream): g at every chunk start, chunks right to left
+//       (C matvecs instead of T steps);
+//   T2c (B x chunks blocks): each chunk's steps from its incoming g, writing
+//       dg as train_bptt_kernel does.
+// Same gradients up to the summation order (tests/test_train.py).
+// ---------------------------------------------------------------------------
+constexpr int kL = 16;                       // steps per chunk
+
+// forward values of step t for unit j: z and the three a's (see above)
+__device__ __forceinline__ void bptt_coef(const float* rc, float hp, int j, float& z, float& ar, float& az,
+                                          float& an) {
+    const float r = rc[32 + j], zz = rc[64 + j], n = rc[96 + j], ghn = rc[128 + j];
+    const float c = (1.f - zz) * (1.f - n * n);
+    z = zz;
+    ar = c * ghn * r * (1.f - r);
+    az = (hp - n) * zz * (1.f - zz);
+    an = c * r;
+}
+
+// T2a: one wave per (stream, chunk).  The chunk's forward values are staged
+// in LDS first (one load latency); per step the 32 x 32 M_{t+1} is built in
+// LDS (column-major: sM[k][i] = M[i][k], 48 FMAs per lane from W_hh in
+// registers), then P <- M P with a 4 x 4 output tile per lane (two b128 LDS
+// reads per 16 FMAs) and q <- dh_head + M q.
+__global__ __launch_bounds__(64) void bptt_chunk_map_kernel(TrainArgs p) {
+    __shared__ __attribute__((aligned(16))) float sC[kL][4][32];   // z, a_r, a_z, a_n of step t0 + s + 1
+    __shared__ __attribute__((aligned(16))) float sD[kL][32];      // dh_head of step t0 + s
+    __shared__ __attribute__((aligned(16))) float sM[32][32];      // M^T
+    __shared__ __attribute__((aligned(16))) float sP[2][32][32];
+    __shared__ __attribute__((aligned(16))) float sq[2][32];
+    const int lane = threadIdx.x, i = lane & 31, kh = lane >> 5;
+    const int ib = lane >> 3, jb = lane & 7;       // the lane's 4 x 4 tile of P
+    const int nc = (p.T + kL - 1) / kL;
+    const int b = blockIdx.x / nc, c = blockIdx.x % nc;
+    const int T = p.T, t0 = c * kL, t1 = min(T, t0 + kL);
+    const float* rec0 = p.rec + (int64_t)b * T * kRec;
+    const float* h0 = p.h + (int64_t)b * p.Tmax * 32;
+    const float* W_hh = p.w + 96 * 64;
+    float w[3][16];                                // W_hh[32 g + 16 kh + kk][i]
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) w[g][kk] = W_hh[(32 * g + 16 * kh + kk) * 32 + i];
+    // stage the chunk: items (s, unit) = (e >> 5, e & 31), 8 per lane; M_T = 0 (z = a = 0)
+#pragma unroll
+    for (int u = 0; u < kL * 32 / 64; ++u) {
+        const int e = lane + 64 * u, s = e >> 5, j = e & 31;
+        const int t = t0 + s;
+        float z = 0.f, ar = 0.f, az = 0.f, an = 0.f, dhh = 0.f;
+        if (t < t1) {
+            dhh = rec0[(int64_t)t * kRec + j];
+            if (t + 1 < T) bptt_coef(rec0 + (int64_t)(t + 1) * kRec, h0[(int64_t)t * 32 + j], j, z, ar, az, an);
+        }
+        sD[s][j] = dhh;
+        sC[s][0][j] = z;
+        sC[s][1][j] = ar;
+        sC[s][2][j] = az;
+        sC[s][3][j] = an;
+    }
+    float pt[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) pt[a][cc] = (t1 < T && 4 * ib + a == 4 * jb + cc) ? 1.f : 0.f;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+        *reinterpret_cast<float4*>(&sP[0][4 * ib + a][4 * jb]) = make_float4(pt[a][0], pt[a][1], pt[a][2], pt[a][3]);
+    if (kh == 0) sq[0][i] = 0.f;
+    wave_fence();
+    int cur = 0;
+    for (int s = t1 - t0 - 1; s >= 0; --s) {
+        // M^T[k][i] for k = 16 kh + kk
+        const float zi = sC[s][0][i];
+        const float4* ar4 = reinterpret_cast<const float4*>(&sC[s][1][16 * kh]);
+        const float4* az4 = reinterpret_cast<const float4*>(&sC[s][2][16 * kh]);
+        const float4* an4 = reinterpret_cast<const float4*>(&sC[s][3][16 * kh]);
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) {
+            const float4 vr = ar4[k4], vz = az4[k4], vn = an4[k4];
+            const float r_[4] = {vr.x, vr.y, vr.z, vr.w}, z_[4] = {vz.x, vz.y, vz.z, vz.w},
+                        n_[4] = {vn.x, vn.y, vn.z, vn.w};
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const int kk = 4 * k4 + q4, k = 16 * kh + kk;
+                float m = fmaf(w[0][kk], r_[q4], fmaf(w[1][kk], z_[q4], w[2][kk] * n_[q4]));
+                if (k == i) m += zi;
+                sM[k][i] = m;
+            }
+        }
+        wave_fence();
+        // P <- M P (4 x 4 tile), q <- dh_head + M q
+        float acc[4][4] = {};
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            const float4 m4 = *reinterpret_cast<const float4*>(&sM[k][4 * ib]);
+            const float4 p4 = *reinterpret_cast<const float4*>(&sP[cur][k][4 * jb]);
+            const float mv[4] = {m4.x, m4.y, m4.z, m4.w}, pv[4] = {p4.x, p4.y, p4.z, p4.w};
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int cc = 0; cc < 4; ++cc) acc[a][cc] = fmaf(mv[a], pv[cc], acc[a][cc]);
+        }
+        float qa = 0.f, qb = 0.f;
+#pragma unroll
+        for (int kk = 0; kk < 16; kk += 2) {
+            const int k = 16 * kh + kk;
+            qa = fmaf(sM[k][i], sq[cur][k], qa);
+            qb = fmaf(sM[k + 1][i], sq[cur][k + 1], qb);
+        }
+        const float part = qa + qb;
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(part), __float_as_uint(part), false, false);
+        const float other = __uint_as_float(kh ? sw[0] : sw[1]);
+        const float qn = sD[s][i] + (kh ? (other + part) : (part + other));
+        const int nx = cur ^ 1;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+            *reinterpret_cast<float4*>(&sP[nx][4 * ib + a][4 * jb]) = make_float4(acc[a][0], acc[a][1], acc[a][2], acc[a][3]);
+        if (kh == 0) sq[nx][i] = qn;
+        wave_fence();                              // sM / sP[cur] reads done, sP[nx] written
+        cur = nx;
+    }
+    float* Pc = p.scan_p + ((int64_t)b * nc + c) * 1024;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int e = 4 * (lane + 64 * u);
+        *reinterpret_cast<float4*>(Pc + e) = *reinterpret_cast<const float4*>(&sP[cur][0][0] + e);
+    }
+    if (kh == 0) p.scan_q[((int64_t)b * nc + c) * 32 + i] = sq[cur][i];
+}
+
+// T2b: G[c] = g at chunk c's first step = P_c G[c+1] + q_c, c = nc-1 .. 0
+__global__ __launch_bounds__(64) void bptt_chunk_carry_kernel(TrainArgs p) {
+    __shared__ __attribute__((aligned(16))) float sG[32];
+    const int lane = threadIdx.x, i = lane & 31, jh = lane >> 5;
+    const int b = blockIdx.x;
+    const int nc = (p.T + kL - 1) / kL;
+    const float* P0 = p.scan_p + (int64_t)b * nc * 1024;
+    const float* q0 = p.scan_q + (int64_t)b * nc * 32;
+    float* G0 = p.scan_g + (int64_t)b * nc * 32;
+    float gi = q0[(int64_t)(nc - 1) * 32 + i];
+    if (jh == 0) G0[(int64_t)(nc - 1) * 32 + i] = gi;
+    float4 pn[4];
+    auto ldp = [&](int c, float4 (&v)[4]) {
+        const float4* row = reinterpret_cast<const float4*>(P0 + (int64_t)c * 1024 + i * 32 + 16 * jh);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) v[m] = row[m];
+    };
+    float qn = 0.f;
+    if (nc >= 2) {
+        ldp(nc - 2, pn);
+        qn = q0[(int64_t)(nc - 2) * 32 + i];
+    }
+    for (int c = nc - 2; c >= 0; --c) {
+        float4 pc[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) pc[m] = pn[m];
+        const float qc = qn;
+        if (c >= 1) {
+            ldp(c - 1, pn);
+            qn = q0[(int64_t)(c - 1) * 32 + i];
+        }
+        if (jh == 0) sG[i] = gi;
+        wave_fence();
+        const float4* g4 = reinterpret_cast<const float4*>(sG + 16 * jh);
+        float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const float4 gv = g4[m];
+            a0 = fmaf(pc[m].x, gv.x, a0);
+            a1 = fmaf(pc[m].y, gv.y, a1);
+            a0 = fmaf(pc[m].z, gv.z, a0);
+            a1 = fmaf(pc[m].w, gv.w, a1);
+        }
+        const float part = a0 + a1;
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(part), __float_as_uint(part), false, false);
+        const float other = __uint_as_float(jh ? sw[0] : sw[1]);
+        gi = qc + (jh ? (other + part) : (part + other));
+        if (jh == 0) G0[(int64_t)c * 32 + i] = gi;
+        wave_fence();
+    }
+}
+
+// T2c: chunk c's steps t1-1 .. t0 from g_{t1} = G[c+1] (the last chunk: carry 0)
+__global__ __launch_bounds__(64) void bptt_chunk_fill_kernel(TrainArgs p) {
+    __shared__ __attribute__((aligned(16))) float sG[96];
+    const int lane = threadIdx.x, j = lane & 31, kh = lane >> 5;
+    const int nc = (p.T + kL - 1) / kL;
+    const int b = blockIdx.x / nc, c = blockIdx.x % nc;
+    const int T = p.T, t0 = c * kL, t1 = min(T, t0 + kL);
+    const float* W_hh = p.w + 96 * 64;
+    float wT[48];
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) wT[16 * g + q] = W_hh[(32 * g + 16 * kh + q) * 32 + j];
+    const float* rec0 = p.rec + (int64_t)b * T * kRec;
+    float* dg0 = p.dg + (int64_t)b * T * kDg;
+    const float* h0 = p.h + (int64_t)b * p.Tmax * 32;
+    // steps t1 (seed: g given, no dg) .. t0, all inputs loaded up front
+    float v[kL + 1][6];
+#pragma unroll
+    for (int s = 0; s <= kL; ++s) {
+        const int t = min(t1 - s, T - 1);
+        const float* rc = rec0 + (int64_t)max(t, 0) * kRec;
+        v[s][0] = rc[j]; v[s][1] = rc[32 + j]; v[s][2] = rc[64 + j]; v[s][3] = rc[96 + j]; v[s][4] = rc[128 + j];
+        v[s][5] = t > 0 ? h0[(int64_t)(t - 1) * 32 + j] : 0.f;
+    }
+    const bool seed = t1 < T;
+    float carry = 0.f;
+    const float gseed = seed ? p.scan_g[((int64_t)b * nc + c + 1) * 32 + j] : 0.f;
+#pragma unroll
+    for (int s = 0; s <= kL; ++s) {
+        const int t = t1 - s;                      // s = 0: the seed step t1
+        if (s == 0 && !seed) continue;
+        if (t < t0) break;
+        const float r = v[s][1], z = v[s][2], n = v[s][3], ghn = v[s][4], hp = v[s][5];
+        const float dh = s == 0 ? gseed : v[s][0] + carry;
+        const float dn = dh * (1.f - z);
+        const float dzz = dh * (hp - n);
+        const float dan = dn * (1.f - n * n);
+        const float dar = dan * ghn * r * (1.f - r);
+        const float daz = dzz * z * (1.f - z);
+        const float dghn = dan * r;
+        if (kh == 0) {
+            if (s > 0) {
+                float* d = dg0 + (int64_t)t * kDg;
+                d[j] = dar;
+                d[32 + j] = daz;
+                d[64 + j] = dan;
+                d[96 + j] = dghn;
+            }
+            sG[j] = dar;
+            sG[32 + j] = daz;
+            sG[64 + j] = dghn;
+        }
+        wave_fence();
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+            const float4* g4 = reinterpret_cast<const float4*>(sG + 32 * g + 16 * kh);
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const float4 gv = g4[q4];
+                acc[0] = fmaf(wT[16 * g + 4 * q4], gv.x, acc[0]);
+                acc[1] = fmaf(wT[16 * g + 4 * q4 + 1], gv.y, acc[1]);
+                acc[2] = fmaf(wT[16 * g + 4 * q4 + 2], gv.z, acc[2]);
+                acc[3] = fmaf(wT[16 * g + 4 * q4 + 3], gv.w, acc[3]);
+            }
+        }
+        const float part = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(part), __float_as_uint(part), false, false);
+        const float other = __uint_as_float(kh ? sw[0] : sw[1]);
+        carry = fmaf(dh, z, kh ? (other + part) : (part + other));
+        wave_fence();
+    }
+}
+
+int train_scan_chunks(int T) { return (T + kL - 1) / kL; }
+
 // ---------------------------------------------------------------------------
 // T3: weight-gradient partials.  LDS frame row (floats):
 //   [0, 96)   dgi = (dar, daz, dan)          [96, 192) dgh = (dar, daz, dghn)
@@ -451,6 +720,33 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ prm, cons
     prm[i] = pv - step_size * (mn / denom);
 }
 
+// The same update over up to kAdamMax tensors in one launch (one optimizer
+// param group): element i belongs to tensor k with off[k] <= i < off[k + 1].
+__global__ __launch_bounds__(256) void adam_multi_kernel(AdamList L, float beta1, float beta2, float eps, float wd) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= L.off[L.n]) return;
+    int k = 0;
+    while (i >= L.off[k + 1]) ++k;
+    const int64_t j = i - L.off[k];
+    float g = L.g[k][j];
+    const float pv = L.p[k][j];
+    if (wd != 0.f) g = fmaf(wd, pv, g);
+    const float mv = L.m[k][j];
+    const float mn = fmaf(1.f - beta1, g - mv, mv);
+    const float vn = fmaf(beta2, L.v[k][j], (1.f - beta2) * g * g);
+    L.m[k][j] = mn;
+    L.v[k][j] = vn;
+    const float denom = sqrtf(vn) / L.bc2_sqrt[k] + eps;
+    L.p[k][j] = pv - L.step_size[k] * (mn / denom);
+}
+
+hipError_t launch_adam_multi(const AdamList& L, float beta1, float beta2, float eps, float wd, hipStream_t st) {
+    const int64_t n = L.off[L.n];
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, L, beta1, beta2, eps, wd);
+    return hipGetLastError();
+}
+
 hipError_t launch_norm_global(const double2* mom, int B, int64_t n, float* cvals, hipStream_t st) {
     hipLaunchKernelGGL(norm_global_kernel, dim3(3), dim3(256), 0, st, mom, B, n, cvals);
     return hipGetLastError();
@@ -470,7 +766,18 @@ hipError_t launch_train_backward(const TrainArgs& a, int nblk, const float* grad
     const int64_t nf = (int64_t)a.B * a.T;
     const int hblocks = (int)std::min<int64_t>((nf + 7) / 8, 2 * (int64_t)a.num_cus);
     hipLaunchKernelGGL(train_head_kernel, dim3(hblocks), dim3(256), train_head_smem_bytes(), st, a);
-    hipLaunchKernelGGL(train_bptt_kernel, dim3(a.B), dim3(64), 0, st, a);
+    // the scan does ~32x the serial recursion's FLOPs: it wins while the
+    // B waves of the serial form leave most of the chip idle (measured at
+    // T = 626: B = 16 62 vs 232 us, B = 256 316 vs 238 us)
+    const int nc_ = (a.T + kL - 1) / kL;
+    if (a.scan_p && a.T > 4 * kL && (int64_t)a.B * nc_ <= 32 * (int64_t)a.num_cus) {
+        const int nc = nc_;
+        hipLaunchKernelGGL(bptt_chunk_map_kernel, dim3(a.B * nc), dim3(64), 0, st, a);
+        hipLaunchKernelGGL(bptt_chunk_carry_kernel, dim3(a.B), dim3(64), 0, st, a);
+        hipLaunchKernelGGL(bptt_chunk_fill_kernel, dim3(a.B * nc), dim3(64), 0, st, a);
+    } else {
+        hipLaunchKernelGGL(train_bptt_kernel, dim3(a.B), dim3(64), 0, st, a);
+    }
     const int64_t stages = (nf + kWgF - 1) / kWgF;
     const int64_t per = ((stages + nblk - 1) / nblk) * kWgF;
     hipLaunchKernelGGL(train_wgrad_kernel, dim3(nblk), dim3(kWgThreads), 0, st, a, per);

@@ -189,6 +189,11 @@ int64_t aec_train_generation(const aec_handle* h);
 aec_status aec_adam_step(aec_handle* h, float* params, const float* grad, float* exp_avg, float* exp_avg_sq,
                          size_t n, int64_t step, float lr, float beta1, float beta2, float eps, float weight_decay,
                          void* stream);
+/* The same update over `count` tensors (one param group) in one launch per 16
+ * tensors: host arrays of device pointers, element counts and 1-based steps. */
+aec_status aec_adam_step_multi(aec_handle* h, float* const* params, const float* const* grads, float* const* exp_avg,
+                               float* const* exp_avg_sq, const int64_t* sizes, const int64_t* steps, int32_t count,
+                               float lr, float beta1, float beta2, float eps, float weight_decay, void* stream);
 
 /* Frame / output-length integers (bit-exact framing contract). */
 int64_t aec_num_frames(int64_t n_samples);   /* n//256 + 1 */

@@ -187,6 +187,24 @@ def test_native_adam_matches_oracle(golden_weights):
         pr, mr, vr = O.adam_step(pr, g.astype(np.float64), mr, vr, step, lr=1e-3, weight_decay=0.01)
     torch.cuda.synchronize()
     assert np.abs(p.cpu().numpy() - pr).max() <= 2e-6
+    # the multi-tensor launch (one param group): 3 tensors at different steps
+    sizes = [12544, 77, 4096]
+    ps = [torch.from_numpy(rng.standard_normal(s).astype(np.float32)).to(dev) for s in sizes]
+    ms = [torch.zeros(s, device=dev) for s in sizes]
+    vs = [torch.zeros(s, device=dev) for s in sizes]
+    refs = [(t.cpu().numpy().astype(np.float64), np.zeros(s), np.zeros(s)) for t, s in zip(ps, sizes)]
+    for step in range(1, 4):
+        gs = [(rng.standard_normal(s) * 1e-3).astype(np.float32) for s in sizes]
+        steps = [step, step + 1, step]
+        gts = [torch.from_numpy(g).to(dev) for g in gs]          # kept alive across the async launch
+        h.adam_step_multi([t.data_ptr() for t in ps], [t.data_ptr() for t in gts],
+                          [t.data_ptr() for t in ms], [t.data_ptr() for t in vs], sizes, steps, 1e-3, 0.9, 0.999,
+                          1e-8, 0.0, st)
+        torch.cuda.synchronize()
+        refs = [O.adam_step(pr_, g.astype(np.float64), mr_, vr_, s_, lr=1e-3)
+                for (pr_, mr_, vr_), g, s_ in zip(refs, gs, steps)]
+    for t, (pr_, _, _) in zip(ps, refs):
+        assert np.abs(t.cpu().numpy() - pr_).max() <= 2e-6
 
 
 @pytest.mark.gpu
@@ -277,3 +295,35 @@ def test_torch_train_port_matches_reference(tg, golden_weights, golden_erb):
         assert abs(loss - float(tg[f'loss{it}'])) <= 1e-5 * float(tg[f'loss{it}'])
         for k, p in zip(PARAM_KEYS, port.params):
             assert _rel(p.grad.numpy(), tg[f'grad{it}/{k}']) <= 1e-4, (it, k)
+
+
+@pytest.mark.gpu
+def test_chunked_scan_bptt_matches_serial(monkeypatch, golden_weights, golden_erb):
+    """The chunked-scan BPTT (aec_train.hip T2a-c, used when T > 64) against
+    the one-wave-per-stream serial recursion (AEC_BPTT_SERIAL=1) on ragged
+    chunk counts (T = 157: a 13-step last chunk)."""
+    torch = _gpu()
+    from aec_amd import _lib, synth
+    dev = 'cuda:0'
+    B, N = 4, 40000
+    mic, ref, near = (torch.from_numpy(a).to(dev) for a in synth.batch(B, N, seed0=8100))
+    blob = torch.from_numpy(np.concatenate([golden_weights[k].reshape(-1) for k in PARAM_KEYS])).float().to(dev)
+    grads = {}
+    for serial in ('0', '1'):
+        monkeypatch.setenv('AEC_BPTT_SERIAL', serial)
+        h = _lib.Handle(0)
+        h.set_erb(golden_erb.astype(np.float32))
+        st = torch.cuda.current_stream().cuda_stream
+        loss = torch.empty((), device=dev)
+        g = torch.empty(blob.numel(), device=dev)
+        h.set_weights_device(blob.data_ptr(), blob.numel(), st)
+        h.train_forward(mic.data_ptr(), ref.data_ptr(), near.data_ptr(), N, B, N, None, 1, loss.data_ptr(), st)
+        h.train_backward(None, g.data_ptr(), st)
+        torch.cuda.synchronize()
+        grads[serial] = g.cpu().numpy()
+        del h
+    o = 0
+    for k in PARAM_KEYS:
+        n = golden_weights[k].size
+        assert _rel(grads['0'][o:o + n], grads['1'][o:o + n].astype(np.float64)) <= 1e-5, k
+        o += n
