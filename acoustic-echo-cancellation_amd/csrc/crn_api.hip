@@ -81,6 +81,9 @@ struct aec_crn_handle {
     bool mx8 = false;                              // dtype 2: MX-fp8 LSTM input projections
     aec::DevTables* d_tab = nullptr;
     std::vector<Packed> enc, dec;                  // dec: 2 per level (even, odd)
+    std::vector<Packed> decf;                      // per level: both parities in one GEMM (see pack_decoder_fused)
+    int dec_fuse_max = 128;                        // CRN_DEC_FUSE: fuse the parities of levels with <= this many
+                                                   // output channels (HBM-bound layers); 0 = never
     std::vector<Packed> lih, lhh;                  // per LSTM layer
     bool have_params = false;
     // workspace
@@ -413,6 +416,38 @@ static aec_status pack_decoder(aec_crn_handle* h, Packed& pk, const RealConv& r,
     return s;
 }
 
+// Both parities of a decoder level as ONE GEMM over the rows of parity 0
+// (bins m-1, m, m+1): columns [0, Co) parity 0 (taps 4, 2, 0), columns
+// [Co, 2 Co) parity 1 (zero at bin m-1, taps 3, 1 at m, m+1).  The
+// memory-bound levels read their input rows once instead of twice; the
+// epilogue routes the parity-1 columns to the odd output bins (RowEpi nsplit).
+static aec_status pack_decoder_fused(aec_crn_handle* h, Packed& pk, const RealConv& r, int act, float alpha) {
+    const int Cin = r.Ci, C = Cin / 2, Co = r.Co;
+    pk.N = 2 * Co;
+    pk.K = 3 * Cin;
+    const int bn = crn::gemm_bn(pk.N);
+    pk.npad = (pk.N + bn - 1) / bn * bn;
+    pk.kpad = kpad_for(pk.K, h->es);
+    pk.alpha = alpha;
+    pk.act = act;
+    auto ref = [&](int q) {
+        if (q < C / 2) return q;
+        if (q < C) return C + (q - C / 2);
+        if (q < 3 * C / 2) return C / 2 + (q - C);
+        return q;
+    };
+    std::vector<double> w((size_t)pk.npad * pk.kpad, 0.0), b(pk.N);
+    for (int o = 0; o < Co; ++o) {
+        b[o] = b[Co + o] = r.b[o];
+        for (int j = 0; j < 3; ++j)
+            for (int q = 0; q < Cin; ++q) {
+                w[(size_t)o * pk.kpad + j * Cin + q] = r.w[((size_t)o * Cin + ref(q)) * 5 + (4 - 2 * j)];
+                if (j > 0) w[(size_t)(Co + o) * pk.kpad + j * Cin + q] = r.w[((size_t)o * Cin + ref(q)) * 5 + (5 - 2 * j)];
+            }
+    }
+    return upload_packed(h, pk, w, b);
+}
+
 // LSTM cell(s): unit order u' = d*Q + c <-> reference u = c*D + d; W_hh gate
 // row p(q, u') = ((u'/16)*4 + q)*16 + u'%16 (i|f|g|o per 16 units), W_ih /
 // bias gate row u'*4 + q (so Gx holds a unit's 4 gates contiguously)
@@ -489,6 +524,14 @@ static aec_status load_params(aec_crn_handle* h, const float* params, size_t n) 
         if (!cur.ok) return crn_fail(h, AEC_ERR_INVALID_ARG, "parameter blob too short");
         for (int par = 0; par < 2; ++par) {
             aec_status s = pack_decoder(h, h->dec[2 * d + par], r, par, act, alpha);
+            if (s != AEC_OK) return s;
+        }
+        // fused parities: bf16 / f32 stores of 16 B never straddle the parity
+        // split when Co % 8 == 0; the mask level (Co = 2, f32) stays split
+        // (measured, C3 bf16 decoder: unfused 7.31 ms, fused up to Co = 64 6.58, 128 6.42, 256 6.61);
+        // with dtype fp8 the levels the MX GEMM takes (Co >= 128) stay split
+        if (cl != 1 && co <= h->dec_fuse_max && co % 8 == 0 && !(h->mx8 && co >= 128)) {
+            aec_status s = pack_decoder_fused(h, h->decf[d], r, act, alpha);
             if (s != AEC_OK) return s;
         }
     }
@@ -679,6 +722,30 @@ static aec_status run_decoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipS
         const int cl = L - d;
         const int Fin = 256 >> cl, Fo = 2 * Fin;
         const int64_t ld_in = 2 * ch[cl];
+        if (h->decf[d].w) {                // both parities in one GEMM (pack_decoder_fused)
+            const Packed& pk = h->decf[d];
+            RowSrc a{};
+            a.src = bf.cat[cl];
+            a.M = F * Fin;
+            a.K = pk.K;
+            a.rshift = ilog2(Fin);
+            a.rs_hi = Fin * ld_in;
+            a.rs_lo = ld_in;
+            a.kshift = ilog2(ld_in);
+            a.ks = ld_in;
+            a.pmul = 1;
+            a.padd = -1;
+            a.plim = Fin;
+            a.base_off = -ld_in;
+            a.src_elems = F * Fin * ld_in;
+            const int64_t ldo = 2 * ch[cl - 1];
+            RowEpi e{bf.cat[cl - 1], a.M, pk.N, a.rshift, Fo * ldo, 2 * ldo, 0, pk.bias, pk.alpha, pk.act};
+            e.nsplit = pk.N / 2;
+            e.split_add = ldo;
+            CRN_TRY(h, (crn::launch_gemm_rows<T, T>(a, reinterpret_cast<const T*>(pk.w), pk.kpad,
+                                                     (int)(pk.kpad * sizeof(T) / crn::kStageBytes), e, pk.npad, st)));
+            continue;
+        }
         for (int par = 0; par < 2; ++par) {
             const Packed& pk = h->dec[2 * d + par];
             RowSrc a{};
@@ -976,6 +1043,8 @@ aec_status aec_crn_create(const aec_crn_config* cfg, const float* params, size_t
     }
     h->enc.assign(h->L, Packed{});
     h->dec.assign(2 * h->L, Packed{});
+    h->decf.assign(h->L, Packed{});
+    if (const char* m = std::getenv("CRN_DEC_FUSE")) h->dec_fuse_max = std::atoi(m);
     h->lih.assign(h->nrnn, Packed{});
     h->lhh.assign(h->nrnn, Packed{});
     if (params) {
@@ -1232,7 +1301,7 @@ void aec_crn_destroy(aec_crn_handle* h) {
     aec::DeviceGuard dg(h->device);
     stream_free(h);
     for (void* p : h->allocs) (void)hipFree(p);
-    for (auto* v : {&h->enc, &h->dec, &h->lih, &h->lhh})
+    for (auto* v : {&h->enc, &h->dec, &h->decf, &h->lih, &h->lhh})
         for (Packed& pk : *v) {
             if (pk.w) (void)hipFree(pk.w);
             if (pk.bias) (void)hipFree(pk.bias);

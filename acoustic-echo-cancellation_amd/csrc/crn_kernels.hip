@@ -628,7 +628,8 @@ __device__ __forceinline__ void rows_epilogue(const f32x4 (&acc)[FM][FN], const 
             for (int fn = 0; fn < FN; ++fn) {
                 float v = acc[fm][fn][r] + bias[fn];
                 v = act == 1 ? (v >= 0.f ? v : alpha * v) : act == 2 ? tanhf(v) : v;
-                if (nok[fn]) orow[fn * 16] = to_elem<OutT>(v);
+                const int n = nb + fn * 16 + (lane & 15);
+                if (nok[fn]) orow[fn * 16 + (n >= e.nsplit ? e.split_add - e.nsplit : 0)] = to_elem<OutT>(v);
             }
         }
 }
@@ -676,8 +677,8 @@ __device__ __forceinline__ void rows_epilogue_lds(const f32x4 (&acc)[FM][FN], co
             const int n = nb + ch * EPC;
             if (m < e.M && n < e.N) {
                 const u32x4 v = *reinterpret_cast<const u32x4*>(wlds + row * RB + ch * 16);
-                OutT* o =
-                    reinterpret_cast<OutT*>(e.out) + (m >> e.oshift) * e.o_hi + (m & omask) * e.o_lo + e.o_add + n;
+                OutT* o = reinterpret_cast<OutT*>(e.out) + (m >> e.oshift) * e.o_hi + (m & omask) * e.o_lo + e.o_add +
+                          (n >= e.nsplit ? e.split_add + (n - e.nsplit) : n);   // a chunk never straddles nsplit
 #if CRN_EPI_NT
                 __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(o));
 #else

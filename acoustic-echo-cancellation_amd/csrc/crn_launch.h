@@ -65,6 +65,10 @@ struct RowEpi {
     float alpha;
     int32_t act;
     int32_t mode = 0;           // timing experiments only (CRN_GEMM_MODE): bit0 skip the epilogue
+    // column split (the decoder's fused parities): columns n >= nsplit are
+    // stored at element offset split_add + (n - nsplit) instead of n
+    int32_t nsplit = 0x7fffffff;
+    int64_t split_add = 0;
 };
 
 // One LSTM frame step for CELLS weight sets x S input sequences (v1: 1x1,
