@@ -105,8 +105,8 @@ class _TrainStep(torch.autograd.Function):
                                       'on loss (scripts/train1.py:207-212), not on out_wav')
         h, dev = ctx.h, ctx.dev
         if h.train_generation() != ctx.gen:
-            raise RuntimeError('Little_net (gfx950): backward of an older forward (another training forward '
-                               'ran in between); call backward before the next training forward')
+            raise RuntimeError('Little_net (gfx950): backward of an older forward (another forward ran on this '
+                               'module and device in between); call backward before the next forward')
         grad = torch.empty(sum(int(np.prod(s)) for s in ctx.shapes), device=dev, dtype=torch.float32)
         gl = g_loss.detach().float().contiguous() if g_loss is not None else None
         stream = torch.cuda.current_stream(dev).cuda_stream

@@ -538,6 +538,9 @@ aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref
     const int64_t Tmax = aec_num_frames(nmax);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     AEC_ON_DEVICE(h);
+    // this call overwrites the features a pending aec_train_backward would read
+    h->train_B = 0;
+    ++h->train_gen;
     aec_status s = ensure_ws(h, B, Tmax);
     if (s != AEC_OK) return s;
     s = prepare_lists(h, lengths3, B, nsig_in, st);

@@ -173,7 +173,9 @@ aec_status aec_erb_tables_check(const float* erb_257xbands, const float* mags, c
  *   aec_train_backward(h, grad_loss, grad, st)
  *        loss.backward() for the last aec_train_forward: grad (device, 12,544
  *        floats, blob order) = grad_loss * d loss / d params; grad_loss is a
- *        device scalar (NULL = 1).
+ *        device scalar (NULL = 1).  An aec_process / aec_process_siglens call
+ *        in between overwrites the forward's features: the backward then
+ *        fails with AEC_ERR_INVALID_ARG.
  *   aec_train_generation(h)
  *        count of aec_train_forward calls (an autograd binding checks that
  *        its backward belongs to the latest forward).

@@ -327,3 +327,23 @@ def test_chunked_scan_bptt_matches_serial(monkeypatch, golden_weights, golden_er
         n = golden_weights[k].size
         assert _rel(grads['0'][o:o + n], grads['1'][o:o + n].astype(np.float64)) <= 1e-5, k
         o += n
+
+
+@pytest.mark.gpu
+def test_inference_call_invalidates_pending_backward(tg, golden_weights, golden_erb):
+    """An inference forward on the same handle between the training forward
+    and its backward overwrites the saved features: the backward must fail
+    loudly, not return gradients of the wrong batch."""
+    torch = _gpu()
+    dev = 'cuda:0'
+    net = _net(golden_weights, dev)
+    erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
+    mic, ref, near = (torch.from_numpy(tg[f'{s}0']).to(dev) for s in ('mic', 'ref', 'near'))
+    with torch.enable_grad():
+        _, loss = net(mic, ref, near, erb_t)
+    with torch.no_grad():
+        net.eval()
+        net(mic[:1], ref[:1], near[:1], erb_t)
+        net.train()
+    with pytest.raises(RuntimeError, match='older forward'):
+        loss.backward()
