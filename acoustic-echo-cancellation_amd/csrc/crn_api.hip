@@ -820,6 +820,8 @@ static aec_status run_persist(aec_crn_handle* h, int l, int32_t B, int64_t Tmax,
         a.spin_limit = 1 << 22;
         static const int pmode = [] { const char* v = getenv("CRN_PERSIST_MODE"); return v ? atoi(v) : 0; }();
         a.mode = pmode;
+        static const int pra = [] { const char* v = getenv("CRN_PERSIST_RA"); return v ? atoi(v) : 1; }();
+        a.read_ahead = pra;
         CRN_TRY(h, hipMemsetAsync(h->psync, 0, crn::kPersistSyncInts * sizeof(int), st));
         static const bool dbg = getenv("CRN_PERSIST_DBG") != nullptr;
         long long* dd = nullptr;

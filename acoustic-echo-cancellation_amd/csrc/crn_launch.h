@@ -164,6 +164,7 @@ struct PersistArgs {
                                 // bit0 h loads out of range (zeros), bit1 no MFMA phase, bit2 no team wait,
                                 // bit3 no h stores, bit4 Gx loads out of range, bit5 no cell update
     long long* dbg = nullptr;   // version 2 timing probe (CRN_PERSIST_DBG): [block][wave][2 phases][24 events]
+    int32_t read_ahead = 1;     // version 2: read the next phase's counter at chunk 7 (CRN_PERSIST_RA, A/B)
 };
 constexpr int kPersistErr = 8 * 2 * 16;          // error word (after 8 teams x 2 halves of counters)
 constexpr int kPersistSyncInts = kPersistErr + 16;

@@ -461,8 +461,22 @@ __global__ __launch_bounds__(kPThreads, 1) void lstm_persist2_kernel(PersistArgs
                                                      16, vo, (int)(so + (uint32_t)i * 32768u), 0, CRN_PERSIST_AUX);
         }
     };
+    // counter of the next phase's half read ahead (chunk 7 of the current phase): when the team is
+    // already there, the next poll skips its device-scope round trip.  A vector load through an
+    // offset the compiler cannot see as zero, so it is neither scalarised nor waited for at once.
+    int pre_v = 0, pre_hm = -1;
+    auto read_ahead = [&](int hm) {
+        int z;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+        pre_v = __hip_atomic_load(p.sync + (team * 2 + hm) * 16 + z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pre_hm = hm;
+    };
     auto poll = [&](int hm, int target) {
         if (stalled) return;
+        if (pre_hm == hm) {
+            pre_hm = -1;
+            if (__builtin_amdgcn_readfirstlane(pre_v) >= target) return;
+        }
         int bad = 0;
         if (lane == 0) {
             int* cnt = p.sync + (team * 2 + hm) * 16;
@@ -631,6 +645,8 @@ __global__ __launch_bounds__(kPThreads, 1) void lstm_persist2_kernel(PersistArgs
                 mark(HM, tm, 3 + 2 * j);                     // chunk j landed (this wave's view)
                 __builtin_amdgcn_s_barrier();
                 if constexpr (j == 5) arrive(HF);
+                if constexpr (j == 7)
+                    if (p.read_ahead && (HM == 0 || tm + 1 < T)) read_ahead(HF);   // the next phase polls half HF
                 if constexpr (j + 3 < 8) issue_a(HM, std::integral_constant<int, j + 3>{}, ry);
                 if constexpr (j == 4) load_gx(std::integral_constant<int, HF>{}, tf + 1, tf + 1 < T);
                 const char* base = abuf(Jc) + kh * (kQH * 128);
