@@ -347,3 +347,23 @@ def test_inference_call_invalidates_pending_backward(tg, golden_weights, golden_
         net.train()
     with pytest.raises(RuntimeError, match='older forward'):
         loss.backward()
+
+
+def test_adam_state_dict_and_steplr_follow_torch():
+    """train1.py:153-154 builds Adam + StepLR and checkpoints
+    optimizer.state_dict() (train1.py:244-246): the native Adam keeps torch's
+    param-group keys, accepts torch's state_dict and drives StepLR (CPU: no
+    step taken)."""
+    import torch
+    from aec_amd.train import Adam
+    p = [torch.nn.Parameter(torch.zeros(3)), torch.nn.Parameter(torch.zeros(2))]
+    ref = torch.optim.Adam([{'params': p}], lr=LR, amsgrad=False)
+    ours = Adam([{'params': p}], lr=LR, amsgrad=False)
+    g_ref, g_ours = ref.state_dict()['param_groups'][0], ours.state_dict()['param_groups'][0]
+    for k in ('lr', 'betas', 'eps', 'weight_decay', 'amsgrad', 'params'):
+        assert g_ref[k] == g_ours[k], k
+    ours.load_state_dict(ref.state_dict())
+    sched = torch.optim.lr_scheduler.StepLR(ours, step_size=5, gamma=0.5)   # train_conf lr_decay_*
+    for _ in range(5):
+        sched.step()
+    assert ours.param_groups[0]['lr'] == pytest.approx(LR * 0.5)
