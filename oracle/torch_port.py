@@ -109,4 +109,4 @@ class TorchTrainPort(TorchPort):
             loss = self.loss(mic, ref, near)
         loss.backward()
         self.opt.step()
-        return float(loss)
+        return float(loss.detach())

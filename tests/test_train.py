@@ -259,7 +259,7 @@ def test_train_10s_batch16_vs_oracle(golden_weights, golden_erb):
         _, loss = net(*(torch.from_numpy(a).to(dev) for a in (mic, ref, near)), erb_t)
     loss.backward()
     ol, og = O.train_loss_and_grads(mic, ref, near, golden_erb.astype(np.float32), golden_weights)
-    assert abs(float(loss) - ol) <= 1e-4 * ol
+    assert abs(float(loss.detach()) - ol) <= 1e-4 * ol
     for k, p in net.named_parameters():
         assert _rel(p.grad.cpu().numpy(), og[k]) <= 1e-3, k
 
