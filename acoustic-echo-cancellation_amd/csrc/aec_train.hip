@@ -20,11 +20,12 @@
 //                          gradients and dh_{t-1} = dh z + W_hh^T dg (W_hh^T in
 //                          registers, split over the wave halves as the
 //                          forward step is) -> dg [B*T][4][32] = dar, daz, dan, dghn
-//   T3 train_wgrad_kernel  every parameter gradient is a sum over frames of an
-//                          outer product of two per-frame vectors (or of one
-//                          vector, for the biases): blocks stage frame records
-//                          in LDS and each thread accumulates ~25 of the 12,544
-//                          blob entries -> part [nblk][12544] (no atomics)
+//   T3 train_wgrad_mfma_kernel  every weight gradient is a GEMM over frames
+//                          (sum of outer products of two per-frame vectors):
+//                          blocks stage frame records in LDS and run them
+//                          through v_mfma_f32_16x16x4_f32, 4 frames per
+//                          instruction; biases are plain sums -> part
+//                          [nblk][12544] (no atomics)
 //   T4 train_reduce_kernel grad = grad_loss * sum over blocks (fixed order, f64)
 //   adam_kernel            torch.optim.Adam's update, one thread per element
 #include <hip/hip_runtime.h>
@@ -42,9 +43,7 @@ namespace {
 constexpr int kRec = 8 * 32;           // per-frame record floats (T1 -> T2, T3)
 constexpr int kDg = 4 * 32;            // per-frame gate gradients (T2 -> T3)
 constexpr int kWgF = 32;               // frames per T3 LDS stage
-constexpr int kWgRow = 452;            // T3 LDS frame row (see train_wgrad_kernel)
-constexpr int kWgThreads = 512;
-constexpr int kWgPer = (kWeights + kWgThreads - 1) / kWgThreads;   // 25 outputs per thread
+constexpr int kWgRow = 452;            // T3 LDS frame row (see train_wgrad_mfma_kernel; 4 floats of padding)
 
 __device__ __forceinline__ float sig_acc(float x) { return 1.f / (1.f + expf(-x)); }
 }  // namespace
@@ -590,41 +589,37 @@ int train_scan_chunks(int T) { return (T + kL - 1) / kL; }
 //   [0, 96)   dgi = (dar, daz, dan)          [96, 192) dgh = (dar, daz, dghn)
 //   [192,256) x = (mic_erb, |mic - ref|)      [256,288) h_{t-1}
 //   [288,320) dz1   [320,384) (h_t, mic_erb)  [384,416) dz2   [416,448) o
-//   [448]     1.0 (bias columns)
-// Blob entry e (state_dict order) = sum over frames of row[A(e)] * row[B(e)].
 // Block k owns the frames [k * per, (k + 1) * per) of the flattened B*T.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t wg_pair(int e) {
-    int a, c;
-    if (e < 6144) { a = e / 64; c = 192 + e % 64; }                          // W_ih
-    else if (e < 9216) { e -= 6144; a = 96 + e / 32; c = 256 + e % 32; }    // W_hh
-    else if (e < 9312) { a = e - 9216; c = 448; }                           // b_ih
-    else if (e < 9408) { a = 96 + e - 9312; c = 448; }                      // b_hh
-    else if (e < 11456) { e -= 9408; a = 288 + e / 64; c = 320 + e % 64; }  // linear1.weight
-    else if (e < 11488) { a = 288 + e - 11456; c = 448; }                   // linear1.bias
-    else if (e < 12512) { e -= 11488; a = 384 + e / 32; c = 416 + e % 32; } // linear2.weight
-    else { a = 384 + e - 12512; c = 448; }                                  // linear2.bias
-    return (uint32_t)a | ((uint32_t)c << 16);
-}
+// T3 on the matrix cores: every weight gradient is a GEMM over frames,
+// dW[g][c] = sum_f A[f][g] B[f][c] (A, B per-frame vectors of the staged rows),
+// so v_mfma_f32_16x16x4_f32 takes 4 frames per instruction (lane l: A at
+// row (f0 + l / 16), column g0 + l % 16; B likewise; D holds dW[g0 + 4 (l / 16)
+// + r][c0 + l % 16]).  48 16x16 tiles per block: waves 0-1 W_ih (3 row tiles x
+// 4 column tiles each), wave 2 W_hh (6 x 2), wave 3 linear1 (2 x 4) and
+// linear2 (2 x 2); the 256 bias entries are plain sums (one per thread).
+typedef float wg_f32x4 __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(kWgThreads) void train_wgrad_kernel(TrainArgs p, int64_t per) {
+__global__ __launch_bounds__(256) void train_wgrad_mfma_kernel(TrainArgs p, int64_t per) {
     __shared__ __attribute__((aligned(16))) float sR[kWgF * kWgRow];
-    const int tid = threadIdx.x;
-    uint32_t pr[kWgPer];
-    float acc[kWgPer];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int fr = lane & 15, fk = lane >> 4;
+    wg_f32x4 acc[12];
 #pragma unroll
-    for (int i = 0; i < kWgPer; ++i) {
-        const int e = tid + i * kWgThreads;
-        pr[i] = e < kWeights ? wg_pair(e) : (448u | (448u << 16));
-        acc[i] = 0.f;
-    }
+    for (int i = 0; i < 12; ++i) acc[i] = wg_f32x4{0.f, 0.f, 0.f, 0.f};
+    // bias entry of this thread: row offset and blob index
+    const int boff = tid < 192 ? tid : (tid < 224 ? 288 + tid - 192 : 384 + tid - 224);
+    const int bblob = tid < 96 ? 9216 + tid : (tid < 192 ? 9312 + tid - 96 : (tid < 224 ? 11456 + tid - 192
+                                                                                       : 12512 + tid - 224));
+    float bacc = 0.f;
     const int T = p.T;
     const int64_t nf = (int64_t)p.B * T;
     const int64_t g0 = (int64_t)blockIdx.x * per, g1 = min(nf, g0 + per);
     for (int64_t gs = g0; gs < g1; gs += kWgF) {
         const int nfr = (int)min((int64_t)kWgF, g1 - gs);
         __syncthreads();                                  // previous stage consumed
-        for (int e = tid; e < kWgF * 32; e += kWgThreads) {
+        for (int e = tid; e < kWgF * 32; e += 256) {
             const int f = e >> 5, j = e & 31;
             float* row = sR + f * kWgRow;
             if (f < nfr) {
@@ -644,24 +639,82 @@ __global__ __launch_bounds__(kWgThreads) void train_wgrad_kernel(TrainArgs p, in
                 row[352 + j] = me;
                 row[384 + j] = rc[192 + j];
                 row[416 + j] = rc[224 + j];
-                if (j == 0) row[448] = 1.f;
             } else {
-                for (int c = j; c < kWgRow; c += 32) row[c] = 0.f;
+                for (int c = j; c < 448; c += 32) row[c] = 0.f;
             }
         }
         __syncthreads();
-        for (int f = 0; f < nfr; ++f) {
-            const float* row = sR + f * kWgRow;
+#pragma unroll 2
+        for (int f0 = 0; f0 < kWgF; f0 += 4) {
+            const float* rk = sR + (f0 + fk) * kWgRow + fr;
+            auto mm = [&](int i, float a, float b) {
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[i], 0, 0, 0);
+            };
+            if (wave < 2) {                                   // W_ih: A = dgi [0, 96), B = x [192, 256)
+                float bv[4];
 #pragma unroll
-            for (int i = 0; i < kWgPer; ++i) acc[i] = fmaf(row[pr[i] & 0xffff], row[pr[i] >> 16], acc[i]);
+                for (int c = 0; c < 4; ++c) bv[c] = rk[192 + 16 * c];
+#pragma unroll
+                for (int r = 0; r < 3; ++r) {
+                    const float av = rk[16 * (3 * wave + r)];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) mm(4 * r + c, av, bv[c]);
+                }
+            } else if (wave == 2) {                           // W_hh: A = dgh [96, 192), B = h_{t-1} [256, 288)
+                const float b0 = rk[256], b1 = rk[256 + 16];
+#pragma unroll
+                for (int r = 0; r < 6; ++r) {
+                    const float av = rk[96 + 16 * r];
+                    mm(2 * r, av, b0);
+                    mm(2 * r + 1, av, b1);
+                }
+            } else {                                          // linear1: dz1 x (h, mic); linear2: dz2 x o
+                float bv[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) bv[c] = rk[320 + 16 * c];
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    const float av = rk[288 + 16 * r];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) mm(4 * r + c, av, bv[c]);
+                }
+                const float o0 = rk[416], o1 = rk[416 + 16];
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    const float av = rk[384 + 16 * r];
+                    mm(8 + 2 * r, av, o0);
+                    mm(8 + 2 * r + 1, av, o1);
+                }
+            }
         }
+        for (int f = 0; f < nfr; ++f) bacc += sR[f * kWgRow + boff];
     }
     float* part = p.part + (int64_t)blockIdx.x * kWeights;
+    auto put = [&](int i, int base, int ld, int g0_, int c0) {
 #pragma unroll
-    for (int i = 0; i < kWgPer; ++i) {
-        const int e = tid + i * kWgThreads;
-        if (e < kWeights) part[e] = acc[i];
+        for (int r = 0; r < 4; ++r) part[base + (g0_ + 4 * fk + r) * ld + c0 + fr] = acc[i][r];
+    };
+    if (wave < 2) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) put(4 * r + c, 0, 64, 16 * (3 * wave + r), 16 * c);
+    } else if (wave == 2) {
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) put(2 * r + c, 6144, 32, 16 * r, 16 * c);
+    } else {
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) put(4 * r + c, 9408, 64, 16 * r, 16 * c);
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) put(8 + 2 * r + c, 11488, 32, 16 * r, 16 * c);
     }
+    part[bblob] = bacc;
 }
 
 // T4: grad[e] = grad_loss * sum_k part[k][e]: block = 64 entries x 4 waves,
@@ -780,7 +833,7 @@ hipError_t launch_train_backward(const TrainArgs& a, int nblk, const float* grad
     }
     const int64_t stages = (nf + kWgF - 1) / kWgF;
     const int64_t per = ((stages + nblk - 1) / nblk) * kWgF;
-    hipLaunchKernelGGL(train_wgrad_kernel, dim3(nblk), dim3(kWgThreads), 0, st, a, per);
+    hipLaunchKernelGGL(train_wgrad_mfma_kernel, dim3(nblk), dim3(256), 0, st, a, per);
     hipLaunchKernelGGL(train_reduce_kernel, dim3((kWeights + 63) / 64), dim3(256), 0, st, a, nblk, grad_loss, grad);
     return hipGetLastError();
 }
