@@ -274,6 +274,146 @@ __device__ __forceinline__ void gemm_core_dma(f32x4 (&acc)[FM][FN], char* smem, 
     }
 }
 
+// Software-pipelined form of gemm_core_dma for two 128-B stage buffers: a
+// stage's fragments are read into registers one k-chunk ahead (set X = k-chunk
+// 0, set Y = k-chunk 1), so a stage buffer is free once its second chunk is in
+// registers. Iteration st:
+//   read Y (stage st, chunk 1); MFMAs on X;
+//   wait for this wave's DMAs and its LDS reads, barrier (stage st+1 landed
+//   everywhere, nobody reads buffer st&1 again);
+//   issue stage st+2 into buffer st&1; read X (stage st+1, chunk 0); MFMAs on Y.
+// The LDS read latency and the DMA issue run under the other chunk's MFMAs
+// instead of in front of them; the DMA still has one stage of MFMAs to land.
+// Same MFMA order per accumulator as gemm_core_dma (bit-identical results).
+// TRANS: the operands are swapped in every MFMA, so acc[fm][fn] holds the
+// transposed 16x16 block (lane: row m = lane & 15, columns n = 4 (lane >> 4)
+// + r): four adjacent output columns per lane (packed epilogue stores).
+template <typename T, int BM, int BN, int FM, int FN, class AO, class BO, int NW = 8, bool TRANS = false>
+__device__ __forceinline__ void gemm_core_dma_pipe(f32x4 (&acc)[FM][FN], char* smem, __amdgpu_buffer_rsrc_t ra,
+                                                   __amdgpu_buffer_rsrc_t rb, const AO& aoff, const BO& boff,
+                                                   int nstages, int wr0, int wc0) {
+    constexpr int RB = 128, RPI = 8, CPR = 8;
+    static_assert(BM % (RPI * NW) == 0 && BN % (RPI * NW) == 0, "tile");
+    constexpr int LA = BM / (RPI * NW), LB = BN / (RPI * NW);
+    constexpr int STAGE = (BM + BN) * RB;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int q_l = lane & (CPR - 1);
+    // live = false: the same instructions with out-of-range offsets (the
+    // hardware writes zeros, no memory traffic), so the loop body stays one
+    // basic block the MFMAs can be interleaved with
+    // offsets of stage st (computed ahead, in the MFMA phase before the barrier)
+    auto offs = [&](int st, bool live, uint32_t(&vo)[LA + LB]) {
+#pragma unroll
+        for (int i = 0; i < LA; ++i) {
+            const int row = RPI * (NW * i + wave) + lane / CPR;
+            const uint32_t o = aoff(i, st * RB + swz_slot<RB>(row, q_l) * 16);
+            vo[i] = live ? o : 0x80000000u;
+        }
+#pragma unroll
+        for (int i = 0; i < LB; ++i) {
+            const int row = RPI * (NW * i + wave) + lane / CPR;
+            const uint32_t o = boff(i, st * RB + swz_slot<RB>(row, q_l) * 16);
+            vo[LA + i] = live ? o : 0x80000000u;
+        }
+    };
+    auto issue_at = [&](int st, const uint32_t(&vo)[LA + LB]) {
+        char* buf = smem + (st & 1) * STAGE;
+#pragma unroll
+        for (int i = 0; i < LA; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                ra, (__attribute__((address_space(3))) void*)(buf + RPI * (NW * i + wave) * RB), 16, vo[i], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < LB; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rb, (__attribute__((address_space(3))) void*)(buf + BM * RB + RPI * (NW * i + wave) * RB), 16,
+                vo[LA + i], 0, 0, 0);
+    };
+    auto issue = [&](int st, bool live) {
+        uint32_t vo[LA + LB];
+        offs(st, live, vo);
+        issue_at(st, vo);
+    };
+    const int fr = lane & 15, g = lane >> 4;
+    auto rd = [&](int st, int kc, u32x4(&af)[FM], u32x4(&bf)[FN]) {
+        const char* sA = smem + (st & 1) * STAGE;
+        const char* sB = sA + BM * RB;
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+            const int r = wr0 + fm * 16 + fr;
+            af[fm] = *reinterpret_cast<const u32x4*>(sA + r * RB + swz_slot<RB>(r, kc * 4 + g) * 16);
+        }
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+            const int r = wc0 + fn * 16 + fr;
+            bf[fn] = *reinterpret_cast<const u32x4*>(sB + r * RB + swz_slot<RB>(r, kc * 4 + g) * 16);
+        }
+    };
+    auto rda = [&](int st, int kc, int fm) -> u32x4 {
+        const int r = wr0 + fm * 16 + fr;
+        return *reinterpret_cast<const u32x4*>(smem + (st & 1) * STAGE + r * RB + swz_slot<RB>(r, kc * 4 + g) * 16);
+    };
+    auto rdb = [&](int st, int kc, u32x4(&bf)[FN]) {
+        const char* sB = smem + (st & 1) * STAGE + BM * RB;
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+            const int r = wc0 + fn * 16 + fr;
+            bf[fn] = *reinterpret_cast<const u32x4*>(sB + r * RB + swz_slot<RB>(r, kc * 4 + g) * 16);
+        }
+    };
+    // MFMA row fm of one chunk, then the A fragment of the same row of the
+    // next chunk into the registers that row just released
+    u32x4 xa[FM], xb[FN], ya[FM], yb[FN];
+    issue(0, true);
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    issue(1, nstages > 1);
+    rd(0, 0, xa, xb);
+    for (int st = 0; st < nstages; ++st) {
+        uint32_t vo[LA + LB];
+        offs(st + 2, st + 2 < nstages, vo);
+        rdb(st, 1, yb);
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) {
+                if constexpr (TRANS) mma_chunk(acc[fm][fn], xb[fn], xa[fm], T{});
+                else mma_chunk(acc[fm][fn], xa[fm], xb[fn], T{});
+            }
+            ya[fm] = rda(st, 1, fm);
+        }
+        if constexpr (FM == 8 && FN == 4) {                 // row of MFMAs, then 2 / 1 LDS reads
+#define CRN_G(n) __builtin_amdgcn_sched_group_barrier(0x008, 4, 0); __builtin_amdgcn_sched_group_barrier(0x100, n, 0);
+            CRN_G(2) CRN_G(2) CRN_G(2) CRN_G(2) CRN_G(1) CRN_G(1) CRN_G(1) CRN_G(1)
+#undef CRN_G
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(0x0070);                 // vmcnt(0) expcnt(7) lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        issue_at(st + 2, vo);
+        // (after the last stage these read a stale buffer; the values are unused)
+        rdb(st + 1, 0, xb);
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) {
+                if constexpr (TRANS) mma_chunk(acc[fm][fn], yb[fn], ya[fm], T{});
+                else mma_chunk(acc[fm][fn], ya[fm], yb[fn], T{});
+            }
+            xa[fm] = rda(st + 1, 0, fm);
+        }
+        if constexpr (FM == 8 && FN == 4) {                 // row of MFMAs, LDS reads, one DMA
+#define CRN_G(n)                                                                                   \
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0); __builtin_amdgcn_sched_group_barrier(0x100, n, 0); \
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            CRN_G(2) CRN_G(2) CRN_G(2) CRN_G(2) CRN_G(1) CRN_G(1) CRN_G(1) CRN_G(1)
+#undef CRN_G
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    wait_vm<0>();                                          // the trailing (empty) DMAs, before the epilogue reuses LDS
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint64_t bytes) {
     const uint32_t nr = bytes > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)bytes;
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nr, 0x00020000);

@@ -690,6 +690,78 @@ __device__ __forceinline__ void rows_epilogue_lds(const f32x4 (&acc)[FM][FN], co
     }
 }
 
+// Epilogue for transposed accumulators (gemm_core_dma_pipe<TRANS>): a lane
+// holds four adjacent columns of one row per 16x16 block, written to the
+// wave's staging rows as one 8-B (bf16) / 16-B (f32) LDS store (rows padded by
+// 16 B: the 16 rows of a store land on distinct banks), then leaves as 16-B
+// row chunks exactly as rows_epilogue_lds.
+template <typename OutT, int FN>
+constexpr int epi_t_row_bytes() { return FN * 16 * (int)sizeof(OutT) + 16; }
+
+template <typename OutT, int FM, int FN, int PF>
+__device__ __forceinline__ void rows_epilogue_lds_t(const f32x4 (&acc)[FM][FN], const RowEpi& e, int64_t mb, int nb,
+                                                    int lane, char* wlds) {
+    static_assert(FM % PF == 0, "passes");
+    constexpr int RS = epi_t_row_bytes<OutT, FN>();      // staged row stride (bytes)
+    constexpr int CPR = FN * 16 * (int)sizeof(OutT) / 16;
+    constexpr int EPC = 16 / (int)sizeof(OutT);
+    const int g = lane >> 4, fr = lane & 15;
+    float bias[FN][4];
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int n = nb + fn * 16 + 4 * g + r;
+            bias[fn][r] = n < e.N ? e.bias[n] : 0.f;
+        }
+    const int act = e.act;
+    const float alpha = e.alpha;
+    const int64_t omask = (1ll << e.oshift) - 1;
+#pragma unroll
+    for (int p0 = 0; p0 < FM; p0 += PF) {
+#pragma unroll
+        for (int f = 0; f < PF; ++f)
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) {
+                OutT o4[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float v = acc[p0 + f][fn][r] + bias[fn][r];
+                    v = act == 1 ? (v >= 0.f ? v : alpha * v) : act == 2 ? tanhf(v) : v;
+                    o4[r] = to_elem<OutT>(v);
+                }
+                char* dst = wlds + (f * 16 + fr) * RS + (fn * 16 + 4 * g) * (int)sizeof(OutT);
+                if constexpr (sizeof(OutT) == 2) {
+                    uint2 w;
+                    w.x = (uint32_t)o4[0] | ((uint32_t)o4[1] << 16);
+                    w.y = (uint32_t)o4[2] | ((uint32_t)o4[3] << 16);
+                    *reinterpret_cast<uint2*>(dst) = w;
+                } else {
+                    *reinterpret_cast<float4*>(dst) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+                }
+            }
+        aec::wave_fence();
+#pragma unroll
+        for (int it = 0; it < PF * 16 * CPR / 64; ++it) {
+            const int c = it * 64 + lane;
+            const int row = c / CPR, ch = c % CPR;
+            const int64_t m = mb + p0 * 16 + row;
+            const int n = nb + ch * EPC;
+            if (m < e.M && n < e.N) {
+                const u32x4 v = *reinterpret_cast<const u32x4*>(wlds + row * RS + ch * 16);
+                OutT* o = reinterpret_cast<OutT*>(e.out) + (m >> e.oshift) * e.o_hi + (m & omask) * e.o_lo + e.o_add +
+                          (n >= e.nsplit ? e.split_add + (n - e.nsplit) : n);
+#if CRN_EPI_NT
+                __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(o));
+#else
+                *reinterpret_cast<u32x4*>(o) = v;
+#endif
+            }
+        }
+        aec::wave_fence();
+    }
+}
+
 // largest pass count PF (dividing FM) whose NW staging areas fit in `bytes`
 template <typename OutT, int FM, int FN, int NW>
 constexpr int epi_passes(size_t bytes) {
@@ -733,7 +805,7 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(RowSrc a, const T* __res
 }
 
 // Same GEMM through the LDS-DMA main loop (tiles with BM, BN multiples of 32).
-template <typename T, typename OutT, int WM, int WN, int FM, int FN, int NBUF, int RB>
+template <typename T, typename OutT, int WM, int WN, int FM, int FN, int NBUF, int RB, int PIPE = 0>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_rows_dma_kernel(RowSrc a, const T* __restrict__ bt, int64_t ldb,
                                                                      int nstages, RowEpi e) {
     constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
@@ -769,8 +841,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_rows_dma_kernel(RowSrc a, c
         const int k = kbyte / ES;
         const int tap = k >> a.kshift;
         const int pos = posb[i] + tap;
-        const bool ok = mval[i] && k < a.K && pos >= 0 && pos < a.plim;
-        return ok ? (uint32_t)((rowoff[i] + tap * (int32_t)a.ks + (k & kmask)) * ES) : kOOB;
+        // branch-free: the offset is computed unconditionally and replaced by the
+        // out-of-range marker (no exec-mask branches between the DMA issues)
+        const uint32_t off = (uint32_t)((rowoff[i] + tap * (int32_t)a.ks + (k & kmask)) * ES);
+        const bool ok = mval[i] & (k < a.K) & (pos >= 0) & (pos < a.plim);
+        return ok ? off : kOOB;
     };
     auto boff = [&](int i, int kbyte) -> uint32_t {
         return (uint32_t)((RPI * (NW * i + wave) + lane / (RB / 16)) * (int32_t)ldb * ES + kbyte);
@@ -780,8 +855,16 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_rows_dma_kernel(RowSrc a, c
     for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gemm_core_dma<T, BM, BN, FM, FN, NBUF, decltype(aoff), decltype(boff), NW, RB>(acc, smem, ra, rb, aoff, boff,
-                                                                                   nstages, wr0, wc0);
+    // PIPE: 0 gemm_core_dma; 1 gemm_core_dma_pipe; 2 gemm_core_dma_pipe with
+    // transposed accumulators and the packed epilogue
+    if constexpr (PIPE) {
+        static_assert(NBUF == 2 && RB == 128, "pipelined core: two 128-B stage buffers");
+        gemm_core_dma_pipe<T, BM, BN, FM, FN, decltype(aoff), decltype(boff), NW, (PIPE == 2)>(
+            acc, smem, ra, rb, aoff, boff, nstages, wr0, wc0);
+    } else {
+        gemm_core_dma<T, BM, BN, FM, FN, NBUF, decltype(aoff), decltype(boff), NW, RB>(acc, smem, ra, rb, aoff, boff,
+                                                                                       nstages, wr0, wc0);
+    }
     if (e.mode & 1) {                                  // timing only: keep the MFMAs alive, skip the epilogue
         float sum = 0.f;
 #pragma unroll
@@ -792,6 +875,16 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_rows_dma_kernel(RowSrc a, c
         return;
     }
     __syncthreads();                                   // every wave is done with the stage buffers
+    if constexpr (PIPE == 2) {                         // transposed accumulators: packed staging stores
+        constexpr int RS = epi_t_row_bytes<OutT, FN>();
+        constexpr size_t cap = (size_t)NBUF * (BM + BN) * RB;
+        constexpr int PFT = (size_t)NW * FM * 16 * RS <= cap ? FM
+                            : (size_t)NW * (FM / 2) * 16 * RS <= cap ? FM / 2
+                            : (size_t)NW * (FM / 4) * 16 * RS <= cap ? FM / 4 : 1;
+        static_assert((size_t)NW * PFT * 16 * RS <= cap, "epilogue LDS");
+        rows_epilogue_lds_t<OutT, FM, FN, PFT>(acc, e, m0 + wr0, n0 + wc0, lane, smem + wave * (PFT * 16 * RS));
+        return;
+    }
     constexpr int PF = epi_passes<OutT, FM, FN, NW>((size_t)NBUF * (BM + BN) * RB);
     static_assert(NW * PF * 16 * FN * 16 * sizeof(OutT) <= (size_t)NBUF * (BM + BN) * RB, "epilogue LDS");
     rows_epilogue_lds<OutT, FM, FN, PF>(acc, e, m0 + wr0, n0 + wc0, lane,
@@ -817,10 +910,10 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
         hipLaunchKernelGGL((gemm_rows_kernel<T, OutT, WM, WN, FM, FN>), grid, dim3(256), 0, st, a, bt, ldb,  \
                            nstages, e);                                                                       \
     } while (0)
-#define CRN_GEMM_DMA_RB(WM, WN, FM, FN, NBUF, RB)                                                               \
+#define CRN_GEMM_DMA_RBP(WM, WN, FM, FN, NBUF, RB, PIPE)                                                        \
     do {                                                                                                          \
         constexpr int BM = WM * FM * 16, BN = WN * FN * 16;                                                       \
-        auto kern = gemm_rows_dma_kernel<T, OutT, WM, WN, FM, FN, NBUF, RB>;                                      \
+        auto kern = gemm_rows_dma_kernel<T, OutT, WM, WN, FM, FN, NBUF, RB, PIPE>;                                \
         constexpr size_t lds = (size_t)NBUF * (BM + BN) * RB;                                                     \
         static const hipError_t attr =                                                                            \
             hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, \
@@ -830,19 +923,25 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
         dim3 grid((unsigned)((a.M + BM - 1) / BM) * nbn_);                                                        \
         hipLaunchKernelGGL(kern, grid, dim3(64 * WM * WN), lds, st, a, bt, ldb, nstages * (128 / RB), ee);        \
     } while (0)
+#define CRN_GEMM_DMA_RB(WM, WN, FM, FN, NBUF, RB) CRN_GEMM_DMA_RBP(WM, WN, FM, FN, NBUF, RB, 0)
 #define CRN_GEMM_DMA(WM, WN, FM, FN, NBUF) CRN_GEMM_DMA_RB(WM, WN, FM, FN, NBUF, 128)
     static const int dma = env_int("CRN_GEMM_DMA", 2);    // 0 = register-staged core, else NBUF
     static const int big = env_int("CRN_GEMM_BIG", 0);    // 256x128 tiles (8 waves) for large M (measured slower)
     static const int sq = env_int("CRN_GEMM_SQ", 1);      // 256x256 tiles (8 waves) when N % 256 == 0
     static const int rb64 = env_int("CRN_GEMM_RB64", 0);  // 128x128 tiles with 64-B K slices, 4 buffers
     static const int gmode = env_int("CRN_GEMM_MODE", 0);  // timing experiments only (results invalid unless 0)
+    // CRN_GEMM_PIPE: 0 = gemm_core_dma everywhere; 1 = pipelined core on the
+    // 256x256 tiles; 2 = + transposed accumulators / packed epilogue there;
+    // 3 = pipelined core + packed epilogue on the 128x128 / 128x64 DMA tiles too
+    static const int pipe = env_int("CRN_GEMM_PIPE", 3);
     RowEpi ee = e;
     ee.mode = gmode;
     switch (bn) {
         case 16: CRN_GEMM(4, 1, 4, 1); break;
         case 32: CRN_GEMM(2, 2, 4, 1); break;
         case 64:
-            if (dma == 2) CRN_GEMM_DMA(2, 2, 4, 2, 2);
+            if (dma == 2 && pipe == 3) CRN_GEMM_DMA_RBP(2, 2, 4, 2, 2, 128, 2);
+            else if (dma == 2) CRN_GEMM_DMA(2, 2, 4, 2, 2);
             else if (dma == 3) CRN_GEMM_DMA(2, 2, 4, 2, 3);
             else if (dma >= 4) CRN_GEMM_DMA(2, 2, 4, 2, 4);
             else CRN_GEMM(2, 2, 4, 2);
@@ -850,9 +949,12 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
         default:
             if (e.N % 256 == 0 && a.M >= 4096 && sq >= 1) {
                 if (sq == 2) CRN_GEMM_DMA_RB(2, 4, 8, 4, 4, 64);          // 64-B K slices, 4 buffers
+                else if (pipe >= 2) CRN_GEMM_DMA_RBP(2, 4, 8, 4, 2, 128, 2);   // + transposed acc, packed epilogue
+                else if (pipe) CRN_GEMM_DMA_RBP(2, 4, 8, 4, 2, 128, 1);   // same tile, pipelined core
                 else CRN_GEMM_DMA(2, 4, 8, 4, 2);                         // 256 x 256 tile, 8 waves, 128 KB LDS
             } else if (rb64) CRN_GEMM_DMA_RB(2, 2, 4, 4, 4, 64);
             else if (big && a.M >= 256 * 1024) CRN_GEMM_DMA(4, 2, 4, 4, 2);
+            else if (dma == 2 && pipe == 3) CRN_GEMM_DMA_RBP(2, 2, 4, 4, 2, 128, 2);
             else if (dma == 2) CRN_GEMM_DMA(2, 2, 4, 4, 2);
             else if (dma == 3) CRN_GEMM_DMA(2, 2, 4, 4, 3);
             else if (dma >= 4) CRN_GEMM_DMA(2, 2, 4, 4, 4);
@@ -862,6 +964,7 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
 #undef CRN_GEMM
 #undef CRN_GEMM_DMA
 #undef CRN_GEMM_DMA_RB
+#undef CRN_GEMM_DMA_RBP
     return hipGetLastError();
 }
 
