@@ -321,11 +321,19 @@ def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu, nlms=N
     dom_fl = fl.get(dom, 0)
     ach = dom_fl * B * T / (stage_ms[dom] * 1e-3) / 1e12 if dom_fl else 0.0
     whole = fl['total'] * B * T / (ms_step * 1e-3) / 1e12
+    # HBM bytes of the LSTM stage per batch from the committed PMC passes
+    # (profiles/pmc_latest_crn.json, tools/crn_pmc.sh + tools/crn_pmc_latest.py), same shape and dtype only
+    traffic = None
+    pp = os.path.join(REPO, 'profiles', 'pmc_latest_crn.json')
+    if dom == 'lstm' and not nlms and os.path.exists(pp):
+        pj = json.load(open(pp))
+        if pj.get('dtype') == dtype and pj.get('B') == B and pj.get('N') == n:
+            traffic = pj.get('lstm_stage_hbm_bytes_per_batch')
     res = dict(value=round(value, 1), value_per_gpu=round(value / world, 1), ms_per_step=round(ms_step, 3),
                batches_in_flight=inflight,
                rtf_batch1=rtf1, stage_ms_per_step={k: round(v, 3) for k, v in stage_ms.items()},
                roofline={'bound': 'mfma', 'achieved': round(ach, 1), 'peak': peak, 'unit': 'TFLOP/s',
-                         'frac': round(ach / peak, 4), 'traffic': None,
+                         'frac': round(ach / peak, 4), 'traffic': traffic,
                          'kernel': f'{dom} stage ({"input GEMM + per-frame recurrence steps + combine per layer" if dom == "lstm" else "GEMM launches"})',
                          'alg_flops_per_frame': dom_fl, 'frames_per_launch': B * T},
                pipeline_roofline={'alg_flops_per_frame': fl['total'], 'achieved_tflops': round(whole, 1),
