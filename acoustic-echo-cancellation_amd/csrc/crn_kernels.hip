@@ -698,22 +698,30 @@ __device__ __forceinline__ void rows_epilogue_lds(const f32x4 (&acc)[FM][FN], co
 template <typename OutT, int FN>
 constexpr int epi_t_row_bytes() { return FN * 16 * (int)sizeof(OutT) + 16; }
 
+// the lane's bias values (columns nb + fn*16 + 4 (lane >> 4) + r), loaded
+// before the main loop so their latency is not exposed in the epilogue
+template <int FN>
+__device__ __forceinline__ void load_bias_t(const RowEpi& e, int nb, int lane, f32x4 (&bias)[FN]) {
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+        const int n = nb + fn * 16 + 4 * (lane >> 4);
+        if (n + 4 <= e.N) {
+            bias[fn] = *reinterpret_cast<const f32x4*>(e.bias + n);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bias[fn][r] = n + r < e.N ? e.bias[n + r] : 0.f;
+        }
+    }
+}
+
 template <typename OutT, int FM, int FN, int PF>
 __device__ __forceinline__ void rows_epilogue_lds_t(const f32x4 (&acc)[FM][FN], const RowEpi& e, int64_t mb, int nb,
-                                                    int lane, char* wlds) {
+                                                    int lane, char* wlds, const f32x4 (&bias)[FN]) {
     static_assert(FM % PF == 0, "passes");
     constexpr int RS = epi_t_row_bytes<OutT, FN>();      // staged row stride (bytes)
     constexpr int CPR = FN * 16 * (int)sizeof(OutT) / 16;
     constexpr int EPC = 16 / (int)sizeof(OutT);
     const int g = lane >> 4, fr = lane & 15;
-    float bias[FN][4];
-#pragma unroll
-    for (int fn = 0; fn < FN; ++fn)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int n = nb + fn * 16 + 4 * g + r;
-            bias[fn][r] = n < e.N ? e.bias[n] : 0.f;
-        }
     const int act = e.act;
     const float alpha = e.alpha;
     const int64_t omask = (1ll << e.oshift) - 1;
@@ -747,7 +755,7 @@ __device__ __forceinline__ void rows_epilogue_lds_t(const f32x4 (&acc)[FM][FN], 
             const int row = c / CPR, ch = c % CPR;
             const int64_t m = mb + p0 * 16 + row;
             const int n = nb + ch * EPC;
-            if (m < e.M && n < e.N) {
+            if (m < e.M && n < e.N && !(e.mode & 2)) {     // mode bit 1: timing only, no global stores
                 const u32x4 v = *reinterpret_cast<const u32x4*>(wlds + row * RS + ch * 16);
                 OutT* o = reinterpret_cast<OutT*>(e.out) + (m >> e.oshift) * e.o_hi + (m & omask) * e.o_lo + e.o_add +
                           (n >= e.nsplit ? e.split_add + (n - e.nsplit) : n);
@@ -760,6 +768,14 @@ __device__ __forceinline__ void rows_epilogue_lds_t(const f32x4 (&acc)[FM][FN], 
         }
         aec::wave_fence();
     }
+}
+
+// dynamic LDS of gemm_rows_dma_kernel: the stage buffers (the packed
+// epilogue stages in passes inside them; one pass over 147 KB of LDS for the
+// 256 x 256 tile measured slower: 5.48 vs 5.35 ms on the LSTM shape)
+template <typename OutT, int WM, int WN, int FM, int FN, int NBUF, int RB, int PIPE>
+constexpr size_t dma_lds_bytes() {
+    return (size_t)NBUF * (WM * FM * 16 + WN * FN * 16) * RB;
 }
 
 // largest pass count PF (dividing FM) whose NW staging areas fit in `bytes`
@@ -855,6 +871,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_rows_dma_kernel(RowSrc a, c
     for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 bias_t[FN];
+    if constexpr (PIPE == 2) load_bias_t<FN>(e, n0 + wc0, lane, bias_t);
     // PIPE: 0 gemm_core_dma; 1 gemm_core_dma_pipe; 2 gemm_core_dma_pipe with
     // transposed accumulators and the packed epilogue
     if constexpr (PIPE) {
@@ -877,12 +895,13 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_rows_dma_kernel(RowSrc a, c
     __syncthreads();                                   // every wave is done with the stage buffers
     if constexpr (PIPE == 2) {                         // transposed accumulators: packed staging stores
         constexpr int RS = epi_t_row_bytes<OutT, FN>();
-        constexpr size_t cap = (size_t)NBUF * (BM + BN) * RB;
+        constexpr size_t cap = dma_lds_bytes<OutT, WM, WN, FM, FN, NBUF, RB, PIPE>();
         constexpr int PFT = (size_t)NW * FM * 16 * RS <= cap ? FM
                             : (size_t)NW * (FM / 2) * 16 * RS <= cap ? FM / 2
                             : (size_t)NW * (FM / 4) * 16 * RS <= cap ? FM / 4 : 1;
         static_assert((size_t)NW * PFT * 16 * RS <= cap, "epilogue LDS");
-        rows_epilogue_lds_t<OutT, FM, FN, PFT>(acc, e, m0 + wr0, n0 + wc0, lane, smem + wave * (PFT * 16 * RS));
+        rows_epilogue_lds_t<OutT, FM, FN, PFT>(acc, e, m0 + wr0, n0 + wc0, lane, smem + wave * (PFT * 16 * RS),
+                                               bias_t);
         return;
     }
     constexpr int PF = epi_passes<OutT, FM, FN, NW>((size_t)NBUF * (BM + BN) * RB);
@@ -914,7 +933,7 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
     do {                                                                                                          \
         constexpr int BM = WM * FM * 16, BN = WN * FN * 16;                                                       \
         auto kern = gemm_rows_dma_kernel<T, OutT, WM, WN, FM, FN, NBUF, RB, PIPE>;                                \
-        constexpr size_t lds = (size_t)NBUF * (BM + BN) * RB;                                                     \
+        constexpr size_t lds = dma_lds_bytes<OutT, WM, WN, FM, FN, NBUF, RB, PIPE>();                           \
         static const hipError_t attr =                                                                            \
             hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                 (int)lds);                                                                        \
