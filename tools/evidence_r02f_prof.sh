@@ -4,7 +4,7 @@
 set -uo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
-bash tools/profile.sh r02f_full || exit 1
+bash tools/profile.sh r02f_full --pipeline full --inflight 1 || exit 1
 bash tools/crn_prof.sh r02f_crn --dtype bf16 || exit 1
 bash tools/crn_pmc.sh r02f_crnpmc --dtype bf16 || exit 1
 echo "evidence done"
