@@ -634,13 +634,20 @@ __device__ __forceinline__ void rows_epilogue(const f32x4 (&acc)[FM][FN], const 
         }
 }
 
+template <int ACT>
+__device__ __forceinline__ float apply_act(float v, float alpha) {
+    if constexpr (ACT == 1) return v >= 0.f ? v : alpha * v;
+    else if constexpr (ACT == 2) return tanhf(v);
+    else return v;
+}
+
 // LDS-staged variant: the wave's (FM*16) x (FN*16) tile goes through LDS
 // (after bias + activation) in passes of PF row fragments and leaves as
 // 16-byte row chunks (N and the output channel offsets are multiples of 16
 // bytes).  wlds: the wave's PF*16 x FN*16 staging area.
-template <typename OutT, int FM, int FN, int PF>
-__device__ __forceinline__ void rows_epilogue_lds(const f32x4 (&acc)[FM][FN], const RowEpi& e, int64_t mb, int nb,
-                                                  int lane, char* wlds) {
+template <typename OutT, int FM, int FN, int PF, int ACT>
+__device__ __forceinline__ void rows_epilogue_lds_a(const f32x4 (&acc)[FM][FN], const RowEpi& e, int64_t mb, int nb,
+                                                    int lane, char* wlds) {
     static_assert(FM % PF == 0, "passes");
     constexpr int WC = FN * 16;
     constexpr int RB = WC * (int)sizeof(OutT);          // bytes per staged row
@@ -652,7 +659,6 @@ __device__ __forceinline__ void rows_epilogue_lds(const f32x4 (&acc)[FM][FN], co
         const int n = nb + fn * 16 + (lane & 15);
         bias[fn] = n < e.N ? e.bias[n] : 0.f;
     }
-    const int act = e.act;
     const float alpha = e.alpha;
     const int64_t omask = (1ll << e.oshift) - 1;
     OutT* st = reinterpret_cast<OutT*>(wlds);
@@ -664,8 +670,7 @@ __device__ __forceinline__ void rows_epilogue_lds(const f32x4 (&acc)[FM][FN], co
             for (int r = 0; r < 4; ++r)
 #pragma unroll
                 for (int fn = 0; fn < FN; ++fn) {
-                    float v = acc[p0 + f][fn][r] + bias[fn];
-                    v = act == 1 ? (v >= 0.f ? v : alpha * v) : act == 2 ? tanhf(v) : v;
+                    const float v = apply_act<ACT>(acc[p0 + f][fn][r] + bias[fn], alpha);
                     st[(f * 16 + 4 * (lane >> 4) + r) * WC + fn * 16 + (lane & 15)] = to_elem<OutT>(v);
                 }
         aec::wave_fence();
@@ -688,6 +693,16 @@ __device__ __forceinline__ void rows_epilogue_lds(const f32x4 (&acc)[FM][FN], co
         }
         aec::wave_fence();
     }
+}
+
+// the activation is uniform (e.act): one specialised copy per activation,
+// no per-element branch
+template <typename OutT, int FM, int FN, int PF>
+__device__ __forceinline__ void rows_epilogue_lds(const f32x4 (&acc)[FM][FN], const RowEpi& e, int64_t mb, int nb,
+                                                  int lane, char* wlds) {
+    if (e.act == 1) rows_epilogue_lds_a<OutT, FM, FN, PF, 1>(acc, e, mb, nb, lane, wlds);
+    else if (e.act == 2) rows_epilogue_lds_a<OutT, FM, FN, PF, 2>(acc, e, mb, nb, lane, wlds);
+    else rows_epilogue_lds_a<OutT, FM, FN, PF, 0>(acc, e, mb, nb, lane, wlds);
 }
 
 // Epilogue for transposed accumulators (gemm_core_dma_pipe<TRANS>): a lane
@@ -714,6 +729,36 @@ __device__ __forceinline__ void load_bias_t(const RowEpi& e, int nb, int lane, f
     }
 }
 
+// one staging pass of rows_epilogue_lds_t with the activation fixed at
+// compile time (no per-element branch on the uniform e.act)
+template <typename OutT, int FM, int FN, int PF, int ACT>
+__device__ __forceinline__ void stage_pass_t(const f32x4 (&acc)[FM][FN], int p0, const f32x4 (&bias)[FN], float alpha,
+                                             char* wlds, int fr, int g) {
+    constexpr int RS = epi_t_row_bytes<OutT, FN>();
+#pragma unroll
+    for (int f = 0; f < PF; ++f)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+            OutT o4[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float v = acc[p0 + f][fn][r] + bias[fn][r];
+                if constexpr (ACT == 1) v = v >= 0.f ? v : alpha * v;
+                else if constexpr (ACT == 2) v = tanhf(v);
+                o4[r] = to_elem<OutT>(v);
+            }
+            char* dst = wlds + (f * 16 + fr) * RS + (fn * 16 + 4 * g) * (int)sizeof(OutT);
+            if constexpr (sizeof(OutT) == 2) {
+                uint2 w;
+                w.x = (uint32_t)o4[0] | ((uint32_t)o4[1] << 16);
+                w.y = (uint32_t)o4[2] | ((uint32_t)o4[3] << 16);
+                *reinterpret_cast<uint2*>(dst) = w;
+            } else {
+                *reinterpret_cast<float4*>(dst) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+            }
+        }
+}
+
 template <typename OutT, int FM, int FN, int PF>
 __device__ __forceinline__ void rows_epilogue_lds_t(const f32x4 (&acc)[FM][FN], const RowEpi& e, int64_t mb, int nb,
                                                     int lane, char* wlds, const f32x4 (&bias)[FN]) {
@@ -727,27 +772,9 @@ __device__ __forceinline__ void rows_epilogue_lds_t(const f32x4 (&acc)[FM][FN], 
     const int64_t omask = (1ll << e.oshift) - 1;
 #pragma unroll
     for (int p0 = 0; p0 < FM; p0 += PF) {
-#pragma unroll
-        for (int f = 0; f < PF; ++f)
-#pragma unroll
-            for (int fn = 0; fn < FN; ++fn) {
-                OutT o4[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float v = acc[p0 + f][fn][r] + bias[fn][r];
-                    v = act == 1 ? (v >= 0.f ? v : alpha * v) : act == 2 ? tanhf(v) : v;
-                    o4[r] = to_elem<OutT>(v);
-                }
-                char* dst = wlds + (f * 16 + fr) * RS + (fn * 16 + 4 * g) * (int)sizeof(OutT);
-                if constexpr (sizeof(OutT) == 2) {
-                    uint2 w;
-                    w.x = (uint32_t)o4[0] | ((uint32_t)o4[1] << 16);
-                    w.y = (uint32_t)o4[2] | ((uint32_t)o4[3] << 16);
-                    *reinterpret_cast<uint2*>(dst) = w;
-                } else {
-                    *reinterpret_cast<float4*>(dst) = make_float4(o4[0], o4[1], o4[2], o4[3]);
-                }
-            }
+        if (act == 1) stage_pass_t<OutT, FM, FN, PF, 1>(acc, p0, bias, alpha, wlds, fr, g);
+        else if (act == 2) stage_pass_t<OutT, FM, FN, PF, 2>(acc, p0, bias, alpha, wlds, fr, g);
+        else stage_pass_t<OutT, FM, FN, PF, 0>(acc, p0, bias, alpha, wlds, fr, g);
         aec::wave_fence();
 #pragma unroll
         for (int it = 0; it < PF * 16 * CPR / 64; ++it) {
