@@ -600,11 +600,19 @@ __device__ __forceinline__ void store_out(void* out, int64_t idx, float v) {
     reinterpret_cast<OutT*>(out)[idx] = to_elem<OutT>(v);
 }
 
+// epilogue activation, fixed at compile time: 0 none, 1 PReLU (alpha), 2 tanh
+template <int ACT>
+__device__ __forceinline__ float apply_act(float v, float alpha) {
+    if constexpr (ACT == 1) return v >= 0.f ? v : alpha * v;
+    else if constexpr (ACT == 2) return tanhf(v);
+    else return v;
+}
+
 // Row-GEMM epilogue: bias (loaded once per column fragment), activation,
 // store.  Rows / columns beyond M / N are skipped.
-template <typename OutT, int FM, int FN>
-__device__ __forceinline__ void rows_epilogue(const f32x4 (&acc)[FM][FN], const RowEpi& e, int64_t mb, int nb,
-                                              int lane) {
+template <typename OutT, int FM, int FN, int ACT>
+__device__ __forceinline__ void rows_epilogue_a(const f32x4 (&acc)[FM][FN], const RowEpi& e, int64_t mb, int nb,
+                                                int lane) {
     float bias[FN];
     bool nok[FN];
 #pragma unroll
@@ -614,7 +622,6 @@ __device__ __forceinline__ void rows_epilogue(const f32x4 (&acc)[FM][FN], const 
         bias[fn] = nok[fn] ? e.bias[n] : 0.f;
     }
     const int64_t omask = (1ll << e.oshift) - 1;
-    const int act = e.act;
     const float alpha = e.alpha;
 #pragma unroll
     for (int fm = 0; fm < FM; ++fm)
@@ -626,19 +633,19 @@ __device__ __forceinline__ void rows_epilogue(const f32x4 (&acc)[FM][FN], const 
                          nb + (lane & 15);
 #pragma unroll
             for (int fn = 0; fn < FN; ++fn) {
-                float v = acc[fm][fn][r] + bias[fn];
-                v = act == 1 ? (v >= 0.f ? v : alpha * v) : act == 2 ? tanhf(v) : v;
+                const float v = apply_act<ACT>(acc[fm][fn][r] + bias[fn], alpha);
                 const int n = nb + fn * 16 + (lane & 15);
                 if (nok[fn]) orow[fn * 16 + (n >= e.nsplit ? e.split_add - e.nsplit : 0)] = to_elem<OutT>(v);
             }
         }
 }
 
-template <int ACT>
-__device__ __forceinline__ float apply_act(float v, float alpha) {
-    if constexpr (ACT == 1) return v >= 0.f ? v : alpha * v;
-    else if constexpr (ACT == 2) return tanhf(v);
-    else return v;
+// the activation is uniform (e.act): one specialised copy per activation
+template <typename OutT, int FM, int FN>
+__device__ __forceinline__ void rows_epilogue(const f32x4 (&acc)[FM][FN], const RowEpi& e, int64_t mb, int nb, int lane) {
+    if (e.act == 1) rows_epilogue_a<OutT, FM, FN, 1>(acc, e, mb, nb, lane);
+    else if (e.act == 2) rows_epilogue_a<OutT, FM, FN, 2>(acc, e, mb, nb, lane);
+    else rows_epilogue_a<OutT, FM, FN, 0>(acc, e, mb, nb, lane);
 }
 
 // LDS-staged variant: the wave's (FM*16) x (FN*16) tile goes through LDS
