@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import numpy as np
 import torch
+from torch.autograd.graph import increment_version
 
 from . import _lib, h5lite
 
@@ -111,6 +112,11 @@ class Adam(torch.optim.Optimizer):
                                       [p.numel() for p, _, _ in items], [int(st['step'].item()) for _, _, st in items],
                                       group['lr'], b1, b2, group['eps'], group['weight_decay'],
                                       torch.cuda.current_stream(dev).cuda_stream)
+                # the kernel wrote the parameters through raw pointers: bump their version counters
+                # as torch.optim.Adam's in-place ops do, so caches keyed on (data_ptr, _version) --
+                # Little_net's weight upload -- see the step
+                for p, _, _ in items:
+                    increment_version(p)
         return loss
 
 

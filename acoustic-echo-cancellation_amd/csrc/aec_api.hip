@@ -186,46 +186,45 @@ struct aec_handle {
     int64_t ws_B = 0, ws_T = 0;
     double2* d_mom = nullptr;    // [B][3][kMomChunks]
     float* d_cvals = nullptr;    // [B][3]
-    WorkItem* d_items = nullptr; // analysis work list (rebuilt when the lengths change)
-    int64_t items_cap = 0, nitems = 0;
-    WorkItem* d_sitems = nullptr; // synthesis block-item list
-    int64_t sitems_cap = 0, nsitems = 0;
-    int num_cus = 256;
-    std::vector<int64_t> item_off, sitem_off;   // first analysis / synthesis item of stream b (B+1 entries)
-    // sub-batch pipelining (AEC_SUBBATCH=S, default 1 = off): streams
-    // [b_k, b_k+1) run their chain on internal stream k; chain k+1 starts its
-    // moments/analysis once chain k's analysis is done, meant to overlap its
-    // FFT work with chain k's latency-bound recurrence.  Measured slower on
-    // MI355X (S=2: 0.80 ms vs 0.69 ms per 256-stream step): the persistent
-    // analysis grid fills every CU's LDS and the GRU's 244-VGPR waves cannot
-    // co-reside, so the sub-batch GRUs serialise.  Kept for co-residency work.
-    static constexpr int kMaxSub = 4;
-    int sub_max = 1;
-    hipStream_t sst[kMaxSub] = {};
-    hipEvent_t ev_start = nullptr, ev_ana[kMaxSub] = {}, ev_done[kMaxSub] = {};
+    // work lists of the last batch shape (prepare_lists): one device block
+    // [items | sitems | len | slen] rewritten in stream order from a ring of two
+    // pinned host slots; no device-wide synchronisation when the lengths change
+    char* d_lists = nullptr;
+    size_t lists_cap = 0;
+    WorkItem* d_items = nullptr; // analysis work list (4-frame items)
+    WorkItem* d_sitems = nullptr; // synthesis block-item list (15 hops)
     int64_t* d_len = nullptr;    // [B] mic length: sets the frame count and output length
     int32_t* d_slen = nullptr;   // [B][4] per-signal lengths (mic, ref, near, -): normaliser + zero padding
+    int64_t nitems = 0, nsitems = 0;
+    struct ListSlot {
+        char* host = nullptr;    // pinned
+        size_t cap = 0;
+        hipEvent_t ev = nullptr; // recorded after the upload from this slot
+        bool pending = false;
+    };
+    ListSlot slots[2];
+    int slot_next = 0;
+    int last_nsig = 0;
+    int num_cus = 256;
+    std::vector<int64_t> item_off, sitem_off;   // first analysis / synthesis item of stream b (B+1 entries)
+    // ordering of this handle's calls: a call on another stream than the last one
+    // waits (on the device) for the last one, since they share the workspace
+    hipEvent_t ev_last = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool have_last = false;
     float* d_feats = nullptr;    // [B][T][96]
     float* d_est = nullptr;      // [B][T][32]
     float* d_dbg = nullptr;      // [2][B][T][32]  (h, mask)
     float2* d_spec = nullptr;    // [B][T][256] NLMS error spectrum (nlms_taps > 0 only)
     std::vector<int64_t> last_lens;                 // [B][3] of the last call (work lists rebuilt on change)
-    // host staging of the work lists (kept alive while their async copies run)
-    std::vector<WorkItem> h_items, h_sitems;
-    std::vector<int32_t> h_slen;
+    std::vector<WorkItem> h_items, h_sitems;        // host copies of the last work lists
     int debug = 0;
     int gru_mode = 0;            // AEC_GRU_MODE (timing experiments; results invalid unless 0)
     int nlms_mode = 0;           // AEC_NLMS_MODE (timing experiments; results invalid unless 0)
     int nlms_prio = 0;           // AEC_NLMS_PRIO: wave priorities mic|ref|nlms digits (0: all equal, fastest measured)
     int nlms_erb = 1;            // AEC_NLMS_ERB: role running the mic_erb pass (1 ref, 2 nlms)
-    int nlms16 = 0;              // AEC_NLMS16: 16-wave NLMS analysis (aec_nlms16.hip, taps <= 4; measured slower)
     int fused = 1;               // AEC_FUSED_SYNTH: GRU + synthesis in one kernel (NLMS path)
     int fused_mode = 0;          // AEC_FUSED_MODE (timing experiments; results invalid unless 0)
-    int pipe = 0;                // AEC_PIPE: the fused per-stream pipeline (aec_pipe.hip) for B >= pipe_minb
-    int pipe_minb = 1;           // AEC_PIPE_MINB
-    int pipe_mode = 0;           // AEC_PIPE_MODE (timing experiments; results invalid unless 0)
-    float2* d_ring = nullptr;    // [B][kPipeRingRows][256] pipeline error-spectrum ring
-    int64_t ring_B = 0;
     int small_b = 64;            // AEC_SMALLB: NLMS batches up to this many streams take the split path
                                  // (per 10 s step: B = 1 0.477 -> 0.336 ms, B = 16 0.486 -> 0.354,
                                  // B = 64 0.504 -> 0.485; B = 128 slower)
@@ -371,15 +370,10 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
     if (const char* m = std::getenv("AEC_NLMS_MODE")) h->nlms_mode = std::atoi(m);
     if (const char* m = std::getenv("AEC_NLMS_PRIO")) h->nlms_prio = std::atoi(m);
     if (const char* m = std::getenv("AEC_NLMS_ERB")) h->nlms_erb = std::atoi(m);
-    if (const char* m = std::getenv("AEC_NLMS16")) h->nlms16 = std::atoi(m);
     if (const char* m = std::getenv("AEC_FUSED_SYNTH")) h->fused = std::atoi(m);
     if (const char* m = std::getenv("AEC_FUSED_MODE")) h->fused_mode = std::atoi(m);
     if (const char* m = std::getenv("AEC_SMALLB")) h->small_b = std::atoi(m);
-    if (const char* m = std::getenv("AEC_PIPE")) h->pipe = std::atoi(m);
-    if (const char* m = std::getenv("AEC_PIPE_MINB")) h->pipe_minb = std::atoi(m);
-    if (const char* m = std::getenv("AEC_PIPE_MODE")) h->pipe_mode = std::atoi(m);
     if (const char* m = std::getenv("AEC_BPTT_SERIAL")) h->bptt_serial = std::atoi(m);
-    if (const char* m = std::getenv("AEC_SUBBATCH")) h->sub_max = std::max(1, std::min(aec_handle::kMaxSub, std::atoi(m)));
     {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
@@ -388,12 +382,9 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
     auto bail = [&](aec_status s) { aec_destroy(h); return s; };
     DeviceGuard dg(device);
     if (dg.err != hipSuccess) return bail(AEC_ERR_HIP);
-    for (int k = 0; k < aec_handle::kMaxSub; ++k) {
-        if (hipStreamCreateWithFlags(&h->sst[k], hipStreamNonBlocking) != hipSuccess) return bail(AEC_ERR_HIP);
-        if (hipEventCreateWithFlags(&h->ev_ana[k], hipEventDisableTiming) != hipSuccess) return bail(AEC_ERR_HIP);
-        if (hipEventCreateWithFlags(&h->ev_done[k], hipEventDisableTiming) != hipSuccess) return bail(AEC_ERR_HIP);
-    }
-    if (hipEventCreateWithFlags(&h->ev_start, hipEventDisableTiming) != hipSuccess) return bail(AEC_ERR_HIP);
+    if (hipEventCreateWithFlags(&h->ev_last, hipEventDisableTiming) != hipSuccess) return bail(AEC_ERR_HIP);
+    for (auto& sl : h->slots)
+        if (hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) != hipSuccess) return bail(AEC_ERR_HIP);
 
     if (hipMalloc(&h->d_w, kWeights32 * sizeof(float)) != hipSuccess) return bail(AEC_ERR_OOM);
     if (hipMemset(h->d_w, 0, kWeights32 * sizeof(float)) != hipSuccess) return bail(AEC_ERR_HIP);
@@ -410,22 +401,22 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
     return AEC_OK;
 }
 
+// Grow-only workspace.  Growth (a larger batch or longer streams than any
+// call before) frees buffers that kernels of earlier calls on any stream may
+// still read, so it synchronises the device; a fixed or shrinking shape never
+// does.
 static aec_status ensure_ws(aec_handle* h, int64_t B, int64_t T) {
     if (B <= h->ws_B && T <= h->ws_T) return AEC_OK;
     const int64_t nB = B > h->ws_B ? B : h->ws_B;
     const int64_t nT = T > h->ws_T ? T : h->ws_T;
     HIP_TRY(h, hipDeviceSynchronize());
-    (void)hipFree(h->d_mom); (void)hipFree(h->d_cvals); (void)hipFree(h->d_len); (void)hipFree(h->d_feats);
-    (void)hipFree(h->d_est); (void)hipFree(h->d_dbg); (void)hipFree(h->d_spec); (void)hipFree(h->d_slen);
-    h->d_mom = nullptr; h->d_cvals = nullptr; h->d_len = nullptr; h->d_feats = h->d_est = h->d_dbg = nullptr;
-    h->d_slen = nullptr;
+    (void)hipFree(h->d_mom); (void)hipFree(h->d_cvals); (void)hipFree(h->d_feats);
+    (void)hipFree(h->d_est); (void)hipFree(h->d_dbg); (void)hipFree(h->d_spec);
+    h->d_mom = nullptr; h->d_cvals = nullptr; h->d_feats = h->d_est = h->d_dbg = nullptr;
     h->d_spec = nullptr;
     h->ws_B = h->ws_T = 0;
-    h->last_lens.clear();
     HIP_TRY(h, hipMalloc(&h->d_mom, nB * 3 * kMomChunks * sizeof(double2)));
     HIP_TRY(h, hipMalloc(&h->d_cvals, nB * 3 * sizeof(float)));
-    HIP_TRY(h, hipMalloc(&h->d_len, nB * sizeof(int64_t)));
-    HIP_TRY(h, hipMalloc(&h->d_slen, nB * 4 * sizeof(int32_t)));
     HIP_TRY(h, hipMalloc(&h->d_feats, nB * nT * 96 * sizeof(float)));
     HIP_TRY(h, hipMalloc(&h->d_est, nB * nT * 32 * sizeof(float)));
     HIP_TRY(h, hipMalloc(&h->d_dbg, 2 * nB * nT * 32 * sizeof(float)));
@@ -436,60 +427,100 @@ static aec_status ensure_ws(aec_handle* h, int64_t B, int64_t T) {
 }
 
 // Host-built work lists of a batch (analysis items of 4 frames, synthesis
-// items of 15 hops) and the per-stream lengths; rebuilt only when the
-// lengths change.
+// items of 15 hops) and the per-stream lengths; rebuilt only when the lengths
+// (or whether near is given) change.  The lists go to the device in stream
+// order (one copy from a pinned staging slot): kernels of this handle's earlier
+// calls are ordered before it on the same stream, and a call on another stream
+// first waits for the last one (begin_call).  The host waits only when it
+// reuses a staging slot whose copy (two list changes ago) is still in flight,
+// or when the device block must grow.
+static size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }
+
 static aec_status prepare_lists(aec_handle* h, const int64_t* lengths3, int32_t B, int nsig_in, hipStream_t st) {
-    if (h->last_lens.size() != (size_t)B * 3 ||
-        std::memcmp(h->last_lens.data(), lengths3, (size_t)B * 3 * sizeof(int64_t)) != 0) {
-        // kernels of an earlier call (on any stream) may still read the work lists
-        HIP_TRY(h, hipDeviceSynchronize());
-        h->last_lens.assign(lengths3, lengths3 + (size_t)B * 3);
-        h->h_slen.assign((size_t)B * 4, 0);
-        std::vector<int64_t> lens(B);
-        for (int b = 0; b < B; ++b) {
-            lens[b] = lengths3[3 * b];
-            for (int sg = 0; sg < 3; ++sg) h->h_slen[4 * b + sg] = (int32_t)(sg < nsig_in ? lengths3[3 * b + sg] : lens[b]);
-        }
-        // analysis work list: 4-frame items of every stream, valid frames only
-        std::vector<WorkItem>& items = h->h_items;
-        items.clear();
-        h->item_off.assign(B + 1, 0);
-        for (int b = 0; b < B; ++b) {
-            h->item_off[b] = (int64_t)items.size();
-            const int64_t T = aec_num_frames(lens[b]);
-            for (int64_t wt = 0; wt < T; wt += 4) items.push_back({b, (int32_t)wt, lens[b]});
-        }
-        h->item_off[B] = (int64_t)items.size();
-        // synthesis work list: 15 output hops per block item
-        std::vector<WorkItem>& sitems = h->h_sitems;
-        sitems.clear();
-        h->sitem_off.assign(B + 1, 0);
-        for (int b = 0; b < B; ++b) {
-            h->sitem_off[b] = (int64_t)sitems.size();
-            const int64_t nhop = lens[b] / 256;
-            for (int64_t h0 = 0; h0 < nhop; h0 += kHopsOut) sitems.push_back({b, (int32_t)h0, lens[b]});
-        }
-        h->sitem_off[B] = (int64_t)sitems.size();
-        if ((int64_t)items.size() > h->items_cap || (int64_t)sitems.size() > h->sitems_cap) {
-            if (h->d_items) HIP_TRY(h, hipFree(h->d_items));
-            if (h->d_sitems) HIP_TRY(h, hipFree(h->d_sitems));
-            h->d_items = h->d_sitems = nullptr;
-            HIP_TRY(h, hipMalloc(&h->d_items, std::max<size_t>(1, items.size()) * sizeof(WorkItem)));
-            HIP_TRY(h, hipMalloc(&h->d_sitems, std::max<size_t>(1, sitems.size()) * sizeof(WorkItem)));
-            h->items_cap = (int64_t)items.size();
-            h->sitems_cap = (int64_t)sitems.size();
-        }
-        h->nitems = (int64_t)items.size();
-        h->nsitems = (int64_t)sitems.size();
-        if (!sitems.empty())
-            HIP_TRY(h, hipMemcpyAsync(h->d_sitems, sitems.data(), sitems.size() * sizeof(WorkItem),
-                                      hipMemcpyHostToDevice, st));
-        HIP_TRY(h, hipMemcpyAsync(h->d_len, lens.data(), B * sizeof(int64_t), hipMemcpyHostToDevice, st));
-        HIP_TRY(h, hipMemcpyAsync(h->d_slen, h->h_slen.data(), (size_t)B * 4 * sizeof(int32_t), hipMemcpyHostToDevice, st));
-        HIP_TRY(h, hipMemcpyAsync(h->d_items, items.data(), items.size() * sizeof(WorkItem), hipMemcpyHostToDevice, st));
-        // `lens` is a local: make its (pageable, possibly staged) copy complete before it goes away
-        HIP_TRY(h, hipStreamSynchronize(st));
+    if (h->last_nsig == nsig_in && h->last_lens.size() == (size_t)B * 3 &&
+        std::memcmp(h->last_lens.data(), lengths3, (size_t)B * 3 * sizeof(int64_t)) == 0)
+        return AEC_OK;
+    std::vector<int64_t> lens(B);
+    for (int b = 0; b < B; ++b) lens[b] = lengths3[3 * b];
+    // analysis work list: 4-frame items of every stream, valid frames only
+    std::vector<WorkItem>& items = h->h_items;
+    items.clear();
+    h->item_off.assign(B + 1, 0);
+    for (int b = 0; b < B; ++b) {
+        h->item_off[b] = (int64_t)items.size();
+        const int64_t T = aec_num_frames(lens[b]);
+        for (int64_t wt = 0; wt < T; wt += 4) items.push_back({b, (int32_t)wt, lens[b]});
     }
+    h->item_off[B] = (int64_t)items.size();
+    // synthesis work list: 15 output hops per block item
+    std::vector<WorkItem>& sitems = h->h_sitems;
+    sitems.clear();
+    h->sitem_off.assign(B + 1, 0);
+    for (int b = 0; b < B; ++b) {
+        h->sitem_off[b] = (int64_t)sitems.size();
+        const int64_t nhop = lens[b] / 256;
+        for (int64_t h0 = 0; h0 < nhop; h0 += kHopsOut) sitems.push_back({b, (int32_t)h0, lens[b]});
+    }
+    h->sitem_off[B] = (int64_t)sitems.size();
+    // block layout [items | sitems | len | slen], 16-B aligned pieces
+    const size_t o_si = align16(items.size() * sizeof(WorkItem));
+    const size_t o_len = o_si + align16(sitems.size() * sizeof(WorkItem));
+    const size_t o_slen = o_len + align16((size_t)B * sizeof(int64_t));
+    const size_t bytes = o_slen + align16((size_t)B * 4 * sizeof(int32_t));
+    if (bytes > h->lists_cap) {
+        // earlier kernels of this handle may read the old block: wait for the handle's last call
+        if (h->have_last) HIP_TRY(h, hipEventSynchronize(h->ev_last));
+        if (h->d_lists) HIP_TRY(h, hipFree(h->d_lists));
+        h->d_lists = nullptr;
+        h->lists_cap = 0;
+        const size_t cap = bytes + bytes / 4;
+        HIP_TRY(h, hipMalloc(&h->d_lists, cap));
+        h->lists_cap = cap;
+    }
+    aec_handle::ListSlot& sl = h->slots[h->slot_next];
+    h->slot_next ^= 1;
+    if (sl.pending) HIP_TRY(h, hipEventSynchronize(sl.ev));   // its previous upload has been read
+    sl.pending = false;
+    if (bytes > sl.cap) {
+        if (sl.host) HIP_TRY(h, hipHostFree(sl.host));
+        sl.host = nullptr;
+        sl.cap = 0;
+        HIP_TRY(h, hipHostMalloc(reinterpret_cast<void**>(&sl.host), bytes + bytes / 4));
+        sl.cap = bytes + bytes / 4;
+    }
+    std::memcpy(sl.host, items.data(), items.size() * sizeof(WorkItem));
+    std::memcpy(sl.host + o_si, sitems.data(), sitems.size() * sizeof(WorkItem));
+    std::memcpy(sl.host + o_len, lens.data(), (size_t)B * sizeof(int64_t));
+    int32_t* slen = reinterpret_cast<int32_t*>(sl.host + o_slen);
+    for (int b = 0; b < B; ++b) {
+        for (int sg = 0; sg < 3; ++sg) slen[4 * b + sg] = (int32_t)(sg < nsig_in ? lengths3[3 * b + sg] : lens[b]);
+        slen[4 * b + 3] = 0;
+    }
+    HIP_TRY(h, hipMemcpyAsync(h->d_lists, sl.host, bytes, hipMemcpyHostToDevice, st));
+    HIP_TRY(h, hipEventRecord(sl.ev, st));
+    sl.pending = true;
+    h->d_items = reinterpret_cast<WorkItem*>(h->d_lists);
+    h->d_sitems = reinterpret_cast<WorkItem*>(h->d_lists + o_si);
+    h->d_len = reinterpret_cast<int64_t*>(h->d_lists + o_len);
+    h->d_slen = reinterpret_cast<int32_t*>(h->d_lists + o_slen);
+    h->nitems = (int64_t)items.size();
+    h->nsitems = (int64_t)sitems.size();
+    h->last_lens.assign(lengths3, lengths3 + (size_t)B * 3);
+    h->last_nsig = nsig_in;
+    return AEC_OK;
+}
+
+// Every call that reads or writes the handle's workspace: ordered after the
+// handle's previous call (a device-side wait when the stream changes), and
+// recorded as the handle's last call when it has been queued.
+static aec_status begin_call(aec_handle* h, hipStream_t st) {
+    if (h->have_last && st != h->last_stream) HIP_TRY(h, hipStreamWaitEvent(st, h->ev_last, 0));
+    return AEC_OK;
+}
+static aec_status end_call(aec_handle* h, hipStream_t st) {
+    HIP_TRY(h, hipEventRecord(h->ev_last, st));
+    h->last_stream = st;
+    h->have_last = true;
     return AEC_OK;
 }
 
@@ -541,152 +572,99 @@ aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref
     // this call overwrites the features a pending aec_train_backward would read
     h->train_B = 0;
     ++h->train_gen;
-    aec_status s = ensure_ws(h, B, Tmax);
+    aec_status s = begin_call(h, st);
+    if (s != AEC_OK) return s;
+    s = ensure_ws(h, B, Tmax);
     if (s != AEC_OK) return s;
     s = prepare_lists(h, lengths3, B, nsig_in, st);
     if (s != AEC_OK) return s;
     const int nsig = near ? 3 : 2;
-    if (h->pipe && B >= h->pipe_minb && h->gru_mode == 0 && h->nlms_mode == 0) {
-        // K1 moments, then K6: every stream's whole chain in one block (aec_pipe.hip)
-        if (pipe_smem_bytes(h->sched_len) > 160 * 1024)
-            return fail(h, AEC_ERR_UNSUPPORTED, "erb schedule too long for the pipeline kernel's LDS budget");
-        if (B > h->ring_B) {
-            HIP_TRY(h, hipDeviceSynchronize());
-            if (h->d_ring) HIP_TRY(h, hipFree(h->d_ring));
-            h->d_ring = nullptr;
-            h->ring_B = 0;
-            HIP_TRY(h, hipMalloc(&h->d_ring, (size_t)B * kPipeRingRows * 256 * sizeof(float2)));
-            h->ring_B = B;
+    mark(h, st);
+    HIP_TRY(h, launch_moments(mic, ref, near, ld, h->d_slen, h->d_mom, 0, B, nsig, st));
+    HIP_TRY(h, launch_norm_finalize(h->d_mom, h->d_slen, h->d_cvals, 0, B, nsig, st));
+    if (h->cfg.nlms_taps > 0 && B <= h->small_b && h->nlms_mode == 0) {
+        // few streams: transforms frame-parallel (K2 + rows), recursion per stream, mic_erb frame-parallel
+        const size_t need = (size_t)B * Tmax * 512 + (size_t)B * 256;      // + one dummy row per stream
+        if (need > h->rows_cap) {
+            if (h->have_last) HIP_TRY(h, hipEventSynchronize(h->ev_last));
+            if (h->d_rows) HIP_TRY(h, hipFree(h->d_rows));
+            h->d_rows = nullptr;
+            h->rows_cap = 0;
+            HIP_TRY(h, hipMalloc(&h->d_rows, need * sizeof(float2)));
+            h->rows_cap = need;
         }
-        mark(h, st);
-        HIP_TRY(h, launch_moments(mic, ref, near, ld, h->d_slen, h->d_mom, 0, B, nsig, st));
-        mark(h, st);
-        PipeArgs a{};
+        AnalysisArgs a{};
         a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
-        a.ld = ld; a.lens = h->d_len; a.slen = h->d_slen; a.b0 = 0; a.nsig = nsig;
-        a.mom = h->d_mom; a.tables = reinterpret_cast<const float*>(h->d_tab);
-        a.sched = h->d_sched; a.sched_len = h->sched_len; a.bintab = h->d_bintab; a.w = h->d_w;
-        a.ring = h->d_ring; a.out = out; a.ld_out = ld_out; a.loss = loss;
+        a.ld = ld; a.items = h->d_items; a.nitems = h->nitems;
+        a.num_cus = h->num_cus; a.cvals = h->d_cvals; a.slen = h->d_slen;
+        a.tables = reinterpret_cast<const float*>(h->d_tab);
+        a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
+        a.feats = h->d_feats; a.Tmax = Tmax; a.rows = h->d_rows;
+        mark(h, st);
+        HIP_TRY(h, launch_analysis(a, st));
+        HIP_TRY(h, launch_nlms_recursion(h->d_rows, h->d_spec, h->d_len, Tmax, h->cfg.nlms_taps, h->cfg.nlms_mu,
+                                         h->cfg.nlms_beta, h->cfg.nlms_delta, 0, B, h->d_rows + (size_t)B * Tmax * 512,
+                                         st));
+        HIP_TRY(h, launch_mic_erb(h->d_spec, h->d_feats, h->d_len, Tmax, h->d_sched, h->sched_len, h->d_items,
+                                  h->nitems, st));
+    } else if (h->cfg.nlms_taps > 0) {
+        if (nlms_smem_bytes(h->sched_len, h->cfg.nlms_taps) > 160 * 1024)
+            return fail(h, AEC_ERR_UNSUPPORTED, "erb schedule too long for the NLMS kernel's LDS budget");
+        NlmsArgs a{};
+        a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
+        a.ld = ld; a.lens = h->d_len; a.slen = h->d_slen; a.b0 = 0; a.cvals = h->d_cvals;
+        a.tables = reinterpret_cast<const float*>(h->d_tab);
+        a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
+        a.feats = h->d_feats; a.Tmax = Tmax; a.spec = h->d_spec;
         a.taps = h->cfg.nlms_taps; a.mu = h->cfg.nlms_mu; a.beta = h->cfg.nlms_beta; a.delta = h->cfg.nlms_delta;
-        if (h->debug) {
-            a.feats = h->d_feats; a.est = h->d_est;
-            a.dbg_h = h->d_dbg; a.dbg_mask = h->d_dbg + (size_t)B * Tmax * 32;
-        }
-        a.Tmax = Tmax;
-        a.mode = h->pipe_mode;
-        HIP_TRY(h, launch_pipe(a, B, st));
+        a.mode = h->nlms_mode;
+        a.prio = h->nlms_prio;
+        a.erb_role = h->nlms_erb;
         mark(h, st);
+        HIP_TRY(h, launch_nlms_analysis(a, B, st));
+    } else {
+        AnalysisArgs a{};
+        a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
+        a.ld = ld; a.items = h->d_items; a.nitems = h->nitems;
+        a.num_cus = h->num_cus; a.cvals = h->d_cvals; a.slen = h->d_slen;
+        a.tables = reinterpret_cast<const float*>(h->d_tab);
+        a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
+        a.feats = h->d_feats; a.Tmax = Tmax;
         mark(h, st);
-        mark(h, st);
-        h->last_B = B;
-        h->last_T = Tmax;
-        return AEC_OK;
+        HIP_TRY(h, launch_analysis(a, st));
     }
-    const int S = std::max(1, std::min(h->sub_max, B / 32));
-    if (S > 1) HIP_TRY(h, hipEventRecord(h->ev_start, st));
-    for (int k = 0; k < S; ++k) {
-        const int b0 = (int)((int64_t)B * k / S), b1 = (int)((int64_t)B * (k + 1) / S);
-        hipStream_t ks = S > 1 ? h->sst[k] : st;
-        if (S > 1) {
-            HIP_TRY(h, hipStreamWaitEvent(ks, h->ev_start, 0));
-            if (k > 0) HIP_TRY(h, hipStreamWaitEvent(ks, h->ev_ana[k - 1], 0));
-        }
-        mark(h, ks);
-        HIP_TRY(h, launch_moments(mic, ref, near, ld, h->d_slen, h->d_mom, b0, b1 - b0, nsig, ks));
-        HIP_TRY(h, launch_norm_finalize(h->d_mom, h->d_slen, h->d_cvals, b0, b1, nsig, ks));
+    mark(h, st);
 
-        if (h->cfg.nlms_taps > 0 && B <= h->small_b && h->nlms_mode == 0) {
-            // few streams: transforms frame-parallel (K2 + rows), recursion per stream, mic_erb frame-parallel
-            const size_t need = (size_t)B * Tmax * 512 + (size_t)B * 256;      // + one dummy row per stream
-            if (need > h->rows_cap) {
-                HIP_TRY(h, hipStreamSynchronize(ks));
-                if (h->d_rows) HIP_TRY(h, hipFree(h->d_rows));
-                h->d_rows = nullptr;
-                h->rows_cap = 0;
-                HIP_TRY(h, hipMalloc(&h->d_rows, need * sizeof(float2)));
-                h->rows_cap = need;
-            }
-            AnalysisArgs a{};
-            a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
-            a.ld = ld; a.items = h->d_items + h->item_off[b0]; a.nitems = h->item_off[b1] - h->item_off[b0];
-            a.num_cus = h->num_cus; a.cvals = h->d_cvals; a.slen = h->d_slen;
-            a.tables = reinterpret_cast<const float*>(h->d_tab);
-            a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
-            a.feats = h->d_feats; a.Tmax = Tmax; a.rows = h->d_rows;
-            mark(h, ks);
-            HIP_TRY(h, launch_analysis(a, ks));
-            HIP_TRY(h, launch_nlms_recursion(h->d_rows, h->d_spec, h->d_len, Tmax, h->cfg.nlms_taps, h->cfg.nlms_mu,
-                                             h->cfg.nlms_beta, h->cfg.nlms_delta, b0, b1 - b0,
-                                             h->d_rows + (size_t)B * Tmax * 512, ks));
-            HIP_TRY(h, launch_mic_erb(h->d_spec, h->d_feats, h->d_len, Tmax, h->d_sched, h->sched_len,
-                                      h->d_items + h->item_off[b0], h->item_off[b1] - h->item_off[b0], ks));
-        } else if (h->cfg.nlms_taps > 0) {
-            if (nlms_smem_bytes(h->sched_len, h->cfg.nlms_taps) > 160 * 1024)
-                return fail(h, AEC_ERR_UNSUPPORTED, "erb schedule too long for the NLMS kernel's LDS budget");
-            NlmsArgs a{};
-            a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
-            a.ld = ld; a.lens = h->d_len; a.slen = h->d_slen; a.b0 = b0; a.cvals = h->d_cvals;
-            a.tables = reinterpret_cast<const float*>(h->d_tab);
-            a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
-            a.feats = h->d_feats; a.Tmax = Tmax; a.spec = h->d_spec;
-            a.taps = h->cfg.nlms_taps; a.mu = h->cfg.nlms_mu; a.beta = h->cfg.nlms_beta; a.delta = h->cfg.nlms_delta;
-            a.mode = h->nlms_mode;
-            a.prio = h->nlms_prio;
-            a.erb_role = h->nlms_erb;
-            mark(h, ks);
-            if (h->nlms16 && nlms16_supported(a.taps, a.sched_len))
-                HIP_TRY(h, launch_nlms16(a, b1 - b0, ks));
-            else
-                HIP_TRY(h, launch_nlms_analysis(a, b1 - b0, ks));
-        } else {
-            AnalysisArgs a{};
-            a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
-            a.ld = ld; a.items = h->d_items + h->item_off[b0]; a.nitems = h->item_off[b1] - h->item_off[b0];
-            a.num_cus = h->num_cus; a.cvals = h->d_cvals; a.slen = h->d_slen;
-            a.tables = reinterpret_cast<const float*>(h->d_tab);
-            a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
-            a.feats = h->d_feats; a.Tmax = Tmax;
-            mark(h, ks);
-            HIP_TRY(h, launch_analysis(a, ks));
-        }
-        mark(h, ks);
-        if (S > 1) HIP_TRY(h, hipEventRecord(h->ev_ana[k], ks));
+    GruArgs g{};
+    g.feats = h->d_feats; g.Tmax = Tmax; g.lens = h->d_len; g.w = h->d_w;
+    g.est = h->d_est; g.loss = loss; g.has_near = near != nullptr;
+    g.dbg_h = h->debug ? h->d_dbg : nullptr;
+    g.dbg_mask = h->debug ? h->d_dbg + B * Tmax * 32 : nullptr;
+    g.mode = h->gru_mode;
+    g.b0 = 0;
 
-        GruArgs g{};
-        g.feats = h->d_feats; g.Tmax = Tmax; g.lens = h->d_len; g.w = h->d_w;
-        g.est = h->d_est; g.loss = loss; g.has_near = near != nullptr;
-        g.dbg_h = h->debug ? h->d_dbg : nullptr;
-        g.dbg_mask = h->debug ? h->d_dbg + B * Tmax * 32 : nullptr;
-        g.mode = h->gru_mode;
-        g.b0 = b0;
-
-        SynthArgs y{};
-        y.mic = mic; y.ld = ld; y.items = h->d_sitems + h->sitem_off[b0];
-        y.nitems = h->sitem_off[b1] - h->sitem_off[b0]; y.num_cus = h->num_cus;
-        y.cvals = h->d_cvals;
-        y.tables = reinterpret_cast<const float*>(h->d_tab);
-        y.bintab = h->d_bintab; y.est = h->d_est; y.Tmax = Tmax;
-        y.out = out; y.ld_out = ld_out;
-        y.spec = h->cfg.nlms_taps > 0 ? h->d_spec : nullptr;
-        y.fmode = h->fused_mode;
-        if (y.spec && h->fused && h->gru_mode == 0) {
-            // one kernel: the synthesis runs two chunks behind the recurrence
-            HIP_TRY(h, launch_gru_synth(g, y, b1 - b0, ks));
-            mark(h, ks);
-            mark(h, ks);
-        } else {
-            HIP_TRY(h, launch_gru(g, b1 - b0, ks));
-            mark(h, ks);
-            HIP_TRY(h, launch_synthesis(y, ks));
-            mark(h, ks);
-        }
-        if (S > 1) HIP_TRY(h, hipEventRecord(h->ev_done[k], ks));
+    SynthArgs y{};
+    y.mic = mic; y.ld = ld; y.items = h->d_sitems; y.nitems = h->nsitems; y.num_cus = h->num_cus;
+    y.cvals = h->d_cvals;
+    y.tables = reinterpret_cast<const float*>(h->d_tab);
+    y.bintab = h->d_bintab; y.est = h->d_est; y.Tmax = Tmax;
+    y.out = out; y.ld_out = ld_out;
+    y.spec = h->cfg.nlms_taps > 0 ? h->d_spec : nullptr;
+    y.fmode = h->fused_mode;
+    if (y.spec && h->fused && h->gru_mode == 0) {
+        // one kernel: the synthesis runs two chunks behind the recurrence
+        HIP_TRY(h, launch_gru_synth(g, y, B, st));
+        mark(h, st);
+        mark(h, st);
+    } else {
+        HIP_TRY(h, launch_gru(g, B, st));
+        mark(h, st);
+        HIP_TRY(h, launch_synthesis(y, st));
+        mark(h, st);
     }
-    if (S > 1)
-        for (int k = 0; k < S; ++k) HIP_TRY(h, hipStreamWaitEvent(st, h->ev_done[k], 0));
     h->last_B = B;
     h->last_T = Tmax;
-    return AEC_OK;
+    return end_call(h, st);
 }
 
 aec_status aec_debug_copy(aec_handle* h, int32_t what, float* dst, size_t n, void* stream) {
@@ -820,10 +798,14 @@ aec_status aec_set_weights_device(aec_handle* h, const float* w, size_t n, void*
     if (!h) return AEC_ERR_INVALID_ARG;
     if (!w || n != kWeights32) return fail(h, AEC_ERR_INVALID_ARG, "weights blob must hold 12544 floats");
     AEC_ON_DEVICE(h);
-    HIP_TRY(h, hipMemcpyAsync(h->d_w, w, n * sizeof(float), hipMemcpyDeviceToDevice,
-                              reinterpret_cast<hipStream_t>(stream)));
+    // stream-ordered after the handle's last call (on whichever stream it ran), which may still
+    // read the old blob; kernels of this call's stream that follow see the new one
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    aec_status s = begin_call(h, st);
+    if (s != AEC_OK) return s;
+    HIP_TRY(h, hipMemcpyAsync(h->d_w, w, n * sizeof(float), hipMemcpyDeviceToDevice, st));
     h->have_w = true;
-    return AEC_OK;
+    return end_call(h, st);
 }
 
 aec_status aec_train_forward(aec_handle* h, const float* mic, const float* ref, const float* near, int64_t n,
@@ -839,7 +821,9 @@ aec_status aec_train_forward(aec_handle* h, const float* mic, const float* ref, 
     const int64_t T = aec_num_frames(n);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     AEC_ON_DEVICE(h);
-    aec_status s = ensure_ws(h, B, T);
+    aec_status s = begin_call(h, st);
+    if (s != AEC_OK) return s;
+    s = ensure_ws(h, B, T);
     if (s != AEC_OK) return s;
     const int64_t frames = (int64_t)B * T;
     const int nblk = train_wgrad_blocks(B, (int)T, h->num_cus);
@@ -895,7 +879,7 @@ aec_status aec_train_forward(aec_handle* h, const float* mic, const float* ref, 
     h->train_B = B;
     h->train_T = (int32_t)T;
     ++h->train_gen;
-    return AEC_OK;
+    return end_call(h, st);
 }
 
 int64_t aec_train_generation(const aec_handle* h) { return h ? h->train_gen : -1; }
@@ -926,8 +910,11 @@ aec_status aec_train_backward(aec_handle* h, const float* grad_loss, float* grad
         t.scan_q = h->d_scan + (size_t)t.B * nc * 1024;
         t.scan_g = t.scan_q + (size_t)t.B * nc * 32;
     }
-    HIP_TRY(h, launch_train_backward(t, nblk, grad_loss, grad, reinterpret_cast<hipStream_t>(stream)));
-    return AEC_OK;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    aec_status s = begin_call(h, st);
+    if (s != AEC_OK) return s;
+    HIP_TRY(h, launch_train_backward(t, nblk, grad_loss, grad, st));
+    return end_call(h, st);
 }
 
 aec_status aec_adam_step(aec_handle* h, float* params, const float* grad, float* exp_avg, float* exp_avg_sq,
@@ -981,17 +968,18 @@ aec_status aec_adam_step_multi(aec_handle* h, float* const* params, const float*
 void aec_destroy(aec_handle* h) {
     if (!h) return;
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
-    for (int k = 0; k < aec_handle::kMaxSub; ++k) {
-        if (h->sst[k]) (void)hipStreamDestroy(h->sst[k]);
-        if (h->ev_ana[k]) (void)hipEventDestroy(h->ev_ana[k]);
-        if (h->ev_done[k]) (void)hipEventDestroy(h->ev_done[k]);
-    }
-    if (h->ev_start) (void)hipEventDestroy(h->ev_start);
     DeviceGuard dg(h->device);
+    if (h->have_last) (void)hipEventSynchronize(h->ev_last);
+    if (h->ev_last) (void)hipEventDestroy(h->ev_last);
+    for (auto& sl : h->slots) {
+        if (sl.pending) (void)hipEventSynchronize(sl.ev);
+        if (sl.ev) (void)hipEventDestroy(sl.ev);
+        if (sl.host) (void)hipHostFree(sl.host);
+    }
     (void)hipFree(h->d_w); (void)hipFree(h->d_tab); (void)hipFree(h->d_sched); (void)hipFree(h->d_bintab);
-    (void)hipFree(h->d_mom); (void)hipFree(h->d_cvals); (void)hipFree(h->d_items); (void)hipFree(h->d_sitems); (void)hipFree(h->d_len);
+    (void)hipFree(h->d_mom); (void)hipFree(h->d_cvals); (void)hipFree(h->d_lists);
     (void)hipFree(h->d_feats); (void)hipFree(h->d_est); (void)hipFree(h->d_dbg); (void)hipFree(h->d_spec);
-    (void)hipFree(h->d_state); (void)hipFree(h->d_rows); (void)hipFree(h->d_slen); (void)hipFree(h->d_ring);
+    (void)hipFree(h->d_state); (void)hipFree(h->d_rows);
     (void)hipFree(h->d_th); (void)hipFree(h->d_tloss); (void)hipFree(h->d_rec); (void)hipFree(h->d_dg);
     (void)hipFree(h->d_part); (void)hipFree(h->d_scan);
     delete h;

@@ -124,41 +124,6 @@ struct StreamStepArgs {
     float mu, beta, delta;
 };
 
-// K6 fused per-stream pipeline (aec_pipe.hip): STFT -> [FD-NLMS] -> ERB ->
-// GRU -> head -> synthesis -> overlap-add of one stream per block.
-struct PipeArgs {
-    const float* sig[3];     // mic, ref, near [B][ld]
-    int64_t ld;
-    const int64_t* lens;     // [B] mic length: frame count, output length
-    const int32_t* slen;     // [B][4] per-signal lengths (mic, ref, near, -)
-    int b0;                  // first stream of this launch (block i runs stream b0 + i)
-    int nsig;                // 3 with near (loss), else 2
-    const double2* mom;      // [B][3][kMomChunks] normaliser partials (moments_kernel)
-    const float* tables;     // DevTables
-    const float* sched;      // ERB forward schedule
-    int sched_len;
-    const float* bintab;     // ERB transpose table float4[257]
-    const float* w;          // weights blob (state_dict order)
-    float2* ring;            // [B][kPipeRingRows][256] error-spectrum ring (L2-resident hand-off)
-    float* out;
-    int64_t ld_out;
-    float* loss;             // [B] or null
-    int taps;
-    float mu, beta, delta;
-    // debug intermediates (aec_set_debug): null unless enabled
-    float* feats;            // [B][Tmax][96] mic_erb | ref_erb | near_erb
-    float* est;              // [B][Tmax][32]
-    float* dbg_h;            // [B][Tmax][32]
-    float* dbg_mask;         // [B][Tmax][32]
-    int64_t Tmax;
-    int mode;                // timing experiments only (AEC_PIPE_MODE; results invalid unless 0): bits skip
-                             // a role's work: 1 GRU, 2 SY + OLA, 4 HD, 8 NL, 16 MIC + mic_erb, 32 REF, 64 gi, 128 NEAR
-};
-constexpr int kPipeFrames = 8;                       // frames per pipeline tick
-constexpr int kPipeRingRows = 4 * kPipeFrames;       // E rows kept per stream (4 chunks)
-size_t pipe_smem_bytes(int sched_len);
-hipError_t launch_pipe(const PipeArgs& a, int nb, hipStream_t st);
-
 // dynamic LDS bytes (must match the carve in the kernels)
 inline size_t analysis_smem_bytes(int sched_len) {
     return (size_t)sched_len * 16 * 16 + 32 * 8 + (258 * 2 + 256 * 2 + 512 + (size_t)kFPB * kGroupFloats) * 4;
@@ -180,10 +145,6 @@ hipError_t launch_norm_finalize(const double2* mom, const int32_t* slen, float* 
                                 hipStream_t st);
 hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t st);
 hipError_t launch_nlms_analysis(const NlmsArgs& a, int nb, hipStream_t st);
-// the 16-wave form (aec_nlms16.hip): one transform and one ERB pass per
-// transform wave and tick; taps 1..4, schedule length <= 48
-bool nlms16_supported(int taps, int sched_len);
-hipError_t launch_nlms16(const NlmsArgs& a, int nb, hipStream_t st);
 // small-batch NLMS path (few streams: the per-stream K2n block would leave the
 // chip idle): K2 with spectrum rows, then the recursion per (stream, bin) and
 // the mic_erb pass over all frames

@@ -107,11 +107,13 @@ struct aec_crn_handle {
     std::vector<int64_t> proc_lens;                //   and its lengths
     std::vector<void*> allocs;
     StreamState* ss = nullptr;                     // aec_crn_stream_* state
-    // persistent LSTM recurrence (crn_persist.hip; AEC_CRN_PERSIST=0: one launch per frame, 1 / 2: kernel version)
-    int persist = 2;
+    // persistent LSTM recurrence (crn_persist.hip; AEC_CRN_PERSIST=0: one launch per frame)
+    int persist = 1;
     int num_cus = 0;
     int* psync = nullptr;                          // arrival counters + error word
-    int* perr_host = nullptr;                      // pinned copy of the error word
+    int* perr_host = nullptr;                      // pinned copy of the error word, read back per call
+    hipEvent_t perr_ev = nullptr;                  // recorded after that copy
+    bool persist_pending = false;                  // this call launched persistent grids: check before returning
     // profiling
     int profile = 0;
     std::vector<hipEvent_t> ev;
@@ -795,14 +797,18 @@ static std::mutex g_persist_mu;
 static hipEvent_t g_persist_ev[64] = {};
 
 static aec_status run_persist(aec_crn_handle* h, int l, int32_t B, int64_t Tmax, hipStream_t st) {
-    if (h->perr_host && *h->perr_host) {
-        h->persist = 0;
-        return crn_fail(h, AEC_ERR_HIP, "persistent LSTM recurrence timed out waiting for its team (disabled)");
-    }
     std::lock_guard<std::mutex> lk(g_persist_mu);
     hipEvent_t& ev = g_persist_ev[h->device & 63];
     if (!ev) CRN_TRY(h, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     CRN_TRY(h, hipStreamWaitEvent(st, ev, 0));
+    if (!h->persist_pending) {   // first persistent launch of this call: clear the error word
+        CRN_TRY(h, hipMemsetAsync(h->psync + crn::kPersistErr, 0, sizeof(int), st));
+        h->persist_pending = true;
+    }
+    // polls before a wave gives up; AEC_CRN_SPIN_LIMIT (read per call) forces a timeout in the tests
+    const char* sl = getenv("AEC_CRN_SPIN_LIMIT");
+    const int spin = sl ? std::max(1, atoi(sl)) : crn::kPersistSpinLimit;
+    static const int pra = [] { const char* v = getenv("CRN_PERSIST_RA"); return v ? atoi(v) : 1; }();
     // one block per CU: 64 streams (two teams of 32 blocks) per 64 CUs, at most 256 streams per launch
     const int32_t chunk = 64 * std::min(4, h->num_cus / 64);
     for (int32_t b0 = 0; b0 < B; b0 += chunk) {
@@ -817,43 +823,36 @@ static aec_status run_persist(aec_crn_handle* h, int l, int32_t B, int64_t Tmax,
         a.nb = nb;
         a.T = (int)Tmax;
         a.G = (nb + 63) / 64;
-        a.spin_limit = 1 << 22;
-        static const int pmode = [] { const char* v = getenv("CRN_PERSIST_MODE"); return v ? atoi(v) : 0; }();
-        a.mode = pmode;
-        static const int pra = [] { const char* v = getenv("CRN_PERSIST_RA"); return v ? atoi(v) : 1; }();
+        a.spin_limit = spin;
         a.read_ahead = pra;
-        CRN_TRY(h, hipMemsetAsync(h->psync, 0, crn::kPersistSyncInts * sizeof(int), st));
-        static const bool dbg = getenv("CRN_PERSIST_DBG") != nullptr;
-        long long* dd = nullptr;
-        if (dbg && Tmax > 301) {
-            CRN_TRY(h, hipMalloc(reinterpret_cast<void**>(&dd), 256 * 4 * 2 * 24 * sizeof(long long)));
-            CRN_TRY(h, hipMemsetAsync(dd, 0, 256 * 4 * 2 * 24 * sizeof(long long), st));
-            a.dbg = dd;
-        }
-        CRN_TRY(h, crn::launch_lstm_persist(a, h->persist, st));
-        if (dd) {   // per event: mean ticks since the phase start over blocks and waves
-            std::vector<long long> v(256 * 4 * 2 * 24);
-            CRN_TRY(h, hipMemcpyAsync(v.data(), dd, v.size() * sizeof(long long), hipMemcpyDeviceToHost, st));
-            CRN_TRY(h, hipStreamSynchronize(st));
-            (void)hipFree(dd);
-            for (int hm = 0; hm < 2; ++hm) {
-                double sum[24] = {};
-                int n = 0;
-                for (int b = 0; b < 64 * a.G; ++b)
-                    for (int w = 0; w < 4; ++w) {
-                        const long long* e = &v[((b * 4 + w) * 2 + hm) * 24];
-                        if (!e[0] || !e[18]) continue;
-                        for (int k = 1; k < 19; ++k) sum[k] += (double)(e[k] - e[0]);
-                        ++n;
-                    }
-                fprintf(stderr, "persist2 dbg H%d n=%d poll %.0f", hm, n, sum[1] / n);
-                for (int k = 0; k < 8; ++k) fprintf(stderr, " | c%d %.0f %.0f", k, sum[2 + 2 * k] / n, sum[3 + 2 * k] / n);
-                fprintf(stderr, " | end %.0f\n", sum[18] / n);
-            }
-        }
-        CRN_TRY(h, hipMemcpyAsync(h->perr_host, h->psync + crn::kPersistErr, sizeof(int), hipMemcpyDeviceToHost, st));
+        // arrival counters only: the error word keeps any timeout of this call's earlier launches
+        CRN_TRY(h, hipMemsetAsync(h->psync, 0, crn::kPersistCounters * sizeof(int), st));
+        CRN_TRY(h, crn::launch_lstm_persist(a, st));
     }
     CRN_TRY(h, hipEventRecord(ev, st));
+    return AEC_OK;
+}
+
+// After the last persistent launch of a call: copy the error word to the host
+// (stream-ordered, right behind the LSTM stage) and record an event; before
+// the call returns, the host waits for that event (persist_wait), so a
+// timed-out grid fails the call that launched it.  The host then waits only
+// until the LSTM stage has run: the decoder and back kernels are already
+// queued behind it.
+static aec_status persist_copy(aec_crn_handle* h, hipStream_t st) {
+    if (!h->persist_pending) return AEC_OK;
+    CRN_TRY(h, hipMemcpyAsync(h->perr_host, h->psync + crn::kPersistErr, sizeof(int), hipMemcpyDeviceToHost, st));
+    CRN_TRY(h, hipEventRecord(h->perr_ev, st));
+    return AEC_OK;
+}
+
+static aec_status persist_wait(aec_crn_handle* h) {
+    if (!h->persist_pending) return AEC_OK;
+    h->persist_pending = false;
+    CRN_TRY(h, hipEventSynchronize(h->perr_ev));
+    if (*h->perr_host)
+        return crn_fail(h, AEC_ERR_HIP,
+                        "persistent LSTM recurrence: a block timed out waiting for its team (outputs invalid)");
     return AEC_OK;
 }
 
@@ -900,6 +899,8 @@ static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int
         s = run_lstm_combine<T>(h, bf, l, h->y, BT, st);
         if (s != AEC_OK) return s;
     }
+    s = persist_copy(h, st);
+    if (s != AEC_OK) return s;
     mark(h, st);
     s = run_decoder<T>(h, bf, BT, st);
     if (s != AEC_OK) return s;
@@ -1034,7 +1035,7 @@ aec_status aec_crn_create(const aec_crn_config* cfg, const float* params, size_t
     aec::DevTables tab;
     aec::build_dev_tables(tab);
     if (hipMemcpy(h->d_tab, &tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess) return bail(AEC_ERR_HIP);
-    if (const char* v = getenv("AEC_CRN_PERSIST")) h->persist = atoi(v);
+    if (const char* v = getenv("AEC_CRN_PERSIST")) h->persist = atoi(v) != 0;
     if (hipDeviceGetAttribute(&h->num_cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) h->num_cus = 0;
     if (h->es == 2 && crn::persist_supported(h->H, h->CELLS, h->S, h->num_cus)) {
         // team arrival counters + error word, and a pinned copy of the error word
@@ -1042,6 +1043,7 @@ aec_status aec_crn_create(const aec_crn_config* cfg, const float* params, size_t
             return bail(AEC_ERR_OOM);
         if (hipHostMalloc(reinterpret_cast<void**>(&h->perr_host), sizeof(int)) != hipSuccess) return bail(AEC_ERR_OOM);
         *h->perr_host = 0;
+        if (hipEventCreateWithFlags(&h->perr_ev, hipEventDisableTiming) != hipSuccess) return bail(AEC_ERR_HIP);
     }
     h->enc.assign(h->L, Packed{});
     h->dec.assign(2 * h->L, Packed{});
@@ -1105,8 +1107,14 @@ aec_status aec_crn_process(aec_crn_handle* h, const float* mic, const float* far
     for (int b = 0; b < B; ++b) mx = std::max(mx, 256 * (lengths[b] / 256));
     if (out && ld_out < mx) return crn_fail(h, AEC_ERR_INVALID_ARG, "ld_out too small");
     if (h->profile) h->ev_used = 0;
+    h->persist_pending = false;
     s = h->es == 4 ? run<float>(h, mic, far, B, ld, Tmax, out, ld_out, spec, mask, st)
                    : run<bf16_t>(h, mic, far, B, ld, Tmax, out, ld_out, spec, mask, st);
+    if (s != AEC_OK) {
+        h->persist_pending = false;
+        return s;
+    }
+    s = persist_wait(h);                        // a persistent-grid timeout fails this call
     if (s != AEC_OK) return s;
     h->last_B = B;
     h->last_T = Tmax;
@@ -1311,6 +1319,7 @@ void aec_crn_destroy(aec_crn_handle* h) {
             if (pk.wsc) (void)hipFree(pk.wsc);
         }
     if (h->d_tab) (void)hipFree(h->d_tab);
+    if (h->perr_ev) (void)hipEventDestroy(h->perr_ev);
     if (h->psync) (void)hipFree(h->psync);
     if (h->perr_host) (void)hipHostFree(h->perr_host);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);

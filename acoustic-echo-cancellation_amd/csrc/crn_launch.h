@@ -153,26 +153,24 @@ struct PersistArgs {
     const bf16_t* whh;          // packed W_hh [CELLS*4H][H]
     const bf16_t* gx;           // [T][B][S][CELLS*4H] (frame f = t*B + b)
     bf16_t* y;                  // [T][B][CELLS][S][H]: the layer output and the h hand-off
-    int* sync;                  // kPersistSyncInts ints zeroed per launch: arrival counters (one 64-B
-                                // line each: [team] in v1, [team][half] in v2), error word at kPersistErr
+    int* sync;                  // arrival counters (one 64-B line each, [team][half]; kPersistCounters
+                                // ints, zeroed per launch), then the error word at kPersistErr (cleared
+                                // once per aec_crn_process, set by a wave whose poll timed out)
     int32_t B;                  // streams of the batch (frame row stride)
     int32_t b0, nb;             // this launch's streams b0 .. b0 + nb - 1 (nb <= 256)
     int32_t T;
     int32_t G;                  // row groups (1..4)
-    int32_t spin_limit;         // polls before a block gives up (error word set)
-    int32_t mode = 0;           // timing experiments only (CRN_PERSIST_MODE; results invalid unless 0):
-                                // bit0 h loads out of range (zeros), bit1 no MFMA phase, bit2 no team wait,
-                                // bit3 no h stores, bit4 Gx loads out of range, bit5 no cell update
-    long long* dbg = nullptr;   // version 2 timing probe (CRN_PERSIST_DBG): [block][wave][2 phases][24 events]
-    int32_t read_ahead = 1;     // version 2: read the next phase's counter at chunk 7 (CRN_PERSIST_RA, A/B)
+    int32_t spin_limit;         // polls before a wave gives up (error word set)
+    int32_t read_ahead = 1;     // read the next phase's counter at chunk 7 (CRN_PERSIST_RA, A/B)
 };
-constexpr int kPersistErr = 8 * 2 * 16;          // error word (after 8 teams x 2 halves of counters)
+constexpr int kPersistCounters = 8 * 2 * 16;     // 8 teams x 2 halves, one 64-B line each
+constexpr int kPersistErr = kPersistCounters;    // error word
 constexpr int kPersistSyncInts = kPersistErr + 16;
+constexpr int kPersistSpinLimit = 1 << 22;       // default polls before a wave gives up (AEC_CRN_SPIN_LIMIT)
 bool persist_supported(int H, int cells, int seqs, int num_cus);
-// version 1: one phase per frame (gates GEMM, then cell update and hand-off);
-// version 2: the team's rows in two halves whose phases alternate, so each
-// half's cell update and hand-off run under the other half's MFMAs
-hipError_t launch_lstm_persist(const PersistArgs& a, int version, hipStream_t st);
+// the team's rows in two halves whose phases alternate, so each half's cell
+// update and hand-off run under the other half's MFMAs
+hipError_t launch_lstm_persist(const PersistArgs& a, hipStream_t st);
 
 // tile width the host must pad the weight rows (N) to for a GEMM of N columns
 inline int gemm_bn(int N) { return N <= 16 ? 16 : N <= 32 ? 32 : N <= 64 ? 64 : 128; }

@@ -65,6 +65,13 @@ def path_flops(pipeline):
     return PIPE['flops'] + (SURVEY_NLMS_FLOPS if pipeline == 'full' else 0)
 
 
+# The driver contract: `value` is the whole job's throughput (all ranks' frames / the
+# max-over-ranks time), from which the driver computes the scaling efficiency itself;
+# BASELINE's metric is per GPU, which is `value_per_gpu` (= value / n_gpus).
+VALUE_SEMANTICS = ('value = aggregate frames/s of all ranks (frames of every rank / max-over-ranks time); '
+                   'value_per_gpu = value / n_gpus (the metric\'s per-GPU figure)')
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -84,7 +91,8 @@ def parse():
     ap.add_argument('--crn-nlms', action='store_true',
                     help='--pipeline crn: feed the DCCRN the FD-NLMS error spectrum (C5, include/aec_crn.h)')
     ap.add_argument('--no-rtf', action='store_true', help='skip the batch-1 latency probe (profiling runs)')
-    ap.add_argument('--sweep', action='store_true', help='also report a batch sweep')
+    ap.add_argument('--no-sweep', action='store_true',
+                    help='skip the batch sweep (B = 1 ... 4096 streams, 3 calls each, after the timed region)')
     ap.add_argument('--inflight', type=int, default=2,
                     help='batches in flight (HIP streams, one handle each; 1 = strictly sequential)')
     ap.add_argument('--no-c3', action='store_true', help='skip the BASELINE config 3 (DCCRN bf16) figure')
@@ -523,6 +531,8 @@ def main_crn(args):
                        'frame': '256-sample hop', 'pipeline': 'crn', 'batches_in_flight': r['batches_in_flight'],
                        'parallelism': f'streams sharded, {world} rank(s)'},
             'value_per_gpu': r['value_per_gpu'],
+            'aggregate_frames_per_s': r['value'],
+            'value_semantics': VALUE_SEMANTICS,
             'xRT': round(r['value'] * 256 / 16000, 1),
         }
         line.update({k: r[k] for k in ('rtf_batch1', 'stage_ms_per_step', 'roofline', 'pipeline_roofline',
@@ -620,7 +630,9 @@ def main():
             lat.append(time.perf_counter() - t1)
         rtf1 = float(np.median(lat)) / args.seconds if lat else None
         sweep = None
-        if args.sweep and rank == 0:
+        if not args.no_sweep and world == 1:
+            # frames/s at B concurrent streams per call (one batch in flight, 3 synchronous calls
+            # after one warm-up); the drop-in's own operating point is B = 1 (test.py:139)
             sweep = {}
             for bb in [1, 16, 64, 256, 1024, 4096]:
                 if bb > B:
@@ -633,7 +645,9 @@ def main():
                 for _ in range(3):
                     net.forward_ragged(mm, rr, nn_, erb, [n] * bb)
                 torch.cuda.synchronize(dev)
-                sweep[bb] = round(bb * T * 3 / (time.perf_counter() - t1), 1)
+                sweep[str(bb)] = round(bb * T * 3 / (time.perf_counter() - t1), 1)
+                del mm, rr, nn_
+            torch.cuda.empty_cache()
 
     frames_total = world * B * T * args.steps
     value = frames_total / el
@@ -643,13 +657,7 @@ def main():
     calls_per_step = max(calls, 1) / prof_steps
     per_kernel_ms = {k: kms[i] / prof_steps for i, k in enumerate(KERNELS)}
     per_launch_ms = {k: kms[i] / max(calls, 1) for i, k in enumerate(KERNELS)}
-    pipe = os.environ.get('AEC_PIPE', '0') not in ('', '0')
-    if pipe:
-        # K1 moments + K6 (aec_pipe.hip): the whole chain in one launch, timed in the 'analysis' slot
-        kernels_per_call = ['moments_kernel', 'pipe_kernel']
-        for d in (per_kernel_ms, per_launch_ms):
-            d['pipe'] = d.pop('analysis') + d.pop('gru') + d.pop('synthesis')
-    elif args.pipeline == 'full' and os.environ.get('AEC_FUSED_SYNTH', '1') != '0':
+    if args.pipeline == 'full' and os.environ.get('AEC_FUSED_SYNTH', '1') != '0':
         # one fused launch: its time is in the 'gru' slot, the 'synthesis' slot is an empty interval
         kernels_per_call = ['moments_kernel', 'norm_finalize_kernel', 'nlms_analysis_kernel', 'gru_synth_kernel']
         for d in (per_kernel_ms, per_launch_ms):
@@ -672,12 +680,12 @@ def main():
     c3 = None
     if world == 1 and not args.no_c3:
         # BASELINE config 3 (DCCRN bf16, 256 x 10 s) in the same driver-timed run
-        c3 = run_crn(args, dev, rank, world, 'bf16', args.c3_steps, 2, 256, 160000, False)
+        c3 = run_crn(args, dev, rank, world, 'bf16', args.c3_steps, 2, 256, 160000, not args.no_cpu)
         c3 = dict(workload=crn_workload(args, 'bf16', 256), dtype='bf16', steps=args.c3_steps,
                   batches_in_flight=c3['batches_in_flight'],
                   frames_per_s=c3['value'], ms_per_step=c3['ms_per_step'], rtf_batch1=c3['rtf_batch1'],
                   stage_ms_per_step=c3['stage_ms_per_step'], roofline=c3['roofline'],
-                  pipeline_roofline=c3['pipeline_roofline'])
+                  pipeline_roofline=c3['pipeline_roofline'], erle=c3['erle'], cpu_baseline=c3['cpu_baseline'])
     c5 = None
     if world == 1 and not args.no_c3:
         # C5: the same network fed by the FD-NLMS error spectrum (NLMS -> CRN composition)
@@ -718,6 +726,8 @@ def main():
                        'frame': '256-sample hop', 'pipeline': args.pipeline, 'batches_in_flight': inflight,
                        'parallelism': f'streams sharded, {world} rank(s)'},
             'value_per_gpu': round(value / world, 1),
+            'aggregate_frames_per_s': round(value, 1),
+            'value_semantics': VALUE_SEMANTICS,
             'xRT': round(value * 256 / 16000, 1),
             'rtf_batch1': rtf1,
             'kernel_ms_per_step': {k: round(v, 4) for k, v in per_kernel_ms.items()},

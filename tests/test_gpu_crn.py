@@ -6,13 +6,19 @@ Tolerances (relative RMS, written here):
 * f32 path (exact f32 MFMA): out_wav, out_spec, mask, near_specs <= 1e-4
   (observed float32-reference vs float64-oracle: ~6e-7);
 * bf16 path (bf16 storage / MFMA, f32 accumulate): out_wav <= BF16_WAV_TOL,
-  mask <= BF16_MASK_TOL (reduced precision; the f32 path is the parity gate);
+  mask <= BF16_MASK_TOL (reduced precision; the f32 path is the parity gate;
+  observed out_wav relative RMS vs the reference 0.0018-0.0034 on the
+  goldens, so the bar is ~3x the observed error);
 * fp8 path (bf16 + MX-fp8 GEMMs for the LSTM input projections and the
   wide conv layers, encoder 4-5 / decoder levels 5-6: e4m3 weights and
   activations, E8M0 scale per 32 k): out_wav <= FP8_WAV_TOL, mask <=
   FP8_MASK_TOL against the reference, and within FP8_VS_BF16_TOL of the bf16
   path (the only change is those GEMMs' operand rounding; observed out_wav
-  relative RMS vs the reference 0.0035-0.0045 against bf16's 0.0024-0.0034);
+  relative RMS vs the reference 0.0025-0.0045);
+* BASELINE config 3's own shape (256 x 10 s in one call, 626-frame
+  recurrence): three rows against the reference op mix (oracle/torch_crn_port,
+  f32, pinned by tests/test_crn_oracle.py) within the same bars, and ERLE
+  within C3_ERLE_DB of it;
 * integer framing (T, output length) bit-exact; batch composition (ragged
   rows in one call vs one call per row) bit-exact on every path.
 """
@@ -32,11 +38,12 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), 'golden')
 META = json.load(open(os.path.join(GOLD, 'crn_meta.json')))
 F32_TOL = 1e-4
-BF16_WAV_TOL = 5e-2
-BF16_MASK_TOL = 5e-2
-FP8_WAV_TOL = 1e-1
-FP8_MASK_TOL = 1e-1
-FP8_VS_BF16_TOL = 1e-1
+BF16_WAV_TOL = 1e-2
+BF16_MASK_TOL = 1e-2
+FP8_WAV_TOL = 2e-2
+FP8_MASK_TOL = 2e-2
+FP8_VS_BF16_TOL = 2e-2
+C3_ERLE_DB = 0.1
 
 
 def rel(a, b):
@@ -253,15 +260,14 @@ def test_bf16_batch256_embeds_goldens():
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize('version', ['1', '2'])
-def test_persistent_recurrence_matches_step_kernel(monkeypatch, version):
+def test_persistent_recurrence_matches_step_kernel(monkeypatch):
     """The persistent LSTM recurrence (crn_persist.hip: one launch per layer,
-    W_hh resident, h exchanged between the blocks of a team; version 1 one
-    phase per frame, version 2 two row halves in alternating phases) against
+    W_hh resident, h exchanged between the blocks of a team, two row halves
+    in alternating phases) against
     the per-frame step kernel (AEC_CRN_PERSIST=0) on a 300-stream bf16 batch
     (two persistent launches per layer: 256 + 44 streams).  All are bf16 with
     f32 accumulation; the persistent kernels sum the two K halves separately
-    (and version 2 uses its own sigmoid / tanh algebra), so the bound is the
+    (and use their own sigmoid / tanh algebra), so the bound is the
     bf16 one (relative RMS <= 1e-2), not bit equality.  A second call checks
     that the first left no timeout flag behind."""
     if not torch.cuda.is_available():
@@ -271,7 +277,7 @@ def test_persistent_recurrence_matches_step_kernel(monkeypatch, version):
     mic, far, _ = synth.batch(B, n, seed0=900)
     M, F = (torch.from_numpy(a).to('cuda:0') for a in (mic, far))
     outs = {}
-    for flag in ('0', version):
+    for flag in ('0', '1'):
         monkeypatch.setenv('AEC_CRN_PERSIST', flag)            # read when the handle is created
         net, m, conf = build('v2E_16000', 'bf16')
         with torch.no_grad():
@@ -279,6 +285,74 @@ def test_persistent_recurrence_matches_step_kernel(monkeypatch, version):
             o2, _, _ = net.forward_ragged(M[:3], F[:3], [n] * 3, want_spec=False)
         torch.cuda.synchronize()
         outs[flag] = (o.cpu().numpy(), o2.cpu().numpy())
-    assert np.isfinite(outs[version][0]).all()
-    assert rel(outs[version][0], outs['0'][0]) <= 1e-2
-    assert np.array_equal(outs[version][1], outs[version][0][:3])   # batch composition stays bit-exact
+    assert np.isfinite(outs['1'][0]).all()
+    assert rel(outs['1'][0], outs['0'][0]) <= 1e-2
+    assert np.array_equal(outs['1'][1], outs['1'][0][:3])   # batch composition stays bit-exact
+
+
+def test_persistent_timeout_fails_that_call(monkeypatch):
+    """A persistent-grid timeout is reported by the call that hit it: with the
+    poll bound forced to one poll (AEC_CRN_SPIN_LIMIT, read per call) the
+    waves give up waiting for their team, the grid drains, and that
+    forward_ragged raises; the next call with the normal bound on the same
+    handle succeeds and equals a fresh handle's output bit for bit."""
+    monkeypatch.delenv('AEC_CRN_PERSIST', raising=False)
+    net, m, conf = build('v2E_16000', 'bf16')
+    from aec_amd import synth
+    B, n = 64, 32000
+    mic, far, _ = synth.batch(B, n, seed0=950)
+    M, F = (torch.from_numpy(a).to('cuda:0') for a in (mic, far))
+    monkeypatch.setenv('AEC_CRN_SPIN_LIMIT', '1')
+    with torch.no_grad(), pytest.raises(RuntimeError, match='timed out'):
+        net.forward_ragged(M, F, [n] * B, want_spec=False)
+    monkeypatch.delenv('AEC_CRN_SPIN_LIMIT')
+    with torch.no_grad():
+        o, _, _ = net.forward_ragged(M, F, [n] * B, want_spec=False)
+        fresh, _, _ = build('v2E_16000', 'bf16')
+        o2, _, _ = fresh.forward_ragged(M, F, [n] * B, want_spec=False)
+    torch.cuda.synchronize()
+    assert torch.isfinite(o).all()
+    assert torch.equal(o, o2)
+
+
+@pytest.mark.parametrize('dtype', ['bf16', 'fp8'])
+def test_c3_shape_long_rows_match_reference_port(dtype):
+    """BASELINE config 3's exact shape: 256 streams x 160,000 samples in one
+    call (626-frame bf16 / fp8 recurrence, the persistent LSTM kernel, the
+    row GEMMs at their benchmark sizes).  Three far-end single-talk rows
+    (first, middle, last) are checked against the reference op mix
+    (oracle/torch_crn_port.py: conv2d / conv_transpose2d / nn.LSTM in f32,
+    pinned to the reference goldens by tests/test_crn_oracle.py): out_wav
+    relative RMS within the dtype's bar and ERLE within C3_ERLE_DB dB.  The
+    other 253 rows are seeded noise scenes (they only have to be there)."""
+    import sys
+    net, m, conf = build('v2E_16000', dtype)
+    from aec_amd import synth
+    from torch_crn_port import TorchCrnPort
+    import aec_oracle as O
+    B, n = 256, 160000
+    rows = (0, 131, 255)
+    g = torch.Generator(device='cuda:0').manual_seed(31)
+    M = 0.05 * torch.randn(B, n, device='cuda:0', generator=g)
+    F = 0.1 * torch.randn(B, n, device='cuda:0', generator=g)
+    sc = {r: synth.scene(n, 7100 + r, double_talk=False) for r in rows}
+    for r in rows:
+        M[r] = torch.from_numpy(sc[r][0]).cuda()
+        F[r] = torch.from_numpy(sc[r][1]).cuda()
+    with torch.no_grad():
+        out, _, _ = net.forward_ragged(M, F, [n] * B, want_spec=False)
+    torch.cuda.synchronize()
+    got = out[list(rows)].cpu().numpy()
+    assert got.shape == (3, 256 * (n // 256))
+    assert np.isfinite(got).all()
+    w = C.make_weights(conf, 2, m['weight_seed'])
+    port = TorchCrnPort(w, conf, 2)
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    ref = port(torch.from_numpy(np.stack([sc[r][0] for r in rows])),
+               torch.from_numpy(np.stack([sc[r][1] for r in rows]))).numpy()
+    tol = BF16_WAV_TOL if dtype == 'bf16' else FP8_WAV_TOL
+    errs = [rel(got[i], ref[i]) for i in range(3)]
+    d_erle = [O.erle_db(sc[r][0], got[i]) - O.erle_db(sc[r][0], ref[i]) for i, r in enumerate(rows)]
+    print(f'{dtype} C3 rows rel {errs} erle delta {d_erle}')
+    assert max(errs) <= tol, errs
+    assert max(abs(d) for d in d_erle) <= C3_ERLE_DB, d_erle

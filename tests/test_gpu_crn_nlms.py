@@ -13,7 +13,9 @@ written here):
 * E (the NLMS error spectrum, fp32 recursion vs float64): <= 1e-4;
 * f32 network fed E: out_wav, out_spec, mask <= 1e-4 (the CRN's own f32 bar);
   v1 loss within 1e-4 relative;
-* bf16 network fed E: out_wav <= 5e-2 (the CRN's bf16 bar);
+* bf16 network fed E: out_wav <= 1e-2 (the CRN's bf16 bar);
+* fp8 per-hop step (64 streams): every stream within 2e-2 of the fp8 batch
+  forward, three within the CRN's fp8 bar (2e-2) of the oracle;
 * streaming (hipGraph-replayed per-hop step, NLMS state carried per stream)
   vs batch: <= 1e-5 f32 (the CRN streaming bar; the NLMS arithmetic itself is
   the same NlmsBin code on the same fp32 operands);
@@ -38,7 +40,7 @@ META = json.load(open(os.path.join(GOLD, 'crn_meta.json')))
 NLMS = dict(taps=4, mu=0.3, beta=0.5, delta=1e-4)
 E_TOL = 1e-4
 F32_TOL = 1e-4
-BF16_WAV_TOL = 5e-2
+BF16_WAV_TOL = 1e-2
 
 
 def rel(a, b):
@@ -185,33 +187,38 @@ def test_error_spec_needs_nlms_handle():
         net.error_spectra('cuda:0')
 
 
-FP8_WAV_TOL = 1e-1
+FP8_WAV_TOL = 2e-2
 
 
 def test_fp8_nlms_stream_step_close_to_oracle():
     """BASELINE config 5's unit: the hipGraph-captured per-hop step with the
-    FD-NLMS in front and MX-fp8 LSTM input projections (dtype 'fp8'), against
-    the float64 oracle (crn_oracle + aec_oracle.nlms) within the fp8 bar of
-    tests/test_gpu_crn.py (relative RMS <= 1e-1), and against the fp8 batch
-    forward of the same network (<= 2e-2: the step kernels are the batch
-    kernels; the streaming front / back restate the batch transforms)."""
+    FD-NLMS in front and MX-fp8 GEMMs (dtype 'fp8'), 64 concurrent streams
+    (the 64 x 64-tile MX GEMM at M = 64 x 128 bins), against the fp8 batch
+    forward of the same network for every stream (<= 2e-2: the step kernels
+    are the batch kernels; the streaming front / back restate the batch
+    transforms) and against the float64 oracle (crn_oracle + aec_oracle.nlms)
+    for three streams within the fp8 bar of tests/test_gpu_crn.py."""
     net, m, conf, w = build('v2E_2125', 'fp8')
-    n = 16000
-    mic, far, _, _ = synth.scene(n, 93, return_echo=True)
+    B, n = 64, 16000
+    sig = [synth.scene(n, 930 + b, return_echo=True) for b in range(B)]
     nh = n // 256 + 1
-    M = torch.zeros(1, 256 * (nh + 1), device='cuda:0')
+    M = torch.zeros(B, 256 * (nh + 1), device='cuda:0')
     F = torch.zeros_like(M)
-    M[0, :n] = torch.from_numpy(mic).cuda()
-    F[0, :n] = torch.from_numpy(far).cuda()
-    net.stream_open(1)
+    M[:, :n] = torch.from_numpy(np.stack([s[0] for s in sig])).cuda()
+    F[:, :n] = torch.from_numpy(np.stack([s[1] for s in sig])).cuda()
+    net.stream_open(B)
     outs = []
     with torch.no_grad():
         for k in range(nh):
             outs.append(net.stream_step(M[:, 256 * k:256 * (k + 1)], F[:, 256 * k:256 * (k + 1)]).clone())
-        ref_out, _, _ = net.forward_ragged(T(mic), T(far), [n], want_spec=False)
+        ref_out, _, _ = net.forward_ragged(M[:, :n].contiguous(), F[:, :n].contiguous(), [n] * B, want_spec=False)
     torch.cuda.synchronize()
-    got = torch.cat(outs[1:], dim=1)[0, :256 * (n // 256)].cpu().numpy()
-    r = C.forward(w, conf, 2, mic, far, nlms=NLMS)
+    no = 256 * (n // 256)
+    got = torch.cat(outs[1:], dim=1)[:, :no].cpu().numpy()
+    ref_out = ref_out.cpu().numpy()
     assert np.isfinite(got).all()
-    assert rel(got, r['out_wav']) <= FP8_WAV_TOL
-    assert rel(got, ref_out[0].cpu().numpy()) <= 2e-2
+    errs = [rel(got[b], ref_out[b]) for b in range(B)]
+    assert max(errs) <= 2e-2, (int(np.argmax(errs)), max(errs))
+    for b in (0, 31, 63):
+        r = C.forward(w, conf, 2, sig[b][0], sig[b][1], nlms=NLMS)
+        assert rel(got[b], r['out_wav']) <= FP8_WAV_TOL, b

@@ -171,7 +171,6 @@ def test_fused_synthesis_bit_exact(golden_weights, golden_erb, monkeypatch):
     erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
     M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
     res = {}
-    monkeypatch.setenv('AEC_PIPE', '0')                         # the multi-kernel path (not aec_pipe.hip)
     for fused in ('0', '1'):
         monkeypatch.setenv('AEC_FUSED_SYNTH', fused)            # read when the handle is created
         net = _net(golden_weights, NLMS)
@@ -204,7 +203,6 @@ def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatc
     erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
     M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
     res = {}
-    monkeypatch.setenv('AEC_PIPE', '0')                         # the multi-kernel paths (not aec_pipe.hip)
     for small in ('0', '64'):
         monkeypatch.setenv('AEC_SMALLB', small)                 # read when the handle is created
         net = _net(golden_weights, NLMS)
@@ -277,99 +275,3 @@ def test_nlms_10s_batch_vs_oracle(nlms_net, golden_weights, golden_erb):
         assert _loss_ok(float(loss[b]), l), b
     assert np.array_equal(out1[0].cpu().numpy(), out[0])
     assert float(loss1[0]) == pytest.approx(float(loss[0]), rel=1e-6)
-
-
-def _pipe_vs_kernels(golden_weights, golden_erb, monkeypatch, nlms, seed, siglens=False):
-    """Run the same ragged batch through the fused per-stream pipeline
-    (aec_pipe.hip, AEC_PIPE=1) and through the multi-kernel path (AEC_PIPE=0)."""
-    from aec_amd import synth
-    lens = [33333, 4097, 255, 16000, 256, 2100, 160000]
-    L = max(lens)
-    rows = [synth.scene(n, seed + i) for i, n in enumerate(lens)]
-    mic, ref, near = (np.zeros((len(lens), L), np.float32) for _ in range(3))
-    l3 = np.zeros((len(lens), 3), np.int64)
-    for i, (m, r, nn_) in enumerate(rows):
-        n = lens[i]
-        d = min(13, n % 256) if siglens else 0       # ref / near a few samples shorter, same frame count
-        mic[i, :n], ref[i, :n - d], near[i, :n - d // 2] = m, r[:n - d], nn_[:n - d // 2]
-        l3[i] = (n, n - d, n - d // 2)
-    dev = 'cuda:0'
-    erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
-    M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
-    T = L // 256 + 1
-    res = {}
-    for pipe in ('0', '1'):
-        monkeypatch.setenv('AEC_PIPE', pipe)                   # read when the handle is created
-        net = _net(golden_weights, nlms)
-        net.set_debug(True)
-        with torch.no_grad():
-            out, loss = net.forward_ragged(M, R, N, erb_t, l3 if siglens else lens)
-        feats = {k: net.debug_intermediate(k, len(lens), T).cpu().numpy()
-                 for k in ('mic_erb', 'ref_erb', 'near_erb', 'gru_out', 'mask', 'est_erb')}
-        torch.cuda.synchronize()
-        res[pipe] = (out.cpu().numpy(), loss.cpu().numpy(), feats)
-    (o0, l0, f0), (o1, l1, f1) = res['0'], res['1']
-    assert np.array_equal(o0, o1)
-    np.testing.assert_allclose(l1, l0, rtol=1e-6)
-    for k in f0:
-        for i, n in enumerate(lens):
-            assert np.array_equal(f0[k][i, :n // 256 + 1], f1[k][i, :n // 256 + 1], equal_nan=True), (k, i)
-
-
-def test_pipeline_kernel_bit_exact_nlms(golden_weights, golden_erb, monkeypatch):
-    """K6 (aec_pipe.hip: one block runs a stream's STFT -> NLMS -> ERB -> GRU ->
-    head -> synthesis -> OLA) against the multi-kernel NLMS path: the same
-    per-frame arithmetic, so waveform and every intermediate are bit-identical
-    (loss summed in another order, <= 1e-6 relative).  Ragged lengths cover
-    partial chunks, streams shorter than one chunk and a 10 s stream."""
-    _pipe_vs_kernels(golden_weights, golden_erb, monkeypatch, NLMS, 900)
-
-
-def test_pipeline_kernel_bit_exact_bypass(golden_weights, golden_erb, monkeypatch):
-    """K6 with the NLMS bypassed (Little_net's own path, E = M) against
-    analysis_kernel + gru_kernel + synthesis_kernel, with per-signal lengths."""
-    _pipe_vs_kernels(golden_weights, golden_erb, monkeypatch, None, 950, siglens=True)
-
-
-@pytest.mark.parametrize('taps,siglens', [(4, False), (4, True), (1, False), (2, True), (3, False)])
-def test_nlms16_kernel_bit_exact(golden_weights, golden_erb, monkeypatch, taps, siglens):
-    """The 16-wave NLMS analysis (aec_nlms16.hip, AEC_NLMS16=1; off by default:
-    measured 0.358 vs 0.335 ms) against the 12-wave nlms_analysis_kernel: the
-    same per-frame functions in the same order, so the features, the waveform
-    (through the E spectrum) and est_erb are bit-identical.  Per-block path
-    forced (AEC_SMALLB=0); ragged lengths cover partial chunks, a stream
-    shorter than one chunk and a 10 s stream; siglens: ref / near shorter."""
-    from aec_amd import synth
-    lens = [33333, 4097, 255, 16000, 256, 2100, 160000]
-    L = max(lens)
-    rows = [synth.scene(n, 1200 + 10 * taps + i) for i, n in enumerate(lens)]
-    mic, ref, near = (np.zeros((len(lens), L), np.float32) for _ in range(3))
-    l3 = np.zeros((len(lens), 3), np.int64)
-    for i, (m, r, nn_) in enumerate(rows):
-        n = lens[i]
-        d = min(13, n % 256) if siglens else 0
-        mic[i, :n], ref[i, :n - d], near[i, :n - d // 2] = m, r[:n - d], nn_[:n - d // 2]
-        l3[i] = (n, n - d, n - d // 2)
-    dev = 'cuda:0'
-    erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
-    M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
-    T = L // 256 + 1
-    res = {}
-    monkeypatch.setenv('AEC_PIPE', '0')
-    monkeypatch.setenv('AEC_SMALLB', '0')
-    for k16 in ('0', '1'):
-        monkeypatch.setenv('AEC_NLMS16', k16)                   # read when the handle is created
-        net = _net(golden_weights, dict(NLMS, taps=taps))
-        net.set_debug(True)
-        with torch.no_grad():
-            out, loss = net.forward_ragged(M, R, N, erb_t, l3 if siglens else lens)
-        feats = {k: net.debug_intermediate(k, len(lens), T).cpu().numpy()
-                 for k in ('mic_erb', 'ref_erb', 'near_erb', 'est_erb')}
-        torch.cuda.synchronize()
-        res[k16] = (out.cpu().numpy(), loss.cpu().numpy(), feats)
-    (o0, l0, f0), (o1, l1, f1) = res['0'], res['1']
-    assert np.array_equal(o0, o1)
-    assert np.array_equal(l0, l1, equal_nan=True)
-    for k in f0:
-        for i, n in enumerate(lens):
-            assert np.array_equal(f0[k][i, :n // 256 + 1], f1[k][i, :n // 256 + 1], equal_nan=True), (k, i)
