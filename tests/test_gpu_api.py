@@ -42,7 +42,7 @@ def test_two_handles_two_streams_overlap(golden_weights, golden_erb):
     erb = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
     nets = [_net(golden_weights), _net(golden_weights)]          # one handle each
     streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
-    B, L = 8, 96000
+    B, L = 16, 320000              # 20 s streams: ~0.4 ms of GPU work per call, above the host's issue time
     g = torch.Generator(device=dev).manual_seed(12)
     sig = [[0.1 * torch.randn(B, L, device=dev, generator=g) for _ in range(3)] for _ in range(2)]
     rng = np.random.default_rng(5)
@@ -88,9 +88,9 @@ def test_list_cache_keys_on_near(golden_weights, golden_erb):
     dev = torch.device('cuda:0')
     erb = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
     from aec_amd import synth
-    n = 16000 + 200
+    n = 16250                                    # 63 hops; the shorter signals keep the frame count
     mic, ref, near = (torch.from_numpy(a).to(dev) for a in synth.batch(2, n, seed0=77))
-    l3 = np.array([[n, n, n - 150], [n, n - 100, n - 190]], np.int64)
+    l3 = np.array([[n, n, n - 110], [n, n - 100, n - 120]], np.int64)
     net = _net(golden_weights)
     with torch.no_grad():
         net.forward_ragged(mic, ref, None, erb, l3)
@@ -98,7 +98,8 @@ def test_list_cache_keys_on_near(golden_weights, golden_erb):
         o2, l2 = _net(golden_weights).forward_ragged(mic, ref, near, erb, l3)
     torch.cuda.synchronize()
     assert torch.equal(o, o2)
-    assert torch.equal(l, l2)
+    # row 0's near is silent over its stored length: the reference's loss is 0/0 = NaN there
+    assert np.array_equal(l.cpu().numpy(), l2.cpu().numpy(), equal_nan=True)
 
 
 def test_native_adam_step_reaches_eval_forward(golden_weights, golden_erb):
