@@ -936,39 +936,73 @@ struct StreamState {
     uint8_t* as = nullptr;
     void* ring_y[8][2] = {};             // per LSTM layer: h ring (two frames)
     float* cst[8] = {};                  // per LSTM layer: c
-    float* hop = nullptr;                // [2 parity][2 signal][B][256] input hop ring (mic, far)
+    float* hop = nullptr;                // [2 parity][2 signal][B][256] hop ring (mic, far): the front kernel
+                                         //   copies each call's hops in, for the next call and the back kernel
     float* tail = nullptr;               // [B][256] overlap-add tail
-    float* out = nullptr;                // [B][256] output hop
     float2* nrows = nullptr;             // NLMS: packed rows [B][2][256]
     float2* nstate = nullptr;            //       recursion state [B][2*taps][256]
     float2* espec = nullptr;             //       E rows [B][256]
+    // one hipGraph per ring parity; the caller's hop / output buffers change per call, so the
+    // front and back kernel nodes get this call's pointers by hipGraphExecKernelNodeSetParams
+    // (a host-side update: no copy kernels in the step)
+    hipGraph_t gsrc[2] = {nullptr, nullptr};
     hipGraphExec_t graph[2] = {nullptr, nullptr};
+    hipGraphNode_t front_node[2] = {nullptr, nullptr}, back_node[2] = {nullptr, nullptr};
+    crn::StreamFrontArgs front_args[2];
+    crn::StreamBackArgs back_args[2];
     hipStream_t cap = nullptr;           // capture stream
+};
+
+// the caller's buffers of one aec_crn_stream_step call
+struct StreamIo {
+    const float* mic;
+    const float* far;
+    int64_t ld_in;
+    float* out;
+    int64_t ld_out;
 };
 
 static void stream_free(aec_crn_handle* h) {
     if (!h->ss) return;
-    for (int p = 0; p < 2; ++p)
+    for (int p = 0; p < 2; ++p) {
         if (h->ss->graph[p]) (void)hipGraphExecDestroy(h->ss->graph[p]);
+        if (h->ss->gsrc[p]) (void)hipGraphDestroy(h->ss->gsrc[p]);
+    }
     for (void* p : h->ss->allocs) (void)hipFree(p);
     if (h->ss->cap) (void)hipStreamDestroy(h->ss->cap);
     delete h->ss;
     h->ss = nullptr;
 }
 
+// the kernel node the last launch on a capturing stream added (null when not capturing)
+static hipGraphNode_t last_node(hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    const hipGraphNode_t* deps = nullptr;
+    size_t nd = 0;
+    if (hipStreamGetCaptureInfo_v2(st, &cs, nullptr, nullptr, &deps, &nd) != hipSuccess) return nullptr;
+    return cs == hipStreamCaptureStatusActive && nd == 1 ? deps[0] : nullptr;
+}
+
 template <typename T>
-static aec_status stream_launches(aec_crn_handle* h, int par, hipStream_t st) {
+static aec_status stream_launches(aec_crn_handle* h, int par, const StreamIo& io, hipStream_t st) {
     StreamState& ss = *h->ss;
     const int B = ss.B;
     const Bufs bf{ss.x0, ss.cat.data(), ss.gx, ss.xn, ss.mask, ss.aq, ss.as};
-    const float* cur_mic = ss.hop + (size_t)(par * 2 + 0) * B * 256;
-    const float* cur_far = ss.hop + (size_t)(par * 2 + 1) * B * 256;
+    float* cur_mic = ss.hop + (size_t)(par * 2 + 0) * B * 256;
+    float* cur_far = ss.hop + (size_t)(par * 2 + 1) * B * 256;
     const float* prev_mic = ss.hop + (size_t)((1 - par) * 2 + 0) * B * 256;
     const float* prev_far = ss.hop + (size_t)((1 - par) * 2 + 1) * B * 256;
     const aec_crn_config& c = h->cfg;
-    crn::StreamFrontArgs fa{prev_mic, cur_mic, prev_far, cur_far, h->d_tab, ss.x0, B};
+    // the frame = [previous hop (ring), this call's hop (caller's buffer)]; the front kernel
+    // copies this hop into the ring slot of this parity
+    crn::StreamFrontArgs fa{prev_mic, io.mic, prev_far, io.far, h->d_tab, ss.x0, B};
+    fa.ld_cur = io.ld_in;
+    fa.save_mic = cur_mic;
+    fa.save_far = cur_far;
     if (c.nlms_taps > 0) fa.rows = ss.nrows;
     CRN_TRY(h, crn::launch_stream_front<T>(fa, st));
+    ss.front_node[par] = last_node(st);
+    ss.front_args[par] = fa;
     if (c.nlms_taps > 0) {
         crn::StreamNlmsArgs na{ss.nrows, ss.nstate, ss.espec, ss.x0, B, c.nlms_mu, c.nlms_beta, c.nlms_delta};
         CRN_TRY(h, crn::launch_stream_nlms<T>(na, c.nlms_taps, st));
@@ -985,9 +1019,39 @@ static aec_status stream_launches(aec_crn_handle* h, int par, hipStream_t st) {
     }
     s = run_decoder<T>(h, bf, B, st);
     if (s != AEC_OK) return s;
-    crn::StreamBackArgs ba{prev_mic, cur_mic, h->d_tab, reinterpret_cast<const float2*>(ss.mask), ss.tail, ss.out, B};
+    crn::StreamBackArgs ba{prev_mic, cur_mic, h->d_tab, reinterpret_cast<const float2*>(ss.mask), ss.tail, io.out, B};
+    ba.ld_out = io.ld_out;
     if (c.nlms_taps > 0) ba.espec = ss.espec;
     CRN_TRY(h, crn::launch_stream_back(ba, mask_mode(h), st));
+    ss.back_node[par] = last_node(st);
+    ss.back_args[par] = ba;
+    return AEC_OK;
+}
+
+// point the captured front / back kernel nodes of parity `par` at this call's buffers
+static aec_status stream_set_io(aec_crn_handle* h, int par, const StreamIo& io) {
+    StreamState& ss = *h->ss;
+    crn::StreamFrontArgs& fa = ss.front_args[par];
+    crn::StreamBackArgs& ba = ss.back_args[par];
+    if (fa.cur_mic == io.mic && fa.cur_far == io.far && fa.ld_cur == io.ld_in && ba.out == io.out &&
+        ba.ld_out == io.ld_out)
+        return AEC_OK;
+    fa.cur_mic = io.mic;
+    fa.cur_far = io.far;
+    fa.ld_cur = io.ld_in;
+    ba.out = io.out;
+    ba.ld_out = io.ld_out;
+    hipKernelNodeParams kp{};
+    CRN_TRY(h, hipGraphKernelNodeGetParams(ss.front_node[par], &kp));
+    void* fargs[] = {&fa};
+    kp.kernelParams = fargs;
+    kp.extra = nullptr;
+    CRN_TRY(h, hipGraphExecKernelNodeSetParams(ss.graph[par], ss.front_node[par], &kp));
+    CRN_TRY(h, hipGraphKernelNodeGetParams(ss.back_node[par], &kp));
+    void* bargs[] = {&ba};
+    kp.kernelParams = bargs;
+    kp.extra = nullptr;
+    CRN_TRY(h, hipGraphExecKernelNodeSetParams(ss.graph[par], ss.back_node[par], &kp));
     return AEC_OK;
 }
 extern "C" {
@@ -1201,7 +1265,6 @@ aec_status aec_crn_stream_open(aec_crn_handle* h, int32_t B) {
     }
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.hop), (size_t)4 * B * 256 * sizeof(float)));
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.tail), (size_t)B * 256 * sizeof(float)));
-    CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.out), (size_t)B * 256 * sizeof(float)));
     if (h->cfg.nlms_taps > 0) {
         CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.nrows), (size_t)B * 512 * sizeof(float2)));
         CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.nstate), (size_t)B * 2 * h->cfg.nlms_taps * 256 * sizeof(float2)));
@@ -1246,13 +1309,7 @@ aec_status aec_crn_stream_step(aec_crn_handle* h, const float* mic, const float*
     aec::DeviceGuard dg(h->device);   // the caller's current device is restored on return
     if (dg.err != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
     const int par = (int)(ss.k & 1);
-    const int B = ss.B;
-    CRN_TRY(h, hipMemcpy2DAsync(ss.hop + (size_t)(par * 2 + 0) * B * 256, 256 * sizeof(float), mic,
-                                (size_t)ld_in * sizeof(float), 256 * sizeof(float), (size_t)B, hipMemcpyDeviceToDevice,
-                                st));
-    CRN_TRY(h, hipMemcpy2DAsync(ss.hop + (size_t)(par * 2 + 1) * B * 256, 256 * sizeof(float), far,
-                                (size_t)ld_in * sizeof(float), 256 * sizeof(float), (size_t)B, hipMemcpyDeviceToDevice,
-                                st));
+    const StreamIo io{mic, far, ld_in, out, ld_out};
     static const int use_graph = [] {
         const char* v = getenv("AEC_CRN_GRAPH");
         return v ? atoi(v) : 1;
@@ -1263,16 +1320,23 @@ aec_status aec_crn_stream_step(aec_crn_handle* h, const float* mic, const float*
             // capture the ~26 launches of one frame once per ring parity; replay every hop
             hipGraph_t g = nullptr;
             if (hipStreamBeginCapture(ss.cap, hipStreamCaptureModeThreadLocal) == hipSuccess) {
-                const aec_status s = h->es == 4 ? stream_launches<float>(h, par, ss.cap)
-                                                : stream_launches<bf16_t>(h, par, ss.cap);
+                const aec_status s = h->es == 4 ? stream_launches<float>(h, par, io, ss.cap)
+                                                : stream_launches<bf16_t>(h, par, io, ss.cap);
                 const hipError_t e = hipStreamEndCapture(ss.cap, &g);
-                if (s == AEC_OK && e == hipSuccess && g) {
-                    if (hipGraphInstantiate(&ss.graph[par], g, nullptr, nullptr, 0) != hipSuccess)
+                if (s == AEC_OK && e == hipSuccess && g && ss.front_node[par] && ss.back_node[par]) {
+                    if (hipGraphInstantiate(&ss.graph[par], g, nullptr, nullptr, 0) == hipSuccess) {
+                        ss.gsrc[par] = g;              // the node handles belong to it
+                        g = nullptr;
+                    } else {
                         ss.graph[par] = nullptr;
+                    }
                 }
                 if (g) (void)hipGraphDestroy(g);
                 (void)hipGetLastError();
             }
+        } else {
+            const aec_status s = stream_set_io(h, par, io);
+            if (s != AEC_OK) return s;
         }
         if (ss.graph[par]) {
             CRN_TRY(h, hipGraphLaunch(ss.graph[par], st));
@@ -1280,11 +1344,9 @@ aec_status aec_crn_stream_step(aec_crn_handle* h, const float* mic, const float*
         }
     }
     if (!launched) {
-        const aec_status s = h->es == 4 ? stream_launches<float>(h, par, st) : stream_launches<bf16_t>(h, par, st);
+        const aec_status s = h->es == 4 ? stream_launches<float>(h, par, io, st) : stream_launches<bf16_t>(h, par, io, st);
         if (s != AEC_OK) return s;
     }
-    CRN_TRY(h, hipMemcpy2DAsync(out, (size_t)ld_out * sizeof(float), ss.out, 256 * sizeof(float), 256 * sizeof(float),
-                                (size_t)B, hipMemcpyDeviceToDevice, st));
     ss.k++;
     return AEC_OK;
 }

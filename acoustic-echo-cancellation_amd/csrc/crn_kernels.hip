@@ -305,6 +305,23 @@ __device__ __forceinline__ void stage_frame(float* reg, const float* prev, const
         r1[i] = c4[i];
     }
 }
+// The current hop from the caller's buffer (any alignment: cal = 16-B aligned rows), optionally
+// saved into the ring slot `save` for the next call.
+__device__ __forceinline__ void stage_frame_io(float* reg, const float* prev, const float* cur, bool cal, float* save,
+                                               int lb) {
+    const float4* p4 = reinterpret_cast<const float4*>(prev) + lb * 4;
+    float4* r0 = reinterpret_cast<float4*>(reg) + lb * 4;
+    float4* r1 = reinterpret_cast<float4*>(reg + aec::kHopStride) + lb * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        r0[i] = p4[i];
+        const int e = 16 * lb + 4 * i;
+        const float4 c = cal ? *reinterpret_cast<const float4*>(cur + e)
+                             : make_float4(cur[e], cur[e + 1], cur[e + 2], cur[e + 3]);
+        r1[i] = c;
+        if (save) *reinterpret_cast<float4*>(save + e) = c;
+    }
+}
 
 template <typename T>
 __global__ __launch_bounds__(256) void crn_stream_front_kernel(StreamFrontArgs p) {
@@ -325,10 +342,13 @@ __global__ __launch_bounds__(256) void crn_stream_front_kernel(StreamFrontArgs p
     const int bb = b < p.B ? b : p.B - 1;
     float* reg = sGrp + g * kGroupFloats;
     float2 ma[8], mb[8], m128, fa[8], fb[8], f128;
+    const bool cal = (p.ld_cur & 3) == 0 && ((reinterpret_cast<uintptr_t>(p.cur_mic) | reinterpret_cast<uintptr_t>(p.cur_far)) & 15) == 0;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-        stage_frame(reg, (s == 0 ? p.prev_mic : p.prev_far) + (int64_t)bb * 256,
-                    (s == 0 ? p.cur_mic : p.cur_far) + (int64_t)bb * 256, lb);
+        float* save = s == 0 ? p.save_mic : p.save_far;
+        stage_frame_io(reg, (s == 0 ? p.prev_mic : p.prev_far) + (int64_t)bb * 256,
+                       (s == 0 ? p.cur_mic : p.cur_far) + (int64_t)bb * p.ld_cur, cal,
+                       save && b < p.B ? save + (int64_t)b * 256 : nullptr, lb);
         aec::wave_fence();
         float2 v[16];
         aec::load_frame(v, reg, sHann, 0, lb);
@@ -430,7 +450,7 @@ __global__ __launch_bounds__(256) void crn_stream_back_kernel(StreamBackArgs p) 
     aec::wave_fence();
     if (b >= p.B) return;
     float* tail = p.tail + (int64_t)b * 256;
-    float* out = p.out + (int64_t)b * 256;
+    float* out = p.out + (int64_t)b * p.ld_out;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int r = lb + 16 * i;

@@ -87,14 +87,17 @@ struct StepArgs {
 
 // Streaming (one hop per stream): frame = [prev hop, cur hop] of each stream
 struct StreamFrontArgs {
-    const float* prev_mic;      // [B][256]
-    const float* cur_mic;
+    const float* prev_mic;      // [B][256] (the hop ring)
+    const float* cur_mic;       // [B][ld_cur]: this call's hop, read in place from the caller's buffer
     const float* prev_far;
     const float* cur_far;
     const aec::DevTables* tab;
     void* x0;                   // [B][256][8]
     int32_t B;
     float2* rows = nullptr;     // non-null (NLMS): write the packed rows [B][2][256] instead of X0
+    int64_t ld_cur = 256;       // row stride of cur_mic / cur_far (elements)
+    float* save_mic = nullptr;  // non-null: copy the current hops into the ring ([B][256]) for the
+    float* save_far = nullptr;  //   next call's frame and the back kernel
 };
 // NLMS streaming step: one block per stream, bin slot per lane; state
 // [B][2*TAPS][256] float2 (taps, far history r[t-1..t-TAPS+1], power — the
@@ -113,9 +116,10 @@ struct StreamBackArgs {
     const aec::DevTables* tab;
     const float2* mask;         // [B][256]
     float* tail;                // [B][256] overlap-add state (in / out)
-    float* out;                 // [B][256] output hop (the previous hop of the stream)
+    float* out;                 // [B][ld_out] output hop (the previous hop of the stream): the caller's buffer
     int32_t B;
     const float2* espec = nullptr;   // non-null (NLMS): mask the E rows [B][256] instead of the mic frame
+    int64_t ld_out = 256;
 };
 
 template <typename T>
