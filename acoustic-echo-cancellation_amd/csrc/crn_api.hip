@@ -93,8 +93,13 @@ struct aec_crn_handle {
     void* gx = nullptr;
     void* y = nullptr;
     void* xn = nullptr;
-    uint8_t* aq = nullptr;                         // dtype 2: quantized LSTM input rows + scales
+    uint8_t* aq = nullptr;                         // dtype 2: quantized rows + scales (layers without a shadow)
     uint8_t* as = nullptr;
+    bool mx8_shadow = true;                        // AEC_CRN_MX8_SHADOW=0 at create: every MX GEMM quantises its rows
+                                                   //   first (the A/B and bit-equality reference)
+    std::vector<uint8_t*> cat8, cats;              // dtype 2: MX-fp8 shadows of cat[l] (null: none), see shadow_level
+    uint8_t* xn8 = nullptr;                        //   and of xn
+    uint8_t* xns = nullptr;
     float* cst = nullptr;
     float* mask = nullptr;
     float2* nrows = nullptr;                       // NLMS: packed mic / far rows [B][T][2][256]
@@ -558,6 +563,24 @@ static size_t mx8_row_bytes(const aec_crn_handle* h) {
     return m;
 }
 
+// dtype 2: cat[l] gets an MX-fp8 shadow (written by every producer's epilogue,
+// read in place by the MX GEMMs: no separate quantisation pass) when an MX
+// layer consumes it and its rows qualify for the in-place gather (128 | 2^kshift):
+// encoder layer l, decoder level l, or the first LSTM layer (l == L)
+static bool shadow_level(const aec_crn_handle* h, int l) {
+    if (!h->mx8 || !h->mx8_shadow || l < 1 || l > h->L) return false;
+    // cat[L]'s dec half comes from the LSTM combine, which writes a shadow for NavieComplexLSTM (v2) only
+    if (l == h->L && h->CELLS * h->S != 4) return false;
+    const int* ch = h->cfg.conv_channels;
+    if (l < h->L && h->enc[l].wq && ch[l] % 128 == 0) return true;
+    const int d = h->L - l;
+    if ((h->dec[2 * d].wq || h->dec[2 * d + 1].wq) && (2 * ch[l]) % 128 == 0) return true;
+    return l == h->L && h->Q % 128 == 0 && (2 * ch[l]) % 128 == 0;
+}
+static bool shadow_xn(const aec_crn_handle* h) {
+    return h->mx8 && h->mx8_shadow && h->nrnn > 1 && h->Q % 128 == 0 && h->CELLS * h->S == 4;
+}
+
 static aec_status ensure_ws(aec_crn_handle* h, int64_t B, int64_t T) {
     if (B <= h->ws_B && T <= h->ws_T) return AEC_OK;
     for (void* p : h->allocs) (void)hipFree(p);
@@ -583,6 +606,20 @@ static aec_status ensure_ws(aec_crn_handle* h, int64_t B, int64_t T) {
         const size_t qb = (size_t)BT * mx8_row_bytes(h);
         CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->aq), qb));
         CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->as), qb / 32));
+    }
+    h->cat8.assign(h->L + 1, nullptr);
+    h->cats.assign(h->L + 1, nullptr);
+    for (int l = 1; l <= h->L; ++l)
+        if (shadow_level(h, l)) {
+            const size_t n8 = (size_t)BT * (256 >> l) * 2 * ch[l];
+            CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->cat8[l]), n8));
+            CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->cats[l]), n8 / 32));
+        }
+    h->xn8 = h->xns = nullptr;
+    if (shadow_xn(h)) {
+        const size_t n8 = (size_t)BT * h->S * h->H;
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->xn8), n8));
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->xns), n8 / 32));
     }
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->cst), (size_t)nB * h->CELLS * h->S * h->H * sizeof(float)));
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&h->mask), (size_t)BT * 256 * 2 * sizeof(float)));
@@ -615,14 +652,45 @@ struct Bufs {
     void* gx;
     void* xn;
     float* mask;
-    uint8_t* aq;            // dtype 2: quantized LSTM input rows [F*S][H] + scales [F*S][H/32]
+    uint8_t* aq;            // dtype 2: quantized rows [rows][K] + scales [rows][K/32] (layers without a shadow)
     uint8_t* as;
+    uint8_t* const* cat8;   // dtype 2: MX-fp8 shadows of cat[l] (e4m3 [F][bins][2 ch], E8M0 per 32), null: none
+    uint8_t* const* cats;
+    uint8_t* xn8;           //   and of xn
+    uint8_t* xns;
 };
+
+// an output with an MX-fp8 shadow (bf16 GEMM epilogues only)
+template <typename T>
+static void set_shadow(crn::RowEpi& e, uint8_t* q8, uint8_t* qs) {
+    if (sizeof(T) == 2 && q8 && e.N % 128 == 0) {      // the 128-column tiles: 32-column groups in lane quads
+        e.q8 = q8;
+        e.qs = qs;
+    }
+}
+
+// dtype 2 GEMM over the implicit rows `a`: in place from the source's MX-fp8 shadow
+// (q8 / qs, written by its producers), else quantised into bf.aq / bf.as first
+template <typename T>
+static aec_status mx8_gemm(aec_crn_handle* h, const crn::RowSrc& a, const uint8_t* q8, const uint8_t* qs,
+                           const Bufs& bf, const uint8_t* wq, const uint8_t* wsc, int K, const crn::RowEpi& e, int npad,
+                           hipStream_t st) {
+    if (q8) {
+        crn::RowSrc a8 = a;
+        a8.src = q8;
+        CRN_TRY(h, crn::launch_gemm_mx8_rows<T>(a8, qs, wq, wsc, K, e, npad, st));
+        return AEC_OK;
+    }
+    CRN_TRY(h, crn::launch_mx8_quant(a, bf.aq, bf.as, st));
+    CRN_TRY(h, crn::launch_gemm_mx8<T>(bf.aq, bf.as, wq, wsc, K, e, npad, st));
+    return AEC_OK;
+}
 
 template <typename T>
 static aec_status run_encoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipStream_t st) {
     using crn::RowEpi;
     using crn::RowSrc;
+    aec_status s = AEC_OK;
     const int* ch = h->cfg.conv_channels;
     for (int i = 0; i < h->L; ++i) {
         const int Fin = 256 >> i, Fo = Fin / 2;
@@ -646,9 +714,11 @@ static aec_status run_encoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipS
         a.src_elems = F * Fin * ld_in;
         const int64_t ldo = 2 * ch[i + 1];
         RowEpi e{bf.cat[i + 1], a.M, pk.N, a.rshift, Fo * ldo, ldo, ch[i + 1], pk.bias, pk.alpha, pk.act};
+        set_shadow<T>(e, bf.cat8[i + 1], bf.cats[i + 1]);
         if (pk.wq) {                       // dtype 2: e4m3 rows + E8M0 scales, scaled-MFMA GEMM
-            CRN_TRY(h, crn::launch_mx8_quant(a, bf.aq, bf.as, st));
-            CRN_TRY(h, crn::launch_gemm_mx8<T>(bf.aq, bf.as, pk.wq, pk.wsc, pk.kpad, e, pk.npad8, st));
+            s = mx8_gemm<T>(h, a, i > 0 ? bf.cat8[i] : nullptr, i > 0 ? bf.cats[i] : nullptr, bf, pk.wq, pk.wsc,
+                            pk.kpad, e, pk.npad8, st);
+            if (s != AEC_OK) return s;
             continue;
         }
         CRN_TRY(h, (crn::launch_gemm_rows<T, T>(a, reinterpret_cast<const T*>(pk.w), pk.kpad,
@@ -689,11 +759,9 @@ static aec_status run_lstm_input(aec_crn_handle* h, const Bufs& bf, int l, int64
     a.src_elems = F * D * ld_in;
     const Packed& ih = h->lih[l];
     RowEpi e{bf.gx, a.M, ih.N, 0, (int64_t)C * 4 * H, 0, 0, ih.bias, 0.f, 0};
-    if (h->mx8) {                          // e4m3 rows + E8M0 scales, then the scaled-MFMA GEMM
-        CRN_TRY(h, crn::launch_mx8_quant(a, bf.aq, bf.as, st));
-        CRN_TRY(h, crn::launch_gemm_mx8<T>(bf.aq, bf.as, ih.wq, ih.wsc, ih.kpad, e, ih.npad, st));
-        return AEC_OK;
-    }
+    if (h->mx8)                            // e4m3 rows + E8M0 scales, scaled-MFMA GEMM
+        return mx8_gemm<T>(h, a, l == 0 ? bf.cat8[L] : bf.xn8, l == 0 ? bf.cats[L] : bf.xns, bf, ih.wq, ih.wsc,
+                           ih.kpad, e, ih.npad, st);
     CRN_TRY(h, (crn::launch_gemm_rows<T, T>(a, reinterpret_cast<const T*>(ih.w), ih.kpad,
                                              (int)(ih.kpad * sizeof(T) / crn::kStageBytes), e, ih.npad, st)));
     return AEC_OK;
@@ -709,8 +777,10 @@ static aec_status run_lstm_combine(aec_crn_handle* h, const Bufs& bf, int l, con
     const bool last = l + 1 == h->nrnn;
     T* dst = reinterpret_cast<T*>(last ? bf.cat[L] : bf.xn);
     const int64_t ldd = last ? 2 * ch[L] : (int64_t)S * Q;
+    uint8_t* q8 = sizeof(T) == 2 ? (last ? bf.cat8[L] : bf.xn8) : nullptr;
+    uint8_t* qs = sizeof(T) == 2 ? (last ? bf.cats[L] : bf.xns) : nullptr;
     CRN_TRY(h, crn::launch_lstm_combine<T>(reinterpret_cast<const T*>(y), dst, F, h->H, h->CELLS, S, ilog2(Q),
-                                           h->D * ldd, ldd, st));
+                                           h->D * ldd, ldd, st, q8, qs));
     return AEC_OK;
 }
 
@@ -744,6 +814,7 @@ static aec_status run_decoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipS
             RowEpi e{bf.cat[cl - 1], a.M, pk.N, a.rshift, Fo * ldo, 2 * ldo, 0, pk.bias, pk.alpha, pk.act};
             e.nsplit = pk.N / 2;
             e.split_add = ldo;
+            set_shadow<T>(e, bf.cat8[cl - 1], bf.cats[cl - 1]);
             CRN_TRY(h, (crn::launch_gemm_rows<T, T>(a, reinterpret_cast<const T*>(pk.w), pk.kpad,
                                                      (int)(pk.kpad * sizeof(T) / crn::kStageBytes), e, pk.npad, st)));
             continue;
@@ -767,9 +838,11 @@ static aec_status run_decoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipS
             if (cl != 1) {
                 const int64_t ldo = 2 * ch[cl - 1];
                 RowEpi e{bf.cat[cl - 1], a.M, pk.N, a.rshift, Fo * ldo, 2 * ldo, par * ldo, pk.bias, pk.alpha, pk.act};
+                set_shadow<T>(e, bf.cat8[cl - 1], bf.cats[cl - 1]);
                 if (pk.wq) {               // dtype 2 (see conv_mx8)
-                    CRN_TRY(h, crn::launch_mx8_quant(a, bf.aq, bf.as, st));
-                    CRN_TRY(h, crn::launch_gemm_mx8<T>(bf.aq, bf.as, pk.wq, pk.wsc, pk.kpad, e, pk.npad8, st));
+                    const aec_status s = mx8_gemm<T>(h, a, bf.cat8[cl], bf.cats[cl], bf, pk.wq, pk.wsc, pk.kpad, e,
+                                                     pk.npad8, st);
+                    if (s != AEC_OK) return s;
                     continue;
                 }
                 CRN_TRY(h, (crn::launch_gemm_rows<T, T>(a, reinterpret_cast<const T*>(pk.w), pk.kpad,
@@ -860,7 +933,8 @@ template <typename T>
 static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int32_t B, int64_t ld, int64_t Tmax,
                       float* out, int64_t ld_out, float* spec, float* mask_out, hipStream_t st) {
     const int64_t BT = (int64_t)B * Tmax;
-    const Bufs bf{h->x0, h->cat.data(), h->gx, h->xn, h->mask, h->aq, h->as};
+    const Bufs bf{h->x0, h->cat.data(), h->gx, h->xn, h->mask, h->aq, h->as, h->cat8.data(), h->cats.data(), h->xn8,
+                  h->xns};
     const int H = h->H, S = h->S, C = h->CELLS;
     const bool persist = sizeof(T) == 2 && h->persist && h->psync && crn::persist_supported(H, C, S, h->num_cus);
     mark(h, st);
@@ -934,6 +1008,9 @@ struct StreamState {
     float* mask = nullptr;
     uint8_t* aq = nullptr;               // dtype 2 (see Bufs)
     uint8_t* as = nullptr;
+    std::vector<uint8_t*> cat8, cats;
+    uint8_t* xn8 = nullptr;
+    uint8_t* xns = nullptr;
     void* ring_y[8][2] = {};             // per LSTM layer: h ring (two frames)
     float* cst[8] = {};                  // per LSTM layer: c
     float* hop = nullptr;                // [2 parity][2 signal][B][256] hop ring (mic, far): the front kernel
@@ -987,7 +1064,8 @@ template <typename T>
 static aec_status stream_launches(aec_crn_handle* h, int par, const StreamIo& io, hipStream_t st) {
     StreamState& ss = *h->ss;
     const int B = ss.B;
-    const Bufs bf{ss.x0, ss.cat.data(), ss.gx, ss.xn, ss.mask, ss.aq, ss.as};
+    const Bufs bf{ss.x0, ss.cat.data(), ss.gx, ss.xn, ss.mask, ss.aq, ss.as, ss.cat8.data(), ss.cats.data(), ss.xn8,
+                  ss.xns};
     float* cur_mic = ss.hop + (size_t)(par * 2 + 0) * B * 256;
     float* cur_far = ss.hop + (size_t)(par * 2 + 1) * B * 256;
     const float* prev_mic = ss.hop + (size_t)((1 - par) * 2 + 0) * B * 256;
@@ -1100,6 +1178,7 @@ aec_status aec_crn_create(const aec_crn_config* cfg, const float* params, size_t
     aec::build_dev_tables(tab);
     if (hipMemcpy(h->d_tab, &tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess) return bail(AEC_ERR_HIP);
     if (const char* v = getenv("AEC_CRN_PERSIST")) h->persist = atoi(v) != 0;
+    if (const char* v = getenv("AEC_CRN_MX8_SHADOW")) h->mx8_shadow = atoi(v) != 0;
     if (hipDeviceGetAttribute(&h->num_cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) h->num_cus = 0;
     if (h->es == 2 && crn::persist_supported(h->H, h->CELLS, h->S, h->num_cus)) {
         // team arrival counters + error word, and a pinned copy of the error word
@@ -1256,6 +1335,18 @@ aec_status aec_crn_stream_open(aec_crn_handle* h, int32_t B) {
         const size_t qb = (size_t)B * mx8_row_bytes(h);
         CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.aq), qb));
         CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.as), qb / 32));
+    }
+    ss.cat8.assign(h->L + 1, nullptr);
+    ss.cats.assign(h->L + 1, nullptr);
+    for (int l = 1; l <= h->L; ++l)
+        if (shadow_level(h, l)) {
+            const size_t n8 = (size_t)B * (256 >> l) * 2 * ch[l];
+            CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.cat8[l]), n8));
+            CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.cats[l]), n8 / 32));
+        }
+    if (shadow_xn(h)) {
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.xn8), (size_t)B * S * H));
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.xns), (size_t)B * S * H / 32));
     }
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.mask), (size_t)B * 256 * 2 * sizeof(float)));
     for (int l = 0; l < h->nrnn; ++l) {

@@ -435,15 +435,16 @@ constexpr uint32_t kOOB = 0x80000000u;
 // 4 B]; a stage's scales (bytes 4 st .. 4 st+3 of every row's scale row) come
 // by one 4-byte DMA per lane: wave w, lane l fetches row 64 w + l of [A | B]
 // (BM + BN == 64 NW), so every wave issues LA + LB + 1 DMAs per stage.
-// rs / soff: the wave's scale descriptor (A or B, wave-uniform) and the lane's
-// byte offset of its scale row (kOOB: zero scale byte, row out of range).
+// rs / soff(st): the wave's scale descriptor (A or B, wave-uniform) and the
+// lane's byte offset of its row's 4 scale bytes of stage st (kOOB: zero
+// scales: the row, or the conv tap, is out of range).
 // --------------------------------------------------------------------------
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 
-template <int BM, int BN, int FM, int FN, int NBUF, class AO, class BO, int NW>
+template <int BM, int BN, int FM, int FN, int NBUF, class AO, class BO, int NW, class SO>
 __device__ __forceinline__ void gemm_core_mx8(f32x4 (&acc)[FM][FN], char* smem, __amdgpu_buffer_rsrc_t ra,
                                               __amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rs, const AO& aoff,
-                                              const BO& boff, uint32_t soff, int nstages, int wr0, int wc0) {
+                                              const BO& boff, const SO& soff, int nstages, int wr0, int wc0) {
     constexpr int RB = 128, RPI = 8;
     static_assert(BM % (RPI * NW) == 0 && BN % (RPI * NW) == 0 && NBUF >= 2 && BM + BN == 64 * NW, "tile");
     constexpr int LA = BM / (RPI * NW), LB = BN / (RPI * NW);
@@ -468,8 +469,7 @@ __device__ __forceinline__ void gemm_core_mx8(f32x4 (&acc)[FM][FN], char* smem, 
                 0, 0);
         }
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rs, (__attribute__((address_space(3))) void*)(buf + (BM + BN) * RB + wave * 256), 4,
-            soff == kOOB ? kOOB : soff + 4 * st, 0, 0, 0);
+            rs, (__attribute__((address_space(3))) void*)(buf + (BM + BN) * RB + wave * 256), 4, soff(st), 0, 0, 0);
     };
 #pragma unroll
     for (int s = 0; s < NBUF - 1; ++s)

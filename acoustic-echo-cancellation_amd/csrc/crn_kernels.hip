@@ -628,6 +628,43 @@ __device__ __forceinline__ float apply_act(float v, float alpha) {
     else return v;
 }
 
+// MX-fp8 shadow of one 16-B output chunk (8 bf16, columns n .. n+7) whose
+// 32-column group's 4 chunks sit in lanes 4j .. 4j+3: the group's E8M0 scale
+// (amax over the 4 lanes) and the chunk's 8 e4m3 bytes, by mx8_quant_kernel's
+// rule on the same bf16 values (so an MX GEMM reading the shadow in place sees
+// the bytes the separate quantisation pass would have written).  ok: the
+// chunk is a real output (its bytes / scale are stored); every lane of the
+// wave must call it (cross-lane reduction).
+__device__ __forceinline__ void mx8_chunk(const u32x4& v, bool ok, uint8_t* q8, uint8_t* qs, int64_t eo, bool lead) {
+    float x[8];
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        x[2 * i] = __uint_as_float(v[i] << 16);
+        x[2 * i + 1] = __uint_as_float(v[i] & 0xFFFF0000u);
+        amax = fmaxf(amax, fmaxf(fabsf(x[2 * i]), fabsf(x[2 * i + 1])));
+    }
+    if (!ok) amax = 0.f;
+    amax = fmaxf(amax, __shfl_xor(amax, 1));
+    amax = fmaxf(amax, __shfl_xor(amax, 2));
+    const int ebits = (int)((__float_as_uint(amax) >> 23) & 0xFF);     // floor(log2 amax) + 127
+    const int code = ebits > 8 ? ebits - 8 : 0;                          // E8M0: 2^(code - 127)
+    uint32_t pk[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        float y[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y[j] = fminf(fmaxf(ldexpf(x[4 * i + j], 127 - code), -448.f), 448.f);
+        int w = __builtin_amdgcn_cvt_pk_fp8_f32(y[0], y[1], 0, false);
+        w = __builtin_amdgcn_cvt_pk_fp8_f32(y[2], y[3], w, true);
+        pk[i] = (uint32_t)w;
+    }
+    if (ok) {
+        *reinterpret_cast<uint2*>(q8 + eo) = make_uint2(pk[0], pk[1]);
+        if (lead) qs[eo >> 5] = (uint8_t)code;
+    }
+}
+
 // Row-GEMM epilogue: bias (loaded once per column fragment), activation,
 // store.  Rows / columns beyond M / N are skipped.
 template <typename OutT, int FM, int FN, int ACT>
@@ -707,16 +744,20 @@ __device__ __forceinline__ void rows_epilogue_lds_a(const f32x4 (&acc)[FM][FN], 
             const int row = c / CPR, ch = c % CPR;
             const int64_t m = mb + p0 * 16 + row;
             const int n = nb + ch * EPC;
-            if (m < e.M && n < e.N) {
-                const u32x4 v = *reinterpret_cast<const u32x4*>(wlds + row * RB + ch * 16);
-                OutT* o = reinterpret_cast<OutT*>(e.out) + (m >> e.oshift) * e.o_hi + (m & omask) * e.o_lo + e.o_add +
-                          (n >= e.nsplit ? e.split_add + (n - e.nsplit) : n);   // a chunk never straddles nsplit
+            const bool ok = m < e.M && n < e.N;
+            const u32x4 v = *reinterpret_cast<const u32x4*>(wlds + row * RB + ch * 16);
+            const int64_t eo = (m >> e.oshift) * e.o_hi + (m & omask) * e.o_lo + e.o_add +
+                               (n >= e.nsplit ? e.split_add + (n - e.nsplit) : n);   // a chunk never straddles nsplit
+            if (ok) {
+                OutT* o = reinterpret_cast<OutT*>(e.out) + eo;
 #if CRN_EPI_NT
                 __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(o));
 #else
                 *reinterpret_cast<u32x4*>(o) = v;
 #endif
             }
+            if constexpr (sizeof(OutT) == 2 && CPR % 4 == 0)
+                if (e.q8) mx8_chunk(v, ok, e.q8, e.qs, eo, (ch & 3) == 0);
         }
         aec::wave_fence();
     }
@@ -809,16 +850,20 @@ __device__ __forceinline__ void rows_epilogue_lds_t(const f32x4 (&acc)[FM][FN], 
             const int row = c / CPR, ch = c % CPR;
             const int64_t m = mb + p0 * 16 + row;
             const int n = nb + ch * EPC;
-            if (m < e.M && n < e.N && !(e.mode & 2)) {     // mode bit 1: timing only, no global stores
-                const u32x4 v = *reinterpret_cast<const u32x4*>(wlds + row * RS + ch * 16);
-                OutT* o = reinterpret_cast<OutT*>(e.out) + (m >> e.oshift) * e.o_hi + (m & omask) * e.o_lo + e.o_add +
-                          (n >= e.nsplit ? e.split_add + (n - e.nsplit) : n);
+            const bool ok = m < e.M && n < e.N && !(e.mode & 2);     // mode bit 1: timing only, no global stores
+            const u32x4 v = *reinterpret_cast<const u32x4*>(wlds + row * RS + ch * 16);
+            const int64_t eo = (m >> e.oshift) * e.o_hi + (m & omask) * e.o_lo + e.o_add +
+                               (n >= e.nsplit ? e.split_add + (n - e.nsplit) : n);
+            if (ok) {
+                OutT* o = reinterpret_cast<OutT*>(e.out) + eo;
 #if CRN_EPI_NT
                 __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(o));
 #else
                 *reinterpret_cast<u32x4*>(o) = v;
 #endif
             }
+            if constexpr (sizeof(OutT) == 2 && CPR % 4 == 0)
+                if (e.q8) mx8_chunk(v, ok, e.q8, e.qs, eo, (ch & 3) == 0);
         }
         aec::wave_fence();
     }
@@ -1108,11 +1153,16 @@ hipError_t launch_mx8_quant(const RowSrc& a, uint8_t* q, uint8_t* s, hipStream_t
 
 // C[M][N] = dequant(A) dequant(B)^T (+ bias, RowEpi) with A q [M][K] / s [M][K/32],
 // B (weights, rows n) q [npad][K] / s [npad][K/32]; 1-D grid, column blocks fastest.
-template <typename OutT, int WM, int WN, int FM, int FN, int NBUF>
+// IMPL: A is gathered in place from an MX-fp8 shadow map through the RowSrc `ia`
+// (the bf16 GEMM's implicit conv / LSTM-input rows, one byte per element; aq = the
+// e4m3 map, as = its scale map, one E8M0 per 32 elements at element offset / 32):
+// the rows the separate quantisation pass would have materialised, read where they lie.
+template <typename OutT, int WM, int WN, int FM, int FN, int NBUF, bool IMPL>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_mx8_kernel(const uint8_t* __restrict__ aq,
                                                                 const uint8_t* __restrict__ as,
                                                                 const uint8_t* __restrict__ bq,
-                                                                const uint8_t* __restrict__ bs, int K, RowEpi e) {
+                                                                const uint8_t* __restrict__ bs, int K, RowEpi e,
+                                                                RowSrc ia) {
     constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
     constexpr int NW = WM * WN;
     constexpr int LA = BM / (8 * NW);
@@ -1125,66 +1175,128 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mx8_kernel(const uint8_t* _
     const int wr0 = (wave / WN) * FM * 16, wc0 = (wave % WN) * FN * 16;
     const int KB = K / 32;
     const int64_t mrem = e.M - m0;
-    const __amdgpu_buffer_rsrc_t ra = make_rsrc(aq + m0 * K, (uint64_t)mrem * K);
     const __amdgpu_buffer_rsrc_t rb = make_rsrc(bq + (int64_t)n0 * K, (uint64_t)BN * K);
-    const __amdgpu_buffer_rsrc_t rsa = make_rsrc(as + m0 * KB, (uint64_t)mrem * KB);
     const __amdgpu_buffer_rsrc_t rsb = make_rsrc(bs + (int64_t)n0 * KB, (uint64_t)BN * KB);
     const bool sc_a = wv * 64 < BM;                      // wave-uniform: this wave fetches A (else B) scales
     const int srow = wave * 64 + lane - (sc_a ? 0 : BM);
-    const uint32_t soff = (sc_a && srow >= mrem) ? kOOB : (uint32_t)(srow * KB);
-    uint32_t arow[LA];
-#pragma unroll
-    for (int i = 0; i < LA; ++i) {
-        const int r = 8 * (NW * i + wave) + lane / 8;
-        arow[i] = r < mrem ? (uint32_t)(r * K) : kOOB;
-    }
-    auto aoff = [&](int i, int kbyte) -> uint32_t { return arow[i] == kOOB ? kOOB : arow[i] + kbyte; };
     auto boff = [&](int i, int kbyte) -> uint32_t { return (uint32_t)((8 * (NW * i + wave) + lane / 8) * K + kbyte); };
     f32x4 acc[FM][FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gemm_core_mx8<BM, BN, FM, FN, NBUF, decltype(aoff), decltype(boff), NW>(acc, smem, ra, rb, sc_a ? rsa : rsb, aoff,
-                                                                          boff, soff, K / 128, wr0, wc0);
+    if constexpr (IMPL) {
+        // element (= byte) offsets relative to row group hi0, as gemm_rows_dma_kernel's loader
+        const int64_t hi0 = m0 >> ia.rshift;
+        const __amdgpu_buffer_rsrc_t ra = make_rsrc(aq + hi0 * ia.rs_hi, (uint64_t)(ia.src_elems - hi0 * ia.rs_hi));
+        const __amdgpu_buffer_rsrc_t rsa =
+            make_rsrc(as + hi0 * ia.rs_hi / 32, (uint64_t)(ia.src_elems - hi0 * ia.rs_hi) / 32);
+        auto rowinfo = [&](int64_t m, int32_t& off, int32_t& pb, bool& mv) {
+            const int64_t hi = m >> ia.rshift;
+            const int lo = (int)(m & ((1ll << ia.rshift) - 1));
+            off = (int32_t)((hi - hi0) * ia.rs_hi + (int64_t)lo * ia.rs_lo + ia.base_off);
+            pb = lo * ia.pmul + ia.padd;
+            mv = m < ia.M;
+        };
+        int32_t rowoff[LA], posb[LA];
+        bool mval[LA];
+#pragma unroll
+        for (int i = 0; i < LA; ++i) rowinfo(m0 + 8 * (NW * i + wave) + lane / 8, rowoff[i], posb[i], mval[i]);
+        const int kmask = (1 << ia.kshift) - 1;
+        auto aoff = [&](int i, int kbyte) -> uint32_t {
+            const int tap = kbyte >> ia.kshift;
+            const int pos = posb[i] + tap;
+            const uint32_t off = (uint32_t)(rowoff[i] + tap * (int32_t)ia.ks + (kbyte & kmask));
+            const bool ok = mval[i] & (kbyte < ia.K) & (pos >= 0) & (pos < ia.plim);
+            return ok ? off : kOOB;
+        };
+        // the lane's scale row (A: row srow of the tile; its 4 scales of stage st sit in one tap)
+        int32_t soff0 = 0, spb = 0;
+        bool smv = false;
+        if (sc_a) rowinfo(m0 + srow, soff0, spb, smv);
+        auto soff = [&](int st) -> uint32_t {
+            if (!sc_a) return (uint32_t)(srow * KB + 4 * st);
+            const int k0 = 128 * st;
+            const int tap = k0 >> ia.kshift;
+            const int pos = spb + tap;
+            const bool ok = smv & (pos >= 0) & (pos < ia.plim);
+            return ok ? (uint32_t)((soff0 + tap * (int32_t)ia.ks + (k0 & kmask)) >> 5) : kOOB;
+        };
+        gemm_core_mx8<BM, BN, FM, FN, NBUF, decltype(aoff), decltype(boff), NW, decltype(soff)>(
+            acc, smem, ra, rb, sc_a ? rsa : rsb, aoff, boff, soff, K / 128, wr0, wc0);
+    } else {
+        const __amdgpu_buffer_rsrc_t ra = make_rsrc(aq + m0 * K, (uint64_t)mrem * K);
+        const __amdgpu_buffer_rsrc_t rsa = make_rsrc(as + m0 * KB, (uint64_t)mrem * KB);
+        const uint32_t s0 = (sc_a && srow >= mrem) ? kOOB : (uint32_t)(srow * KB);
+        uint32_t arow[LA];
+#pragma unroll
+        for (int i = 0; i < LA; ++i) {
+            const int r = 8 * (NW * i + wave) + lane / 8;
+            arow[i] = r < mrem ? (uint32_t)(r * K) : kOOB;
+        }
+        auto aoff = [&](int i, int kbyte) -> uint32_t { return arow[i] == kOOB ? kOOB : arow[i] + kbyte; };
+        auto soff = [&](int st) -> uint32_t { return s0 == kOOB ? kOOB : s0 + 4 * st; };
+        gemm_core_mx8<BM, BN, FM, FN, NBUF, decltype(aoff), decltype(boff), NW, decltype(soff)>(
+            acc, smem, ra, rb, sc_a ? rsa : rsb, aoff, boff, soff, K / 128, wr0, wc0);
+    }
     __syncthreads();
     constexpr int PF = epi_passes<OutT, FM, FN, NW>((size_t)NBUF * (BM + BN) * 132);
     rows_epilogue_lds<OutT, FM, FN, PF>(acc, e, m0 + wr0, n0 + wc0, lane,
                                         smem + wave * (PF * 16 * FN * 16 * (int)sizeof(OutT)));
 }
 
-template <typename OutT, int WM, int WN, int FM, int FN, int NBUF>
+template <typename OutT, int WM, int WN, int FM, int FN, int NBUF, bool IMPL>
 static hipError_t launch_mx8_cfg(const uint8_t* aq, const uint8_t* as, const uint8_t* bq, const uint8_t* bs, int K,
-                                 const RowEpi& e, int npad, hipStream_t st) {
+                                 const RowEpi& e, int npad, const RowSrc& ia, hipStream_t st) {
     constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
     if (K % 128 || npad % BN || e.N > npad) return hipErrorInvalidValue;
-    auto kern = gemm_mx8_kernel<OutT, WM, WN, FM, FN, NBUF>;
+    auto kern = gemm_mx8_kernel<OutT, WM, WN, FM, FN, NBUF, IMPL>;
     constexpr size_t lds = (size_t)NBUF * (BM + BN) * 132;
     static_assert(lds <= 160 * 1024, "LDS");
     static const hipError_t attr =
         hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (attr != hipSuccess) return attr;
     const unsigned grid = (unsigned)((e.M + BM - 1) / BM) * (unsigned)(npad / BN);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WM * WN), lds, st, aq, as, bq, bs, K, e);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WM * WN), lds, st, aq, as, bq, bs, K, e, ia);
     return hipGetLastError();
 }
 
 // 256 x 256 tiles (8 waves, 128 x 64 per wave) for the batch GEMMs; 64 x 64
 // tiles (2 waves) when the 256-tile grid would not cover the CUs (the
 // per-hop streaming step: M = streams x bins)
-template <typename OutT>
-hipError_t launch_gemm_mx8(const uint8_t* aq, const uint8_t* as, const uint8_t* bq, const uint8_t* bs, int K,
-                           const RowEpi& e, int npad, hipStream_t st) {
+template <typename OutT, bool IMPL>
+static hipError_t launch_mx8_any(const uint8_t* aq, const uint8_t* as, const uint8_t* bq, const uint8_t* bs, int K,
+                                 const RowEpi& e, int npad, const RowSrc& ia, hipStream_t st) {
     if (e.M <= 0) return hipSuccess;
     const int64_t big_tiles = (e.M + 255) / 256 * ((npad + 255) / 256);
     if (big_tiles < 256 && npad % 64 == 0)
-        return launch_mx8_cfg<OutT, 2, 1, 2, 4, 2>(aq, as, bq, bs, K, e, npad, st);
-    return launch_mx8_cfg<OutT, 2, 4, 8, 4, 2>(aq, as, bq, bs, K, e, npad, st);
+        return launch_mx8_cfg<OutT, 2, 1, 2, 4, 2, IMPL>(aq, as, bq, bs, K, e, npad, ia, st);
+    return launch_mx8_cfg<OutT, 2, 4, 8, 4, 2, IMPL>(aq, as, bq, bs, K, e, npad, ia, st);
+}
+
+template <typename OutT>
+hipError_t launch_gemm_mx8(const uint8_t* aq, const uint8_t* as, const uint8_t* bq, const uint8_t* bs, int K,
+                           const RowEpi& e, int npad, hipStream_t st) {
+    return launch_mx8_any<OutT, false>(aq, as, bq, bs, K, e, npad, RowSrc{}, st);
+}
+template <typename OutT>
+hipError_t launch_gemm_mx8_rows(const RowSrc& a, const uint8_t* as_map, const uint8_t* bq, const uint8_t* bs, int K,
+                                const RowEpi& e, int npad, hipStream_t st) {
+    // a 128-k stage inside one tap, and every row / tap offset a multiple of 128 elements (the
+    // stage's 4 scale bytes are one aligned 4-byte DMA)
+    if (((1 << a.kshift) % 128) || a.K != K || a.M != e.M || a.rs_hi % 128 || a.rs_lo % 128 || a.ks % 128 ||
+        a.base_off % 128)
+        return hipErrorInvalidValue;
+    return launch_mx8_any<OutT, true>(reinterpret_cast<const uint8_t*>(a.src), as_map, bq, bs, K, e, npad, a, st);
 }
 template hipError_t launch_gemm_mx8<bf16_t>(const uint8_t*, const uint8_t*, const uint8_t*, const uint8_t*, int,
                                             const RowEpi&, int, hipStream_t);
 template hipError_t launch_gemm_mx8<float>(const uint8_t*, const uint8_t*, const uint8_t*, const uint8_t*, int,
                                            const RowEpi&, int, hipStream_t);
+template hipError_t launch_gemm_mx8_rows<bf16_t>(const RowSrc&, const uint8_t*, const uint8_t*, const uint8_t*, int,
+                                                 const RowEpi&, int, hipStream_t);
+template hipError_t launch_gemm_mx8_rows<float>(const RowSrc&, const uint8_t*, const uint8_t*, const uint8_t*, int,
+                                                const RowEpi&, int, hipStream_t);
 
 template hipError_t launch_gemm_rows<float, float>(const RowSrc&, const float*, int64_t, int, const RowEpi&, int,
                                                    hipStream_t);
@@ -1463,17 +1575,38 @@ template hipError_t launch_lstm_step<bf16_t>(const StepArgs&, int, int, hipStrea
 template <typename T, int CELLS, int S>
 __global__ __launch_bounds__(256) void lstm_combine_kernel(const T* __restrict__ y, T* __restrict__ dst,
                                                            int64_t nframes, int H, int dshift, int64_t ldf,
-                                                           int64_t ldd) {
+                                                           int64_t ldd, uint8_t* __restrict__ q8,
+                                                           uint8_t* __restrict__ qs) {
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;    // (frame, j)
-    if (idx >= nframes * H) return;
+    if (idx >= nframes * H) return;                                  // wave-uniform (H % 64 == 0)
     const int64_t f = idx / H;
     const int j = (int)(idx - f * H);
     const T* row = y + f * (CELLS * S) * (int64_t)H + j;
     const int64_t o = f * ldf + (int64_t)(j >> dshift) * ldd + (j & ((1 << dshift) - 1));
     if (CELLS * S == 4) {   // rows (cell, s): 0 = R(x_r), 1 = R(x_i), 2 = I(x_r), 3 = I(x_i)
         const float rr = to_f32(row[0]), ri = to_f32(row[H]), ir = to_f32(row[2 * H]), ii = to_f32(row[3 * H]);
-        dst[o] = to_elem<T>(rr - ii);
-        dst[o + (1 << dshift)] = to_elem<T>(ri + ir);
+        const T vr = to_elem<T>(rr - ii), vi = to_elem<T>(ri + ir);
+        dst[o] = vr;
+        dst[o + (1 << dshift)] = vi;
+        if constexpr (sizeof(T) == 2) {
+            if (q8) {
+                // MX-fp8 shadow (RowEpi::q8 layout): the 32 channels of a group are 32 adjacent
+                // threads (j), one E8M0 per group from the amax over them, mx8_quant_kernel's rule
+                float x[2] = {to_f32(vr), to_f32(vi)};
+                const int64_t oo[2] = {o, o + (1 << dshift)};
+#pragma unroll
+                for (int h2 = 0; h2 < 2; ++h2) {
+                    float amax = fabsf(x[h2]);
+#pragma unroll
+                    for (int s = 1; s < 32; s <<= 1) amax = fmaxf(amax, __shfl_xor(amax, s));
+                    const int ebits = (int)((__float_as_uint(amax) >> 23) & 0xFF);
+                    const int code = ebits > 8 ? ebits - 8 : 0;
+                    const float v = fminf(fmaxf(ldexpf(x[h2], 127 - code), -448.f), 448.f);
+                    q8[oo[h2]] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(v, 0.f, 0, false) & 0xFF);
+                    if ((j & 31) == 0) qs[oo[h2] >> 5] = (uint8_t)code;
+                }
+            }
+        }
     } else {
         dst[o] = row[0];
     }
@@ -1481,22 +1614,23 @@ __global__ __launch_bounds__(256) void lstm_combine_kernel(const T* __restrict__
 
 template <typename T>
 hipError_t launch_lstm_combine(const T* y, T* dst, int64_t nframes, int H, int cells, int seqs, int dshift,
-                               int64_t ldf, int64_t ldd, hipStream_t st) {
+                               int64_t ldf, int64_t ldd, hipStream_t st, uint8_t* q8, uint8_t* qs) {
     const int64_t n = nframes * H;
     if (n <= 0) return hipSuccess;
+    if (q8 && (H % 64 || (1 << dshift) % 32 || cells * seqs != 4)) return hipErrorInvalidValue;
     const dim3 grid((unsigned)((n + 255) / 256));
     if (cells == 2 && seqs == 2)
         hipLaunchKernelGGL((lstm_combine_kernel<T, 2, 2>), grid, dim3(256), 0, st, y, dst, nframes, H, dshift, ldf,
-                           ldd);
+                           ldd, q8, qs);
     else
         hipLaunchKernelGGL((lstm_combine_kernel<T, 1, 1>), grid, dim3(256), 0, st, y, dst, nframes, H, dshift, ldf,
-                           ldd);
+                           ldd, q8, qs);
     return hipGetLastError();
 }
 template hipError_t launch_lstm_combine<float>(const float*, float*, int64_t, int, int, int, int, int64_t, int64_t,
-                                               hipStream_t);
+                                               hipStream_t, uint8_t*, uint8_t*);
 template hipError_t launch_lstm_combine<bf16_t>(const bf16_t*, bf16_t*, int64_t, int, int, int, int, int64_t,
-                                                int64_t, hipStream_t);
+                                                int64_t, hipStream_t, uint8_t*, uint8_t*);
 
 // --------------------------------------------------------------------------
 template <typename T>

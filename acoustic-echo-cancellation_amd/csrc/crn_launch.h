@@ -69,6 +69,11 @@ struct RowEpi {
     // stored at element offset split_add + (n - nsplit) instead of n
     int32_t nsplit = 0x7fffffff;
     int64_t split_add = 0;
+    // MX-fp8 shadow of the output (bf16 outputs, N % 32 == 0): e4m3 bytes at the output's element
+    // offsets (q8) and one E8M0 scale per 32-column group at element offset / 32 (qs), the
+    // operand an MX GEMM consumer reads in place (launch_gemm_mx8_rows); null: none
+    uint8_t* q8 = nullptr;
+    uint8_t* qs = nullptr;
 };
 
 // One LSTM frame step for CELLS weight sets x S input sequences (v1: 1x1,
@@ -141,6 +146,12 @@ hipError_t launch_mx8_quant(const RowSrc& a, uint8_t* q, uint8_t* s, hipStream_t
 template <typename OutT>
 hipError_t launch_gemm_mx8(const uint8_t* aq, const uint8_t* as, const uint8_t* bq, const uint8_t* bs, int K,
                            const RowEpi& e, int npad, hipStream_t st);
+// the same GEMM with the A operand gathered in place from an MX-fp8 shadow map (RowEpi::q8 / qs
+// of its producer): a = the bf16 GEMM's RowSrc with src = the e4m3 map (one byte per element),
+// as_map = its scale map; needs 2^kshift % 128 == 0 (a 128-k stage inside one tap)
+template <typename OutT>
+hipError_t launch_gemm_mx8_rows(const RowSrc& a, const uint8_t* as_map, const uint8_t* bq, const uint8_t* bs, int K,
+                                const RowEpi& e, int npad, hipStream_t st);
 template <typename T>
 hipError_t launch_front(const FrontArgs& a, int B, hipStream_t st);
 hipError_t launch_back(const BackArgs& a, int B, int mode, hipStream_t st);
@@ -148,7 +159,8 @@ template <typename T>
 hipError_t launch_lstm_step(const StepArgs& a, int cells, int seqs, hipStream_t st);
 template <typename T>
 hipError_t launch_lstm_combine(const T* y, T* dst, int64_t nframes, int H, int cells, int seqs, int dshift,
-                               int64_t ldf, int64_t ldd, hipStream_t st);
+                               int64_t ldf, int64_t ldd, hipStream_t st, uint8_t* q8 = nullptr,
+                               uint8_t* qs = nullptr);
 
 // Persistent LSTM recurrence (crn_persist.hip): all T frames of one layer in
 // one launch for up to 256 streams (64 G blocks, G = ceil(nb / 64) row

@@ -356,3 +356,34 @@ def test_c3_shape_long_rows_match_reference_port(dtype):
     print(f'{dtype} C3 rows rel {errs} erle delta {d_erle}')
     assert max(errs) <= tol, errs
     assert max(abs(d) for d in d_erle) <= C3_ERLE_DB, d_erle
+
+
+def test_fp8_shadow_operands_bit_exact(monkeypatch):
+    """dtype fp8: the MX-fp8 GEMMs read their e4m3 operands in place from
+    shadows their producers' epilogues write (encoder / decoder GEMMs and the
+    LSTM combine), with no quantisation pass; AEC_CRN_MX8_SHADOW=0 quantises
+    the implicit rows first.  Same rule (E8M0 per 32 k from the bf16 values)
+    on the same values, so the batch forward (ragged rows: M tails, conv
+    padding taps) and the hipGraph per-hop step are bit-identical."""
+    from aec_amd import synth
+    lens = [16000, 9000, 12345, 256, 4000]
+    L = max(lens)
+    sig = [synth.scene(n, 500 + i) for i, n in enumerate(lens)]
+    pad = lambda k: torch.tensor(np.stack([np.pad(s[k], (0, L - len(s[k]))) for s in sig]), device='cuda:0')
+    res = {}
+    for flag in ('0', '1'):
+        monkeypatch.setenv('AEC_CRN_MX8_SHADOW', flag)            # read when the handle is created
+        net, m, conf = build('v2E_16000', 'fp8')
+        with torch.no_grad():
+            out, spec, _ = net.forward_ragged(pad(0), pad(1), lens)
+            net.stream_open(len(lens))
+            hops = [net.stream_step(pad(0)[:, 256 * k:256 * (k + 1)].contiguous(),
+                                    pad(1)[:, 256 * k:256 * (k + 1)].contiguous()).clone() for k in range(12)]
+        torch.cuda.synchronize()
+        res[flag] = (out.cpu(), spec.cpu(), torch.stack(hops).cpu())
+    (o0, s0, h0), (o1, s1, h1) = res['0'], res['1']
+    assert torch.equal(o0, o1)
+    assert torch.equal(h0, h1)
+    for i, n in enumerate(lens):                        # frames past a row's end are unspecified
+        tn = n // 256 + 1
+        assert torch.equal(s0[i, :, :tn], s1[i, :, :tn]), i
