@@ -686,6 +686,14 @@ def main():
                   frames_per_s=c3['value'], ms_per_step=c3['ms_per_step'], rtf_batch1=c3['rtf_batch1'],
                   stage_ms_per_step=c3['stage_ms_per_step'], roofline=c3['roofline'],
                   pipeline_roofline=c3['pipeline_roofline'], erle=c3['erle'], cpu_baseline=c3['cpu_baseline'])
+    c3f = None
+    if world == 1 and not args.no_c3:
+        # the same C3 batch with dtype fp8 (MX-fp8 LSTM input projections and wide conv layers,
+        # e4m3 operands written by the producing epilogues)
+        c3f = run_crn(args, dev, rank, world, 'fp8', args.c3_steps, 2, 256, 160000, False)
+        c3f = dict(workload=crn_workload(args, 'fp8', 256), dtype='fp8', steps=args.c3_steps,
+                   batches_in_flight=c3f['batches_in_flight'], frames_per_s=c3f['value'],
+                   ms_per_step=c3f['ms_per_step'], stage_ms_per_step=c3f['stage_ms_per_step'])
     c5 = None
     if world == 1 and not args.no_c3:
         # C5: the same network fed by the FD-NLMS error spectrum (NLMS -> CRN composition)
@@ -742,6 +750,7 @@ def main():
             'erle': erle,
             'cpu_baseline': cpu,
             'c3_crn_bf16': c3,
+            'c3_crn_fp8': c3f,
             'c5_nlms_crn_bf16': c5,
             'c5_stream_fp8': c5s,
             'train_step': tr,
