@@ -452,7 +452,11 @@ static aec_status pack_decoder_fused(aec_crn_handle* h, Packed& pk, const RealCo
                 if (j > 0) w[(size_t)(Co + o) * pk.kpad + j * Cin + q] = r.w[((size_t)o * Cin + ref(q)) * 5 + (5 - 2 * j)];
             }
     }
-    return upload_packed(h, pk, w, b);
+    aec_status s = upload_packed(h, pk, w, b);
+    // dtype 2: the wide levels on the MX GEMM (parity 1's zero tap is a whole number of 128-k
+    // stages, so each parity's sum is the unfused GEMM's, bit for bit)
+    if (s == AEC_OK && act == 1 && conv_mx8(h, pk, Cin)) s = upload_mx8(h, pk, w);
+    return s;
 }
 
 // LSTM cell(s): unit order u' = d*Q + c <-> reference u = c*D + d; W_hh gate
@@ -536,8 +540,9 @@ static aec_status load_params(aec_crn_handle* h, const float* params, size_t n) 
         // fused parities: bf16 / f32 stores of 16 B never straddle the parity
         // split when Co % 8 == 0; the mask level (Co = 2, f32) stays split
         // (measured, C3 bf16 decoder: unfused 7.31 ms, fused up to Co = 64 6.58, 128 6.42, 256 6.61);
-        // with dtype fp8 the levels the MX GEMM takes (Co >= 128) stay split
-        if (cl != 1 && co <= h->dec_fuse_max && co % 8 == 0 && !(h->mx8 && co >= 128)) {
+        // with dtype fp8 the levels the MX GEMM takes (Co >= 128) are fused too (one launch per level
+        // instead of two in the per-hop step)
+        if (cl != 1 && co % 8 == 0 && (co <= h->dec_fuse_max || (h->mx8 && h->dec_fuse_max >= 0))) {
             aec_status s = pack_decoder_fused(h, h->decf[d], r, act, alpha);
             if (s != AEC_OK) return s;
         }
@@ -658,7 +663,22 @@ struct Bufs {
     uint8_t* const* cats;
     uint8_t* xn8;           //   and of xn
     uint8_t* xns;
+    // split-K workspace of the MX conv GEMMs (per-hop streaming only; null: no split)
+    float* skp = nullptr;
+    int* skc = nullptr;
+    int64_t sk_bytes = 0;
+    int32_t skc_n = 0;
 };
+
+// K slices of an MX conv GEMM in the per-hop step (its grid alone covers a fraction of the
+// CUs): >= 3 stages of 128 k per slice.  Chosen per layer, never from the row count.
+static int conv_ksplit(int kpad) {
+    static const int mx = [] { const char* v = getenv("AEC_CRN_SPLITK"); return v ? atoi(v) : 4; }();
+    const int nst = kpad / 128;
+    int ks = 1;
+    while (ks * 2 <= mx && nst >= 6 * ks) ks *= 2;
+    return ks;
+}
 
 // an output with an MX-fp8 shadow (bf16 GEMM epilogues only)
 template <typename T>
@@ -673,8 +693,16 @@ static void set_shadow(crn::RowEpi& e, uint8_t* q8, uint8_t* qs) {
 // (q8 / qs, written by its producers), else quantised into bf.aq / bf.as first
 template <typename T>
 static aec_status mx8_gemm(aec_crn_handle* h, const crn::RowSrc& a, const uint8_t* q8, const uint8_t* qs,
-                           const Bufs& bf, const uint8_t* wq, const uint8_t* wsc, int K, const crn::RowEpi& e, int npad,
-                           hipStream_t st) {
+                           const Bufs& bf, const uint8_t* wq, const uint8_t* wsc, int K, const crn::RowEpi& e0, int npad,
+                           hipStream_t st, bool conv = false) {
+    crn::RowEpi e = e0;
+    if (conv && bf.skp) {
+        e.ksplit = conv_ksplit(K);
+        e.skp = bf.skp;
+        e.skc = bf.skc;
+        e.sk_bytes = bf.sk_bytes;
+        e.skc_n = bf.skc_n;
+    }
     if (q8) {
         crn::RowSrc a8 = a;
         a8.src = q8;
@@ -684,6 +712,26 @@ static aec_status mx8_gemm(aec_crn_handle* h, const crn::RowSrc& a, const uint8_
     CRN_TRY(h, crn::launch_mx8_quant(a, bf.aq, bf.as, st));
     CRN_TRY(h, crn::launch_gemm_mx8<T>(bf.aq, bf.as, wq, wsc, K, e, npad, st));
     return AEC_OK;
+}
+
+// split-K workspace the MX conv GEMMs of a B-row step need (conv_ksplit per layer)
+static void splitk_need(const aec_crn_handle* h, int64_t B, int64_t* bytes, int64_t* tiles) {
+    const int* ch = h->cfg.conv_channels;
+    *bytes = 0;
+    *tiles = 0;
+    auto need = [&](int64_t M, int N, int kpad) {
+        *bytes = std::max(*bytes, crn::mx8_splitk_bytes(M, N, conv_ksplit(kpad)));
+        *tiles = std::max(*tiles, crn::mx8_splitk_tiles(M, N));
+    };
+    for (int i = 0; i < h->L; ++i)
+        if (h->enc[i].wq) need(B * (128 >> i), ch[i + 1], h->enc[i].kpad);
+    for (int d = 0; d < h->L; ++d) {
+        if (h->decf[d].wq) need(B * (256 >> (h->L - d)), h->decf[d].N, h->decf[d].kpad);
+        for (int par = 0; par < 2; ++par) {
+            const Packed& pk = h->dec[2 * d + par];
+            if (pk.wq) need(B * (256 >> (h->L - d)), pk.N, pk.kpad);
+        }
+    }
 }
 
 template <typename T>
@@ -717,7 +765,7 @@ static aec_status run_encoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipS
         set_shadow<T>(e, bf.cat8[i + 1], bf.cats[i + 1]);
         if (pk.wq) {                       // dtype 2: e4m3 rows + E8M0 scales, scaled-MFMA GEMM
             s = mx8_gemm<T>(h, a, i > 0 ? bf.cat8[i] : nullptr, i > 0 ? bf.cats[i] : nullptr, bf, pk.wq, pk.wsc,
-                            pk.kpad, e, pk.npad8, st);
+                            pk.kpad, e, pk.npad8, st, true);
             if (s != AEC_OK) return s;
             continue;
         }
@@ -815,6 +863,12 @@ static aec_status run_decoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipS
             e.nsplit = pk.N / 2;
             e.split_add = ldo;
             set_shadow<T>(e, bf.cat8[cl - 1], bf.cats[cl - 1]);
+            if (pk.wq) {                   // dtype 2 (see conv_mx8)
+                const aec_status s = mx8_gemm<T>(h, a, bf.cat8[cl], bf.cats[cl], bf, pk.wq, pk.wsc, pk.kpad, e,
+                                                 pk.npad8, st, true);
+                if (s != AEC_OK) return s;
+                continue;
+            }
             CRN_TRY(h, (crn::launch_gemm_rows<T, T>(a, reinterpret_cast<const T*>(pk.w), pk.kpad,
                                                      (int)(pk.kpad * sizeof(T) / crn::kStageBytes), e, pk.npad, st)));
             continue;
@@ -841,7 +895,7 @@ static aec_status run_decoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipS
                 set_shadow<T>(e, bf.cat8[cl - 1], bf.cats[cl - 1]);
                 if (pk.wq) {               // dtype 2 (see conv_mx8)
                     const aec_status s = mx8_gemm<T>(h, a, bf.cat8[cl], bf.cats[cl], bf, pk.wq, pk.wsc, pk.kpad, e,
-                                                     pk.npad8, st);
+                                                     pk.npad8, st, true);
                     if (s != AEC_OK) return s;
                     continue;
                 }
@@ -881,6 +935,9 @@ static aec_status run_persist(aec_crn_handle* h, int l, int32_t B, int64_t Tmax,
     // polls before a wave gives up; AEC_CRN_SPIN_LIMIT (read per call) forces a timeout in the tests
     const char* sl = getenv("AEC_CRN_SPIN_LIMIT");
     const int spin = sl ? std::max(1, atoi(sl)) : crn::kPersistSpinLimit;
+    // AEC_CRN_PERSIST_STALL=1 (read per call, tests only): the poll targets are never reached
+    const char* ss = getenv("AEC_CRN_PERSIST_STALL");
+    const int stall = ss && atoi(ss) != 0 ? (1 << 30) : 0;
     static const int pra = [] { const char* v = getenv("CRN_PERSIST_RA"); return v ? atoi(v) : 1; }();
     // one block per CU: 64 streams (two teams of 32 blocks) per 64 CUs, at most 256 streams per launch
     const int32_t chunk = 64 * std::min(4, h->num_cus / 64);
@@ -898,6 +955,7 @@ static aec_status run_persist(aec_crn_handle* h, int l, int32_t B, int64_t Tmax,
         a.G = (nb + 63) / 64;
         a.spin_limit = spin;
         a.read_ahead = pra;
+        a.stall = stall;
         // arrival counters only: the error word keeps any timeout of this call's earlier launches
         CRN_TRY(h, hipMemsetAsync(h->psync, 0, crn::kPersistCounters * sizeof(int), st));
         CRN_TRY(h, crn::launch_lstm_persist(a, st));
@@ -1011,6 +1069,10 @@ struct StreamState {
     std::vector<uint8_t*> cat8, cats;
     uint8_t* xn8 = nullptr;
     uint8_t* xns = nullptr;
+    float* skp = nullptr;                // split-K partial tiles / tile counters of the MX conv GEMMs (Bufs)
+    int* skc = nullptr;
+    int64_t sk_bytes = 0;
+    int32_t skc_n = 0;
     void* ring_y[8][2] = {};             // per LSTM layer: h ring (two frames)
     float* cst[8] = {};                  // per LSTM layer: c
     float* hop = nullptr;                // [2 parity][2 signal][B][256] hop ring (mic, far): the front kernel
@@ -1064,8 +1126,8 @@ template <typename T>
 static aec_status stream_launches(aec_crn_handle* h, int par, const StreamIo& io, hipStream_t st) {
     StreamState& ss = *h->ss;
     const int B = ss.B;
-    const Bufs bf{ss.x0, ss.cat.data(), ss.gx, ss.xn, ss.mask, ss.aq, ss.as, ss.cat8.data(), ss.cats.data(), ss.xn8,
-                  ss.xns};
+    const Bufs bf{ss.x0,       ss.cat.data(), ss.gx,   ss.xn,  ss.mask,     ss.aq,    ss.as, ss.cat8.data(),
+                  ss.cats.data(), ss.xn8,      ss.xns, ss.skp, ss.skc, ss.sk_bytes, ss.skc_n};
     float* cur_mic = ss.hop + (size_t)(par * 2 + 0) * B * 256;
     float* cur_far = ss.hop + (size_t)(par * 2 + 1) * B * 256;
     const float* prev_mic = ss.hop + (size_t)((1 - par) * 2 + 0) * B * 256;
@@ -1349,6 +1411,16 @@ aec_status aec_crn_stream_open(aec_crn_handle* h, int32_t B) {
         CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.xns), (size_t)B * S * H / 32));
     }
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.mask), (size_t)B * 256 * 2 * sizeof(float)));
+    if (h->mx8) {
+        int64_t skb = 0, skt = 0;
+        splitk_need(h, B, &skb, &skt);
+        if (skb > 0 && skt <= INT32_MAX) {
+            CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.skp), (size_t)skb));
+            CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.skc), (size_t)skt * sizeof(int)));   // zeroed
+            ss.sk_bytes = skb;
+            ss.skc_n = (int32_t)skt;
+        }
+    }
     for (int l = 0; l < h->nrnn; ++l) {
         CRN_TRY(h, alloc(&ss.ring_y[l][0], (size_t)B * C * S * H * es));
         CRN_TRY(h, alloc(&ss.ring_y[l][1], (size_t)B * C * S * H * es));

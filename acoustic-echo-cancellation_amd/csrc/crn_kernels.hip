@@ -1157,19 +1157,32 @@ hipError_t launch_mx8_quant(const RowSrc& a, uint8_t* q, uint8_t* s, hipStream_t
 // (the bf16 GEMM's implicit conv / LSTM-input rows, one byte per element; aq = the
 // e4m3 map, as = its scale map, one E8M0 per 32 elements at element offset / 32):
 // the rows the separate quantisation pass would have materialised, read where they lie.
+// ksplit > 1 (split-K, small grids): block b runs K slice b / ntiles of output tile
+// b % ntiles (the slices of one stage range run together), stages [s0, s1); every
+// slice stores its f32 partial tile write-through (sc1) into e.skp, drains, and one
+// lane adds to the tile's counter e.skc[tile] (agent scope); the slice that draws
+// ksplit - 1 reads the other partials with sc1 loads, adds them in slice order to
+// its own in slice order (the same sum whichever slice reduces), resets the counter
+// and runs the epilogue (the in-launch hand-off of the CDNA guide's Guideline 16,
+// counter form).  The sum of slices can differ from ksplit = 1 in the last bits.
 template <typename OutT, int WM, int WN, int FM, int FN, int NBUF, bool IMPL>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_mx8_kernel(const uint8_t* __restrict__ aq,
                                                                 const uint8_t* __restrict__ as,
                                                                 const uint8_t* __restrict__ bq,
                                                                 const uint8_t* __restrict__ bs, int K, RowEpi e,
-                                                                RowSrc ia) {
+                                                                RowSrc ia, int ksplit) {
     constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
     constexpr int NW = WM * WN;
     constexpr int LA = BM / (8 * NW);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int nbn = (e.N + BN - 1) / BN;
-    const int64_t m0 = (int64_t)(blockIdx.x / nbn) * BM;
-    const int n0 = (int)(blockIdx.x % nbn) * BN;
+    const int ntiles = (int)(gridDim.x / (unsigned)ksplit);
+    const int tile = (int)(blockIdx.x % (unsigned)ntiles), slice = (int)(blockIdx.x / (unsigned)ntiles);
+    const int64_t m0 = (int64_t)(tile / nbn) * BM;
+    const int n0 = (int)(tile % nbn) * BN;
+    const int nst = K / 128;
+    const int s0 = slice * nst / ksplit, s1 = (slice + 1) * nst / ksplit;
+    const int kb0 = s0 * 128;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     const int wr0 = (wave / WN) * FM * 16, wc0 = (wave % WN) * FN * 16;
@@ -1179,7 +1192,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mx8_kernel(const uint8_t* _
     const __amdgpu_buffer_rsrc_t rsb = make_rsrc(bs + (int64_t)n0 * KB, (uint64_t)BN * KB);
     const bool sc_a = wv * 64 < BM;                      // wave-uniform: this wave fetches A (else B) scales
     const int srow = wave * 64 + lane - (sc_a ? 0 : BM);
-    auto boff = [&](int i, int kbyte) -> uint32_t { return (uint32_t)((8 * (NW * i + wave) + lane / 8) * K + kbyte); };
+    auto boff = [&](int i, int kbyte) -> uint32_t {
+        return (uint32_t)((8 * (NW * i + wave) + lane / 8) * K + kb0 + kbyte);
+    };
     f32x4 acc[FM][FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -1204,6 +1219,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mx8_kernel(const uint8_t* _
         for (int i = 0; i < LA; ++i) rowinfo(m0 + 8 * (NW * i + wave) + lane / 8, rowoff[i], posb[i], mval[i]);
         const int kmask = (1 << ia.kshift) - 1;
         auto aoff = [&](int i, int kbyte) -> uint32_t {
+            kbyte += kb0;
             const int tap = kbyte >> ia.kshift;
             const int pos = posb[i] + tap;
             const uint32_t off = (uint32_t)(rowoff[i] + tap * (int32_t)ia.ks + (kbyte & kmask));
@@ -1215,6 +1231,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mx8_kernel(const uint8_t* _
         bool smv = false;
         if (sc_a) rowinfo(m0 + srow, soff0, spb, smv);
         auto soff = [&](int st) -> uint32_t {
+            st += s0;
             if (!sc_a) return (uint32_t)(srow * KB + 4 * st);
             const int k0 = 128 * st;
             const int tap = k0 >> ia.kshift;
@@ -1223,21 +1240,71 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mx8_kernel(const uint8_t* _
             return ok ? (uint32_t)((soff0 + tap * (int32_t)ia.ks + (k0 & kmask)) >> 5) : kOOB;
         };
         gemm_core_mx8<BM, BN, FM, FN, NBUF, decltype(aoff), decltype(boff), NW, decltype(soff)>(
-            acc, smem, ra, rb, sc_a ? rsa : rsb, aoff, boff, soff, K / 128, wr0, wc0);
+            acc, smem, ra, rb, sc_a ? rsa : rsb, aoff, boff, soff, s1 - s0, wr0, wc0);
     } else {
         const __amdgpu_buffer_rsrc_t ra = make_rsrc(aq + m0 * K, (uint64_t)mrem * K);
         const __amdgpu_buffer_rsrc_t rsa = make_rsrc(as + m0 * KB, (uint64_t)mrem * KB);
-        const uint32_t s0 = (sc_a && srow >= mrem) ? kOOB : (uint32_t)(srow * KB);
+        const uint32_t so0 = (sc_a && srow >= mrem) ? kOOB : (uint32_t)(srow * KB);
         uint32_t arow[LA];
 #pragma unroll
         for (int i = 0; i < LA; ++i) {
             const int r = 8 * (NW * i + wave) + lane / 8;
             arow[i] = r < mrem ? (uint32_t)(r * K) : kOOB;
         }
-        auto aoff = [&](int i, int kbyte) -> uint32_t { return arow[i] == kOOB ? kOOB : arow[i] + kbyte; };
-        auto soff = [&](int st) -> uint32_t { return s0 == kOOB ? kOOB : s0 + 4 * st; };
+        auto aoff = [&](int i, int kbyte) -> uint32_t { return arow[i] == kOOB ? kOOB : arow[i] + kb0 + kbyte; };
+        auto soff = [&](int st) -> uint32_t { return so0 == kOOB ? kOOB : so0 + 4 * (s0 + st); };
         gemm_core_mx8<BM, BN, FM, FN, NBUF, decltype(aoff), decltype(boff), NW, decltype(soff)>(
-            acc, smem, ra, rb, sc_a ? rsa : rsb, aoff, boff, soff, K / 128, wr0, wc0);
+            acc, smem, ra, rb, sc_a ? rsa : rsb, aoff, boff, soff, s1 - s0, wr0, wc0);
+    }
+    if (ksplit > 1) {
+        // partial tile [tile][slice][fm][fn][wave][lane] f32x4: one 1-KiB write-through store per fragment
+        constexpr int TILE = FM * FN * NW * 64;                     // f32x4 per partial tile
+        const __amdgpu_buffer_rsrc_t rp =
+            make_rsrc(e.skp + (size_t)tile * ksplit * TILE * 4, (uint64_t)ksplit * TILE * 16);
+        auto poff = [&](int sl, int fm, int fn) -> uint32_t {
+            return (uint32_t)((((sl * FM + fm) * FN + fn) * NW + wave) * 64 + lane) * 16u;
+        };
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) {
+                const f32x4 v = acc[fm][fn];
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])},
+                    rp, poff(slice, fm, fn), 0, 16);
+            }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");              // every storing wave drains
+        __syncthreads();
+        int* flag = reinterpret_cast<int*>(smem);
+        if (threadIdx.x == 0)
+            *flag = __hip_atomic_fetch_add(e.skc + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (*flag != ksplit - 1) return;                              // block-uniform: not the reducer
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");        // no load above the counter (sc1 loads)
+        // the sum in slice order whichever slice reduces (its own partial from registers)
+        f32x4 own[FM][FN];
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) {
+                own[fm][fn] = acc[fm][fn];
+                acc[fm][fn] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        for (int sl = 0; sl < ksplit; ++sl) {
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+                for (int fn = 0; fn < FN; ++fn) {
+                    f32x4 v = own[fm][fn];
+                    if (sl != slice) {
+                        const auto w = __builtin_amdgcn_raw_buffer_load_b128(rp, poff(sl, fm, fn), 0, 16);
+                        v = f32x4{__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]),
+                                  __uint_as_float(w[3])};
+                    }
+                    acc[fm][fn] += v;
+                }
+        }
+        if (threadIdx.x == 0) __hip_atomic_store(e.skc + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     constexpr int PF = epi_passes<OutT, FM, FN, NW>((size_t)NBUF * (BM + BN) * 132);
@@ -1256,10 +1323,19 @@ static hipError_t launch_mx8_cfg(const uint8_t* aq, const uint8_t* as, const uin
     static const hipError_t attr =
         hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (attr != hipSuccess) return attr;
-    const unsigned grid = (unsigned)((e.M + BM - 1) / BM) * (unsigned)(npad / BN);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WM * WN), lds, st, aq, as, bq, bs, K, e, ia);
+    const int64_t tiles = (e.M + BM - 1) / BM * ((e.N + BN - 1) / BN);   // column tiles past N: none
+    const int ksplit = e.ksplit > 1 ? e.ksplit : 1;
+    if (ksplit > 1 && (!e.skp || !e.skc || tiles > e.skc_n || K / 128 < ksplit ||
+                       tiles * ksplit * BM * BN * 4 > e.sk_bytes))
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(tiles * ksplit)), dim3(64 * WM * WN), lds, st, aq, as, bq, bs, K, e, ia,
+                       ksplit);
     return hipGetLastError();
 }
+
+// split-K runs the 64 x 64 tile (launch_mx8_any)
+int64_t mx8_splitk_tiles(int64_t M, int N) { return (M + 63) / 64 * ((N + 63) / 64); }
+int64_t mx8_splitk_bytes(int64_t M, int N, int ksplit) { return mx8_splitk_tiles(M, N) * ksplit * 64 * 64 * 4; }
 
 // 256 x 256 tiles (8 waves, 128 x 64 per wave) for the batch GEMMs; 64 x 64
 // tiles (2 waves) when the 256-tile grid would not cover the CUs (the
@@ -1269,7 +1345,7 @@ static hipError_t launch_mx8_any(const uint8_t* aq, const uint8_t* as, const uin
                                  const RowEpi& e, int npad, const RowSrc& ia, hipStream_t st) {
     if (e.M <= 0) return hipSuccess;
     const int64_t big_tiles = (e.M + 255) / 256 * ((npad + 255) / 256);
-    if (big_tiles < 256 && npad % 64 == 0)
+    if ((big_tiles < 256 || e.ksplit > 1) && npad % 64 == 0)
         return launch_mx8_cfg<OutT, 2, 1, 2, 4, 2, IMPL>(aq, as, bq, bs, K, e, npad, ia, st);
     return launch_mx8_cfg<OutT, 2, 4, 8, 4, 2, IMPL>(aq, as, bq, bs, K, e, npad, ia, st);
 }

@@ -74,7 +74,19 @@ struct RowEpi {
     // operand an MX GEMM consumer reads in place (launch_gemm_mx8_rows); null: none
     uint8_t* q8 = nullptr;
     uint8_t* qs = nullptr;
+    // split-K (launch_gemm_mx8*): ksplit > 1 runs the 64 x 64 tile grid ksplit times over K
+    // slices; skp holds the f32 partial tiles (sk_bytes >= mx8_splitk_bytes), skc one arrival
+    // counter per output tile (skc_n >= mx8_splitk_tiles ints, zero between launches).  The
+    // caller picks ksplit per layer (never from M), so a row's result does not depend on the
+    // batch it sits in.
+    int32_t ksplit = 1;
+    int32_t skc_n = 0;
+    float* skp = nullptr;
+    int* skc = nullptr;
+    int64_t sk_bytes = 0;
 };
+int64_t mx8_splitk_tiles(int64_t M, int N);
+int64_t mx8_splitk_bytes(int64_t M, int N, int ksplit);
 
 // One LSTM frame step for CELLS weight sets x S input sequences (v1: 1x1,
 // v2 NavieComplexLSTM: 2x2), gate columns packed per 16 units (i|f|g|o).
@@ -178,6 +190,7 @@ struct PersistArgs {
     int32_t G;                  // row groups (1..4)
     int32_t spin_limit;         // polls before a wave gives up (error word set)
     int32_t read_ahead = 1;     // read the next phase's counter at chunk 7 (CRN_PERSIST_RA, A/B)
+    int32_t stall = 0;          // added to every poll target (tests only: a team that never arrives)
 };
 constexpr int kPersistCounters = 8 * 2 * 16;     // 8 teams x 2 halves, one 64-B line each
 constexpr int kPersistErr = kPersistCounters;    // error word

@@ -208,6 +208,7 @@ __global__ __launch_bounds__(kPThreads, 1) void lstm_persist2_kernel(PersistArgs
     };
     auto poll = [&](int hm, int target) {
         if (stalled) return;
+        target += p.stall;
         if (pre_hm == hm) {
             pre_hm = -1;
             if (__builtin_amdgcn_readfirstlane(pre_v) >= target) return;

@@ -292,20 +292,23 @@ def test_persistent_recurrence_matches_step_kernel(monkeypatch):
 
 def test_persistent_timeout_fails_that_call(monkeypatch):
     """A persistent-grid timeout is reported by the call that hit it: with the
-    poll bound forced to one poll (AEC_CRN_SPIN_LIMIT, read per call) the
-    waves give up waiting for their team, the grid drains, and that
-    forward_ragged raises; the next call with the normal bound on the same
-    handle succeeds and equals a fresh handle's output bit for bit."""
+    poll targets made unreachable (AEC_CRN_PERSIST_STALL, read per call: a
+    team that never arrives) and the poll bound cut to 64 polls
+    (AEC_CRN_SPIN_LIMIT), every wave gives up waiting, the grid drains, and
+    that forward_ragged raises; the next call with the normal settings on the
+    same handle succeeds and equals a fresh handle's output bit for bit."""
     monkeypatch.delenv('AEC_CRN_PERSIST', raising=False)
     net, m, conf = build('v2E_16000', 'bf16')
     from aec_amd import synth
     B, n = 64, 32000
     mic, far, _ = synth.batch(B, n, seed0=950)
     M, F = (torch.from_numpy(a).to('cuda:0') for a in (mic, far))
-    monkeypatch.setenv('AEC_CRN_SPIN_LIMIT', '1')
+    monkeypatch.setenv('AEC_CRN_SPIN_LIMIT', '64')
+    monkeypatch.setenv('AEC_CRN_PERSIST_STALL', '1')
     with torch.no_grad(), pytest.raises(RuntimeError, match='timed out'):
         net.forward_ragged(M, F, [n] * B, want_spec=False)
     monkeypatch.delenv('AEC_CRN_SPIN_LIMIT')
+    monkeypatch.delenv('AEC_CRN_PERSIST_STALL')
     with torch.no_grad():
         o, _, _ = net.forward_ragged(M, F, [n] * B, want_spec=False)
         fresh, _, _ = build('v2E_16000', 'bf16')
