@@ -134,7 +134,8 @@ __global__ __launch_bounds__(kFusedThreads, 1) void gru_synth_kernel(GruArgs p, 
     }
 
     {
-        // role priorities (AEC_FUSED_MODE bits 3-4 synthesis, 5-6 head, 7-8 gi; timing experiments)
+        // role priorities (AEC_FUSED_MODE bits 3-4 synthesis, 5-6 head, 7-8 gi; timing experiments;
+        // bits 9 / 10 / 11 skip the recurrence / head / gi, tools/modes_r03.sh)
         const int role_prio = wave == 0 ? 0 : (wave <= kGiWaves ? (y.fmode >> 7) & 3
                               : (wave <= kGiWaves + kHeadWaves ? (y.fmode >> 5) & 3 : (y.fmode >> 3) & 3));
         switch (role_prio) {
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(kFusedThreads, 1) void gru_synth_kernel(GruArgs p, 
         float* hb = sHb;
         if (lane < 32) hb[lane] = 0.f;
         for (int c = -3; c <= nch + 2; ++c) {
-            if (c >= 0 && c < nch) {
+            if (c >= 0 && c < nch && !(y.fmode & 512)) {
                 const int f_end = min(kCH, T - c * kCH);
                 const float* gi = sGi + (c & 1) * kCH * 96;
                 float gr = gi[j], gz = gi[32 + j], gn = gi[64 + j];
@@ -221,7 +222,7 @@ __global__ __launch_bounds__(kFusedThreads, 1) void gru_synth_kernel(GruArgs p, 
             }
             if (c + 3 < nch) load_chunk(c + 3);
             const int cg = c + 1;
-            if (cg >= 0 && cg < nch) {
+            if (cg >= 0 && cg < nch && !(y.fmode & 2048)) {
 #pragma unroll 2
                 for (int i = 0; i < kCH / 2; ++i) {
                     const int f = fq + 2 * i;
@@ -245,7 +246,7 @@ __global__ __launch_bounds__(kFusedThreads, 1) void gru_synth_kernel(GruArgs p, 
         const bool oal = ((y.ld_out & 3) == 0) && ((reinterpret_cast<uintptr_t>(y.out) & 15) == 0);
         for (int c = -3; c <= nch + 2; ++c) {
             const int ch = c - 1;
-            if (ch >= 0 && ch < nch) {
+            if (ch >= 0 && ch < nch && !(y.fmode & 1024)) {
                 for (int f = fg; f < kCH; f += kHeadGrp) {
                     const int t = ch * kCH + f;
                     float est = 0.f;
