@@ -85,6 +85,7 @@ struct aec_crn_handle {
     int dec_fuse_max = 128;                        // CRN_DEC_FUSE: fuse the parities of levels with <= this many
                                                    // output channels (HBM-bound layers); 0 = never
     std::vector<Packed> lih, lhh;                  // per LSTM layer
+    std::vector<Packed> lcat;                      // dtype 2, v2: [W_ih | W_hh] MX rows (lstm_step_mx8_kernel)
     bool have_params = false;
     // workspace
     int64_t ws_B = 0, ws_T = 0;
@@ -462,10 +463,14 @@ static aec_status pack_decoder_fused(aec_crn_handle* h, Packed& pk, const RealCo
 // LSTM cell(s): unit order u' = d*Q + c <-> reference u = c*D + d; W_hh gate
 // row p(q, u') = ((u'/16)*4 + q)*16 + u'%16 (i|f|g|o per 16 units), W_ih /
 // bias gate row u'*4 + q (so Gx holds a unit's 4 gates contiguously)
-static aec_status pack_lstm(aec_crn_handle* h, Cursor& cur, Packed& ih, Packed& hh) {
+static aec_status pack_lstm(aec_crn_handle* h, Cursor& cur, Packed& ih, Packed& hh, Packed& cat) {
     const int H = h->H, D = h->D, Q = h->Q, C = h->CELLS;
     const size_t G = (size_t)4 * H;
     std::vector<double> wih((size_t)C * G * H), whh((size_t)C * G * H), bias((size_t)C * G);
+    // dtype 2, NavieComplexLSTM: [W_ih | W_hh] rows (K = 2H) in W_hh's row order for the fused
+    // per-hop layer step (lstm_step_mx8_kernel)
+    const bool want_cat = h->mx8 && C * h->S == 4 && H % 256 == 0;
+    std::vector<double> wcat(want_cat ? (size_t)C * G * 2 * H : 0);
     auto perm = [&](int up) { return (up % Q) * D + up / Q; };
     for (int cell = 0; cell < C; ++cell) {
         const float* Wih = cur.take(G * H);
@@ -484,6 +489,11 @@ static aec_status pack_lstm(aec_crn_handle* h, Cursor& cur, Packed& ih, Packed& 
                     wih[pi * H + kp] = Wih[src * H + perm(kp)];
                     whh[p * H + kp] = Whh[src * H + perm(kp)];
                 }
+                if (want_cat)
+                    for (int kp = 0; kp < H; ++kp) {
+                        wcat[p * 2 * H + kp] = Wih[src * H + perm(kp)];
+                        wcat[p * 2 * H + H + kp] = Whh[src * H + perm(kp)];
+                    }
                 bias[pi] = (double)bih[src] + (double)bhh[src];
             }
     }
@@ -498,7 +508,13 @@ static aec_status pack_lstm(aec_crn_handle* h, Cursor& cur, Packed& ih, Packed& 
         s = upload_mx8(h, ih, wih);
         if (s != AEC_OK) return s;
     }
-    return upload_packed(h, hh, whh, bias);
+    s = upload_packed(h, hh, whh, bias);
+    if (s == AEC_OK && want_cat) {
+        cat.N = (int)(C * G);
+        cat.K = cat.kpad = 2 * H;
+        s = upload_mx8(h, cat, wcat);
+    }
+    return s;
 }
 
 static aec_status load_params(aec_crn_handle* h, const float* params, size_t n) {
@@ -548,7 +564,7 @@ static aec_status load_params(aec_crn_handle* h, const float* params, size_t n) 
         }
     }
     for (int l = 0; l < h->nrnn; ++l) {
-        aec_status s = pack_lstm(h, cur, h->lih[l], h->lhh[l]);
+        aec_status s = pack_lstm(h, cur, h->lih[l], h->lhh[l], h->lcat[l]);
         if (s != AEC_OK) return s;
     }
     if (!cur.ok || cur.off != n) return crn_fail(h, AEC_ERR_INVALID_ARG, "parameter blob layout mismatch");
@@ -1074,6 +1090,11 @@ struct StreamState {
     int64_t sk_bytes = 0;
     int32_t skc_n = 0;
     void* ring_y[8][2] = {};             // per LSTM layer: h ring (two frames)
+    uint8_t* ring_q[8][2] = {};          // dtype 2 MX layer step: h ring as e4m3 [B][C][S][H] + E8M0 [B][C][S][H/32]
+    uint8_t* ring_s[8][2] = {};
+    float* hx = nullptr;                 //   h_t f32 [B][C][S][H] (cell-pair hand-off)
+    int* mx_cnt = nullptr;               //   arrival counters (zero between launches)
+    bool mx_step = false;
     float* cst[8] = {};                  // per LSTM layer: c
     float* hop = nullptr;                // [2 parity][2 signal][B][256] hop ring (mic, far): the front kernel
                                          //   copies each call's hops in, for the next call and the back kernel
@@ -1122,6 +1143,74 @@ static hipGraphNode_t last_node(hipStream_t st) {
     return cs == hipStreamCaptureStatusActive && nd == 1 ? deps[0] : nullptr;
 }
 
+// dtype 2, NavieComplexLSTM, per-hop: layer l as ONE launch (lstm_step_mx8_kernel): [x | h]
+// against [W_ih | W_hh] on the scaled MFMA, the cell update and the combination.  x is read
+// in place from its MX-fp8 shadow (the encoder's / previous combination's epilogue), or,
+// without one (AEC_CRN_MX8_SHADOW=0), quantised first into bf.aq / bf.as by the same rule.
+static aec_status run_lstm_mx_step(aec_crn_handle* h, StreamState& ss, const Bufs& bf, int l, int par, hipStream_t st) {
+    const int* ch = h->cfg.conv_channels;
+    const int L = h->L, H = h->H, S = h->S, D = h->D, Q = h->Q, B = ss.B;
+    const bool last = l + 1 == h->nrnn;
+    crn::StepMxArgs ma{};
+    ma.wq = h->lcat[l].wq;
+    ma.wsc = h->lcat[l].wsc;
+    ma.bias = h->lih[l].bias;
+    // x rows (b, s): the bf16 GEMM's implicit LSTM-input rows (run_lstm_input)
+    const int64_t ld_in = l == 0 ? 2 * ch[L] : (int64_t)S * Q;
+    const int64_t choff = l == 0 ? ch[L] : 0;
+    const uint8_t* x8 = l == 0 ? bf.cat8[L] : bf.xn8;
+    const uint8_t* xs = l == 0 ? bf.cats[L] : bf.xns;
+    if (x8) {
+        ma.xq = x8;
+        ma.xs = xs;
+        ma.x_f = D * ld_in;
+        ma.x_s = Q;
+        ma.x_t = ld_in;
+        ma.x_sh = ilog2(Q);
+        ma.x_0 = choff;
+        ma.x_elems = (int64_t)B * D * ld_in;
+    } else {
+        crn::RowSrc a{};
+        a.src = l == 0 ? bf.cat[L] : bf.xn;
+        a.M = (int64_t)B * S;
+        a.K = H;
+        a.rshift = ilog2(S);
+        a.rs_hi = D * ld_in;
+        a.rs_lo = Q;
+        a.kshift = ilog2(Q);
+        a.ks = ld_in;
+        a.plim = D;
+        a.base_off = choff;
+        a.src_elems = (int64_t)B * D * ld_in;
+        CRN_TRY(h, crn::launch_mx8_quant(a, bf.aq, bf.as, st));
+        ma.xq = bf.aq;                              // dense rows [(b, s)][H]
+        ma.xs = bf.as;
+        ma.x_f = (int64_t)S * H;
+        ma.x_s = H;
+        ma.x_t = 0;
+        ma.x_sh = ilog2(H);
+        ma.x_0 = 0;
+        ma.x_elems = (int64_t)B * S * H;
+    }
+    ma.hq_prev = ss.ring_q[l][1 - par];
+    ma.hs_prev = ss.ring_s[l][1 - par];
+    ma.hq_cur = ss.ring_q[l][par];
+    ma.hs_cur = ss.ring_s[l][par];
+    ma.cst = ss.cst[l];
+    ma.hx = ss.hx;
+    ma.cnt = ss.mx_cnt;
+    ma.dst = reinterpret_cast<crn::bf16_t*>(last ? bf.cat[L] : bf.xn);
+    ma.ldd = last ? 2 * ch[L] : (int64_t)S * Q;
+    ma.ldf = D * ma.ldd;
+    ma.dshift = ilog2(Q);
+    ma.q8 = last ? bf.cat8[L] : bf.xn8;
+    ma.qs = last ? bf.cats[L] : bf.xns;
+    ma.B = B;
+    ma.H = H;
+    CRN_TRY(h, crn::launch_lstm_step_mx8(ma, st));
+    return AEC_OK;
+}
+
 template <typename T>
 static aec_status stream_launches(aec_crn_handle* h, int par, const StreamIo& io, hipStream_t st) {
     StreamState& ss = *h->ss;
@@ -1150,6 +1239,13 @@ static aec_status stream_launches(aec_crn_handle* h, int par, const StreamIo& io
     aec_status s = run_encoder<T>(h, bf, B, st);
     if (s != AEC_OK) return s;
     for (int l = 0; l < h->nrnn; ++l) {
+        if (ss.mx_step) {
+            if constexpr (sizeof(T) == 2) {
+                s = run_lstm_mx_step(h, ss, bf, l, par, st);
+                if (s != AEC_OK) return s;
+            }
+            continue;
+        }
         s = run_lstm_input<T>(h, bf, l, B, st);
         if (s != AEC_OK) return s;
         crn::StepArgs sa{h->lhh[l].w, ss.gx, ss.ring_y[l][1 - par], ss.ring_y[l][par], ss.cst[l], B, h->H, 0, 0};
@@ -1255,6 +1351,7 @@ aec_status aec_crn_create(const aec_crn_config* cfg, const float* params, size_t
     h->decf.assign(h->L, Packed{});
     if (const char* m = std::getenv("CRN_DEC_FUSE")) h->dec_fuse_max = std::atoi(m);
     h->lih.assign(h->nrnn, Packed{});
+    h->lcat.assign(h->nrnn, Packed{});
     h->lhh.assign(h->nrnn, Packed{});
     if (params) {
         const aec_status s = load_params(h, params, n);
@@ -1421,9 +1518,25 @@ aec_status aec_crn_stream_open(aec_crn_handle* h, int32_t B) {
             ss.skc_n = (int32_t)skt;
         }
     }
+    // dtype 2, NavieComplexLSTM: the recurrence runs as lstm_step_mx8_kernel (AEC_CRN_STEP_MX=0: the bf16
+    // step + combine, A/B only)
+    const char* step_mx_env = getenv("AEC_CRN_STEP_MX");
+    const int step_mx = step_mx_env ? atoi(step_mx_env) : 1;
+    ss.mx_step = step_mx != 0 && h->mx8 && C * S == 4 && h->nrnn > 0 && h->lcat[0].wq != nullptr;
+    if (ss.mx_step) {
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.hx), (size_t)B * C * S * H * sizeof(float)));
+        CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.mx_cnt), (size_t)crn::lstm_step_mx8_counters(H, B) * sizeof(int)));
+    }
     for (int l = 0; l < h->nrnn; ++l) {
-        CRN_TRY(h, alloc(&ss.ring_y[l][0], (size_t)B * C * S * H * es));
-        CRN_TRY(h, alloc(&ss.ring_y[l][1], (size_t)B * C * S * H * es));
+        if (ss.mx_step) {
+            for (int r = 0; r < 2; ++r) {
+                CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.ring_q[l][r]), (size_t)B * C * S * H));
+                CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.ring_s[l][r]), (size_t)B * C * S * H / 32));
+            }
+        } else {
+            CRN_TRY(h, alloc(&ss.ring_y[l][0], (size_t)B * C * S * H * es));
+            CRN_TRY(h, alloc(&ss.ring_y[l][1], (size_t)B * C * S * H * es));
+        }
         CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.cst[l]), (size_t)B * C * S * H * sizeof(float)));
     }
     CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.hop), (size_t)4 * B * 256 * sizeof(float)));
@@ -1448,8 +1561,14 @@ aec_status aec_crn_stream_reset(aec_crn_handle* h, int32_t b, void* stream) {
     const size_t hrow = (size_t)h->CELLS * h->S * h->H;       // elements of one stream's h / c rows
     const int b0 = b < 0 ? 0 : b, nb = b < 0 ? ss.B : 1;
     for (int l = 0; l < h->nrnn; ++l) {
-        for (int r = 0; r < 2; ++r)
-            CRN_TRY(h, hipMemsetAsync(reinterpret_cast<char*>(ss.ring_y[l][r]) + b0 * hrow * es, 0, nb * hrow * es, st));
+        for (int r = 0; r < 2; ++r) {
+            if (ss.mx_step) {
+                CRN_TRY(h, hipMemsetAsync(ss.ring_q[l][r] + b0 * hrow, 0, nb * hrow, st));
+                CRN_TRY(h, hipMemsetAsync(ss.ring_s[l][r] + b0 * hrow / 32, 0, nb * hrow / 32, st));
+            } else {
+                CRN_TRY(h, hipMemsetAsync(reinterpret_cast<char*>(ss.ring_y[l][r]) + b0 * hrow * es, 0, nb * hrow * es, st));
+            }
+        }
         CRN_TRY(h, hipMemsetAsync(ss.cst[l] + b0 * hrow, 0, nb * hrow * sizeof(float), st));
     }
     for (int q = 0; q < 4; ++q)
@@ -1536,7 +1655,7 @@ void aec_crn_destroy(aec_crn_handle* h) {
     aec::DeviceGuard dg(h->device);
     stream_free(h);
     for (void* p : h->allocs) (void)hipFree(p);
-    for (auto* v : {&h->enc, &h->dec, &h->decf, &h->lih, &h->lhh})
+    for (auto* v : {&h->enc, &h->dec, &h->decf, &h->lih, &h->lhh, &h->lcat})
         for (Packed& pk : *v) {
             if (pk.w) (void)hipFree(pk.w);
             if (pk.bias) (void)hipFree(pk.bias);

@@ -294,72 +294,63 @@ __global__ __launch_bounds__(256) void crn_back_kernel(BackArgs p) {
 // hop layout load_frame reads) and runs the same transform code as the
 // batch kernels, so a streamed frame is bit-identical to the batch frame.
 // --------------------------------------------------------------------------
-__device__ __forceinline__ void stage_frame(float* reg, const float* prev, const float* cur, int lb) {
-    const float4* p4 = reinterpret_cast<const float4*>(prev) + lb * 4;
-    const float4* c4 = reinterpret_cast<const float4*>(cur) + lb * 4;
-    float4* r0 = reinterpret_cast<float4*>(reg) + lb * 4;
-    float4* r1 = reinterpret_cast<float4*>(reg + aec::kHopStride) + lb * 4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        r0[i] = p4[i];
-        r1[i] = c4[i];
-    }
-}
-// The current hop from the caller's buffer (any alignment: cal = 16-B aligned rows), optionally
-// saved into the ring slot `save` for the next call.
-__device__ __forceinline__ void stage_frame_io(float* reg, const float* prev, const float* cur, bool cal, float* save,
-                                               int lb) {
-    const float4* p4 = reinterpret_cast<const float4*>(prev) + lb * 4;
-    float4* r0 = reinterpret_cast<float4*>(reg) + lb * 4;
-    float4* r1 = reinterpret_cast<float4*>(reg + aec::kHopStride) + lb * 4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        r0[i] = p4[i];
-        const int e = 16 * lb + 4 * i;
-        const float4 c = cal ? *reinterpret_cast<const float4*>(cur + e)
-                             : make_float4(cur[e], cur[e + 1], cur[e + 2], cur[e + 3]);
-        r1[i] = c;
-        if (save) *reinterpret_cast<float4*>(save + e) = c;
-    }
-}
-
+// The per-hop front / back kernels are latency chains (one frame per stream,
+// one 16-lane group per stream): every global load that does not depend on
+// another (the hops, E row, mask row, OLA tail) is issued before the table
+// staging barrier, so the chain holds one memory round trip, not three or four.
 template <typename T>
 __global__ __launch_bounds__(256) void crn_stream_front_kernel(StreamFrontArgs p) {
-    __shared__ __attribute__((aligned(16))) float smem[256 * 2 + 258 * 2 + 512 + 16 * kGroupFloats];
+    __shared__ __attribute__((aligned(16))) float smem[256 * 2 + 258 * 2 + 512 + 2 * 16 * kGroupFloats];
     float2* sTwT = reinterpret_cast<float2*>(smem);
     float2* sTw512 = sTwT + 256;
     float* sHann = reinterpret_cast<float*>(sTw512 + 258);
     float* sGrp = sHann + 512;
     const int tid = threadIdx.x;
-    sTwT[tid] = p.tab->twT[tid];
-    sTw512[tid] = p.tab->tw512[tid];
-    if (tid < 2) sTw512[256 + tid] = p.tab->tw512[256 + tid];
-    sHann[tid] = p.tab->hann[tid];
-    sHann[tid + 256] = p.tab->hann[tid + 256];
-    __syncthreads();
     const int g = tid >> 4, lb = tid & 15;
     const int b = blockIdx.x * 16 + g;
     const int bb = b < p.B ? b : p.B - 1;
-    float* reg = sGrp + g * kGroupFloats;
-    float2 ma[8], mb[8], m128, fa[8], fb[8], f128;
     const bool cal = (p.ld_cur & 3) == 0 && ((reinterpret_cast<uintptr_t>(p.cur_mic) | reinterpret_cast<uintptr_t>(p.cur_far)) & 15) == 0;
+    // both signals' frames [previous hop (ring) | current hop (caller)] straight into this
+    // group's two LDS staging regions (the layout load_frame reads), in flight together with
+    // the table loads; the current hops are also saved to the ring
+    float* reg0 = sGrp + g * kGroupFloats;
+    float* reg1 = sGrp + (16 + g) * kGroupFloats;
+    const float2 t0 = p.tab->twT[tid], t1 = p.tab->tw512[tid];
+    const float2 t2 = tid < 2 ? p.tab->tw512[256 + tid] : make_float2(0.f, 0.f);
+    const float h0 = p.tab->hann[tid], h1 = p.tab->hann[tid + 256];
+    auto stage = [&](float* reg, const float* prev, const float* cur, float* save) __attribute__((always_inline)) {
+        const float4* p4 = reinterpret_cast<const float4*>(prev + (int64_t)bb * 256) + lb * 4;
+        cur += (int64_t)bb * p.ld_cur;
+        float4* r0 = reinterpret_cast<float4*>(reg) + lb * 4;
+        float4* r1 = reinterpret_cast<float4*>(reg + aec::kHopStride) + lb * 4;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        float* save = s == 0 ? p.save_mic : p.save_far;
-        stage_frame_io(reg, (s == 0 ? p.prev_mic : p.prev_far) + (int64_t)bb * 256,
-                       (s == 0 ? p.cur_mic : p.cur_far) + (int64_t)bb * p.ld_cur, cal,
-                       save && b < p.B ? save + (int64_t)b * 256 : nullptr, lb);
-        aec::wave_fence();
+        for (int i = 0; i < 4; ++i) {
+            const int e = 16 * lb + 4 * i;
+            const float4 c = cal ? *reinterpret_cast<const float4*>(cur + e) : make_float4(cur[e], cur[e + 1], cur[e + 2], cur[e + 3]);
+            r0[i] = p4[i];
+            r1[i] = c;
+            if (save && b < p.B) *reinterpret_cast<float4*>(save + (int64_t)b * 256 + e) = c;
+        }
+    };
+    stage(reg0, p.prev_mic, p.cur_mic, p.save_mic);
+    stage(reg1, p.prev_far, p.cur_far, p.save_far);
+    sTwT[tid] = t0;
+    sTw512[tid] = t1;
+    if (tid < 2) sTw512[256 + tid] = t2;
+    sHann[tid] = h0;
+    sHann[tid + 256] = h1;
+    __syncthreads();
+    float2 ma[8], mb[8], m128, fa[8], fb[8], f128;
+    auto xform = [&](float* reg, float2 (&xa)[8], float2 (&xb)[8], float2& x128) __attribute__((always_inline)) {
         float2 v[16];
         aec::load_frame(v, reg, sHann, 0, lb);
         aec::wave_fence();
         aec::fft256<false>(v, lb, reg, sTwT);
-        if (s == 0)
-            aec::rfft_unpack(v, lb, sTw512, ma, mb, m128);
-        else
-            aec::rfft_unpack(v, lb, sTw512, fa, fb, f128);
+        aec::rfft_unpack(v, lb, sTw512, xa, xb, x128);
         aec::wave_fence();
-    }
+    };
+    xform(reg0, ma, mb, m128);
+    xform(reg1, fa, fb, f128);
     if (b >= p.B) return;
     if (p.rows) {   // NLMS: packed rows [B][2][256]; crn_stream_nlms_kernel writes X0
         put_row(p.rows + (int64_t)b * 512, lb, true, ma, mb, m128);
@@ -385,6 +376,39 @@ __global__ __launch_bounds__(256) void crn_stream_back_kernel(StreamBackArgs p) 
     float* sCoff = sHann + 512;
     float* sGrp = sCoff + 256;
     const int tid = threadIdx.x;
+    const int g = tid >> 4, lb = tid & 15;
+    const int b = blockIdx.x * 16 + g;
+    const int bb = b < p.B ? b : p.B - 1;
+    float* reg = sGrp + g * kGroupFloats;
+    float2 v[16];
+    float2 xa[8], xb[8], x128;
+    // independent loads first: the E row (or the mic hops), the mask row, the OLA tail
+    if (p.espec) {   // NLMS: this frame's error row
+        aec::row_to_pairs(p.espec + (int64_t)bb * 256, lb, true, xa, xb, x128);
+    } else {             // the mic frame [prev | cur] into this group's staging region
+        const float4* p4 = reinterpret_cast<const float4*>(p.prev_mic + (int64_t)bb * 256) + lb * 4;
+        const float4* c4 = reinterpret_cast<const float4*>(p.cur_mic + (int64_t)bb * 256) + lb * 4;
+        float4* r0 = reinterpret_cast<float4*>(reg) + lb * 4;
+        float4* r1 = reinterpret_cast<float4*>(reg + aec::kHopStride) + lb * 4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            r0[i] = p4[i];
+            r1[i] = c4[i];
+        }
+    }
+    const float2* mrow = p.mask + (int64_t)bb * 256;
+    float2 mka[8], mkb[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const int kk = lb + 16 * m;
+        mka[m] = kk > 0 ? mrow[kk - 1] : make_float2(0.f, 0.f);
+        mkb[m] = mrow[255 - kk];                         // bin 256 - kk >= 1
+    }
+    const float2 mk128 = mrow[127];
+    const float* tail_in = p.tail + (int64_t)bb * 256;
+    float tl[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) tl[i] = tail_in[lb + 16 * i];
     sTwT[tid] = p.tab->twT[tid];
     sTw512[tid] = p.tab->tw512[tid];
     if (tid < 2) sTw512[256 + tid] = p.tab->tw512[256 + tid];
@@ -392,32 +416,18 @@ __global__ __launch_bounds__(256) void crn_stream_back_kernel(StreamBackArgs p) 
     sHann[tid + 256] = p.tab->hann[tid + 256];
     sCoff[tid] = p.tab->inv_coff[tid];
     __syncthreads();
-    const int g = tid >> 4, lb = tid & 15;
-    const int b = blockIdx.x * 16 + g;
-    const int bb = b < p.B ? b : p.B - 1;
-    float* reg = sGrp + g * kGroupFloats;
-    float2 v[16];
-    float2 xa[8], xb[8], x128;
-    if (p.espec) {   // NLMS: this frame's error row
-        aec::row_to_pairs(p.espec + (int64_t)bb * 256, lb, true, xa, xb, x128);
-    } else {
-        stage_frame(reg, p.prev_mic + (int64_t)bb * 256, p.cur_mic + (int64_t)bb * 256, lb);
-        aec::wave_fence();
+    if (!p.espec) {
         aec::load_frame(v, reg, sHann, 0, lb);
         aec::wave_fence();
         aec::fft256<false>(v, lb, reg, sTwT);
         aec::rfft_unpack(v, lb, sTw512, xa, xb, x128);
     }
-    const float2* mrow = p.mask + (int64_t)bb * 256;
-    const float2 z = make_float2(0.f, 0.f);
-    auto mk = [&](int bin) { return bin > 0 ? mrow[bin - 1] : z; };
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
-        const int kk = lb + 16 * m;
-        xa[m] = apply_mask<MODE>(xa[m], mk(kk));
-        xb[m] = apply_mask<MODE>(xb[m], mk(256 - kk));
+        xa[m] = apply_mask<MODE>(xa[m], mka[m]);
+        xb[m] = apply_mask<MODE>(xb[m], mkb[m]);
     }
-    x128 = apply_mask<MODE>(x128, mk(128));
+    x128 = apply_mask<MODE>(x128, mk128);
     float2 Zk[8], Zmk[8];
     aec::static_for<0, 8>([&](auto mi) {
         constexpr int m = decltype(mi)::value;
@@ -454,7 +464,7 @@ __global__ __launch_bounds__(256) void crn_stream_back_kernel(StreamBackArgs p) 
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int r = lb + 16 * i;
-        out[r] = (tail[r] + reg[r]) * sCoff[r];
+        out[r] = (tl[i] + reg[r]) * sCoff[r];
         tail[r] = reg[256 + r];
     }
 }
@@ -1707,6 +1717,279 @@ template hipError_t launch_lstm_combine<float>(const float*, float*, int64_t, in
                                                hipStream_t, uint8_t*, uint8_t*);
 template hipError_t launch_lstm_combine<bf16_t>(const bf16_t*, bf16_t*, int64_t, int, int, int, int, int64_t,
                                                 int64_t, hipStream_t, uint8_t*, uint8_t*);
+
+// --------------------------------------------------------------------------
+// MX-fp8 LSTM layer step of a NavieComplexLSTM (v2, CELLS = S = 2;
+// dccrn.py:435-446 / dccrn2.py:67-78), the per-hop streaming form (C5): the
+// input projection, the recurrence, the cell update and the combination in
+// ONE launch per layer:
+//   gates_cell = [x | h_cell(t-1)] [W_ih,cell | W_hh,cell]^T + b_ih + b_hh
+// on the scaled MFMA (x, h, W_ih and W_hh as OCP e4m3 with one E8M0 scale per
+// 32 k; K = 2H), then c, h of the cell, then
+//   real = R(x_r) - I(x_i), imag = R(x_i) + I(x_r)   (lstm_combine_kernel's map)
+// Block = one cell x 32 units x kMxSB streams x 2 sequences (A: 64 rows of
+// [x | h]; B: the cell's 128 packed rows, i|f|g|o per 16 units).  The two cell
+// blocks of a (unit block, stream block) hand their h over through hx (sc1
+// stores, an agent-scope counter; the CDNA guide's counter hand-off, as the
+// split-K GEMMs): the block that arrives second combines.  Each block writes
+// c (f32) and its h_t as e4m3 + E8M0 (the next hop's A rows: 32 units = one
+// scale group per (cell, s, stream) row); the combined rows leave as bf16 with
+// their MX-fp8 shadow (RowEpi::q8 layout) for the next layer / the decoder.
+// 128-B K stages by LDS-DMA (gemm_core_mx8's staging and operand map), all K
+// scales of the tile staged once up front.  Waves: 2 row halves x 2 unit
+// halves, so the four gates of a (row, unit) meet in one lane.
+// --------------------------------------------------------------------------
+constexpr int kMxSB = 32;
+constexpr int kMxStepStage = (2 * kMxSB + 128) * 128;          // A 64 + B 128 rows x 128 B
+constexpr int kMxStepBufs = 2;
+size_t lstm_step_mx8_lds(int H) { return (size_t)kMxStepBufs * kMxStepStage + (size_t)(2 * kMxSB + 128) * (2 * H / 32); }
+
+// e4m3 of x / 2^(code - 127), 4 values -> one word (mx8_quant_kernel's conversion)
+__device__ __forceinline__ uint32_t mx8_pack4(float x0, float x1, float x2, float x3, int code) {
+    auto q = [&](float x) { return fminf(fmaxf(ldexpf(x, 127 - code), -448.f), 448.f); };
+    int w = __builtin_amdgcn_cvt_pk_fp8_f32(q(x0), q(x1), 0, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(q(x2), q(x3), w, true);
+    return (uint32_t)w;
+}
+__device__ __forceinline__ int mx8_code(float amax) {
+    const int ebits = (int)((__float_as_uint(amax) >> 23) & 0xFF);     // floor(log2 amax) + 127
+    return ebits > 8 ? ebits - 8 : 0;                                    // E8M0: 2^(code - 127)
+}
+
+__global__ __launch_bounds__(256) void lstm_step_mx8_kernel(StepMxArgs p) {
+    constexpr int SB = kMxSB, S = 2, C = 2, U = 32;
+    constexpr int BM = SB * S, BN = 4 * U;              // 64, 128
+    constexpr int RB = 128, RPI = 8, NW = 4, NBUF = kMxStepBufs;
+    constexpr int LA = BM / (RPI * NW), LB = BN / (RPI * NW);
+    constexpr int STAGE = kMxStepStage;
+    constexpr int FM = 2, FN = 4;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int H = p.H, K2 = 2 * H, KB = K2 / 32;        // scale bytes per row
+    const int nx = H / RB, nst = K2 / RB;               // stages of x, of [x | h]
+    uint8_t* sS = reinterpret_cast<uint8_t*>(smem + NBUF * STAGE);   // [BM + BN][KB]
+    const int nsb = (p.B + SB - 1) / SB;
+    const int unit0 = blockIdx.x * U, cell = (int)blockIdx.y / nsb, sblk = (int)blockIdx.y % nsb, b0 = sblk * SB;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int rh = wave >> 1, uh = wave & 1;
+    const int j = uh * 16 + (lane & 15);                // this lane's unit (of the block's 32)
+    auto xoff = [&](int b, int s, int k) -> int64_t {   // element offset of x (b, s, k)
+        return (int64_t)b * p.x_f + (int64_t)s * p.x_s + (int64_t)(k >> p.x_sh) * p.x_t + (k & ((1 << p.x_sh) - 1)) + p.x_0;
+    };
+
+    // 0. this lane's bias (4 gates) and c_prev for its 8 (row, unit) slots: consumed after the GEMM
+    const float4 bias = *reinterpret_cast<const float4*>(p.bias + ((int64_t)cell * H + unit0 + j) * 4);
+    float cv[FM][4];
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int r = rh * 32 + fm * 16 + 4 * (lane >> 4) + rr, s = r / SB, b = b0 + r % SB;
+            cv[fm][rr] = p.cst[(((int64_t)(b < p.B ? b : 0) * C + cell) * S + s) * H + unit0 + j];
+        }
+    // 1. the GEMM over K = [x | h]
+    const __amdgpu_buffer_rsrc_t rax = make_rsrc(p.xq, (uint64_t)p.x_elems);
+    const __amdgpu_buffer_rsrc_t rah = make_rsrc(p.hq_prev, (uint64_t)p.B * C * S * H);
+    const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.wq + ((int64_t)cell * 4 * H + (int64_t)unit0 * 4) * K2, (uint64_t)BN * K2);
+    const int q_l = lane & 7;
+    auto issue = [&](int st) {
+        char* buf = smem + (st % NBUF) * STAGE;
+        const bool isx = st < nx;
+#pragma unroll
+        for (int i = 0; i < LA; ++i) {
+            const int row = RPI * (NW * i + wave) + lane / 8;
+            const int s = row / SB, b = b0 + row % SB;
+            const int kb = (isx ? st : st - nx) * RB + swz_slot<RB>(row, q_l) * 16;
+            const uint32_t vo = b >= p.B ? kOOB
+                              : isx ? (uint32_t)xoff(b, s, kb)
+                                    : (uint32_t)((((int64_t)b * C + cell) * S + s) * H + kb);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(isx ? rax : rah,
+                                                     (__attribute__((address_space(3))) void*)(buf + RPI * (NW * i + wave) * RB),
+                                                     16, vo, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < LB; ++i) {
+            const int row = RPI * (NW * i + wave) + lane / 8;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rb, (__attribute__((address_space(3))) void*)(buf + BM * RB + RPI * (NW * i + wave) * RB), 16,
+                (uint32_t)(row * K2 + st * RB + swz_slot<RB>(row, q_l) * 16), 0, 0, 0);
+        }
+    };
+#pragma unroll
+    for (int i = 0; i < NBUF - 1; ++i) issue(i);
+    // all K scales of the tile -> LDS while the first stage is in flight; sS row = [x | h] 2H/32
+    // bytes (A rows (s, stream)) or the packed weight row's (B): 16-B pieces where they are
+    // contiguous (h, weights), x by taps of 8 scales (a tap of x spans >= 256 k)
+    {
+        for (int i = tid; i < BN * KB / 16; i += 256) {                 // weights
+            const int row = i / (KB / 16), q16 = i % (KB / 16);
+            reinterpret_cast<uint4*>(sS + (BM + row) * KB)[q16] =
+                reinterpret_cast<const uint4*>(p.wsc + ((int64_t)cell * 4 * H + (int64_t)unit0 * 4 + row) * KB)[q16];
+        }
+        for (int i = tid; i < BM * (KB / 2) / 16; i += 256) {          // h_{t-1}
+            const int row = i / (KB / 32), q16 = i % (KB / 32);
+            const int s = row / SB, b = b0 + row % SB;
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (b < p.B) v = reinterpret_cast<const uint4*>(p.hs_prev + (((int64_t)b * C + cell) * S + s) * (H / 32))[q16];
+            reinterpret_cast<uint4*>(sS + row * KB + KB / 2)[q16] = v;
+        }
+        for (int i = tid; i < BM * (KB / 2) / 8; i += 256) {           // x
+            const int row = i / (KB / 16), q8 = i % (KB / 16);
+            const int s = row / SB, b = b0 + row % SB;
+            uint2 v = make_uint2(0u, 0u);
+            if (b < p.B) v = *reinterpret_cast<const uint2*>(p.xs + (xoff(b, s, q8 * 256) >> 5));
+            reinterpret_cast<uint2*>(sS + row * KB)[q8] = v;
+        }
+    }
+    __syncthreads();                                    // scales staged
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int fr = lane & 15, g = lane >> 4;
+    const int wr0 = rh * 32, wc0 = uh * 64;
+    for (int st = 0; st < nst; ++st) {
+        if (st + NBUF - 2 < nst)
+            wait_vm<(NBUF - 2) * (LA + LB)>();
+        else
+            wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        if (st + NBUF - 1 < nst) issue(st + NBUF - 1);
+        const char* sA = smem + (st % NBUF) * STAGE;
+        const char* sB = sA + BM * RB;
+        i32x8 bfr[FN];
+        int sb[FN];
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+            const int r = wc0 + fn * 16 + fr;
+            const u32x4 lo = *reinterpret_cast<const u32x4*>(sB + r * RB + swz_slot<RB>(r, g) * 16);
+            const u32x4 hi = *reinterpret_cast<const u32x4*>(sB + r * RB + swz_slot<RB>(r, 4 + g) * 16);
+            bfr[fn] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+            sb[fn] = sS[(BM + r) * KB + st * 4 + g];
+        }
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+            const int r = wr0 + fm * 16 + fr;
+            const u32x4 lo = *reinterpret_cast<const u32x4*>(sA + r * RB + swz_slot<RB>(r, g) * 16);
+            const u32x4 hi = *reinterpret_cast<const u32x4*>(sA + r * RB + swz_slot<RB>(r, 4 + g) * 16);
+            const i32x8 af = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+            const int sa = sS[r * KB + st * 4 + g];
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn)
+                acc[fm][fn] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bfr[fn], acc[fm][fn], 0, 0, 0, sa, 0, sb[fn]);
+        }
+    }
+    // 2. cell update (gate order i, f, g, o); c -> HBM, h (f32) -> LDS tile sH[row][U] and -> hx (sc1)
+    __syncthreads();                                    // every wave is done with the stage buffers
+    constexpr int HS = U + 4;                           // padded h-tile row (floats)
+    float* sH = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int r = wr0 + fm * 16 + 4 * (lane >> 4) + rr, s = r / SB, b = b0 + r % SB;
+            const float c = fsigmoid(acc[fm][1][rr] + bias.y) * cv[fm][rr] +
+                            fsigmoid(acc[fm][0][rr] + bias.x) * ftanh(acc[fm][2][rr] + bias.z);
+            const float h = fsigmoid(acc[fm][3][rr] + bias.w) * ftanh(c);
+            if (b < p.B) p.cst[(((int64_t)b * C + cell) * S + s) * H + unit0 + j] = c;
+            sH[r * HS + j] = h;
+        }
+    __syncthreads();
+    // 3a. h_t as e4m3 + E8M0 (4 threads per row, 8 units each), and f32 -> hx for the partner block
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.hx, (uint64_t)p.B * C * S * H * 4);
+    {
+        const int row = tid >> 2, q4 = tid & 3;
+        const int s = row / SB, b = b0 + row % SB;
+        const float4* hp = reinterpret_cast<const float4*>(sH + row * HS + q4 * 8);
+        const float4 v0 = hp[0], v1 = hp[1];
+        float amax = fmaxf(fmaxf(fmaxf(fabsf(v0.x), fabsf(v0.y)), fmaxf(fabsf(v0.z), fabsf(v0.w))),
+                           fmaxf(fmaxf(fabsf(v1.x), fabsf(v1.y)), fmaxf(fabsf(v1.z), fabsf(v1.w))));
+        amax = fmaxf(amax, __shfl_xor(amax, 1));
+        amax = fmaxf(amax, __shfl_xor(amax, 2));
+        const int code = mx8_code(amax);
+        if (b < p.B) {
+            const int64_t ro = (((int64_t)b * C + cell) * S + s) * H;
+            *reinterpret_cast<uint2*>(p.hq_cur + ro + unit0 + q4 * 8) =
+                make_uint2(mx8_pack4(v0.x, v0.y, v0.z, v0.w, code), mx8_pack4(v1.x, v1.y, v1.z, v1.w, code));
+            if (q4 == 0) p.hs_cur[ro / 32 + unit0 / 32] = (uint8_t)code;
+            const uint32_t xo = (uint32_t)((ro + unit0 + q4 * 8) * 4);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(v0.x), __float_as_uint(v0.y), __float_as_uint(v0.z), __float_as_uint(v0.w)},
+                                                   rx, xo, 0, 16);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(v1.x), __float_as_uint(v1.y), __float_as_uint(v1.z), __float_as_uint(v1.w)},
+                                                   rx, xo + 16, 0, 16);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem + 32 * 1024);
+    int* cnt = p.cnt + (int64_t)blockIdx.x * nsb + sblk;
+    if (tid == 0) *flag = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*flag != 1) return;                             // block-uniform: the partner combines
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no load above the counter (sc1 loads)
+    // 3b. the combination of stream bl, units jj .. jj + 3 (8 threads per stream): own cell's h
+    //     from LDS, the partner's from hx
+    {
+        const int bl = tid >> 3, jj = (tid & 7) * 4, b = b0 + bl;
+        const int oc = 1 - cell;
+        float4 own[2], oth[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            own[s] = *reinterpret_cast<const float4*>(sH + (s * SB + bl) * HS + jj);
+            const uint32_t xo = (uint32_t)(((((int64_t)(b < p.B ? b : 0) * C + oc) * S + s) * H + unit0 + jj) * 4);
+            const auto w = __builtin_amdgcn_raw_buffer_load_b128(rx, xo, 0, 16);
+            oth[s] = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]), __uint_as_float(w[3]));
+        }
+        const float4 rr = cell == 0 ? own[0] : oth[0], ri = cell == 0 ? own[1] : oth[1];
+        const float4 ir = cell == 0 ? oth[0] : own[0], ii = cell == 0 ? oth[1] : own[1];
+        const float re[4] = {rr.x - ii.x, rr.y - ii.y, rr.z - ii.z, rr.w - ii.w};
+        const float im[4] = {ri.x + ir.x, ri.y + ir.y, ri.z + ir.z, ri.w + ir.w};
+        const int ju = unit0 + jj;
+        const int64_t o = (int64_t)(b < p.B ? b : 0) * p.ldf + (int64_t)(ju >> p.dshift) * p.ldd + (ju & ((1 << p.dshift) - 1));
+#pragma unroll
+        for (int part = 0; part < 2; ++part) {
+            const float* x = part ? im : re;
+            const int64_t oo = o + (part ? (1 << p.dshift) : 0);
+            bf16_t e[4];
+            float xr[4], amax = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                e[i] = f2bf(x[i]);
+                xr[i] = bf2f(e[i]);                     // the shadow quantises the stored bf16 values
+                amax = fmaxf(amax, fabsf(xr[i]));
+            }
+            if (b < p.B)
+                *reinterpret_cast<uint2*>(p.dst + oo) =
+                    make_uint2((uint32_t)e[0] | ((uint32_t)e[1] << 16), (uint32_t)e[2] | ((uint32_t)e[3] << 16));
+            if (p.q8) {
+                amax = fmaxf(amax, __shfl_xor(amax, 1));
+                amax = fmaxf(amax, __shfl_xor(amax, 2));
+                amax = fmaxf(amax, __shfl_xor(amax, 4));
+                const int code = mx8_code(amax);
+                if (b < p.B) {
+                    *reinterpret_cast<uint32_t*>(p.q8 + oo) = mx8_pack4(xr[0], xr[1], xr[2], xr[3], code);
+                    if (jj == 0) p.qs[oo >> 5] = (uint8_t)code;
+                }
+            }
+        }
+    }
+    if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+hipError_t launch_lstm_step_mx8(const StepMxArgs& a, hipStream_t st) {
+    if (a.H % 256 || a.B <= 0 || (1 << a.dshift) % 32 || (1 << a.x_sh) % 256 || !a.hx || !a.cnt ||
+        (a.x_f | a.x_s | a.x_t | a.x_0) % 256)
+        return hipErrorInvalidValue;
+    const size_t lds = lstm_step_mx8_lds(a.H);
+    if (lds > 160 * 1024 || lds < 32 * 1024 + 16) return hipErrorInvalidValue;
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_step_mx8_kernel),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (attr != hipSuccess) return attr;
+    const int nsb = (a.B + kMxSB - 1) / kMxSB;
+    hipLaunchKernelGGL(lstm_step_mx8_kernel, dim3(a.H / 32, 2 * nsb), dim3(256), lds, st, a);
+    return hipGetLastError();
+}
+int64_t lstm_step_mx8_counters(int H, int B) { return (int64_t)(H / 32) * ((B + kMxSB - 1) / kMxSB); }
 
 // --------------------------------------------------------------------------
 template <typename T>

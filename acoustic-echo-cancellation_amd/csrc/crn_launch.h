@@ -102,6 +102,34 @@ struct StepArgs {
     int32_t mode;               // timing experiments only (CRN_STEP_MODE)
 };
 
+// MX-fp8 layer step of a NavieComplexLSTM (CELLS = S = 2): input projection,
+// recurrence, cell update and combination in one launch (lstm_step_mx8_kernel),
+// the per-hop streaming form.
+struct StepMxArgs {
+    const uint8_t* wq;          // [W_ih | W_hh] e4m3 [2*4H][2H] in W_hh's packed row order (pack_lstm),
+    const uint8_t* wsc;         //   E8M0 per 32 k [2*4H][2H/32]
+    const float* bias;          // b_ih + b_hh [2][H][4] (a unit's 4 gates adjacent)
+    const uint8_t* xq;          // layer input x as e4m3: element (b, s, k) at
+    const uint8_t* xs;          //   b*x_f + s*x_s + (k >> x_sh)*x_t + (k & (2^x_sh - 1)) + x_0 (2^x_sh % 256 == 0);
+    int64_t x_f, x_s, x_t, x_0, x_elems;   //   its E8M0 per 32 k at element offset / 32
+    int32_t x_sh;
+    const uint8_t* hq_prev;     // h_{t-1} e4m3 [B][2][2][H], E8M0 per 32 units: hs_prev [B][2][2][H/32]
+    const uint8_t* hs_prev;
+    uint8_t* hq_cur;            // h_t, same layout
+    uint8_t* hs_cur;
+    float* cst;                 // c [B][2][2][H] (read, written)
+    float* hx;                  // h_t f32 [B][2][2][H]: the cell pair's hand-off
+    int* cnt;                   // lstm_step_mx8_counters(H, B) arrival counters, zero between launches
+    bf16_t* dst;                // combined rows: real at b*ldf + (j >> dshift)*ldd + (j & (2^dshift - 1)),
+    int64_t ldf, ldd;           //   imag at + 2^dshift (lstm_combine_kernel's map)
+    int32_t dshift;
+    uint8_t* q8;                // their MX-fp8 shadow (RowEpi::q8 layout), nullable
+    uint8_t* qs;
+    int32_t B, H;
+};
+hipError_t launch_lstm_step_mx8(const StepMxArgs& a, hipStream_t st);
+int64_t lstm_step_mx8_counters(int H, int B);
+
 // Streaming (one hop per stream): frame = [prev hop, cur hop] of each stream
 struct StreamFrontArgs {
     const float* prev_mic;      // [B][256] (the hop ring)

@@ -369,7 +369,7 @@ def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu, nlms=N
 
 def run_c5_stream(dev, B=256, hops=200, dtype='fp8', world=1):
     """BASELINE config 5: the hipGraph-captured per-hop step of the DCCRN
-    (MX-fp8 LSTM input projections and wide conv layers) fed by the FD-NLMS,
+    (MX-fp8 LSTM input projections, recurrence and wide conv layers) fed by the FD-NLMS,
     B concurrent streams per GPU, one 256-sample hop per stream per step
     (aec_crn_stream_step).  With world > 1 every rank steps its own B streams
     (no data-path collective); the timed region is bracketed by barriers and
@@ -402,7 +402,8 @@ def run_c5_stream(dev, B=256, hops=200, dtype='fp8', world=1):
     torch.cuda.empty_cache()
     return dict(workload=f'C5 (BASELINE configs[4]): {world} GPU(s) x {B} concurrent streams, one 256-sample hop per '
                          f'stream per step through the hipGraph-captured STFT -> FD-NLMS (4 taps) -> DCCRN v2 '
-                         f'(net_conf, {dtype}' + (': bf16 + MX-fp8 LSTM input projections and encoder 4-5 / decoder 5-6 convs'
+                         f'(net_conf, {dtype}' + (': bf16 + MX-fp8 LSTM input projections, LSTM recurrence (W_hh, h) and '
+                         'encoder 4-5 / decoder 4-6 convs'
                          if dtype == 'fp8' else '') + ') -> iSTFT step',
                 dtype=dtype, n_gpus=world, streams=B * world, hops=hops, ms_per_hop=round(dt * 1e3, 4),
                 frames_per_s=round(world * B / dt, 1), frames_per_s_per_gpu=round(B / dt, 1),

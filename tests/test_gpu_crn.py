@@ -390,3 +390,42 @@ def test_fp8_shadow_operands_bit_exact(monkeypatch):
     for i, n in enumerate(lens):                        # frames past a row's end are unspecified
         tn = n // 256 + 1
         assert torch.equal(s0[i, :, :tn], s1[i, :, :tn]), i
+
+
+def test_fp8_stream_mx_recurrence(monkeypatch):
+    """dtype fp8 per-hop step (BASELINE config 5): the LSTM recurrence on the
+    scaled MFMA (W_hh and h_{t-1} as e4m3 with an E8M0 scale per 32 k) with the
+    NavieComplexLSTM combination fused into its epilogue (lstm_step_mx8_kernel)
+    against the bf16 step + combine kernels (AEC_CRN_STEP_MX=0, read at
+    stream_open) on 80 streams (three step blocks, the last one partial) of
+    the full net_conf: within FP8_WAV_TOL / 4 relative RMS of each other per
+    stream, and not identical (the MX recurrence really ran); three streams
+    within the fp8 bar of the reference op mix (oracle/torch_crn_port)."""
+    from aec_amd import synth
+    import torch_crn_port as P
+    net, m, conf = build('v2E_16000', 'fp8')
+    B, n = 80, 8000
+    sig = [synth.scene(n, 1700 + b) for b in range(B)]
+    nh = n // 256 + 1
+    M = torch.zeros(B, 256 * (nh + 1), device='cuda:0')
+    F = torch.zeros_like(M)
+    M[:, :n] = torch.from_numpy(np.stack([s[0] for s in sig])).cuda()
+    F[:, :n] = torch.from_numpy(np.stack([s[1] for s in sig])).cuda()
+    res = {}
+    for flag in ('0', '1'):
+        monkeypatch.setenv('AEC_CRN_STEP_MX', flag)
+        net.stream_open(B)
+        with torch.no_grad():
+            outs = [net.stream_step(M[:, 256 * k:256 * (k + 1)], F[:, 256 * k:256 * (k + 1)]).clone()
+                    for k in range(nh)]
+        torch.cuda.synchronize()
+        res[flag] = torch.cat(outs[1:], dim=1)[:, :256 * (n // 256)].cpu().numpy()
+    assert np.isfinite(res['1']).all()
+    errs = [rel(res['1'][b], res['0'][b]) for b in range(B)]
+    assert max(errs) <= FP8_WAV_TOL / 4, (int(np.argmax(errs)), max(errs))
+    assert not np.array_equal(res['1'], res['0'])
+    w = C.make_weights(conf, 2, m['weight_seed'])
+    port = P.TorchCrnPort(w, conf, 2)
+    for b in (0, 40, 79):
+        ref = port(torch.from_numpy(sig[b][0])[None], torch.from_numpy(sig[b][1])[None])[0].numpy()
+        assert rel(res['1'][b], ref) <= FP8_WAV_TOL, b
