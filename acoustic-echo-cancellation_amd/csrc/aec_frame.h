@@ -162,15 +162,9 @@ __device__ __forceinline__ void row_to_pairs(const float2* row, int lb, bool ok,
     x128 = ok ? row[128] : z;
 }
 
-// Synthesis of one frame by its 16-lane group: per-bin ERB gain
-// g[k] = sum_j est_erb[j] erb[k][j] over the <= 2 bands covering bin k
-// (ERB.py:306-307) applied to the spectrum (:309-310), inverse real pack,
-// irFFT-256, Hann window and 1/512 (attention_ccrn.py:82-91).  Leaves the 512
-// windowed time samples in scr[0..511] (natural order) for the overlap-add.
-//   est : the frame's 32 est_erb values;  sBin: float4[257] transpose table
-__device__ __forceinline__ void synth_frame(const float2 (&xa)[8], const float2 (&xb)[8], float2 x128,
-                                            const float* est, const float4* sBin, const float2* sTw512,
-                                            const float2* sTwT, const float* sHann, float* scr, int lb) {
+__device__ __forceinline__ void synth_pack(const float2 (&xa)[8], const float2 (&xb)[8], float2 x128,
+                                           const float* est, const float4* sBin, const float2* sTw512, int lb,
+                                           float2 (&v)[16]) {
     auto gain = [&](int kk) {
         const float4 e = sBin[kk];
         return e.y * est[__float_as_int(e.x)] + e.w * est[__float_as_int(e.z)];
@@ -196,7 +190,6 @@ __device__ __forceinline__ void synth_frame(const float2 (&xa)[8], const float2 
         const float2 S = cscale(x128, gain(128));
         z128 = make_float2(2.f * S.x, -2.f * S.y);   // 2*conj(S[128])
     }
-    float2 v[16];
 #pragma unroll
     for (int a = 0; a < 8; ++a) v[a] = Zk[a];
     static_for<8, 16>([&](auto ai) {
@@ -204,6 +197,10 @@ __device__ __forceinline__ void synth_frame(const float2 (&xa)[8], const float2 
         const float2 mir = mirror16(Zmk[15 - a]);
         v[a] = csel(lb != 0, mir, a == 8 ? z128 : Zmk[(16 - a) & 7]);
     });
+}
+
+// irFFT-256 of the packed frame, window and 1/512 -> scr[0..511] (natural order)
+__device__ __forceinline__ void synth_fft(float2 (&v)[16], const float2* sTwT, const float* sHann, float* scr, int lb) {
     fft256<true>(v, lb, scr, sTwT);
     // v[kP(m2)] = 512 * (x[2m] + i x[2m+1]), m = lb + 16 m2 ; window + 1/512
     float2* s2 = reinterpret_cast<float2*>(scr);
@@ -214,6 +211,20 @@ __device__ __forceinline__ void synth_frame(const float2 (&xa)[8], const float2 
         const float2 w = h2[lb + 16 * m2];
         s2[lb + 16 * m2] = make_float2(z.x * (w.x * (1.f / 512.f)), z.y * (w.y * (1.f / 512.f)));
     }
+}
+
+// Synthesis of one frame by its 16-lane group: per-bin ERB gain
+// g[k] = sum_j est_erb[j] erb[k][j] over the <= 2 bands covering bin k
+// (ERB.py:306-307) applied to the spectrum (:309-310), inverse real pack,
+// irFFT-256, Hann window and 1/512 (attention_ccrn.py:82-91).  Leaves the 512
+// windowed time samples in scr[0..511] (natural order) for the overlap-add.
+//   est : the frame's 32 est_erb values;  sBin: float4[257] transpose table
+__device__ __forceinline__ void synth_frame(const float2 (&xa)[8], const float2 (&xb)[8], float2 x128,
+                                            const float* est, const float4* sBin, const float2* sTw512,
+                                            const float2* sTwT, const float* sHann, float* scr, int lb) {
+    float2 v[16];
+    synth_pack(xa, xb, x128, est, sBin, sTw512, lb, v);
+    synth_fft(v, sTwT, sHann, scr, lb);
 }
 
 // c = mean(x)/std(x, unbiased) from the partials (ERB.py:254-256).

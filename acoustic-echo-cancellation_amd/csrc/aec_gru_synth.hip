@@ -347,14 +347,20 @@ __global__ __launch_bounds__(kFusedThreads, 1) void gru_synth_kernel(GruArgs p, 
             x128 = row[128];
         };
         for (int c = -3; c <= nch + 2; ++c) {
-            // (2) synthesis of chunk c - 2 into ring (c - 2) & 1 (rows loaded last tick)
+            // (2) synthesis of chunk c - 2 into ring (c - 2) & 1 (rows loaded last tick); the
+            // E rows of chunk c - 1 for the next tick are requested as soon as the inverse pack
+            // has consumed this tick's rows, so their load runs under the inverse transform
             const int cs = c - 2;
+            const bool next = c - 1 >= 0 && c - 1 < nch && !(y.fmode & 4);
             if (cs >= 0 && cs < nch && !(y.fmode & 1)) {
                 float* scr = sOut + (cs & 1) * (kSynWaves * 4 * kGroupFloats) + fl * kGroupFloats;
-                synth_frame(xa, xb, x128, sEst + ((cs & 1) * kCH + fl) * kEstS, sBin, sTw512, sTwT, sHann, scr, lb);
+                float2 v[16];
+                synth_pack(xa, xb, x128, sEst + ((cs & 1) * kCH + fl) * kEstS, sBin, sTw512, lb, v);
+                if (next) load_rows(c - 1);
+                synth_fft(v, sTwT, sHann, scr, lb);
+            } else if (next) {
+                load_rows(c - 1);
             }
-            // (3) E rows of chunk c - 1 for the next tick
-            if (c - 1 >= 0 && c - 1 < nch && !(y.fmode & 4)) load_rows(c - 1);
             tick_barrier();
         }
     }

@@ -554,11 +554,13 @@ static aec_status load_params(aec_crn_handle* h, const float* params, size_t n) 
             if (s != AEC_OK) return s;
         }
         // fused parities: bf16 / f32 stores of 16 B never straddle the parity
-        // split when Co % 8 == 0; the mask level (Co = 2, f32) stays split
-        // (measured, C3 bf16 decoder: unfused 7.31 ms, fused up to Co = 64 6.58, 128 6.42, 256 6.61);
-        // with dtype fp8 the levels the MX GEMM takes (Co >= 128) are fused too (one launch per level
-        // instead of two in the per-hop step)
-        if (cl != 1 && co % 8 == 0 && (co <= h->dec_fuse_max || (h->mx8 && h->dec_fuse_max >= 0))) {
+        // split when Co % 8 == 0 (measured, C3 bf16 decoder: unfused 7.31 ms, fused up to
+        // Co = 64 6.58, 128 6.42, 256 6.61); with dtype fp8 the levels the MX GEMM takes
+        // (Co >= 128) are fused too (one launch per level instead of two in the per-hop step).
+        // The mask level (Co = 2, f32 [F][256][2]) is fused as well: the two parities' outputs of
+        // an input bin are the 4 adjacent floats of bins 2i, 2i + 1, so its rows need no split
+        if ((cl != 1 && co % 8 == 0 && (co <= h->dec_fuse_max || (h->mx8 && h->dec_fuse_max >= 0))) ||
+            (cl == 1 && h->dec_fuse_max >= 0)) {
             aec_status s = pack_decoder_fused(h, h->decf[d], r, act, alpha);
             if (s != AEC_OK) return s;
         }
@@ -874,6 +876,13 @@ static aec_status run_decoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipS
             a.plim = Fin;
             a.base_off = -ld_in;
             a.src_elems = F * Fin * ld_in;
+            if (cl == 1) {                 // the mask: row (f, i) -> bins 2i, 2i + 1 = 4 adjacent floats
+                RowEpi e{bf.mask, a.M, pk.N, a.rshift, (int64_t)Fo * 2, 4, 0, pk.bias, pk.alpha, pk.act};
+                CRN_TRY(h, (crn::launch_gemm_rows<T, float>(a, reinterpret_cast<const T*>(pk.w), pk.kpad,
+                                                             (int)(pk.kpad * sizeof(T) / crn::kStageBytes), e,
+                                                             pk.npad, st)));
+                continue;
+            }
             const int64_t ldo = 2 * ch[cl - 1];
             RowEpi e{bf.cat[cl - 1], a.M, pk.N, a.rshift, Fo * ldo, 2 * ldo, 0, pk.bias, pk.alpha, pk.act};
             e.nsplit = pk.N / 2;
