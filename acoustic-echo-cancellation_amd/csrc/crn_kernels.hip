@@ -1081,6 +1081,8 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
                 else if (pipe) CRN_GEMM_DMA_RBP(2, 4, 8, 4, 2, 128, 1);   // same tile, pipelined core
                 else CRN_GEMM_DMA(2, 4, 8, 4, 2);                         // 256 x 256 tile, 8 waves, 128 KB LDS
             } else if (rb64) CRN_GEMM_DMA_RB(2, 2, 4, 4, 4, 64);
+            else if (dma == 2 && pipe == 3 && a.M <= 16384 && npad % 64 == 0)
+                CRN_GEMM_DMA_RBP(2, 2, 4, 2, 2, 128, 2);   // few rows (the per-hop step): 128 x 64 tiles, 2x the blocks
             else if (big && a.M >= 256 * 1024) CRN_GEMM_DMA(4, 2, 4, 4, 2);
             else if (dma == 2 && pipe == 3) CRN_GEMM_DMA_RBP(2, 2, 4, 4, 2, 128, 2);
             else if (dma == 2) CRN_GEMM_DMA(2, 2, 4, 4, 2);
