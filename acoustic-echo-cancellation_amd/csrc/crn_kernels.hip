@@ -1729,7 +1729,7 @@ template hipError_t launch_lstm_combine<bf16_t>(const bf16_t*, bf16_t*, int64_t,
 // on the scaled MFMA (x, h, W_ih and W_hh as OCP e4m3 with one E8M0 scale per
 // 32 k; K = 2H), then c, h of the cell, then
 //   real = R(x_r) - I(x_i), imag = R(x_i) + I(x_r)   (lstm_combine_kernel's map)
-// Block = one cell x 32 units x kMxSB streams x 2 sequences (A: 64 rows of
+// Block = one cell x 32 units x SB streams x 2 sequences (A: 2 SB rows of
 // [x | h]; B: the cell's 128 packed rows, i|f|g|o per 16 units).  The two cell
 // blocks of a (unit block, stream block) hand their h over through hx (sc1
 // stores, an agent-scope counter; the CDNA guide's counter hand-off, as the
@@ -1741,10 +1741,12 @@ template hipError_t launch_lstm_combine<bf16_t>(const bf16_t*, bf16_t*, int64_t,
 // scales of the tile staged once up front.  Waves: 2 row halves x 2 unit
 // halves, so the four gates of a (row, unit) meet in one lane.
 // --------------------------------------------------------------------------
+// SB streams per block, NBUF stage buffers: (32, 2) = 2 blocks per CU, one stage in flight each.
+// Measured slower per hop at 256 streams (0.163 ms): (64, 3) 0.182 (1 block per CU, half the weight
+// re-reads), (16, 2) 0.183, (16, 3) 0.185, (32, 3) 0.189.
 constexpr int kMxSB = 32;
-constexpr int kMxStepStage = (2 * kMxSB + 128) * 128;          // A 64 + B 128 rows x 128 B
-constexpr int kMxStepBufs = 2;
-size_t lstm_step_mx8_lds(int H) { return (size_t)kMxStepBufs * kMxStepStage + (size_t)(2 * kMxSB + 128) * (2 * H / 32); }
+template <int SB, int NBUF>
+constexpr size_t mx_step_lds(int H) { return (size_t)NBUF * (2 * SB + 128) * 128 + (size_t)(2 * SB + 128) * (2 * H / 32); }
 
 // e4m3 of x / 2^(code - 127), 4 values -> one word (mx8_quant_kernel's conversion)
 __device__ __forceinline__ uint32_t mx8_pack4(float x0, float x1, float x2, float x3, int code) {
@@ -1758,13 +1760,14 @@ __device__ __forceinline__ int mx8_code(float amax) {
     return ebits > 8 ? ebits - 8 : 0;                                    // E8M0: 2^(code - 127)
 }
 
+template <int SB, int NBUF>
 __global__ __launch_bounds__(256) void lstm_step_mx8_kernel(StepMxArgs p) {
-    constexpr int SB = kMxSB, S = 2, C = 2, U = 32;
-    constexpr int BM = SB * S, BN = 4 * U;              // 64, 128
-    constexpr int RB = 128, RPI = 8, NW = 4, NBUF = kMxStepBufs;
+    constexpr int S = 2, C = 2, U = 32;
+    constexpr int BM = SB * S, BN = 4 * U;              // A rows (s, stream), B rows (the cell's packed gates)
+    constexpr int RB = 128, RPI = 8, NW = 4;
     constexpr int LA = BM / (RPI * NW), LB = BN / (RPI * NW);
-    constexpr int STAGE = kMxStepStage;
-    constexpr int FM = 2, FN = 4;
+    constexpr int STAGE = (BM + BN) * RB;
+    constexpr int FM = BM / 32, FN = 4;                 // a wave: half the rows x 16 units x 4 gates
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int H = p.H, K2 = 2 * H, KB = K2 / 32;        // scale bytes per row
     const int nx = H / RB, nst = K2 / RB;               // stages of x, of [x | h]
@@ -1785,7 +1788,7 @@ __global__ __launch_bounds__(256) void lstm_step_mx8_kernel(StepMxArgs p) {
     for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-            const int r = rh * 32 + fm * 16 + 4 * (lane >> 4) + rr, s = r / SB, b = b0 + r % SB;
+            const int r = rh * (BM / 2) + fm * 16 + 4 * (lane >> 4) + rr, s = r / SB, b = b0 + r % SB;
             cv[fm][rr] = p.cst[(((int64_t)(b < p.B ? b : 0) * C + cell) * S + s) * H + unit0 + j];
         }
     // 1. the GEMM over K = [x | h]
@@ -1849,7 +1852,7 @@ __global__ __launch_bounds__(256) void lstm_step_mx8_kernel(StepMxArgs p) {
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int fr = lane & 15, g = lane >> 4;
-    const int wr0 = rh * 32, wc0 = uh * 64;
+    const int wr0 = rh * (BM / 2), wc0 = uh * 64;
     for (int st = 0; st < nst; ++st) {
         if (st + NBUF - 2 < nst)
             wait_vm<(NBUF - 2) * (LA + LB)>();
@@ -1899,8 +1902,10 @@ __global__ __launch_bounds__(256) void lstm_step_mx8_kernel(StepMxArgs p) {
     __syncthreads();
     // 3a. h_t as e4m3 + E8M0 (4 threads per row, 8 units each), and f32 -> hx for the partner block
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.hx, (uint64_t)p.B * C * S * H * 4);
-    {
-        const int row = tid >> 2, q4 = tid & 3;
+#pragma unroll
+    for (int rp = 0; rp < (BM + 63) / 64; ++rp) {
+        const int row = rp * 64 + (tid >> 2), q4 = tid & 3;
+        if (BM % 64 && row >= BM) break;                // BM = 32: threads 128.. idle here
         const int s = row / SB, b = b0 + row % SB;
         const float4* hp = reinterpret_cast<const float4*>(sH + row * HS + q4 * 8);
         const float4 v0 = hp[0], v1 = hp[1];
@@ -1931,8 +1936,10 @@ __global__ __launch_bounds__(256) void lstm_step_mx8_kernel(StepMxArgs p) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no load above the counter (sc1 loads)
     // 3b. the combination of stream bl, units jj .. jj + 3 (8 threads per stream): own cell's h
     //     from LDS, the partner's from hx
-    {
-        const int bl = tid >> 3, jj = (tid & 7) * 4, b = b0 + bl;
+#pragma unroll
+    for (int bp = 0; bp < (SB + 31) / 32; ++bp) {
+        const int bl = bp * 32 + (tid >> 3), jj = (tid & 7) * 4, b = b0 + bl;
+        if (SB % 32 && bl >= SB) break;                 // SB = 16: threads 128.. idle here (8-lane groups intact)
         const int oc = 1 - cell;
         float4 own[2], oth[2];
 #pragma unroll
@@ -1982,13 +1989,19 @@ hipError_t launch_lstm_step_mx8(const StepMxArgs& a, hipStream_t st) {
     if (a.H % 256 || a.B <= 0 || (1 << a.dshift) % 32 || (1 << a.x_sh) % 256 || !a.hx || !a.cnt ||
         (a.x_f | a.x_s | a.x_t | a.x_0) % 256)
         return hipErrorInvalidValue;
-    const size_t lds = lstm_step_mx8_lds(a.H);
-    if (lds > 160 * 1024 || lds < 32 * 1024 + 16) return hipErrorInvalidValue;
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_step_mx8_kernel),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (attr != hipSuccess) return attr;
-    const int nsb = (a.B + kMxSB - 1) / kMxSB;
-    hipLaunchKernelGGL(lstm_step_mx8_kernel, dim3(a.H / 32, 2 * nsb), dim3(256), lds, st, a);
+#define CRN_MXSTEP(SB_, NB_)                                                                                      \
+    do {                                                                                                          \
+        auto kern = lstm_step_mx8_kernel<SB_, NB_>;                                                               \
+        const size_t lds = mx_step_lds<SB_, NB_>(a.H);                                                            \
+        if (lds > 160 * 1024 || lds < 32 * 1024 + 16) return hipErrorInvalidValue;                                \
+        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),                   \
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+        if (attr != hipSuccess) return attr;                                                                      \
+        const int nsb = (a.B + SB_ - 1) / SB_;                                                                    \
+        hipLaunchKernelGGL(kern, dim3(a.H / 32, 2 * nsb), dim3(256), lds, st, a);                                 \
+    } while (0)
+    CRN_MXSTEP(kMxSB, 2);
+#undef CRN_MXSTEP
     return hipGetLastError();
 }
 int64_t lstm_step_mx8_counters(int H, int B) { return (int64_t)(H / 32) * ((B + kMxSB - 1) / kMxSB); }
