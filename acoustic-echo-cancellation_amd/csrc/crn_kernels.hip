@@ -289,8 +289,8 @@ __global__ __launch_bounds__(256) void crn_back_kernel(BackArgs p) {
 }
 
 // --------------------------------------------------------------------------
-// Streaming front / back: one 16-lane group per stream, 16 streams per block.
-// The group stages its frame [prev hop | cur hop] in its own LDS region (the
+// Streaming front / back: one 16-lane group per stream (front: per stream and
+// signal), 16 groups per block. The group stages its frame [prev hop | cur hop] in its own LDS region (the
 // hop layout load_frame reads) and runs the same transform code as the
 // batch kernels, so a streamed frame is bit-identical to the batch frame.
 // --------------------------------------------------------------------------
@@ -298,29 +298,33 @@ __global__ __launch_bounds__(256) void crn_back_kernel(BackArgs p) {
 // one 16-lane group per stream): every global load that does not depend on
 // another (the hops, E row, mask row, OLA tail) is issued before the table
 // staging barrier, so the chain holds one memory round trip, not three or four.
+// Front: 8 streams per block, the two signals on different waves (groups 0-7 the mic hops of
+// streams 0-7, groups 8-15 their far hops), so each wave's chain holds one transform.
 template <typename T>
 __global__ __launch_bounds__(256) void crn_stream_front_kernel(StreamFrontArgs p) {
-    __shared__ __attribute__((aligned(16))) float smem[256 * 2 + 258 * 2 + 512 + 2 * 16 * kGroupFloats];
+    __shared__ __attribute__((aligned(16))) float smem[256 * 2 + 258 * 2 + 512 + 16 * kGroupFloats];
     float2* sTwT = reinterpret_cast<float2*>(smem);
     float2* sTw512 = sTwT + 256;
     float* sHann = reinterpret_cast<float*>(sTw512 + 258);
     float* sGrp = sHann + 512;
     const int tid = threadIdx.x;
     const int g = tid >> 4, lb = tid & 15;
-    const int b = blockIdx.x * 16 + g;
+    const int far = g >> 3;
+    const int b = blockIdx.x * 8 + (g & 7);
     const int bb = b < p.B ? b : p.B - 1;
     const bool cal = (p.ld_cur & 3) == 0 && ((reinterpret_cast<uintptr_t>(p.cur_mic) | reinterpret_cast<uintptr_t>(p.cur_far)) & 15) == 0;
-    // both signals' frames [previous hop (ring) | current hop (caller)] straight into this
-    // group's two LDS staging regions (the layout load_frame reads), in flight together with
-    // the table loads; the current hops are also saved to the ring
-    float* reg0 = sGrp + g * kGroupFloats;
-    float* reg1 = sGrp + (16 + g) * kGroupFloats;
+    // this group's frame [previous hop (ring) | current hop (caller)] straight into its LDS
+    // staging region (the layout load_frame reads), in flight together with the table loads;
+    // the current hop is also saved to the ring
+    float* reg = sGrp + g * kGroupFloats;
     const float2 t0 = p.tab->twT[tid], t1 = p.tab->tw512[tid];
     const float2 t2 = tid < 2 ? p.tab->tw512[256 + tid] : make_float2(0.f, 0.f);
     const float h0 = p.tab->hann[tid], h1 = p.tab->hann[tid + 256];
-    auto stage = [&](float* reg, const float* prev, const float* cur, float* save) __attribute__((always_inline)) {
+    {
+        const float* prev = far ? p.prev_far : p.prev_mic;
+        const float* cur = (far ? p.cur_far : p.cur_mic) + (int64_t)bb * p.ld_cur;
+        float* save = far ? p.save_far : p.save_mic;
         const float4* p4 = reinterpret_cast<const float4*>(prev + (int64_t)bb * 256) + lb * 4;
-        cur += (int64_t)bb * p.ld_cur;
         float4* r0 = reinterpret_cast<float4*>(reg) + lb * 4;
         float4* r1 = reinterpret_cast<float4*>(reg + aec::kHopStride) + lb * 4;
 #pragma unroll
@@ -331,40 +335,48 @@ __global__ __launch_bounds__(256) void crn_stream_front_kernel(StreamFrontArgs p
             r1[i] = c;
             if (save && b < p.B) *reinterpret_cast<float4*>(save + (int64_t)b * 256 + e) = c;
         }
-    };
-    stage(reg0, p.prev_mic, p.cur_mic, p.save_mic);
-    stage(reg1, p.prev_far, p.cur_far, p.save_far);
+    }
     sTwT[tid] = t0;
     sTw512[tid] = t1;
     if (tid < 2) sTw512[256 + tid] = t2;
     sHann[tid] = h0;
     sHann[tid + 256] = h1;
     __syncthreads();
-    float2 ma[8], mb[8], m128, fa[8], fb[8], f128;
-    auto xform = [&](float* reg, float2 (&xa)[8], float2 (&xb)[8], float2& x128) __attribute__((always_inline)) {
+    float2 xa[8], xb[8], x128;
+    {
         float2 v[16];
         aec::load_frame(v, reg, sHann, 0, lb);
         aec::wave_fence();
         aec::fft256<false>(v, lb, reg, sTwT);
         aec::rfft_unpack(v, lb, sTw512, xa, xb, x128);
         aec::wave_fence();
-    };
-    xform(reg0, ma, mb, m128);
-    xform(reg1, fa, fb, f128);
-    if (b >= p.B) return;
+    }
     if (p.rows) {   // NLMS: packed rows [B][2][256]; crn_stream_nlms_kernel writes X0
-        put_row(p.rows + (int64_t)b * 512, lb, true, ma, mb, m128);
-        put_row(p.rows + (int64_t)b * 512 + 256, lb, true, fa, fb, f128);
+        if (b < p.B) put_row(p.rows + (int64_t)b * 512 + far * 256, lb, true, xa, xb, x128);
         return;
     }
+    // X0 rows interleave both signals per bin: the far groups hand their bins over through
+    // their (now free) staging regions
+    float2* xch = reinterpret_cast<float2*>(reg) + lb * 17;
+    if (far) {
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            xch[m] = xa[m];
+            xch[8 + m] = xb[m];
+        }
+        xch[16] = x128;
+    }
+    __syncthreads();
+    if (far || b >= p.B) return;
+    const float2* fx = reinterpret_cast<const float2*>(reg + 8 * kGroupFloats) + lb * 17;
     T* row = reinterpret_cast<T*>(p.x0) + (int64_t)b * 256 * 8;
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
         const int k = lb + 16 * m;
-        if (k != 0) put_bin<T>(row, k, ma[m], fa[m]);
-        put_bin<T>(row, 256 - k, mb[m], fb[m]);
+        if (k != 0) put_bin<T>(row, k, xa[m], fx[m]);
+        put_bin<T>(row, 256 - k, xb[m], fx[8 + m]);
     }
-    if (lb == 0) put_bin<T>(row, 128, m128, f128);
+    if (lb == 0) put_bin<T>(row, 128, x128, fx[16]);
 }
 
 template <int MODE>
@@ -604,7 +616,7 @@ template hipError_t launch_stream_nlms<bf16_t>(const StreamNlmsArgs&, int, hipSt
 template <typename T>
 hipError_t launch_stream_front(const StreamFrontArgs& a, hipStream_t st) {
     if (a.B <= 0) return hipSuccess;
-    hipLaunchKernelGGL((crn_stream_front_kernel<T>), dim3((unsigned)((a.B + 15) / 16)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((crn_stream_front_kernel<T>), dim3((unsigned)((a.B + 7) / 8)), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 template hipError_t launch_stream_front<float>(const StreamFrontArgs&, hipStream_t);
