@@ -379,6 +379,9 @@ __global__ __launch_bounds__(256) void crn_stream_front_kernel(StreamFrontArgs p
     if (lb == 0) put_bin<T>(row, 128, x128, fx[16]);
 }
 
+// Back: 8 streams per block, two groups per stream: group g < 8 runs the stream's chain,
+// group g + 8 helps with the mask when the E row comes from the NLMS (half the masked bins,
+// handed over through its LDS region); without the NLMS the helper only meets the barriers.
 template <int MODE>
 __global__ __launch_bounds__(256) void crn_stream_back_kernel(StreamBackArgs p) {
     __shared__ __attribute__((aligned(16))) float smem[258 * 2 + 256 * 2 + 512 + 256 + 16 * kGroupFloats];
@@ -389,7 +392,8 @@ __global__ __launch_bounds__(256) void crn_stream_back_kernel(StreamBackArgs p) 
     float* sGrp = sCoff + 256;
     const int tid = threadIdx.x;
     const int g = tid >> 4, lb = tid & 15;
-    const int b = blockIdx.x * 16 + g;
+    const int helper = g >> 3;                          // wave-uniform (waves 2, 3)
+    const int b = blockIdx.x * 8 + (g & 7);
     const int bb = b < p.B ? b : p.B - 1;
     float* reg = sGrp + g * kGroupFloats;
     float2 v[16];
@@ -397,7 +401,7 @@ __global__ __launch_bounds__(256) void crn_stream_back_kernel(StreamBackArgs p) 
     // independent loads first: the E row (or the mic hops), the mask row, the OLA tail
     if (p.espec) {   // NLMS: this frame's error row
         aec::row_to_pairs(p.espec + (int64_t)bb * 256, lb, true, xa, xb, x128);
-    } else {             // the mic frame [prev | cur] into this group's staging region
+    } else if (!helper) {   // the mic frame [prev | cur] into this group's staging region
         const float4* p4 = reinterpret_cast<const float4*>(p.prev_mic + (int64_t)bb * 256) + lb * 4;
         const float4* c4 = reinterpret_cast<const float4*>(p.cur_mic + (int64_t)bb * 256) + lb * 4;
         float4* r0 = reinterpret_cast<float4*>(reg) + lb * 4;
@@ -428,18 +432,40 @@ __global__ __launch_bounds__(256) void crn_stream_back_kernel(StreamBackArgs p) 
     sHann[tid + 256] = p.tab->hann[tid + 256];
     sCoff[tid] = p.tab->inv_coff[tid];
     __syncthreads();
-    if (!p.espec) {
+    if (!p.espec && !helper) {
         aec::load_frame(v, reg, sHann, 0, lb);
         aec::wave_fence();
         aec::fft256<false>(v, lb, reg, sTwT);
         aec::rfft_unpack(v, lb, sTw512, xa, xb, x128);
     }
+    // the mask: the helper takes m = 4..7 and bin 128 of an E row, the chain group the rest
+    float2* xch = reinterpret_cast<float2*>(sGrp + (8 + (g & 7)) * kGroupFloats) + lb * 9;
+    const bool split = p.espec != nullptr;
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
-        xa[m] = apply_mask<MODE>(xa[m], mka[m]);
-        xb[m] = apply_mask<MODE>(xb[m], mkb[m]);
+    for (int m = 0; m < 8; ++m)
+        if (split ? helper == (m >> 2) : !helper) {
+            xa[m] = apply_mask<MODE>(xa[m], mka[m]);
+            xb[m] = apply_mask<MODE>(xb[m], mkb[m]);
+        }
+    if (split ? helper : !helper) x128 = apply_mask<MODE>(x128, mk128);
+    if (split && helper) {
+#pragma unroll
+        for (int m = 4; m < 8; ++m) {
+            xch[m - 4] = xa[m];
+            xch[m] = xb[m];
+        }
+        xch[8] = x128;
     }
-    x128 = apply_mask<MODE>(x128, mk128);
+    __syncthreads();
+    if (helper) return;
+    if (split) {
+#pragma unroll
+        for (int m = 4; m < 8; ++m) {
+            xa[m] = xch[m - 4];
+            xb[m] = xch[m];
+        }
+        x128 = xch[8];
+    }
     float2 Zk[8], Zmk[8];
     aec::static_for<0, 8>([&](auto mi) {
         constexpr int m = decltype(mi)::value;
@@ -624,7 +650,7 @@ template hipError_t launch_stream_front<bf16_t>(const StreamFrontArgs&, hipStrea
 
 hipError_t launch_stream_back(const StreamBackArgs& a, int mode, hipStream_t st) {
     if (a.B <= 0) return hipSuccess;
-    const dim3 grid((unsigned)((a.B + 15) / 16));
+    const dim3 grid((unsigned)((a.B + 7) / 8));
     switch (mode) {
         case 0: hipLaunchKernelGGL(crn_stream_back_kernel<0>, grid, dim3(256), 0, st, a); break;
         case 1: hipLaunchKernelGGL(crn_stream_back_kernel<1>, grid, dim3(256), 0, st, a); break;
