@@ -1103,8 +1103,15 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
     RowEpi ee = e;
     ee.mode = gmode;
     switch (bn) {
-        case 16: CRN_GEMM(4, 1, 4, 1); break;
-        case 32: CRN_GEMM(2, 2, 4, 1); break;
+        // few rows (the per-hop step): half-height tiles, twice the blocks
+        case 16:
+            if (a.M <= 65536) CRN_GEMM(4, 1, 2, 1);
+            else CRN_GEMM(4, 1, 4, 1);
+            break;
+        case 32:
+            if (a.M <= 65536) CRN_GEMM(2, 2, 2, 1);
+            else CRN_GEMM(2, 2, 4, 1);
+            break;
         case 64:
             if (dma == 2 && pipe == 3) CRN_GEMM_DMA_RBP(2, 2, 4, 2, 2, 128, 2);
             else if (dma == 2) CRN_GEMM_DMA(2, 2, 4, 2, 2);
