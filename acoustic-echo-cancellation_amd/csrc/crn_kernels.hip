@@ -787,8 +787,9 @@ __device__ __forceinline__ void rows_epilogue_lds_a(const f32x4 (&acc)[FM][FN], 
                 }
         aec::wave_fence();
 #pragma unroll
-        for (int it = 0; it < PF * 16 * CPR / 64; ++it) {
+        for (int it = 0; it < (PF * 16 * CPR + 63) / 64; ++it) {   // 16 rows x CPR chunks per fragment
             const int c = it * 64 + lane;
+            if ((PF * 16 * CPR) % 64 && c >= PF * 16 * CPR) break;
             const int row = c / CPR, ch = c % CPR;
             const int64_t m = mb + p0 * 16 + row;
             const int n = nb + ch * EPC;
@@ -893,8 +894,9 @@ __device__ __forceinline__ void rows_epilogue_lds_t(const f32x4 (&acc)[FM][FN], 
         else stage_pass_t<OutT, FM, FN, PF, 0>(acc, p0, bias, alpha, wlds, fr, g);
         aec::wave_fence();
 #pragma unroll
-        for (int it = 0; it < PF * 16 * CPR / 64; ++it) {
+        for (int it = 0; it < (PF * 16 * CPR + 63) / 64; ++it) {   // 16 rows x CPR chunks per fragment
             const int c = it * 64 + lane;
+            if ((PF * 16 * CPR) % 64 && c >= PF * 16 * CPR) break;
             const int row = c / CPR, ch = c % CPR;
             const int64_t m = mb + p0 * 16 + row;
             const int n = nb + ch * EPC;
@@ -1103,17 +1105,18 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
     RowEpi ee = e;
     ee.mode = gmode;
     switch (bn) {
-        // few rows (the per-hop step): half-height tiles, twice the blocks
+        // few rows (the per-hop step): quarter-height tiles, 4x the blocks
         case 16:
-            if (a.M <= 65536) CRN_GEMM(4, 1, 2, 1);
+            if (a.M <= 65536) CRN_GEMM(4, 1, 1, 1);
             else CRN_GEMM(4, 1, 4, 1);
             break;
         case 32:
-            if (a.M <= 65536) CRN_GEMM(2, 2, 2, 1);
+            if (a.M <= 65536) CRN_GEMM(2, 2, 1, 1);
             else CRN_GEMM(2, 2, 4, 1);
             break;
-        case 64:
-            if (dma == 2 && pipe == 3) CRN_GEMM_DMA_RBP(2, 2, 4, 2, 2, 128, 2);
+        case 64:   // few rows: 64 x 64 tiles
+            if (dma == 2 && pipe == 3 && a.M <= 65536) CRN_GEMM_DMA_RBP(2, 2, 2, 2, 2, 128, 2);
+            else if (dma == 2 && pipe == 3) CRN_GEMM_DMA_RBP(2, 2, 4, 2, 2, 128, 2);
             else if (dma == 2) CRN_GEMM_DMA(2, 2, 4, 2, 2);
             else if (dma == 3) CRN_GEMM_DMA(2, 2, 4, 2, 3);
             else if (dma >= 4) CRN_GEMM_DMA(2, 2, 4, 2, 4);
