@@ -1793,8 +1793,12 @@ template hipError_t launch_lstm_combine<bf16_t>(const bf16_t*, bf16_t*, int64_t,
 // Measured slower per hop at 256 streams (0.163 ms): (64, 3) 0.182 (1 block per CU, half the weight
 // re-reads), (16, 2) 0.183, (16, 3) 0.185, (32, 3) 0.189.
 constexpr int kMxSB = 32;
-template <int SB, int NBUF>
-constexpr size_t mx_step_lds(int H) { return (size_t)NBUF * (2 * SB + 128) * 128 + (size_t)(2 * SB + 128) * (2 * H / 32); }
+// SREG (H == 1024, NBUF >= 3): the K scales pass through the last stage buffer (free until the
+// loop's first issue) into registers, so the stage buffers alone set the LDS size
+template <int SB, int NBUF, bool SREG = false>
+constexpr size_t mx_step_lds(int H) {
+    return (size_t)NBUF * (2 * SB + 128) * 128 + (SREG ? 0 : (size_t)(2 * SB + 128) * (2 * H / 32));
+}
 
 // e4m3 of x / 2^(code - 127), 4 values -> one word (mx8_quant_kernel's conversion)
 __device__ __forceinline__ uint32_t mx8_pack4(float x0, float x1, float x2, float x3, int code) {
@@ -1808,7 +1812,7 @@ __device__ __forceinline__ int mx8_code(float amax) {
     return ebits > 8 ? ebits - 8 : 0;                                    // E8M0: 2^(code - 127)
 }
 
-template <int SB, int NBUF>
+template <int SB, int NBUF, bool SREG = false>
 __global__ __launch_bounds__(256) void lstm_step_mx8_kernel(StepMxArgs p) {
     constexpr int S = 2, C = 2, U = 32;
     constexpr int BM = SB * S, BN = 4 * U;              // A rows (s, stream), B rows (the cell's packed gates)
@@ -1867,6 +1871,71 @@ __global__ __launch_bounds__(256) void lstm_step_mx8_kernel(StepMxArgs p) {
                 (uint32_t)(row * K2 + st * RB + swz_slot<RB>(row, q_l) * 16), 0, 0, 0);
         }
     };
+    const int fr = lane & 15, g = lane >> 4;
+    const int wr0 = rh * (BM / 2), wc0 = uh * 64;
+    // SREG: the lane's scale bytes of its FM A rows and FN B rows, stage st = byte st of the
+    // 16 (4 words); word 0 byte 0 is always the current stage (shifted down per stage)
+    uint32_t pa[FM][4], pb[FN][4];
+    if constexpr (SREG) {
+        static_assert(NBUF >= 3 && BM == 64, "SREG: H = 1024, 32 streams, a free third buffer");
+        // global loads first (their wait then leaves the stage DMAs in flight): weights 2 x 16 B,
+        // h 16 B (threads < 128), x 8 B per thread
+        uint4 vw[2], vh = make_uint4(0u, 0u, 0u, 0u);
+        uint2 vx = make_uint2(0u, 0u);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int c = tid + 256 * i, row = c >> 2, q16 = c & 3;
+            vw[i] = reinterpret_cast<const uint4*>(p.wsc + ((int64_t)cell * 4 * H + (int64_t)unit0 * 4 + row) * 64)[q16];
+        }
+        {
+            const int row = (tid & 127) >> 1, s = row / SB, b = b0 + row % SB;
+            if (tid < 128 && b < p.B)
+                vh = reinterpret_cast<const uint4*>(p.hs_prev + (((int64_t)b * C + cell) * S + s) * (H / 32))[tid & 1];
+        }
+        {
+            const int row = tid >> 2, q8 = tid & 3, s = row / SB, b = b0 + row % SB;
+            if (b < p.B) vx = *reinterpret_cast<const uint2*>(p.xs + (xoff(b, s, q8 * 256) >> 5));
+        }
+#pragma unroll
+        for (int i = 0; i < NBUF - 1; ++i) issue(i);
+        // transposed into the last stage buffer: sT[row][g][4 words], word q = stages 4q .. 4q + 3
+        uint32_t* sT = reinterpret_cast<uint32_t*>(smem + (NBUF - 1) * STAGE);
+        auto col = [](uint4 v, int gg) {                // byte gg of each word -> one word
+            return ((v.x >> (8 * gg)) & 0xFF) | (((v.y >> (8 * gg)) & 0xFF) << 8) |
+                   (((v.z >> (8 * gg)) & 0xFF) << 16) | (((v.w >> (8 * gg)) & 0xFF) << 24);
+        };
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int c = tid + 256 * i, row = BM + (c >> 2), q16 = c & 3;
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg) sT[row * 16 + gg * 4 + q16] = col(vw[i], gg);
+        }
+        if (tid < 128) {
+            const int row = (tid & 127) >> 1, q = 2 + (tid & 1);   // h scales: stages 8 .. 15
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg) sT[row * 16 + gg * 4 + q] = col(vh, gg);
+        }
+        {
+            const int row = tid >> 2, q8 = tid & 3;     // x tap q8: stages 2 q8, 2 q8 + 1
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg)
+                reinterpret_cast<uint16_t*>(sT + row * 16 + gg * 4 + (q8 >> 1))[q8 & 1] =
+                    (uint16_t)(((vx.x >> (8 * gg)) & 0xFF) | (((vx.y >> (8 * gg)) & 0xFF) << 8));
+        }
+        __syncthreads();
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+            const uint4 v = *reinterpret_cast<const uint4*>(sT + (wr0 + fm * 16 + fr) * 16 + g * 4);
+            pa[fm][0] = v.x, pa[fm][1] = v.y, pa[fm][2] = v.z, pa[fm][3] = v.w;
+        }
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+            const uint4 v = *reinterpret_cast<const uint4*>(sT + (BM + wc0 + fn * 16 + fr) * 16 + g * 4);
+            pb[fn][0] = v.x, pb[fn][1] = v.y, pb[fn][2] = v.z, pb[fn][3] = v.w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the loop's first
+                                                               // barrier lets stage NBUF - 1's DMA into sT
+    } else {
 #pragma unroll
     for (int i = 0; i < NBUF - 1; ++i) issue(i);
     // all K scales of the tile -> LDS while the first stage is in flight; sS row = [x | h] 2H/32
@@ -1894,13 +1963,12 @@ __global__ __launch_bounds__(256) void lstm_step_mx8_kernel(StepMxArgs p) {
         }
     }
     __syncthreads();                                    // scales staged
+    }
     f32x4 acc[FM][FN];
 #pragma unroll
     for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int fr = lane & 15, g = lane >> 4;
-    const int wr0 = rh * (BM / 2), wc0 = uh * 64;
     for (int st = 0; st < nst; ++st) {
         if (st + NBUF - 2 < nst)
             wait_vm<(NBUF - 2) * (LA + LB)>();
@@ -1918,7 +1986,7 @@ __global__ __launch_bounds__(256) void lstm_step_mx8_kernel(StepMxArgs p) {
             const u32x4 lo = *reinterpret_cast<const u32x4*>(sB + r * RB + swz_slot<RB>(r, g) * 16);
             const u32x4 hi = *reinterpret_cast<const u32x4*>(sB + r * RB + swz_slot<RB>(r, 4 + g) * 16);
             bfr[fn] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-            sb[fn] = sS[(BM + r) * KB + st * 4 + g];
+            sb[fn] = SREG ? (int)(pb[fn][0] & 0xFF) : (int)sS[(BM + r) * KB + st * 4 + g];
         }
 #pragma unroll
         for (int fm = 0; fm < FM; ++fm) {
@@ -1926,10 +1994,22 @@ __global__ __launch_bounds__(256) void lstm_step_mx8_kernel(StepMxArgs p) {
             const u32x4 lo = *reinterpret_cast<const u32x4*>(sA + r * RB + swz_slot<RB>(r, g) * 16);
             const u32x4 hi = *reinterpret_cast<const u32x4*>(sA + r * RB + swz_slot<RB>(r, 4 + g) * 16);
             const i32x8 af = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-            const int sa = sS[r * KB + st * 4 + g];
+            const int sa = SREG ? (int)(pa[fm][0] & 0xFF) : (int)sS[r * KB + st * 4 + g];
 #pragma unroll
             for (int fn = 0; fn < FN; ++fn)
                 acc[fm][fn] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bfr[fn], acc[fm][fn], 0, 0, 0, sa, 0, sb[fn]);
+        }
+        if constexpr (SREG) {                           // the next stage's byte -> byte 0 of word 0
+            auto shift = [](uint32_t (&w)[4]) {
+                w[0] = __builtin_amdgcn_alignbit(w[1], w[0], 8);
+                w[1] = __builtin_amdgcn_alignbit(w[2], w[1], 8);
+                w[2] = __builtin_amdgcn_alignbit(w[3], w[2], 8);
+                w[3] >>= 8;
+            };
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm) shift(pa[fm]);
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) shift(pb[fn]);
         }
     }
     // 2. cell update (gate order i, f, g, o); c -> HBM, h (f32) -> LDS tile sH[row][U] and -> hx (sc1)
@@ -2037,10 +2117,10 @@ hipError_t launch_lstm_step_mx8(const StepMxArgs& a, hipStream_t st) {
     if (a.H % 256 || a.B <= 0 || (1 << a.dshift) % 32 || (1 << a.x_sh) % 256 || !a.hx || !a.cnt ||
         (a.x_f | a.x_s | a.x_t | a.x_0) % 256)
         return hipErrorInvalidValue;
-#define CRN_MXSTEP(SB_, NB_)                                                                                      \
+#define CRN_MXSTEP(SB_, NB_, SR_)                                                                                 \
     do {                                                                                                          \
-        auto kern = lstm_step_mx8_kernel<SB_, NB_>;                                                               \
-        const size_t lds = mx_step_lds<SB_, NB_>(a.H);                                                            \
+        auto kern = lstm_step_mx8_kernel<SB_, NB_, SR_>;                                                          \
+        const size_t lds = mx_step_lds<SB_, NB_, SR_>(a.H);                                                       \
         if (lds > 160 * 1024 || lds < 32 * 1024 + 16) return hipErrorInvalidValue;                                \
         static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),                   \
                                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
@@ -2048,7 +2128,12 @@ hipError_t launch_lstm_step_mx8(const StepMxArgs& a, hipStream_t st) {
         const int nsb = (a.B + SB_ - 1) / SB_;                                                                    \
         hipLaunchKernelGGL(kern, dim3(a.H / 32, 2 * nsb), dim3(256), lds, st, a);                                 \
     } while (0)
-    CRN_MXSTEP(kMxSB, 2);
+    const char* sreg_env = getenv("AEC_CRN_MX_SREG");  // read per launch (captured once per stream open)
+    const int sreg = sreg_env ? atoi(sreg_env) : 1;
+    if (a.H == 1024 && sreg)
+        CRN_MXSTEP(kMxSB, 3, true);
+    else
+        CRN_MXSTEP(kMxSB, 2, false);
 #undef CRN_MXSTEP
     return hipGetLastError();
 }

@@ -429,3 +429,33 @@ def test_fp8_stream_mx_recurrence(monkeypatch):
     for b in (0, 40, 79):
         ref = port(torch.from_numpy(sig[b][0])[None], torch.from_numpy(sig[b][1])[None])[0].numpy()
         assert rel(res['1'][b], ref) <= FP8_WAV_TOL, b
+
+
+def test_fp8_stream_mx_scale_paths_bit_exact(monkeypatch):
+    """The MX layer step's two scale paths (lstm_step_mx8_kernel): the K scales
+    read per stage from LDS (AEC_CRN_MX_SREG=0, two stage buffers) and held in
+    registers after a transposed pass through the third stage buffer (default
+    at H = 1024) feed the same scale bytes to the same MFMAs, so 40 streams
+    (two step blocks, the last one partial) of the full net_conf agree bit for
+    bit over 12 hops."""
+    from aec_amd import synth
+    net, m, conf = build('v2E_16000', 'fp8')
+    B, n = 40, 3072
+    sig = [synth.scene(n, 2100 + b) for b in range(B)]
+    nh = n // 256 + 1
+    M = torch.zeros(B, 256 * (nh + 1), device='cuda:0')
+    F = torch.zeros_like(M)
+    M[:, :n] = torch.from_numpy(np.stack([s[0] for s in sig])).cuda()
+    F[:, :n] = torch.from_numpy(np.stack([s[1] for s in sig])).cuda()
+    monkeypatch.setenv('AEC_CRN_STEP_MX', '1')
+    res = {}
+    for flag in ('0', '1'):
+        monkeypatch.setenv('AEC_CRN_MX_SREG', flag)
+        net.stream_open(B)
+        with torch.no_grad():
+            outs = [net.stream_step(M[:, 256 * k:256 * (k + 1)], F[:, 256 * k:256 * (k + 1)]).clone()
+                    for k in range(nh)]
+        torch.cuda.synchronize()
+        res[flag] = torch.cat(outs, dim=1).cpu().numpy()
+    assert np.isfinite(res['1']).all()
+    assert np.array_equal(res['1'], res['0'])
