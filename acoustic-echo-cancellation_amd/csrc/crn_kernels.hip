@@ -379,9 +379,11 @@ __global__ __launch_bounds__(256) void crn_stream_front_kernel(StreamFrontArgs p
     if (lb == 0) put_bin<T>(row, 128, x128, fx[16]);
 }
 
-// Back: 8 streams per block, two groups per stream: group g < 8 runs the stream's chain,
-// group g + 8 helps with the mask when the E row comes from the NLMS (half the masked bins,
-// handed over through its LDS region); without the NLMS the helper only meets the barriers.
+// Back: kBackNG groups per stream (16 / kBackNG streams per block, one wave per role): the
+// groups of wave 0 run the streams' chains, the groups of waves 1 .. kBackNG - 1 help with the
+// mask when the E row comes from the NLMS (8 / kBackNG of the 8 bin slots each, handed over
+// through their LDS regions); without the NLMS the helpers only meet the barrier.
+constexpr int kBackNG = 4;
 template <int MODE>
 __global__ __launch_bounds__(256) void crn_stream_back_kernel(StreamBackArgs p) {
     __shared__ __attribute__((aligned(16))) float smem[258 * 2 + 256 * 2 + 512 + 256 + 16 * kGroupFloats];
@@ -392,8 +394,9 @@ __global__ __launch_bounds__(256) void crn_stream_back_kernel(StreamBackArgs p) 
     float* sGrp = sCoff + 256;
     const int tid = threadIdx.x;
     const int g = tid >> 4, lb = tid & 15;
-    const int helper = g >> 3;                          // wave-uniform (waves 2, 3)
-    const int b = blockIdx.x * 8 + (g & 7);
+    constexpr int SPB = 16 / kBackNG, MPH = 8 / kBackNG;   // streams per block, bin slots per helper
+    const int helper = g / SPB;                         // wave-uniform
+    const int b = blockIdx.x * SPB + g % SPB;
     const int bb = b < p.B ? b : p.B - 1;
     float* reg = sGrp + g * kGroupFloats;
     float2 v[16];
@@ -438,33 +441,39 @@ __global__ __launch_bounds__(256) void crn_stream_back_kernel(StreamBackArgs p) 
         aec::fft256<false>(v, lb, reg, sTwT);
         aec::rfft_unpack(v, lb, sTw512, xa, xb, x128);
     }
-    // the mask: the helper takes m = 4..7 and bin 128 of an E row, the chain group the rest
-    float2* xch = reinterpret_cast<float2*>(sGrp + (8 + (g & 7)) * kGroupFloats) + lb * 9;
+    // the mask: group h of an E row's stream takes bin slots m = h MPH .. h MPH + MPH - 1 (the
+    // last one also bin 128); without the NLMS the chain group masks everything
     const bool split = p.espec != nullptr;
 #pragma unroll
     for (int m = 0; m < 8; ++m)
-        if (split ? helper == (m >> 2) : !helper) {
+        if (split ? helper == m / MPH : !helper) {
             xa[m] = apply_mask<MODE>(xa[m], mka[m]);
             xb[m] = apply_mask<MODE>(xb[m], mkb[m]);
         }
-    if (split ? helper : !helper) x128 = apply_mask<MODE>(x128, mk128);
+    if (split ? helper == kBackNG - 1 : !helper) x128 = apply_mask<MODE>(x128, mk128);
     if (split && helper) {
+        float2* xch = reinterpret_cast<float2*>(reg) + lb * (2 * MPH + 1);
 #pragma unroll
-        for (int m = 4; m < 8; ++m) {
-            xch[m - 4] = xa[m];
-            xch[m] = xb[m];
-        }
-        xch[8] = x128;
+        for (int m = 0; m < 8; ++m)
+            if (helper == m / MPH) {
+                xch[m % MPH] = xa[m];
+                xch[MPH + m % MPH] = xb[m];
+            }
+        if (helper == kBackNG - 1) xch[2 * MPH] = x128;
     }
     __syncthreads();
     if (helper) return;
     if (split) {
 #pragma unroll
-        for (int m = 4; m < 8; ++m) {
-            xa[m] = xch[m - 4];
-            xb[m] = xch[m];
+        for (int h = 1; h < kBackNG; ++h) {
+            const float2* xch = reinterpret_cast<const float2*>(sGrp + (h * SPB + g) * kGroupFloats) + lb * (2 * MPH + 1);
+#pragma unroll
+            for (int i = 0; i < MPH; ++i) {
+                xa[h * MPH + i] = xch[i];
+                xb[h * MPH + i] = xch[MPH + i];
+            }
+            if (h == kBackNG - 1) x128 = xch[2 * MPH];
         }
-        x128 = xch[8];
     }
     float2 Zk[8], Zmk[8];
     aec::static_for<0, 8>([&](auto mi) {
@@ -650,7 +659,7 @@ template hipError_t launch_stream_front<bf16_t>(const StreamFrontArgs&, hipStrea
 
 hipError_t launch_stream_back(const StreamBackArgs& a, int mode, hipStream_t st) {
     if (a.B <= 0) return hipSuccess;
-    const dim3 grid((unsigned)((a.B + 7) / 8));
+    const dim3 grid((unsigned)((a.B + 16 / kBackNG - 1) / (16 / kBackNG)));
     switch (mode) {
         case 0: hipLaunchKernelGGL(crn_stream_back_kernel<0>, grid, dim3(256), 0, st, a); break;
         case 1: hipLaunchKernelGGL(crn_stream_back_kernel<1>, grid, dim3(256), 0, st, a); break;
