@@ -523,6 +523,23 @@ static aec_status end_call(aec_handle* h, hipStream_t st) {
     h->have_last = true;
     return AEC_OK;
 }
+// every exit after begin_call records ev_last on the call's stream, early error returns
+// included: kernels the call already queued stay ordered before the next call on another stream
+struct CallGuard {
+    aec_handle* h;
+    hipStream_t st;
+    bool done = false;
+    ~CallGuard() {
+        if (!done && hipEventRecord(h->ev_last, st) == hipSuccess) {
+            h->last_stream = st;
+            h->have_last = true;
+        }
+    }
+    aec_status end() {
+        done = true;
+        return end_call(h, st);
+    }
+};
 
 aec_status aec_set_debug(aec_handle* h, int32_t enable) {
     if (!h) return AEC_ERR_INVALID_ARG;
@@ -569,11 +586,15 @@ aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref
     const int64_t Tmax = aec_num_frames(nmax);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     AEC_ON_DEVICE(h);
+    const bool nlms_batch = h->cfg.nlms_taps > 0 && !(B <= h->small_b && h->nlms_mode == 0);
+    if (nlms_batch && nlms_smem_bytes(h->sched_len, h->cfg.nlms_taps) > 160 * 1024)   // before any launch
+        return fail(h, AEC_ERR_UNSUPPORTED, "erb schedule too long for the NLMS kernel's LDS budget");
     // this call overwrites the features a pending aec_train_backward would read
     h->train_B = 0;
     ++h->train_gen;
     aec_status s = begin_call(h, st);
     if (s != AEC_OK) return s;
+    CallGuard cg{h, st};
     s = ensure_ws(h, B, Tmax);
     if (s != AEC_OK) return s;
     s = prepare_lists(h, lengths3, B, nsig_in, st);
@@ -608,8 +629,6 @@ aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref
         HIP_TRY(h, launch_mic_erb(h->d_spec, h->d_feats, h->d_len, Tmax, h->d_sched, h->sched_len, h->d_items,
                                   h->nitems, st));
     } else if (h->cfg.nlms_taps > 0) {
-        if (nlms_smem_bytes(h->sched_len, h->cfg.nlms_taps) > 160 * 1024)
-            return fail(h, AEC_ERR_UNSUPPORTED, "erb schedule too long for the NLMS kernel's LDS budget");
         NlmsArgs a{};
         a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
         a.ld = ld; a.lens = h->d_len; a.slen = h->d_slen; a.b0 = 0; a.cvals = h->d_cvals;
@@ -664,7 +683,7 @@ aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref
     }
     h->last_B = B;
     h->last_T = Tmax;
-    return end_call(h, st);
+    return cg.end();
 }
 
 aec_status aec_debug_copy(aec_handle* h, int32_t what, float* dst, size_t n, void* stream) {
@@ -673,6 +692,12 @@ aec_status aec_debug_copy(aec_handle* h, int32_t what, float* dst, size_t n, voi
     if (!dst || n < (size_t)(B * T * 32)) return fail(h, AEC_ERR_INVALID_ARG, "dst too small");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     AEC_ON_DEVICE(h);
+    if (what < 0 || what > 5) return fail(h, AEC_ERR_INVALID_ARG, "unknown intermediate");
+    if ((what == 3 || what == 4) && !h->debug) return fail(h, AEC_ERR_INVALID_ARG, "enable aec_set_debug before aec_process");
+    // ordered after the last call (it may have run on another stream) like any other call
+    aec_status s = begin_call(h, st);
+    if (s != AEC_OK) return s;
+    CallGuard cg{h, st};
     if (what >= 0 && what <= 2) {
         HIP_TRY(h, hipMemcpy2DAsync(dst, 32 * sizeof(float), h->d_feats + 32 * what, 96 * sizeof(float),
                                     32 * sizeof(float), B * T, hipMemcpyDeviceToDevice, st));
@@ -680,12 +705,10 @@ aec_status aec_debug_copy(aec_handle* h, int32_t what, float* dst, size_t n, voi
         if (!h->debug) return fail(h, AEC_ERR_INVALID_ARG, "enable aec_set_debug before aec_process");
         HIP_TRY(h, hipMemcpyAsync(dst, h->d_dbg + (what - 3) * B * T * 32, B * T * 32 * sizeof(float),
                                   hipMemcpyDeviceToDevice, st));
-    } else if (what == 5) {
-        HIP_TRY(h, hipMemcpyAsync(dst, h->d_est, B * T * 32 * sizeof(float), hipMemcpyDeviceToDevice, st));
     } else {
-        return fail(h, AEC_ERR_INVALID_ARG, "unknown intermediate");
+        HIP_TRY(h, hipMemcpyAsync(dst, h->d_est, B * T * 32 * sizeof(float), hipMemcpyDeviceToDevice, st));
     }
-    return AEC_OK;
+    return cg.end();
 }
 
 aec_status aec_profile_enable(aec_handle* h, int32_t enable) {
@@ -803,9 +826,10 @@ aec_status aec_set_weights_device(aec_handle* h, const float* w, size_t n, void*
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     aec_status s = begin_call(h, st);
     if (s != AEC_OK) return s;
+    CallGuard cg{h, st};
     HIP_TRY(h, hipMemcpyAsync(h->d_w, w, n * sizeof(float), hipMemcpyDeviceToDevice, st));
     h->have_w = true;
-    return end_call(h, st);
+    return cg.end();
 }
 
 aec_status aec_train_forward(aec_handle* h, const float* mic, const float* ref, const float* near, int64_t n,
@@ -823,6 +847,7 @@ aec_status aec_train_forward(aec_handle* h, const float* mic, const float* ref, 
     AEC_ON_DEVICE(h);
     aec_status s = begin_call(h, st);
     if (s != AEC_OK) return s;
+    CallGuard cg{h, st};
     s = ensure_ws(h, B, T);
     if (s != AEC_OK) return s;
     const int64_t frames = (int64_t)B * T;
@@ -879,7 +904,7 @@ aec_status aec_train_forward(aec_handle* h, const float* mic, const float* ref, 
     h->train_B = B;
     h->train_T = (int32_t)T;
     ++h->train_gen;
-    return end_call(h, st);
+    return cg.end();
 }
 
 int64_t aec_train_generation(const aec_handle* h) { return h ? h->train_gen : -1; }
@@ -913,8 +938,9 @@ aec_status aec_train_backward(aec_handle* h, const float* grad_loss, float* grad
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     aec_status s = begin_call(h, st);
     if (s != AEC_OK) return s;
+    CallGuard cg{h, st};
     HIP_TRY(h, launch_train_backward(t, nblk, grad_loss, grad, st));
-    return end_call(h, st);
+    return cg.end();
 }
 
 aec_status aec_adam_step(aec_handle* h, float* params, const float* grad, float* exp_avg, float* exp_avg_sq,

@@ -119,6 +119,7 @@ struct aec_crn_handle {
     int* psync = nullptr;                          // arrival counters + error word
     int* perr_host = nullptr;                      // pinned copy of the error word, read back per call
     hipEvent_t perr_ev = nullptr;                  // recorded after that copy
+    int persist_timeouts = 0;                      // consecutive calls that timed out (2: persist = 0)
     bool persist_pending = false;                  // this call launched persistent grids: check before returning
     // profiling
     int profile = 0;
@@ -1006,9 +1007,14 @@ static aec_status persist_wait(aec_crn_handle* h) {
     if (!h->persist_pending) return AEC_OK;
     h->persist_pending = false;
     CRN_TRY(h, hipEventSynchronize(h->perr_ev));
-    if (*h->perr_host)
+    if (*h->perr_host) {
+        // two timed-out calls in a row (co-residency lost, e.g. CUs held by another process): the
+        // handle drops to the per-frame step kernel for every later call
+        if (++h->persist_timeouts >= 2) h->persist = 0;
         return crn_fail(h, AEC_ERR_HIP,
                         "persistent LSTM recurrence: a block timed out waiting for its team (outputs invalid)");
+    }
+    h->persist_timeouts = 0;
     return AEC_OK;
 }
 
@@ -1094,6 +1100,9 @@ struct StreamState {
     std::vector<uint8_t*> cat8, cats;
     uint8_t* xn8 = nullptr;
     uint8_t* xns = nullptr;
+    void* xnb = nullptr;                 // MX layer step, rnn_layers >= 3: the second xn set (bf16 rows,
+    uint8_t* xn8b = nullptr;             //   e4m3 shadow, scales) the odd middle layers write
+    uint8_t* xnsb = nullptr;
     float* skp = nullptr;                // split-K partial tiles / tile counters of the MX conv GEMMs (Bufs)
     int* skc = nullptr;
     int64_t sk_bytes = 0;
@@ -1155,20 +1164,30 @@ static hipGraphNode_t last_node(hipStream_t st) {
 // dtype 2, NavieComplexLSTM, per-hop: layer l as ONE launch (lstm_step_mx8_kernel): [x | h]
 // against [W_ih | W_hh] on the scaled MFMA, the cell update and the combination.  x is read
 // in place from its MX-fp8 shadow (the encoder's / previous combination's epilogue), or,
-// without one (AEC_CRN_MX8_SHADOW=0), quantised first into bf.aq / bf.as by the same rule.
-static aec_status run_lstm_mx_step(aec_crn_handle* h, StreamState& ss, const Bufs& bf, int l, int par, hipStream_t st) {
+// without one (AEC_CRN_MX8_SHADOW=0), quantised first into bf.aq / bf.as by the same rule
+// (*quant: that pass's rows).  A middle layer (neither first nor last, rnn_layers >= 3) reads
+// its input from one xn set and writes the other: blocks that finish early would otherwise
+// overwrite rows other blocks of the same launch still load.
+static void mx_step_args(aec_crn_handle* h, const StreamState& ss, const Bufs& bf, int l, int par,
+                         crn::StepMxArgs& ma, crn::RowSrc* quant) {
     const int* ch = h->cfg.conv_channels;
     const int L = h->L, H = h->H, S = h->S, D = h->D, Q = h->Q, B = ss.B;
     const bool last = l + 1 == h->nrnn;
-    crn::StepMxArgs ma{};
+    const bool in_b = l > 0 && ((l - 1) & 1), out_b = (l & 1) != 0;
+    void* xn_in = in_b ? ss.xnb : bf.xn;
+    void* xn_out = out_b ? ss.xnb : bf.xn;
+    uint8_t* xn8_in = in_b ? ss.xn8b : bf.xn8;
+    uint8_t* xns_in = in_b ? ss.xnsb : bf.xns;
+    ma = crn::StepMxArgs{};
     ma.wq = h->lcat[l].wq;
     ma.wsc = h->lcat[l].wsc;
     ma.bias = h->lih[l].bias;
     // x rows (b, s): the bf16 GEMM's implicit LSTM-input rows (run_lstm_input)
     const int64_t ld_in = l == 0 ? 2 * ch[L] : (int64_t)S * Q;
     const int64_t choff = l == 0 ? ch[L] : 0;
-    const uint8_t* x8 = l == 0 ? bf.cat8[L] : bf.xn8;
-    const uint8_t* xs = l == 0 ? bf.cats[L] : bf.xns;
+    const uint8_t* x8 = l == 0 ? bf.cat8[L] : xn8_in;
+    const uint8_t* xs = l == 0 ? bf.cats[L] : xns_in;
+    if (quant) *quant = crn::RowSrc{};
     if (x8) {
         ma.xq = x8;
         ma.xs = xs;
@@ -1179,19 +1198,20 @@ static aec_status run_lstm_mx_step(aec_crn_handle* h, StreamState& ss, const Buf
         ma.x_0 = choff;
         ma.x_elems = (int64_t)B * D * ld_in;
     } else {
-        crn::RowSrc a{};
-        a.src = l == 0 ? bf.cat[L] : bf.xn;
-        a.M = (int64_t)B * S;
-        a.K = H;
-        a.rshift = ilog2(S);
-        a.rs_hi = D * ld_in;
-        a.rs_lo = Q;
-        a.kshift = ilog2(Q);
-        a.ks = ld_in;
-        a.plim = D;
-        a.base_off = choff;
-        a.src_elems = (int64_t)B * D * ld_in;
-        CRN_TRY(h, crn::launch_mx8_quant(a, bf.aq, bf.as, st));
+        if (quant) {
+            crn::RowSrc& a = *quant;
+            a.src = l == 0 ? bf.cat[L] : xn_in;
+            a.M = (int64_t)B * S;
+            a.K = H;
+            a.rshift = ilog2(S);
+            a.rs_hi = D * ld_in;
+            a.rs_lo = Q;
+            a.kshift = ilog2(Q);
+            a.ks = ld_in;
+            a.plim = D;
+            a.base_off = choff;
+            a.src_elems = (int64_t)B * D * ld_in;
+        }
         ma.xq = bf.aq;                              // dense rows [(b, s)][H]
         ma.xs = bf.as;
         ma.x_f = (int64_t)S * H;
@@ -1208,14 +1228,21 @@ static aec_status run_lstm_mx_step(aec_crn_handle* h, StreamState& ss, const Buf
     ma.cst = ss.cst[l];
     ma.hx = ss.hx;
     ma.cnt = ss.mx_cnt;
-    ma.dst = reinterpret_cast<crn::bf16_t*>(last ? bf.cat[L] : bf.xn);
+    ma.dst = reinterpret_cast<crn::bf16_t*>(last ? bf.cat[L] : xn_out);
     ma.ldd = last ? 2 * ch[L] : (int64_t)S * Q;
     ma.ldf = D * ma.ldd;
     ma.dshift = ilog2(Q);
-    ma.q8 = last ? bf.cat8[L] : bf.xn8;
-    ma.qs = last ? bf.cats[L] : bf.xns;
+    ma.q8 = last ? bf.cat8[L] : out_b ? ss.xn8b : bf.xn8;
+    ma.qs = last ? bf.cats[L] : out_b ? ss.xnsb : bf.xns;
     ma.B = B;
     ma.H = H;
+}
+
+static aec_status run_lstm_mx_step(aec_crn_handle* h, StreamState& ss, const Bufs& bf, int l, int par, hipStream_t st) {
+    crn::StepMxArgs ma;
+    crn::RowSrc q;
+    mx_step_args(h, ss, bf, l, par, ma, &q);
+    if (q.src) CRN_TRY(h, crn::launch_mx8_quant(q, bf.aq, bf.as, st));
     CRN_TRY(h, crn::launch_lstm_step_mx8(ma, st));
     return AEC_OK;
 }
@@ -1532,6 +1559,24 @@ aec_status aec_crn_stream_open(aec_crn_handle* h, int32_t B) {
     const char* step_mx_env = getenv("AEC_CRN_STEP_MX");
     const int step_mx = step_mx_env ? atoi(step_mx_env) : 1;
     ss.mx_step = step_mx != 0 && h->mx8 && C * S == 4 && h->nrnn > 0 && h->lcat[0].wq != nullptr;
+    if (ss.mx_step && h->nrnn > 2) {
+        CRN_TRY(h, alloc(&ss.xnb, (size_t)B * S * H * es));
+        if (shadow_xn(h)) {
+            CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.xn8b), (size_t)B * S * H));
+            CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.xnsb), (size_t)B * S * H / 32));
+        }
+    }
+    if (ss.mx_step) {
+        // the kernel's layout preconditions for every layer (x taps of >= 256 k, ...): configs that
+        // pass the create-time checks but not these keep the bf16 step + combine
+        const Bufs bf{ss.x0,       ss.cat.data(), ss.gx,   ss.xn,  ss.mask,     ss.aq,    ss.as, ss.cat8.data(),
+                      ss.cats.data(), ss.xn8,      ss.xns, ss.skp, ss.skc, ss.sk_bytes, ss.skc_n};
+        for (int l = 0; l < h->nrnn && ss.mx_step; ++l) {
+            crn::StepMxArgs ma;
+            mx_step_args(h, ss, bf, l, 0, ma, nullptr);
+            ss.mx_step = crn::lstm_step_mx8_layout_ok(ma) && h->lcat[l].wq != nullptr;
+        }
+    }
     if (ss.mx_step) {
         CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.hx), (size_t)B * C * S * H * sizeof(float)));
         CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.mx_cnt), (size_t)crn::lstm_step_mx8_counters(H, B) * sizeof(int)));

@@ -2122,10 +2122,12 @@ __global__ __launch_bounds__(256) void lstm_step_mx8_kernel(StepMxArgs p) {
     if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+bool lstm_step_mx8_layout_ok(const StepMxArgs& a) {
+    return a.H % 256 == 0 && a.B > 0 && a.dshift >= 5 && a.x_sh >= 8 && (a.x_f | a.x_s | a.x_t | a.x_0) % 256 == 0;
+}
+
 hipError_t launch_lstm_step_mx8(const StepMxArgs& a, hipStream_t st) {
-    if (a.H % 256 || a.B <= 0 || (1 << a.dshift) % 32 || (1 << a.x_sh) % 256 || !a.hx || !a.cnt ||
-        (a.x_f | a.x_s | a.x_t | a.x_0) % 256)
-        return hipErrorInvalidValue;
+    if (!lstm_step_mx8_layout_ok(a) || !a.hx || !a.cnt) return hipErrorInvalidValue;
 #define CRN_MXSTEP(SB_, NB_, SR_)                                                                                 \
     do {                                                                                                          \
         auto kern = lstm_step_mx8_kernel<SB_, NB_, SR_>;                                                          \

@@ -128,6 +128,9 @@ struct StepMxArgs {
     int32_t B, H;
 };
 hipError_t launch_lstm_step_mx8(const StepMxArgs& a, hipStream_t st);
+// the layout preconditions of lstm_step_mx8_kernel (H % 256, 128-k stages inside one x tap, 32-unit
+// output groups): the pointer-free part of launch_lstm_step_mx8's argument check
+bool lstm_step_mx8_layout_ok(const StepMxArgs& a);
 int64_t lstm_step_mx8_counters(int H, int B);
 
 // Streaming (one hop per stream): frame = [prev hop, cur hop] of each stream

@@ -104,7 +104,14 @@ aec_status aec_crn_set_params(aec_crn_handle* h, const float* params, size_t n_p
  *   spec     : device [B, Tmax, 257] float2 or NULL: the masked spectrum
  *              (out_spec; frames t >= T_b unspecified)
  *   mask     : device [B, Tmax, 256, 2] float32 or NULL: the decoder output
- *              for bins 1..256 (mask_real, mask_imag before F.pad) */
+ *              for bins 1..256 (mask_real, mask_imag before F.pad)
+ * Host blocking: with the persistent LSTM recurrence (bf16 / fp8, the
+ * default when the grid fits the device) the call returns only after the
+ * LSTM stage has run on `stream` (its error word is read back, so a
+ * timed-out grid fails this call); the decoder and back kernels are queued
+ * and run asynchronously.  After two consecutive timed-out calls the handle
+ * switches to the per-frame step kernel for good (AEC_CRN_PERSIST=0 does
+ * that from the start). */
 aec_status aec_crn_process(aec_crn_handle* h, const float* mic, const float* far, const int64_t* lengths, int32_t B,
                            int64_t ld, float* out, int64_t ld_out, float* spec, float* mask, void* stream);
 

@@ -96,7 +96,8 @@ def normalise(x):
     """x - mean(x)/std(x) over the WHOLE array, unbiased std (ERB.py:254-256).
     Called per stream (batch=1 semantics)."""
     x = np.asarray(x, dtype=np.float64)
-    return x - x.mean() / x.std(ddof=1)
+    with np.errstate(invalid='ignore', divide='ignore'):   # silent rows: 0/0 = NaN, the reference's own result
+        return x - x.mean() / x.std(ddof=1)
 
 
 def stft(x):

@@ -36,8 +36,14 @@ def _bases():
 
 
 class TorchCrnPort:
-    def __init__(self, w, conf, version):
-        self.conf, self.version = conf, version
+    """nlms: None (the reference network) or dict(taps, mu, beta, delta): the
+    build-defined FD-NLMS front end of include/aec_crn.h, restated as in
+    crn_oracle.forward(..., nlms=...) — the mic spectrum is replaced (encoder
+    input and masking) by the a-priori error of aec_oracle.nlms (float64)
+    driven by the far spectrum."""
+
+    def __init__(self, w, conf, version, nlms=None):
+        self.conf, self.version, self.nlms = conf, version, nlms
         self.w = {k: torch.from_numpy(np.asarray(v, np.float32)) for k, v in w.items()}
         self.fwd, self.inv, self.win = _bases()
         self.cbn = version == 2 and conf['use_cbn']
@@ -100,6 +106,14 @@ class TorchCrnPort:
         L = len(self.conf['conv_channels']) - 1
         ms, fs = self.stft(mic), self.stft(far)
         mr, mi, fr, fi = ms[:, :257], ms[:, 257:], fs[:, :257], fs[:, 257:]
+        if self.nlms:
+            from aec_oracle import nlms as _nlms
+            nl = self.nlms
+            E = [_nlms((mr[b].double() + 1j * mi[b].double()).numpy().T, (fr[b].double() + 1j * fi[b].double()).numpy().T,
+                       taps=nl.get('taps', 4), mu=nl.get('mu', 0.3), beta=nl.get('beta', 0.5),
+                       delta=nl.get('delta', 1e-4)).T for b in range(mr.shape[0])]
+            mr = torch.from_numpy(np.stack([e.real for e in E]).astype(np.float32))
+            mi = torch.from_numpy(np.stack([e.imag for e in E]).astype(np.float32))
         out = torch.stack([mr, fr, mi, fi], 1)[:, :, 1:]
         skips = []
         for i in range(L):

@@ -69,3 +69,26 @@ def test_torch_port_matches_reference(name):
     out = port(torch.from_numpy(d['mic'])[None], torch.from_numpy(d['far'])[None])[0].numpy()
     assert out.shape == d['out_wav'].shape
     assert rel(out, d['out_wav']) <= 1e-4
+
+
+@pytest.mark.parametrize('name', ['v2E_2125', 'v1_2125'])
+def test_torch_port_nlms_matches_oracle(name):
+    # the NLMS -> CRN composition (no reference counterpart): the torch port's
+    # NLMS front end (the checker of the C4 bench-shape GPU test) against the
+    # float64 oracle's, on a 1 s far-end single-talk scene
+    import torch
+    from torch_crn_port import TorchCrnPort
+    from aec_amd import synth
+    nl = dict(taps=4, mu=0.3, beta=0.5, delta=1e-4)
+    m = META[name]
+    conf = dict(C.NET_CONF)
+    conf.update(m['overrides'])
+    w = C.make_weights(conf, m['version'], m['weight_seed'])
+    mic, far, _ = synth.scene(16000, 321, double_talk=False)
+    r = C.forward(w, conf, m['version'], mic, far, nlms=nl)
+    port = TorchCrnPort(w, conf, m['version'], nlms=nl)
+    out = port(torch.from_numpy(mic)[None], torch.from_numpy(far)[None])[0].numpy()
+    assert rel(out, r['out_wav']) <= 1e-4
+    plain = TorchCrnPort(w, conf, m['version'])(torch.from_numpy(mic)[None], torch.from_numpy(far)[None])[0].numpy()
+    assert rel(plain, r['out_wav']) > 1e-2          # the NLMS really ran
+

@@ -1,0 +1,176 @@
+"""GPU parity at the per-GPU shapes bench.py times for BASELINE configs 4 and 5,
+and the MX layer step's config coverage (include/aec_crn.h).
+
+* C4's per-GPU leg (`c4_nlms_crn_bf16_per_gpu` in the bench line): the
+  NLMS -> DCCRN bf16 batch at 256 x 160,000 samples (626-frame recurrence fed
+  by the FD-NLMS error spectrum, the persistent LSTM kernel, the row GEMMs at
+  their bench sizes).  Three far-end single-talk rows against the reference
+  op mix with the same NLMS front end (oracle/torch_crn_port.py with nlms=,
+  pinned to the float64 oracle by tests/test_crn_oracle.py, which the
+  reference goldens pin): out_wav relative RMS <= BF16_WAV_TOL and ERLE within
+  ERLE_DB dB.
+* C5's per-GPU unit (`c5_stream_fp8`): the hipGraph per-hop NLMS -> DCCRN fp8
+  step at 256 streams (8 MX stream blocks, 512 blocks per layer step) over
+  201 hops: every stream within FP8_WAV_TOL of the fp8 batch forward of the
+  same signal, three within FP8_WAV_TOL of the reference op mix.
+* The MX layer step (lstm_step_mx8_kernel) with rnn_layers = 3 (a middle layer
+  reads one xn set and writes the other) against the bf16 step + combine
+  (AEC_CRN_STEP_MX=0), and a config whose layout the MX step cannot take
+  (Q = 128) falling back to the bf16 step bit for bit.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+import aec_amd
+import crn_oracle as C
+from aec_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+NLMS = dict(taps=4, mu=0.3, beta=0.5, delta=1e-4)
+BF16_WAV_TOL = 1e-2
+FP8_WAV_TOL = 2e-2
+ERLE_DB = 0.1
+WEIGHT_SEED = 1
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.sqrt(np.mean((a - b) ** 2)) / max(np.sqrt(np.mean(b ** 2)), 1e-30))
+
+
+def build(dtype, nlms=NLMS, **over):
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+    conf = copy.deepcopy(aec_amd.net_conf)
+    conf.update(over)
+    net = aec_amd.dccrn2.DCCRN(conf, dtype=dtype, nlms=nlms).eval()
+    w = C.make_weights(conf, 2, WEIGHT_SEED)
+    sd = net.state_dict()
+    for k, v in w.items():
+        sd[k] = torch.from_numpy(v)
+    net.load_state_dict(sd, strict=True)
+    return net.to('cuda:0'), conf, w
+
+
+def port_out(w, conf, sigs, nlms=NLMS):
+    from torch_crn_port import TorchCrnPort
+    import os
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    port = TorchCrnPort(w, conf, 2, nlms=nlms)
+    return port(torch.from_numpy(np.stack([s[0] for s in sigs])), torch.from_numpy(np.stack([s[1] for s in sigs]))).numpy()
+
+
+def test_c4_nlms_crn_bf16_bench_shape():
+    import aec_oracle as O
+    net, conf, w = build('bf16')
+    B, n = 256, 160000
+    rows = (0, 131, 255)
+    g = torch.Generator(device='cuda:0').manual_seed(41)
+    M = 0.05 * torch.randn(B, n, device='cuda:0', generator=g)
+    F = 0.1 * torch.randn(B, n, device='cuda:0', generator=g)
+    sc = {r: synth.scene(n, 8100 + r, double_talk=False) for r in rows}
+    for r in rows:
+        M[r] = torch.from_numpy(sc[r][0]).cuda()
+        F[r] = torch.from_numpy(sc[r][1]).cuda()
+    with torch.no_grad():
+        out, _, _ = net.forward_ragged(M, F, [n] * B, want_spec=False)
+    torch.cuda.synchronize()
+    got = out[list(rows)].cpu().numpy()
+    assert got.shape == (3, 256 * (n // 256))
+    assert np.isfinite(out.cpu().numpy()).all()
+    ref = port_out(w, conf, [sc[r] for r in rows])
+    errs = [rel(got[i], ref[i]) for i in range(3)]
+    d_erle = [O.erle_db(sc[r][0], got[i]) - O.erle_db(sc[r][0], ref[i]) for i, r in enumerate(rows)]
+    print(f'C4 bf16 NLMS rows rel {errs} erle delta {d_erle}')
+    assert max(errs) <= BF16_WAV_TOL, errs
+    assert max(abs(d) for d in d_erle) <= ERLE_DB, d_erle
+
+
+def test_c5_fp8_stream_256_streams():
+    net, conf, w = build('fp8')
+    B, nh = 256, 201
+    n = 256 * (nh - 1)
+    sig = [synth.scene(n, 9300 + b) for b in range(B)]
+    M = torch.zeros(B, 256 * nh, device='cuda:0')
+    F = torch.zeros_like(M)
+    M[:, :n] = torch.from_numpy(np.stack([s[0] for s in sig])).cuda()
+    F[:, :n] = torch.from_numpy(np.stack([s[1] for s in sig])).cuda()
+    net.stream_open(B)
+    outs = []
+    with torch.no_grad():
+        for k in range(nh):
+            outs.append(net.stream_step(M[:, 256 * k:256 * (k + 1)], F[:, 256 * k:256 * (k + 1)]).clone())
+        bref, _, _ = net.forward_ragged(M[:, :n].contiguous(), F[:, :n].contiguous(), [n] * B, want_spec=False)
+    torch.cuda.synchronize()
+    got = torch.cat(outs[1:], dim=1)[:, :n].cpu().numpy()       # step k emits hop k - 1
+    bref = bref.cpu().numpy()
+    assert np.isfinite(got).all()
+    errs = [rel(got[b], bref[b]) for b in range(B)]
+    print(f'C5 256 streams: max rel vs batch {max(errs):.4g} (stream {int(np.argmax(errs))})')
+    assert max(errs) <= FP8_WAV_TOL, (int(np.argmax(errs)), max(errs))
+    rows = (0, 128, 255)
+    ref = port_out(w, conf, [sig[b] for b in rows])
+    e2 = [rel(got[b], ref[i]) for i, b in enumerate(rows)]
+    print(f'C5 rows vs reference op mix {e2}')
+    assert max(e2) <= FP8_WAV_TOL, e2
+
+
+def _stream_run(net, M, F, B, nh):
+    net.stream_open(B)
+    with torch.no_grad():
+        outs = [net.stream_step(M[:, 256 * k:256 * (k + 1)], F[:, 256 * k:256 * (k + 1)]).clone() for k in range(nh)]
+    torch.cuda.synchronize()
+    return torch.cat(outs[1:], dim=1).cpu().numpy()
+
+
+def _stream_inputs(B, n, seed0):
+    nh = n // 256 + 1
+    sig = [synth.scene(n, seed0 + b) for b in range(B)]
+    M = torch.zeros(B, 256 * (nh + 1), device='cuda:0')
+    F = torch.zeros_like(M)
+    M[:, :n] = torch.from_numpy(np.stack([s[0] for s in sig])).cuda()
+    F[:, :n] = torch.from_numpy(np.stack([s[1] for s in sig])).cuda()
+    return sig, M, F, nh
+
+
+def test_fp8_stream_three_lstm_layers(monkeypatch):
+    """rnn_layers = 3: the MX layer step of the middle layer must not read the
+    rows its own launch writes (it ping-pongs two xn sets)."""
+    net, conf, w = build('fp8', nlms=None, rnn_layers=3)
+    B, n = 40, 6144
+    sig, M, F, nh = _stream_inputs(B, n, 2500)
+    res = {}
+    for flag in ('0', '1'):
+        monkeypatch.setenv('AEC_CRN_STEP_MX', flag)                # read at stream_open
+        res[flag] = _stream_run(net, M, F, B, nh)[:, :n]
+    assert np.isfinite(res['1']).all()
+    assert not np.array_equal(res['1'], res['0'])
+    errs = [rel(res['1'][b], res['0'][b]) for b in range(B)]
+    print(f'3 layers, MX vs bf16 recurrence: max rel {max(errs):.4g}')
+    assert max(errs) <= FP8_WAV_TOL / 2, (int(np.argmax(errs)), max(errs))
+    ref = port_out(w, conf, [sig[b] for b in (0, 39)], nlms=None)
+    for i, b in enumerate((0, 39)):
+        assert rel(res['1'][b], ref[i]) <= FP8_WAV_TOL, b
+
+
+def test_fp8_stream_mx_layout_fallback(monkeypatch):
+    """conv_channels ending in 256 (H = 512, Q = 128 units per frequency row):
+    the MX layer step needs 256-k taps, so stream_open keeps the bf16 step +
+    combine — the same launches as AEC_CRN_STEP_MX=0, bit for bit — instead
+    of failing every aec_crn_stream_step."""
+    net, conf, w = build('fp8', nlms=None, conv_channels=[4, 16, 32, 64, 128, 256, 256])
+    B, n = 8, 4096
+    sig, M, F, nh = _stream_inputs(B, n, 2700)
+    res = {}
+    for flag in ('0', '1'):
+        monkeypatch.setenv('AEC_CRN_STEP_MX', flag)
+        res[flag] = _stream_run(net, M, F, B, nh)[:, :n]
+    assert np.isfinite(res['1']).all()
+    assert np.array_equal(res['1'], res['0'])
+    ref = port_out(w, conf, [sig[0]], nlms=None)
+    assert rel(res['1'][0], ref[0]) <= FP8_WAV_TOL
