@@ -103,35 +103,38 @@ def parse():
 
 
 def roofline(pipeline, kernel, ms_per_launch, frames_per_launch, pmc):
-    """Dominant kernel vs the MI355X roofline.  `achieved` = SURVEY.md §8(d)'s
-    per-frame algorithmic figure for the whole path (4,096 B; 82 kFLOP + the
-    NLMS's 19 kFLOP) x the frames one launch processes / the launch's time
-    (HIP events); the governing bound is the larger of the HBM and FP32 times.
-    The kernel's own algorithmic share (the part of the path it implements,
-    DESIGN.md §5) is reported beside it as `kernel_share`."""
+    """Dominant kernel vs the MI355X roofline.  `achieved` = the kernel's own
+    algorithmic work per frame (its share of the path, DESIGN.md §5: the
+    bytes it must move and the FLOPs of the FFT-based algorithm for the part
+    of the path it implements) x the frames one launch processes / the
+    launch's time (HIP events); `bound` is the larger of the HBM and FP32
+    fractions.  `path_priced` repeats the figure with SURVEY.md §8(d)'s
+    whole-path per-frame figures (4,096 B; 82 kFLOP + the NLMS's 19 kFLOP),
+    which charges the whole path to this one kernel (an upper bound)."""
     t = ms_per_launch * 1e-3
     fl = path_flops(pipeline)
-    t_hbm = PIPE['bytes'] / (HBM_PEAK_GBS * 1e9)
-    t_fl = fl / (FP32_PEAK_TFLOPS * 1e12)
     traffic = None
     kname = {'analysis': 'nlms_analysis', 'gru_synthesis': 'gru_synth'}.get(kernel, kernel) \
         if pipeline == 'full' else kernel
     if pmc and pmc.get('pipeline') == pipeline and kname in pmc.get('kernels', {}):
         traffic = pmc['kernels'][kname].get('hbm_bytes_per_launch')
     a = ALG[pipeline].get(kernel, dict(bytes=PIPE['bytes'], flops=fl))
-    share = dict(alg_bytes_per_frame=a['bytes'], alg_flops_per_frame=a['flops'],
-                 achieved_gbs=round(a['bytes'] * frames_per_launch / t / 1e9, 1),
-                 achieved_tflops=round(a['flops'] * frames_per_launch / t / 1e12, 3))
-    share['frac'] = round(max(share['achieved_gbs'] / HBM_PEAK_GBS, share['achieved_tflops'] / FP32_PEAK_TFLOPS), 4)
-    if t_hbm >= t_fl:
-        gbs = PIPE['bytes'] * frames_per_launch / t / 1e9
+    gbs = a['bytes'] * frames_per_launch / t / 1e9
+    tfl = a['flops'] * frames_per_launch / t / 1e12
+    pg = PIPE['bytes'] * frames_per_launch / t / 1e9
+    pt = fl * frames_per_launch / t / 1e12
+    path = dict(alg_bytes_per_frame=PIPE['bytes'], alg_flops_per_frame=fl, achieved_gbs=round(pg, 1),
+                achieved_tflops=round(pt, 3), frac=round(max(pg / HBM_PEAK_GBS, pt / FP32_PEAK_TFLOPS), 4))
+    common = dict(traffic=traffic, traffic_alg_bytes_per_launch=a['bytes'] * frames_per_launch, kernel=kernel,
+                  alg_bytes_per_frame=a['bytes'], alg_flops_per_frame=a['flops'],
+                  frames_per_launch=frames_per_launch, ms_per_launch=round(ms_per_launch, 4),
+                  hbm_frac=round(gbs / HBM_PEAK_GBS, 4), fp32_frac=round(tfl / FP32_PEAK_TFLOPS, 4),
+                  path_priced=path)
+    if gbs / HBM_PEAK_GBS >= tfl / FP32_PEAK_TFLOPS:
         return dict(bound='hbm', achieved=round(gbs, 1), peak=HBM_PEAK_GBS, unit='GB/s',
-                    frac=round(gbs / HBM_PEAK_GBS, 4), traffic=traffic, kernel=kernel,
-                    alg_bytes_per_frame=PIPE['bytes'], frames_per_launch=frames_per_launch, kernel_share=share)
-    tfl = fl * frames_per_launch / t / 1e12
+                    frac=round(gbs / HBM_PEAK_GBS, 4), **common)
     return dict(bound='valu_fp32', achieved=round(tfl, 3), peak=FP32_PEAK_TFLOPS, unit='TFLOP/s',
-                frac=round(tfl / FP32_PEAK_TFLOPS, 4), traffic=traffic, kernel=kernel,
-                alg_flops_per_frame=fl, frames_per_launch=frames_per_launch, kernel_share=share)
+                frac=round(tfl / FP32_PEAK_TFLOPS, 4), **common)
 
 
 def cpu_baseline(seconds, B=256, n=160000):
@@ -367,47 +370,145 @@ def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu, nlms=N
     return res
 
 
-def run_c5_stream(dev, B=256, hops=200, dtype='fp8', world=1):
+FP8_PEAK_TFLOPS = 5000.0      # MI355X_MICROARCH.md: dense FP8 (block-scaled e4m3: 2x the bf16 rate)
+
+
+def c5_flop_split(conf):
+    """Algorithmic FLOP per frame of the per-hop DCCRN v2 step
+    split by the MFMA type the fp8 step runs them on: MX-fp8 = the LSTM layers
+    (W_ih and W_hh, lstm_step_mx8_kernel), encoder layers 4-5 and decoder
+    levels 4-6 (conv_mx8 / the fused-parity MX levels, crn_api.hip); bf16 =
+    the narrow conv layers.  Fixed to configs.net_conf's layout."""
+    ch = conf['conv_channels']
+    fl = crn_flops_per_frame(conf, 2)
+    enc = lambda i: 2 * (256 >> (i + 1)) * ch[i + 1] * 5 * ch[i]
+    dec = lambda c: 2 * (256 >> c) * (2 * ch[c]) * (ch[c - 1] if c != 1 else 2) * 5
+    fp8 = fl['lstm'] + enc(4) + enc(5) + dec(4) + dec(5) + dec(6)
+    return dict(total=fl['total'], fp8=fp8, bf16=fl['total'] - fp8)
+
+
+def c5_roofline(conf, B, ms_per_hop, pmc):
+    """The whole hop (one hipGraph launch of the step's kernels) against the
+    MFMA roofline: time at peak = the MX-fp8 FLOPs at the dense fp8 peak + the
+    bf16 FLOPs at the dense bf16 peak; frac = that time / the measured hop."""
+    sp = c5_flop_split(conf)
+    t = ms_per_hop * 1e-3
+    t_peak = B * (sp['fp8'] / (FP8_PEAK_TFLOPS * 1e12) + sp['bf16'] / (BF16_PEAK_TFLOPS * 1e12))
+    ach = sp['total'] * B / t / 1e12
+    blended = sp['total'] * B / t_peak / 1e12
+    traffic = None
+    if pmc and pmc.get('B') == B:
+        traffic = pmc.get('hbm_bytes_per_hop')
+    return dict(bound='mfma', achieved=round(ach, 1), peak=round(blended, 1), unit='TFLOP/s',
+                frac=round(t_peak / t, 4), traffic=traffic,
+                kernel='the per-hop step (one hipGraph launch: front, NLMS, encoder GEMMs, 2 MX LSTM layer '
+                       'steps, decoder GEMMs, back)',
+                alg_flops_per_frame=sp['total'], fp8_flops_per_frame=sp['fp8'], bf16_flops_per_frame=sp['bf16'],
+                frames_per_launch=B,
+                peak_note='blended: MX-fp8 share at %.0f TF/s, bf16 share at %.0f TF/s' % (FP8_PEAK_TFLOPS,
+                                                                                          BF16_PEAK_TFLOPS),
+                frac_vs_bf16_peak=round(ach / BF16_PEAK_TFLOPS, 4), frac_vs_fp8_peak=round(ach / FP8_PEAK_TFLOPS, 4),
+                traffic_source='profiles/pmc_latest_c5.json (FETCH_SIZE / WRITE_SIZE passes of tools/c5_step.py, '
+                               '2 FETCH + WRITE KiB per the gfx950 correction)' if traffic else None)
+
+
+def cpu_baseline_c5(seconds, net, conf, nlms, B=256):
+    """The per-hop step with the reference op mix on host cores
+    (oracle/torch_crn_port.py TorchCrnStreamPort: one 256-sample hop per
+    stream per call, LSTM / NLMS / overlap-add state carried), bounded sample."""
+    import torch
+    sys.path.insert(0, os.path.join(REPO, 'oracle'))
+    from torch_crn_port import TorchCrnStreamPort
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    w = {k: v.detach().cpu().numpy() for k, v in net.state_dict().items()}
+    port = TorchCrnStreamPort(w, conf, 2, nlms=nlms)
+    port.stream_open(B)
+    g = torch.Generator().manual_seed(5)
+    mic = 0.1 * torch.randn(B, 256, generator=g)
+    far = 0.1 * torch.randn(B, 256, generator=g)
+    port.step(mic, far)
+    hops, t0 = 0, time.perf_counter()
+    while True:
+        port.step(mic, far)
+        hops += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or hops >= 2000:
+            break
+    return dict(value=round(B * hops / el, 1), unit='frames/s', cores=threads, kind='port',
+                ms_per_hop=round(el / hops * 1e3, 3),
+                sample=f'{hops} hops x {B} streams through oracle/torch_crn_port.py TorchCrnStreamPort '
+                       f'(reference op mix: conv1d DFT frame, conv2d / conv_transpose2d, nn.LSTM with carried '
+                       f'state, FD-NLMS per bin, float32), {el:.1f} s wall')
+
+
+def run_c5_stream(dev, B=256, hops=200, dtype='fp8', world=1, with_cpu=False, sweep=(1024, 4096),
+                  cpu_seconds=10.0):
     """BASELINE config 5: the hipGraph-captured per-hop step of the DCCRN
     (MX-fp8 LSTM input projections, recurrence and wide conv layers) fed by the FD-NLMS,
     B concurrent streams per GPU, one 256-sample hop per stream per step
     (aec_crn_stream_step).  With world > 1 every rank steps its own B streams
     (no data-path collective); the timed region is bracketed by barriers and
-    the time is the max over ranks."""
+    the time is the max over ranks.  Input: one random hop pair per stream,
+    resident in the same device buffers every step (the graph's input nodes
+    keep their pointers; parity of the step on real audio is
+    tests/test_gpu_bench_shapes.py)."""
     import torch
     import torch.distributed as dist
     import aec_amd
     from aec_amd import shard
     torch.manual_seed(0)
-    net = aec_amd.dccrn2.DCCRN(dict(aec_amd.net_conf), dtype=dtype, nlms=aec_amd.nlms_conf).eval().to(dev)
-    net.stream_open(B, device=dev)
-    g = torch.Generator(device=dev).manual_seed(5)
-    mic = 0.1 * torch.randn(B, 256, device=dev, generator=g)
-    far = 0.1 * torch.randn(B, 256, device=dev, generator=g)
-    out = torch.empty(B, 256, device=dev)
-    with torch.no_grad():
-        for _ in range(10):
-            net.stream_step(mic, far, out)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(hops):
-            net.stream_step(mic, far, out)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        dt = shard.max_over_ranks(time.perf_counter() - t0) / hops
+    conf = dict(aec_amd.net_conf)
+    net = aec_amd.dccrn2.DCCRN(conf, dtype=dtype, nlms=aec_amd.nlms_conf).eval().to(dev)
+
+    def time_hops(bb, nhops, barrier):
+        net.stream_open(bb, device=dev)
+        g = torch.Generator(device=dev).manual_seed(5)
+        mic = 0.1 * torch.randn(bb, 256, device=dev, generator=g)
+        far = 0.1 * torch.randn(bb, 256, device=dev, generator=g)
+        out = torch.empty(bb, 256, device=dev)
+        with torch.no_grad():
+            for _ in range(10):
+                net.stream_step(mic, far, out)
+            torch.cuda.synchronize(dev)
+            if barrier and world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(nhops):
+                net.stream_step(mic, far, out)
+            torch.cuda.synchronize(dev)
+            if barrier and world > 1:
+                dist.barrier()
+            el = time.perf_counter() - t0
+        return shard.max_over_ranks(el) / nhops if barrier else el / nhops
+
+    dt = time_hops(B, hops, True)
+    streams_sweep = None
+    if world == 1 and sweep:
+        streams_sweep = {str(B): round(B / dt, 1)}
+        for bb in sweep:
+            d2 = time_hops(bb, max(20, hops // 4), False)
+            streams_sweep[str(bb)] = round(bb / d2, 1)
+        time_hops(B, 1, False)                       # leave the bench shape's streams open
+    pmc = None
+    pp = os.path.join(REPO, 'profiles', 'pmc_latest_c5.json')
+    if os.path.exists(pp):
+        pmc = json.load(open(pp))
+    res = dict(workload=f'C5 (BASELINE configs[4]): {world} GPU(s) x {B} concurrent streams, one 256-sample hop per '
+                        f'stream per step through the hipGraph-captured STFT -> FD-NLMS (4 taps) -> DCCRN v2 '
+                        f'(net_conf, {dtype}' + (': bf16 + MX-fp8 LSTM input projections, LSTM recurrence (W_ih, W_hh, '
+                        'x, h) and encoder 4-5 / decoder 4-6 convs'
+                        if dtype == 'fp8' else '') + ') -> iSTFT step; input = one random hop pair per stream, '
+                        'resident in the same device buffers every step',
+               dtype=dtype, n_gpus=world, streams=B * world, hops=hops, ms_per_hop=round(dt * 1e3, 4),
+               frames_per_s=round(world * B / dt, 1), frames_per_s_per_gpu=round(B / dt, 1),
+               rtf=round(dt / 0.016, 5), roofline=c5_roofline(conf, B, dt * 1e3, pmc),
+               streams_sweep_frames_per_s_per_gpu=streams_sweep, cpu_baseline=None)
+    if with_cpu and world == 1:
+        res['cpu_baseline'] = cpu_baseline_c5(cpu_seconds, net, conf, aec_amd.nlms_conf, B)
     del net
     torch.cuda.empty_cache()
-    return dict(workload=f'C5 (BASELINE configs[4]): {world} GPU(s) x {B} concurrent streams, one 256-sample hop per '
-                         f'stream per step through the hipGraph-captured STFT -> FD-NLMS (4 taps) -> DCCRN v2 '
-                         f'(net_conf, {dtype}' + (': bf16 + MX-fp8 LSTM input projections, LSTM recurrence (W_hh, h) and '
-                         'encoder 4-5 / decoder 4-6 convs'
-                         if dtype == 'fp8' else '') + ') -> iSTFT step',
-                dtype=dtype, n_gpus=world, streams=B * world, hops=hops, ms_per_hop=round(dt * 1e3, 4),
-                frames_per_s=round(world * B / dt, 1), frames_per_s_per_gpu=round(B / dt, 1),
-                rtf=round(dt / 0.016, 5))
+    return res
 
 
 def cpu_baseline_train(seconds, B=16, n=160000):
@@ -678,6 +779,7 @@ def main():
     pipe_tfl = path_flops(args.pipeline) * B * T / pipe_t / 1e12
     cpu = None
     erle = None
+    erle_bypass = None
     c3 = None
     if world == 1 and not args.no_c3:
         # BASELINE config 3 (DCCRN bf16, 256 x 10 s) in the same driver-timed run
@@ -695,18 +797,22 @@ def main():
         c3f = dict(workload=crn_workload(args, 'fp8', 256), dtype='fp8', steps=args.c3_steps,
                    batches_in_flight=c3f['batches_in_flight'], frames_per_s=c3f['value'],
                    ms_per_step=c3f['ms_per_step'], stage_ms_per_step=c3f['stage_ms_per_step'])
-    c5 = None
+    c4 = None
     if world == 1 and not args.no_c3:
-        # C5: the same network fed by the FD-NLMS error spectrum (NLMS -> CRN composition)
-        c5 = run_crn(args, dev, rank, world, 'bf16', args.c3_steps, 2, 256, 160000, False, aec_amd.nlms_conf)
-        c5 = dict(workload=crn_workload(args, 'bf16', 256) + ' fed by the FD-NLMS error spectrum (taps 4)',
-                  dtype='bf16', steps=args.c3_steps, batches_in_flight=c5['batches_in_flight'],
-                  frames_per_s=c5['value'], ms_per_step=c5['ms_per_step'],
-                  stage_ms_per_step=c5['stage_ms_per_step'])
+        # C4's per-GPU leg: FD-NLMS + DCCRN post-filter (bf16) on one GPU's shard of utterances
+        c4 = run_crn(args, dev, rank, world, 'bf16', args.c3_steps, 2, 256, 160000, False, aec_amd.nlms_conf)
+        c4 = dict(workload='C4 (BASELINE configs[3]) per-GPU leg: end-to-end STFT -> FD-NLMS (4 taps) -> DCCRN v2 '
+                           'post-filter (dccrn2.py, configs.net_conf, bf16 MFMA) -> iSTFT on one GPU\'s shard of 256 '
+                           'concurrent 10 s 16 kHz utterances (the 8-GPU job runs this per rank, no data-path '
+                           'collective)',
+                  dtype='bf16', steps=args.c3_steps, batches_in_flight=c4['batches_in_flight'],
+                  frames_per_s=c4['value'], ms_per_step=c4['ms_per_step'],
+                  stage_ms_per_step=c4['stage_ms_per_step'])
     c5s = None
     if not args.no_c3:
         # C5 is quoted on 8 GPUs: the per-hop step runs on every rank (streams sharded, weak scaling)
-        c5s = run_c5_stream(dev, world=world)
+        c5s = run_c5_stream(dev, world=world, with_cpu=rank == 0 and world == 1 and not args.no_cpu,
+                            sweep=() if args.no_sweep else (1024, 4096))
     tr = None
     if world == 1 and not args.no_train:
         tr = run_train(dev, 16, 160000, args.train_steps, with_cpu=not args.no_cpu)
@@ -724,6 +830,23 @@ def main():
             return o[0].cpu().numpy()
 
         erle = erle_check(gpu1, lambda m_, r_, n_: aec_oracle.aec_forward(m_, r_, n_, erb_np, w, nlms)[0], n)
+        erle['note'] = ('GPU vs the float64 oracle of the same pipeline; the oracle\'s FD-NLMS is the build\'s own '
+                        '(the reference has none), so this delta is GPU-vs-oracle; erle_bypass is the reference pin')
+        # the one ERLE the reference pins: the Little_net path (NLMS bypass) vs the reference restatement
+        # (aec_oracle.little_net_forward, pinned to the reference goldens), 10 s far-end single talk
+        pf = aec_amd.Little_net(aec_amd.speech_conf, 32).eval()
+        pf.load_state_dict(net.state_dict())
+        pf = pf.to(dev)
+
+        def gpu_pf(m_, r_, n_):
+            with torch.no_grad():
+                o, _ = pf.forward_ragged(*(torch.from_numpy(x)[None].to(dev) for x in (m_, r_, n_)), erb, [len(m_)])
+            return o[0].cpu().numpy()
+
+        erle_bypass = erle_check(gpu_pf, lambda m_, r_, n_: aec_oracle.little_net_forward(m_, r_, n_, erb_np, w)[0], n)
+        erle_bypass['path'] = ('reference Little_net (ERB.py:252-334, NLMS bypass) on the GPU vs its float64 '
+                               'restatement pinned by the reference goldens')
+        del pf
     if rank == 0:
         line = {
             'metric': '16kHz frames/sec/GPU (batched AEC) + RTF@batch=1; ERLE delta vs reference',
@@ -749,10 +872,11 @@ def main():
                                   'hbm_frac': round(pipe_gbs / HBM_PEAK_GBS, 4),
                                   'fp32_frac': round(pipe_tfl / FP32_PEAK_TFLOPS, 4)},
             'erle': erle,
+            'erle_bypass': erle_bypass,
             'cpu_baseline': cpu,
             'c3_crn_bf16': c3,
             'c3_crn_fp8': c3f,
-            'c5_nlms_crn_bf16': c5,
+            'c4_nlms_crn_bf16_per_gpu': c4,
             'c5_stream_fp8': c5s,
             'train_step': tr,
         }

@@ -161,3 +161,94 @@ class TorchCrnPort:
 
 def fixture_port(conf, version, seed):
     return TorchCrnPort(C.make_weights(conf, version, seed), conf, version)
+
+
+class TorchCrnStreamPort(TorchCrnPort):
+    """The same op mix stepped one 256-sample hop per stream per call — the
+    CPU counterpart of aec_crn_stream_step (BASELINE config 5), used as the
+    c5_stream_fp8 cpu_baseline in bench.py.  Frame s = [hop s-1, hop s]; the
+    encoder / decoder convs have time extent 1, so a frame goes through them
+    alone; the LSTM state (h, c) of each NavieComplexLSTM cell x input sequence
+    is carried per stream, the FD-NLMS state (taps, far history, power) per
+    stream and bin, and the iSTFT overlap-adds the previous frame's second
+    half: step s emits hop s-1 of __call__'s out_wav."""
+
+    def stream_open(self, B):
+        L = len(self.conf['conv_channels']) - 1
+        self.B = B
+        self.prev = torch.zeros(2, B, 256)
+        self.tail = torch.zeros(B, 1, 256)
+        self.state = {}
+        if self.nlms:
+            t = self.nlms.get('taps', 4)
+            self.nW = torch.zeros(B, t, 257, dtype=torch.complex128)
+            self.nH = torch.zeros(B, t, 257, dtype=torch.complex128)
+            self.nP = torch.zeros(B, 257, dtype=torch.float64)
+        w2 = self.win ** 2
+        self.coff = (w2[:256] + w2[256:] + 1e-8)[None, None]
+        self.L = L
+
+    def _lstm_step(self, key, x):
+        y, self.state[key] = self.lstms[key[0]](x[None], self.state.get(key))
+        return y[0]
+
+    @torch.no_grad()
+    def step(self, mic_hop, far_hop):
+        """mic_hop / far_hop [B, 256] float32 -> out hop [B, 256]."""
+        frames = torch.stack([torch.cat([self.prev[0], mic_hop], 1), torch.cat([self.prev[1], far_hop], 1)])
+        self.prev = torch.stack([mic_hop, far_hop])
+        s = F.conv1d(frames.reshape(-1, 1, 512), self.fwd)[..., 0].reshape(2, self.B, 514)
+        mr, mi, fr, fi = s[0, :, :257], s[0, :, 257:], s[1, :, :257], s[1, :, 257:]
+        if self.nlms:
+            nl = self.nlms
+            D = torch.complex(mr.double(), mi.double())
+            self.nH = torch.roll(self.nH, 1, dims=1)
+            self.nH[:, 0] = torch.complex(fr.double(), fi.double())
+            e = D - (self.nW * self.nH).sum(1)
+            beta = nl.get('beta', 0.5)
+            self.nP = beta * self.nP + (1 - beta) * (self.nH.abs() ** 2).sum(1)
+            self.nW = self.nW + nl.get('mu', 0.3) * e[:, None] * self.nH.conj() / (self.nP + nl.get('delta', 1e-4))[:, None]
+            mr, mi = e.real.float(), e.imag.float()
+        out = torch.stack([mr, fr, mi, fi], 1)[:, :, 1:, None]
+        skips = []
+        for i in range(self.L):
+            out = self._cconv(out, f'encoder.{i}.0', False)
+            out = F.prelu(self._norm(out, f'encoder.{i}.1', self.cbn), self.w[f'encoder.{i}.2.weight'])
+            skips.append(out)
+        B, Cc, D, _ = out.shape
+        if self.version == 1:
+            out = self._lstm_step(('lstm', 0), out.reshape(B, Cc * D)).reshape(B, Cc, D, 1)
+        else:
+            xr, xi = out[:, :Cc // 2].reshape(B, -1), out[:, Cc // 2:].reshape(B, -1)
+            for l in range(self.conf['rnn_layers']):
+                Rk, Ik = f'enhance.{l}.real_lstm', f'enhance.{l}.imag_lstm'
+                rr, ri = self._lstm_step((Rk, 'r'), xr), self._lstm_step((Ik, 'r'), xr)
+                ir, ii = self._lstm_step((Rk, 'i'), xi), self._lstm_step((Ik, 'i'), xi)
+                xr, xi = rr - ii, ir + ri
+            out = torch.cat([xr.reshape(B, Cc // 2, D), xi.reshape(B, Cc // 2, D)], 1)[..., None]
+        for d in range(self.L):
+            a, b = out, skips[-1 - d]
+            ca, cb = a.shape[1] // 2, b.shape[1] // 2
+            out = torch.cat([a[:, :ca], b[:, :cb], a[:, ca:], b[:, cb:]], 1)
+            out = self._cconv(out, f'decoder.{d}.0', True)
+            if d != self.L - 1:
+                out = F.prelu(self._norm(out, f'decoder.{d}.1', self.cbn), self.w[f'decoder.{d}.2.weight'])
+            elif self.version == 1:
+                out = torch.tanh(self._norm(out, f'decoder.{d}.1', False))
+        mkr, mki = F.pad(out[:, 0, :, 0], [1, 0]), F.pad(out[:, 1, :, 0], [1, 0])
+        mode = 'C' if self.version == 1 else self.conf['masking_mode']
+        if mode == 'E':
+            mags = torch.sqrt(mr ** 2 + mi ** 2 + 1e-8)
+            ph = torch.atan2(mi, mr)
+            mm = torch.sqrt(mkr ** 2 + mki ** 2)
+            mph = torch.atan2(mki / (mm + 1e-8), mkr / (mm + 1e-8))
+            em = torch.tanh(mm) * mags
+            er, ei = em * torch.cos(ph + mph), em * torch.sin(ph + mph)
+        elif mode == 'C':
+            er, ei = mr * mkr - mi * mki, mr * mki + mi * mkr
+        else:
+            er, ei = mr * mkr, mi * mki
+        y = F.conv_transpose1d(torch.cat([er, ei], 1)[..., None], self.inv)     # [B, 1, 512]
+        hop = (self.tail + y[..., :256]) / self.coff
+        self.tail = y[..., 256:]
+        return hop[:, 0]

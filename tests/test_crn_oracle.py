@@ -92,3 +92,29 @@ def test_torch_port_nlms_matches_oracle(name):
     plain = TorchCrnPort(w, conf, m['version'])(torch.from_numpy(mic)[None], torch.from_numpy(far)[None])[0].numpy()
     assert rel(plain, r['out_wav']) > 1e-2          # the NLMS really ran
 
+
+
+@pytest.mark.parametrize('nlms', [None, dict(taps=4, mu=0.3, beta=0.5, delta=1e-4)])
+def test_torch_stream_port_equals_batch_port(nlms):
+    # bench.py's c5_stream_fp8 cpu_baseline: the port stepped one hop per call
+    # reproduces the batch port (step s emits hop s-1 of out_wav)
+    import torch
+    from torch_crn_port import TorchCrnPort, TorchCrnStreamPort
+    from aec_amd import synth
+    m = META['v2E_2125']
+    conf = dict(C.NET_CONF)
+    w = C.make_weights(conf, 2, m['weight_seed'])
+    n, B = 2560, 2
+    sig = [synth.scene(n, 400 + b) for b in range(B)]
+    mic = torch.from_numpy(np.stack([s[0] for s in sig]))
+    far = torch.from_numpy(np.stack([s[1] for s in sig]))
+    ref = TorchCrnPort(w, conf, 2, nlms=nlms)(mic, far).numpy()
+    sp = TorchCrnStreamPort(w, conf, 2, nlms=nlms)
+    sp.stream_open(B)
+    nh = n // 256 + 1
+    pad = lambda x: torch.nn.functional.pad(x, [0, 256 * nh - n])
+    mic, far = pad(mic), pad(far)
+    hops = [sp.step(mic[:, 256 * k:256 * (k + 1)], far[:, 256 * k:256 * (k + 1)]) for k in range(nh)]
+    got = torch.cat(hops[1:], 1).numpy()[:, :ref.shape[1]]
+    assert got.shape == ref.shape
+    assert rel(got, ref) <= 1e-4
