@@ -39,6 +39,9 @@
 #include "aec_tables.h"
 
 namespace aec {
+#ifdef AEC_TICK_PROF
+constexpr int kNlmsWavesProf = 12;
+#endif
 
 // --------------------------------------------------------------------------
 // K1: per-(stream, signal, chunk) float64 partial moments.  The normaliser
@@ -271,6 +274,18 @@ __global__ __launch_bounds__(256, 3) void analysis_kernel(AnalysisArgs p) {
 // HBM traffic beyond K2: the E spectrum, 2 KiB per frame, written once and
 // read back once (L2-resident) for mic_erb.
 // --------------------------------------------------------------------------
+#ifdef AEC_TICK_PROF
+// timing experiments only (tools/tick_prof.py): s_memtime stamps of blocks 0 and 128 per wave and
+// tick: loop top, work done, after barrier 1, after barrier 2
+__device__ unsigned long long g_tick[2][kNlmsWavesProf][48][4];
+#define TICK_STAMP(slot)                                                                               \
+    do {                                                                                               \
+        if ((blockIdx.x == 0 || blockIdx.x == 128) && lane == 0 && c < 48)                             \
+            g_tick[blockIdx.x ? 1 : 0][wave][c][slot] = __builtin_amdgcn_s_memtime();                  \
+    } while (0)
+#else
+#define TICK_STAMP(slot) do {} while (0)
+#endif
 constexpr int kSpecRow = 256;          // float2 per spectrum row
 constexpr int kNlmsWaves = 12;
 constexpr int kERow = 512 + 48;        // floats per LDS error row: 256 float2, then ERB partials
@@ -385,6 +400,7 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
         st.reset(k == 0);
         float2 dd[kFPB], rr[kFPB];
         for (int c = 0; c < nch + 2; ++c) {
+            TICK_STAMP(0);
             const int c1 = c - 1;
             if (c1 >= 0 && c1 < nch && !(p.mode & 1)) {
                 // recursion of chunk c-1 -> E rows (LDS buffer c-1 & 1, spectrum
@@ -408,7 +424,9 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
                 }
             }
             if (erb_role == 2 && c >= 2 && !(p.mode & 4)) mic_erb_pass(c - 2);
+            TICK_STAMP(1);
             __syncthreads();                                          // rows of chunk c complete
+            TICK_STAMP(2);
             if (c < nch) {
 #pragma unroll
                 for (int i = 0; i < kFPB; ++i) {
@@ -418,6 +436,7 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
                 }
             }
             __syncthreads();                                          // rows consumed
+            TICK_STAMP(3);
         }
         return;
     }
@@ -431,6 +450,7 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
         wave_prefetch(pf, row_ref, n_ref, 4 * q, lane, al_ref);
     }
     for (int c = 0; c < nch + 2; ++c) {
+        TICK_STAMP(0);
         const int wt = c * kFPB + 4 * q;
         const int64_t t = wt + gg;
         float2 xa[8], xb[8], x128;
@@ -462,8 +482,11 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
                 row_to_scr(scr, lb, xa, xb, x128);
             }
         }
+        TICK_STAMP(1);
         __syncthreads();                                              // rows of chunk c complete
+        TICK_STAMP(2);
         __syncthreads();                                              // rows consumed
+        TICK_STAMP(3);
     }
 }
 
@@ -755,3 +778,10 @@ hipError_t launch_nlms_analysis(const NlmsArgs& a, int nb, hipStream_t st) {
 }
 
 }  // namespace aec
+
+#ifdef AEC_TICK_PROF
+extern "C" int aec_debug_tick_prof(void* host, size_t bytes) {
+    if (bytes < sizeof(aec::g_tick)) return -1;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(aec::g_tick), sizeof(aec::g_tick)) == hipSuccess ? 0 : -2;
+}
+#endif
