@@ -733,21 +733,22 @@ def main():
         rtf1 = float(np.median(lat)) / args.seconds if lat else None
         sweep = None
         if not args.no_sweep and world == 1:
-            # frames/s at B concurrent streams per call (one batch in flight, 3 synchronous calls
-            # after one warm-up); the drop-in's own operating point is B = 1 (test.py:139)
+            # frames/s at B concurrent streams per call (one batch in flight, 5 synchronous calls
+            # after two warm-ups); the drop-in's own operating point is B = 1 (test.py:139)
             sweep = {}
             for bb in [1, 16, 64, 256, 1024, 4096]:
                 if bb > B:
                     mm, rr, nn_ = (x.repeat((bb + B - 1) // B, 1)[:bb] for x in (mic, ref, near))
                 else:
                     mm, rr, nn_ = mic[:bb], ref[:bb], near[:bb]
-                net.forward_ragged(mm, rr, nn_, erb, [n] * bb)
-                torch.cuda.synchronize(dev)
-                t1 = time.perf_counter()
-                for _ in range(3):
+                for _ in range(2):                     # warm-up: workspace growth, work lists
                     net.forward_ragged(mm, rr, nn_, erb, [n] * bb)
                 torch.cuda.synchronize(dev)
-                sweep[str(bb)] = round(bb * T * 3 / (time.perf_counter() - t1), 1)
+                t1 = time.perf_counter()
+                for _ in range(5):
+                    net.forward_ragged(mm, rr, nn_, erb, [n] * bb)
+                torch.cuda.synchronize(dev)
+                sweep[str(bb)] = round(bb * T * 5 / (time.perf_counter() - t1), 1)
                 del mm, rr, nn_
             torch.cuda.empty_cache()
 
