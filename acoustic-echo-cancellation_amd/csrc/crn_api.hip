@@ -754,12 +754,12 @@ static void splitk_need(const aec_crn_handle* h, int64_t B, int64_t* bytes, int6
 }
 
 template <typename T>
-static aec_status run_encoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipStream_t st) {
+static aec_status run_encoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipStream_t st, int first = 0) {
     using crn::RowEpi;
     using crn::RowSrc;
     aec_status s = AEC_OK;
     const int* ch = h->cfg.conv_channels;
-    for (int i = 0; i < h->L; ++i) {
+    for (int i = first; i < h->L; ++i) {
         const int Fin = 256 >> i, Fo = Fin / 2;
         const int cin = i == 0 ? 8 : ch[i];
         const int64_t ld_in = i == 0 ? 8 : 2 * ch[i];
@@ -1128,6 +1128,10 @@ struct StreamState {
     hipGraphNode_t front_node[2] = {nullptr, nullptr}, back_node[2] = {nullptr, nullptr};
     crn::StreamFrontArgs front_args[2];
     crn::StreamBackArgs back_args[2];
+    // bf16 / fp8: the front, the NLMS step and the narrow encoder levels 0 .. enc_nlev-1 as one
+    // launch (crn_stream_enc_kernel); its graph node is front_node (AEC_CRN_STREAM_FUSE=0: off)
+    int enc_nlev = 0;
+    crn::StreamEncArgs enc_args[2];
     hipStream_t cap = nullptr;           // capture stream
 };
 
@@ -1247,6 +1251,58 @@ static aec_status run_lstm_mx_step(aec_crn_handle* h, StreamState& ss, const Buf
     return AEC_OK;
 }
 
+// the fused front's level table (stream_open checked the shapes: stream_enc_levels)
+static crn::StreamEncArgs stream_enc_args(aec_crn_handle* h, int B) {
+    StreamState& ss = *h->ss;
+    const int* ch = h->cfg.conv_channels;
+    crn::StreamEncArgs ea{};
+    ea.tab = h->d_tab;
+    ea.B = B;
+    if (h->cfg.nlms_taps > 0) {
+        ea.state = ss.nstate;
+        ea.espec = ss.espec;
+        ea.mu = h->cfg.nlms_mu;
+        ea.beta = h->cfg.nlms_beta;
+        ea.delta = h->cfg.nlms_delta;
+    }
+    ea.nlev = ss.enc_nlev;
+    for (int i = 0; i < ss.enc_nlev; ++i) {
+        const Packed& pk = h->enc[i];
+        crn::StreamEncLevel& L = ea.lev[i];
+        L.w = reinterpret_cast<const bf16_t*>(pk.w);
+        L.bias = pk.bias;
+        L.alpha = pk.alpha;
+        L.kpad = pk.kpad;
+        L.N = pk.N;
+        L.nchunk = (pk.K + 31) / 32;
+        L.cin_shift = ilog2(i == 0 ? 8 : ch[i]);
+        L.out = reinterpret_cast<bf16_t*>(ss.cat[i + 1]);
+        L.ldo = 2 * ch[i + 1];
+        L.choff = ch[i + 1];
+    }
+    return ea;
+}
+
+// leading encoder levels crn_stream_enc_kernel can take: bf16 GEMM (not MX), PReLU, 8 output tiles
+// of 16 bins x 16 channels, K <= 160, no MX shadow on the output
+static int stream_enc_levels(const aec_crn_handle* h) {
+    if (h->es != 2) return 0;
+    const char* v = getenv("AEC_CRN_STREAM_FUSE");
+    if (v && atoi(v) == 0) return 0;
+    const int* ch = h->cfg.conv_channels;
+    int n = 0;
+    for (int i = 0; i < std::min(3, h->L); ++i) {
+        const Packed& pk = h->enc[i];
+        const int Fo = 128 >> i, cin = i == 0 ? 8 : ch[i];
+        if (pk.wq || pk.act != 1 || pk.N % 16 || (Fo / 16) * (pk.N / 16) != 8 || 4 % (pk.N / 16) ||
+            (pk.K + 31) / 32 > crn::kStreamEncChunks || ilog2(cin) < 3 || pk.kpad < 32 * ((pk.K + 31) / 32) ||
+            shadow_level(h, i + 1))
+            break;
+        ++n;
+    }
+    return n;
+}
+
 template <typename T>
 static aec_status stream_launches(aec_crn_handle* h, int par, const StreamIo& io, hipStream_t st) {
     StreamState& ss = *h->ss;
@@ -1260,19 +1316,35 @@ static aec_status stream_launches(aec_crn_handle* h, int par, const StreamIo& io
     const aec_crn_config& c = h->cfg;
     // the frame = [previous hop (ring), this call's hop (caller's buffer)]; the front kernel
     // copies this hop into the ring slot of this parity
-    crn::StreamFrontArgs fa{prev_mic, io.mic, prev_far, io.far, h->d_tab, ss.x0, B};
-    fa.ld_cur = io.ld_in;
-    fa.save_mic = cur_mic;
-    fa.save_far = cur_far;
-    if (c.nlms_taps > 0) fa.rows = ss.nrows;
-    CRN_TRY(h, crn::launch_stream_front<T>(fa, st));
-    ss.front_node[par] = last_node(st);
-    ss.front_args[par] = fa;
-    if (c.nlms_taps > 0) {
-        crn::StreamNlmsArgs na{ss.nrows, ss.nstate, ss.espec, ss.x0, B, c.nlms_mu, c.nlms_beta, c.nlms_delta};
-        CRN_TRY(h, crn::launch_stream_nlms<T>(na, c.nlms_taps, st));
+    int first = 0;
+    if (ss.enc_nlev > 0) {
+        crn::StreamEncArgs ea = stream_enc_args(h, B);
+        ea.prev_mic = prev_mic;
+        ea.cur_mic = io.mic;
+        ea.prev_far = prev_far;
+        ea.cur_far = io.far;
+        ea.ld_cur = io.ld_in;
+        ea.save_mic = cur_mic;
+        ea.save_far = cur_far;
+        CRN_TRY(h, crn::launch_stream_enc(ea, c.nlms_taps, st));
+        ss.front_node[par] = last_node(st);
+        ss.enc_args[par] = ea;
+        first = ss.enc_nlev;
+    } else {
+        crn::StreamFrontArgs fa{prev_mic, io.mic, prev_far, io.far, h->d_tab, ss.x0, B};
+        fa.ld_cur = io.ld_in;
+        fa.save_mic = cur_mic;
+        fa.save_far = cur_far;
+        if (c.nlms_taps > 0) fa.rows = ss.nrows;
+        CRN_TRY(h, crn::launch_stream_front<T>(fa, st));
+        ss.front_node[par] = last_node(st);
+        ss.front_args[par] = fa;
+        if (c.nlms_taps > 0) {
+            crn::StreamNlmsArgs na{ss.nrows, ss.nstate, ss.espec, ss.x0, B, c.nlms_mu, c.nlms_beta, c.nlms_delta};
+            CRN_TRY(h, crn::launch_stream_nlms<T>(na, c.nlms_taps, st));
+        }
     }
-    aec_status s = run_encoder<T>(h, bf, B, st);
+    aec_status s = run_encoder<T>(h, bf, B, st, first);
     if (s != AEC_OK) return s;
     for (int l = 0; l < h->nrnn; ++l) {
         if (ss.mx_step) {
@@ -1304,18 +1376,21 @@ static aec_status stream_launches(aec_crn_handle* h, int par, const StreamIo& io
 static aec_status stream_set_io(aec_crn_handle* h, int par, const StreamIo& io) {
     StreamState& ss = *h->ss;
     crn::StreamFrontArgs& fa = ss.front_args[par];
+    crn::StreamEncArgs& ea = ss.enc_args[par];
     crn::StreamBackArgs& ba = ss.back_args[par];
-    if (fa.cur_mic == io.mic && fa.cur_far == io.far && fa.ld_cur == io.ld_in && ba.out == io.out &&
-        ba.ld_out == io.ld_out)
-        return AEC_OK;
-    fa.cur_mic = io.mic;
-    fa.cur_far = io.far;
-    fa.ld_cur = io.ld_in;
+    const bool fused = ss.enc_nlev > 0;
+    const float* cm = fused ? ea.cur_mic : fa.cur_mic;
+    const float* cf = fused ? ea.cur_far : fa.cur_far;
+    const int64_t cl = fused ? ea.ld_cur : fa.ld_cur;
+    if (cm == io.mic && cf == io.far && cl == io.ld_in && ba.out == io.out && ba.ld_out == io.ld_out) return AEC_OK;
+    fa.cur_mic = ea.cur_mic = io.mic;
+    fa.cur_far = ea.cur_far = io.far;
+    fa.ld_cur = ea.ld_cur = io.ld_in;
     ba.out = io.out;
     ba.ld_out = io.ld_out;
     hipKernelNodeParams kp{};
     CRN_TRY(h, hipGraphKernelNodeGetParams(ss.front_node[par], &kp));
-    void* fargs[] = {&fa};
+    void* fargs[] = {fused ? static_cast<void*>(&ea) : static_cast<void*>(&fa)};
     kp.kernelParams = fargs;
     kp.extra = nullptr;
     CRN_TRY(h, hipGraphExecKernelNodeSetParams(ss.graph[par], ss.front_node[par], &kp));
@@ -1600,6 +1675,7 @@ aec_status aec_crn_stream_open(aec_crn_handle* h, int32_t B) {
         CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.nstate), (size_t)B * 2 * h->cfg.nlms_taps * 256 * sizeof(float2)));
         CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.espec), (size_t)B * 256 * sizeof(float2)));
     }
+    ss.enc_nlev = stream_enc_levels(h);
     CRN_TRY(h, hipStreamCreateWithFlags(&ss.cap, hipStreamNonBlocking));
     CRN_TRY(h, hipDeviceSynchronize());
     ss.k = 0;

@@ -170,6 +170,38 @@ struct StreamBackArgs {
     int64_t ld_out = 256;
 };
 
+// Fused per-hop front (crn_stream.hip): frame -> rFFT of mic and far -> [FD-NLMS step] -> X0 ->
+// encoder levels 0 .. nlev-1 (bf16 implicit-GEMM MFMA, 8 tiles of 16 x 16 per level), one block
+// per stream; replaces launch_stream_front + launch_stream_nlms + those levels' row GEMMs.
+constexpr int kStreamEncChunks = 5;   // 32-k chunks per level (K <= 160)
+struct StreamEncLevel {
+    const bf16_t* w;            // packed [npad][kpad] (pack_encoder)
+    const float* bias;
+    float alpha;                // PReLU
+    int32_t kpad, N, nchunk;    // nchunk = ceil(K / 32)
+    int32_t cin_shift;          // log2 of the input map's channels per bin (3: X0's 8)
+    bf16_t* out;                // cat[l + 1] [B][Fo][ldo]: the encoder half at channel offset choff
+    int64_t ldo;
+    int32_t choff;
+};
+struct StreamEncArgs {
+    const float* prev_mic;      // [B][256] hop ring
+    const float* cur_mic;       // [B][ld_cur] this call's hop (caller's buffer)
+    const float* prev_far;
+    const float* cur_far;
+    int64_t ld_cur;
+    float* save_mic;            // [B][256]: the current hops for the next call and the back kernel
+    float* save_far;
+    const aec::DevTables* tab;
+    int32_t B;
+    float2* state;              // NLMS (taps > 0): [B][2 taps][256] (StreamNlmsArgs layout)
+    float2* espec;              //   E rows [B][256]
+    float mu, beta, delta;
+    int32_t nlev;               // 1..3
+    StreamEncLevel lev[3];
+};
+hipError_t launch_stream_enc(const StreamEncArgs& a, int taps, hipStream_t st);
+
 template <typename T>
 hipError_t launch_stream_front(const StreamFrontArgs& a, hipStream_t st);
 hipError_t launch_stream_back(const StreamBackArgs& a, int mode, hipStream_t st);

@@ -462,3 +462,42 @@ def test_fp8_stream_mx_scale_paths_bit_exact(monkeypatch):
         res[flag] = torch.cat(outs, dim=1).cpu().numpy()
     assert np.isfinite(res['1']).all()
     assert np.array_equal(res['1'], res['0'])
+
+
+@pytest.mark.parametrize('dtype', ['bf16', 'fp8'])
+@pytest.mark.parametrize('nlms', [False, True])
+def test_fused_stream_front_bit_exact(monkeypatch, dtype, nlms):
+    """The per-hop step's fused front (crn_stream.hip: frame -> rFFT -> FD-NLMS
+    step -> X0 -> encoder levels 0-2 in one launch per stream) against the
+    separate launches (AEC_CRN_STREAM_FUSE=0, read at stream_open: front
+    kernel, NLMS kernel, row GEMMs): the same transform code, NLMS arithmetic,
+    32-k MFMA chunks in the same order and epilogue, so 37 streams over 14
+    hops agree bit for bit."""
+    from aec_amd import synth
+    m = META['v2E_16000']
+    conf = copy.deepcopy(aec_amd.net_conf)
+    nl = dict(taps=4, mu=0.3, beta=0.5, delta=1e-4) if nlms else None
+    net = aec_amd.dccrn2.DCCRN(conf, dtype=dtype, nlms=nl).eval()
+    sd = net.state_dict()
+    for k, v in C.make_weights(conf, 2, m['weight_seed']).items():
+        sd[k] = torch.from_numpy(v)
+    net.load_state_dict(sd, strict=True)
+    net = net.to('cuda:0')
+    B, n = 37, 3328
+    sig = [synth.scene(n, 2900 + b) for b in range(B)]
+    nh = n // 256 + 1
+    M = torch.zeros(B, 256 * (nh + 1), device='cuda:0')
+    F = torch.zeros_like(M)
+    M[:, :n] = torch.from_numpy(np.stack([s[0] for s in sig])).cuda()
+    F[:, :n] = torch.from_numpy(np.stack([s[1] for s in sig])).cuda()
+    res = {}
+    for flag in ('0', '1'):
+        monkeypatch.setenv('AEC_CRN_STREAM_FUSE', flag)
+        net.stream_open(B)
+        with torch.no_grad():
+            outs = [net.stream_step(M[:, 256 * k:256 * (k + 1)], F[:, 256 * k:256 * (k + 1)]).clone()
+                    for k in range(nh)]
+        torch.cuda.synchronize()
+        res[flag] = torch.cat(outs, dim=1).cpu().numpy()
+    assert np.isfinite(res['1']).all()
+    assert np.array_equal(res['1'], res['0'])
