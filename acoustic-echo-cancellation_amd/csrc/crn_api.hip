@@ -852,12 +852,12 @@ static aec_status run_lstm_combine(aec_crn_handle* h, const Bufs& bf, int l, con
 }
 
 template <typename T>
-static aec_status run_decoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipStream_t st) {
+static aec_status run_decoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipStream_t st, int nd = -1) {
     using crn::RowEpi;
     using crn::RowSrc;
     const int* ch = h->cfg.conv_channels;
     const int L = h->L;
-    for (int d = 0; d < L; ++d) {
+    for (int d = 0; d < (nd < 0 ? L : nd); ++d) {
         const int cl = L - d;
         const int Fin = 256 >> cl, Fo = 2 * Fin;
         const int64_t ld_in = 2 * ch[cl];
@@ -1132,6 +1132,10 @@ struct StreamState {
     // launch (crn_stream_enc_kernel); its graph node is front_node (AEC_CRN_STREAM_FUSE=0: off)
     int enc_nlev = 0;
     crn::StreamEncArgs enc_args[2];
+    // bf16 / fp8: the last three decoder levels, the mask, irFFT and overlap-add as one launch
+    // (crn_stream_dec_kernel); its graph node is back_node (AEC_CRN_STREAM_FUSE=0: off)
+    bool dec_fused = false;
+    crn::StreamDecArgs dec_args[2];
     hipStream_t cap = nullptr;           // capture stream
 };
 
@@ -1283,12 +1287,59 @@ static crn::StreamEncArgs stream_enc_args(aec_crn_handle* h, int B) {
     return ea;
 }
 
+// the fused back's level table: decoder levels cl = 3, 2, 1 (decf[L - 3 .. L - 1])
+static crn::StreamDecArgs stream_dec_args(aec_crn_handle* h, int B) {
+    StreamState& ss = *h->ss;
+    const int* ch = h->cfg.conv_channels;
+    crn::StreamDecArgs da{};
+    for (int l = 0; l < 3; ++l) {
+        const int cl = 3 - l, d = h->L - cl;
+        const Packed& pk = h->decf[d];
+        crn::StreamDecLevel& L = da.lev[l];
+        L.w = reinterpret_cast<const bf16_t*>(pk.w);
+        L.bias = pk.bias;
+        L.alpha = pk.alpha;
+        L.act = pk.act;
+        L.kpad = pk.kpad;
+        L.N = pk.N;
+        L.nchunk = (pk.K + 31) / 32;
+        L.cin_shift = ilog2(2 * ch[cl]);
+        L.src = reinterpret_cast<const bf16_t*>(ss.cat[cl]);
+    }
+    da.tab = h->d_tab;
+    da.espec = h->cfg.nlms_taps > 0 ? ss.espec : nullptr;
+    da.tail = ss.tail;
+    da.B = B;
+    return da;
+}
+
+// the last three decoder levels crn_stream_dec_kernel can take (fused-parity bf16 GEMMs, the
+// map shapes of configs.net_conf's narrow levels)
+static bool stream_dec_ok(const aec_crn_handle* h) {
+    if (h->es != 2 || h->L < 3) return false;
+    const char* v = getenv("AEC_CRN_STREAM_FUSE");   // bit 0: fused front, bit 1: fused back (default 3)
+    if (v && !(atoi(v) & 2)) return false;
+    const int* ch = h->cfg.conv_channels;
+    const int caps[3] = {crn::kStreamDecChunks0, crn::kStreamDecChunks1, crn::kStreamDecChunks2};
+    for (int l = 0; l < 3; ++l) {
+        const int cl = 3 - l, d = h->L - cl, Fin = 256 >> cl;
+        const Packed& pk = h->decf[d];
+        const int NT = (pk.N + 15) / 16;
+        if (!pk.w || pk.wq || (pk.K + 31) / 32 > caps[l] || pk.kpad < 32 * ((pk.K + 31) / 32) || (Fin / 16) * NT != 8 ||
+            4 % NT || Fin * 2 * ch[cl] > 4096 || ilog2(2 * ch[cl]) < 4)
+            return false;
+        if (l < 2 && (pk.act != 1 || pk.N != 2 * ch[cl - 1] || pk.N % 32)) return false;
+        if (l == 2 && (pk.N != 4 || pk.act == 1)) return false;
+    }
+    return true;
+}
+
 // leading encoder levels crn_stream_enc_kernel can take: bf16 GEMM (not MX), PReLU, 8 output tiles
 // of 16 bins x 16 channels, K <= 160, no MX shadow on the output
 static int stream_enc_levels(const aec_crn_handle* h) {
     if (h->es != 2) return 0;
     const char* v = getenv("AEC_CRN_STREAM_FUSE");
-    if (v && atoi(v) == 0) return 0;
+    if (v && !(atoi(v) & 1)) return 0;
     const int* ch = h->cfg.conv_channels;
     int n = 0;
     for (int i = 0; i < std::min(3, h->L); ++i) {
@@ -1361,6 +1412,19 @@ static aec_status stream_launches(aec_crn_handle* h, int par, const StreamIo& io
         s = run_lstm_combine<T>(h, bf, l, ss.ring_y[l][par], B, st);
         if (s != AEC_OK) return s;
     }
+    if (ss.dec_fused) {
+        s = run_decoder<T>(h, bf, B, st, h->L - 3);
+        if (s != AEC_OK) return s;
+        crn::StreamDecArgs da = stream_dec_args(h, B);
+        da.prev_mic = prev_mic;
+        da.cur_mic = cur_mic;
+        da.out = io.out;
+        da.ld_out = io.ld_out;
+        CRN_TRY(h, crn::launch_stream_dec(da, mask_mode(h), st));
+        ss.back_node[par] = last_node(st);
+        ss.dec_args[par] = da;
+        return AEC_OK;
+    }
     s = run_decoder<T>(h, bf, B, st);
     if (s != AEC_OK) return s;
     crn::StreamBackArgs ba{prev_mic, cur_mic, h->d_tab, reinterpret_cast<const float2*>(ss.mask), ss.tail, io.out, B};
@@ -1378,16 +1442,19 @@ static aec_status stream_set_io(aec_crn_handle* h, int par, const StreamIo& io) 
     crn::StreamFrontArgs& fa = ss.front_args[par];
     crn::StreamEncArgs& ea = ss.enc_args[par];
     crn::StreamBackArgs& ba = ss.back_args[par];
+    crn::StreamDecArgs& da = ss.dec_args[par];
     const bool fused = ss.enc_nlev > 0;
     const float* cm = fused ? ea.cur_mic : fa.cur_mic;
     const float* cf = fused ? ea.cur_far : fa.cur_far;
     const int64_t cl = fused ? ea.ld_cur : fa.ld_cur;
-    if (cm == io.mic && cf == io.far && cl == io.ld_in && ba.out == io.out && ba.ld_out == io.ld_out) return AEC_OK;
+    const float* co = ss.dec_fused ? da.out : ba.out;
+    const int64_t clo = ss.dec_fused ? da.ld_out : ba.ld_out;
+    if (cm == io.mic && cf == io.far && cl == io.ld_in && co == io.out && clo == io.ld_out) return AEC_OK;
     fa.cur_mic = ea.cur_mic = io.mic;
     fa.cur_far = ea.cur_far = io.far;
     fa.ld_cur = ea.ld_cur = io.ld_in;
-    ba.out = io.out;
-    ba.ld_out = io.ld_out;
+    ba.out = da.out = io.out;
+    ba.ld_out = da.ld_out = io.ld_out;
     hipKernelNodeParams kp{};
     CRN_TRY(h, hipGraphKernelNodeGetParams(ss.front_node[par], &kp));
     void* fargs[] = {fused ? static_cast<void*>(&ea) : static_cast<void*>(&fa)};
@@ -1395,7 +1462,7 @@ static aec_status stream_set_io(aec_crn_handle* h, int par, const StreamIo& io) 
     kp.extra = nullptr;
     CRN_TRY(h, hipGraphExecKernelNodeSetParams(ss.graph[par], ss.front_node[par], &kp));
     CRN_TRY(h, hipGraphKernelNodeGetParams(ss.back_node[par], &kp));
-    void* bargs[] = {&ba};
+    void* bargs[] = {ss.dec_fused ? static_cast<void*>(&da) : static_cast<void*>(&ba)};
     kp.kernelParams = bargs;
     kp.extra = nullptr;
     CRN_TRY(h, hipGraphExecKernelNodeSetParams(ss.graph[par], ss.back_node[par], &kp));
@@ -1676,6 +1743,7 @@ aec_status aec_crn_stream_open(aec_crn_handle* h, int32_t B) {
         CRN_TRY(h, alloc(reinterpret_cast<void**>(&ss.espec), (size_t)B * 256 * sizeof(float2)));
     }
     ss.enc_nlev = stream_enc_levels(h);
+    ss.dec_fused = stream_dec_ok(h);
     CRN_TRY(h, hipStreamCreateWithFlags(&ss.cap, hipStreamNonBlocking));
     CRN_TRY(h, hipDeviceSynchronize());
     ss.k = 0;

@@ -60,6 +60,26 @@ __device__ __forceinline__ float tanhf_(float x) {
     return 1.f - 2.f / (__expf(2.f * x) + 1.f);
 }
 
+// the decoder's mask on one bin of the (mic or NLMS error) spectrum (dccrn2.py:189-210):
+// shared by the batch and per-hop back kernels (crn_kernels.hip, crn_stream.hip)
+template <int MODE>
+__device__ __forceinline__ float2 apply_mask(float2 x, float2 mk) {
+    if (MODE == 0) {   // 'E' (dccrn2.py:194-208): tanh(|M|) |X|_1e-8 * exp(i (arg X + arg M))
+        const float mags = sqrtf(x.x * x.x + x.y * x.y + 1e-8f);
+        const float ax = sqrtf(x.x * x.x + x.y * x.y);
+        const float am = sqrtf(mk.x * mk.x + mk.y * mk.y);
+        // atan2(0, 0) = 0 -> unit vector (1, 0)
+        const float cx = ax > 0.f ? x.x / ax : 1.f, sx = ax > 0.f ? x.y / ax : 0.f;
+        const float cm = am > 0.f ? mk.x / am : 1.f, sm = am > 0.f ? mk.y / am : 0.f;
+        const float e = tanhf(am) * mags;
+        return make_float2(e * (cx * cm - sx * sm), e * (sx * cm + cx * sm));
+    } else if (MODE == 1) {   // 'C' (dccrn.py:575, dccrn2.py:209)
+        return make_float2(x.x * mk.x - x.y * mk.y, x.x * mk.y + x.y * mk.x);
+    } else {                  // 'R' (dccrn2.py:210-211)
+        return make_float2(x.x * mk.x, x.y * mk.y);
+    }
+}
+
 constexpr int kStageBytes = 128;   // K bytes staged per main-loop step (two 64-B k-chunks)
 constexpr int kRowStride = 144;    // LDS bytes per staged row: 16 rows at one column hit 16 distinct 16-B bank slots
 

@@ -161,24 +161,6 @@ __global__ __launch_bounds__(256) void crn_front_kernel(FrontArgs p) {
 // overlap-adds (structure of the Little_net synthesis kernel, aec_kernels.hip)
 // --------------------------------------------------------------------------
 template <int MODE>
-__device__ __forceinline__ float2 apply_mask(float2 x, float2 mk) {
-    if (MODE == 0) {   // 'E' (dccrn2.py:194-208): tanh(|M|) |X|_1e-8 * exp(i (arg X + arg M))
-        const float mags = sqrtf(x.x * x.x + x.y * x.y + 1e-8f);
-        const float ax = sqrtf(x.x * x.x + x.y * x.y);
-        const float am = sqrtf(mk.x * mk.x + mk.y * mk.y);
-        // atan2(0, 0) = 0 -> unit vector (1, 0)
-        const float cx = ax > 0.f ? x.x / ax : 1.f, sx = ax > 0.f ? x.y / ax : 0.f;
-        const float cm = am > 0.f ? mk.x / am : 1.f, sm = am > 0.f ? mk.y / am : 0.f;
-        const float e = tanhf(am) * mags;
-        return make_float2(e * (cx * cm - sx * sm), e * (sx * cm + cx * sm));
-    } else if (MODE == 1) {   // 'C' (dccrn.py:575, dccrn2.py:209)
-        return make_float2(x.x * mk.x - x.y * mk.y, x.x * mk.y + x.y * mk.x);
-    } else {                  // 'R' (dccrn2.py:210-211)
-        return make_float2(x.x * mk.x, x.y * mk.y);
-    }
-}
-
-template <int MODE>
 __global__ __launch_bounds__(256) void crn_back_kernel(BackArgs p) {
     __shared__ __attribute__((aligned(16))) float smem[258 * 2 + 256 * 2 + 512 + 256 + 4 * kWaveFloats];
     float2* sTw512 = reinterpret_cast<float2*>(smem);

@@ -202,6 +202,35 @@ struct StreamEncArgs {
 };
 hipError_t launch_stream_enc(const StreamEncArgs& a, int taps, hipStream_t st);
 
+// Fused per-hop back (crn_stream.hip): the last three decoder levels (ComplexConvTranspose2d +
+// skip, both parities per GEMM: pack_decoder_fused) with the maps in LDS, the mask, the masked
+// spectrum's irFFT and the overlap-add, one block per stream; replaces those levels' row GEMMs
+// + launch_stream_back.  Level i's input map = [decoder half | encoder half] of cat[cl]; the
+// first map comes whole from HBM, the later ones take the previous level's output as decoder
+// half and the encoder half from HBM.
+constexpr int kStreamDecChunks0 = 12, kStreamDecChunks1 = 6, kStreamDecChunks2 = 3;   // K <= 384 / 192 / 96
+struct StreamDecLevel {
+    const bf16_t* w;            // packed [npad][kpad] (pack_decoder_fused: columns [0, Co) parity 0, [Co, 2 Co) parity 1)
+    const float* bias;
+    float alpha;
+    int32_t act;                // 1 PReLU (levels), 0 none / 2 tanh (the mask level)
+    int32_t kpad, N, nchunk;    // N = 2 Co (4 at the mask level)
+    int32_t cin_shift;          // log2 of the input map's channels per bin (2 ch[cl])
+    const bf16_t* src;          // cat[cl] [B][Fin][2 ch[cl]]: the whole map (level 0) or its encoder half (later levels)
+};
+struct StreamDecArgs {
+    StreamDecLevel lev[3];      // cl = 3, 2, 1 (the last is the mask level)
+    const aec::DevTables* tab;
+    const float2* espec;        // NLMS: E rows [B][256] (the masked spectrum), else the mic frame:
+    const float* prev_mic;      //   [prev hop | cur hop] from the ring
+    const float* cur_mic;
+    float* tail;                // [B][256] overlap-add state
+    float* out;                 // [B][ld_out]
+    int64_t ld_out;
+    int32_t B;
+};
+hipError_t launch_stream_dec(const StreamDecArgs& a, int mode, hipStream_t st);
+
 template <typename T>
 hipError_t launch_stream_front(const StreamFrontArgs& a, hipStream_t st);
 hipError_t launch_stream_back(const StreamBackArgs& a, int mode, hipStream_t st);

@@ -12,10 +12,19 @@
 //                     s=(2,1) p=(2,0) + folded (Complex)BatchNorm + PReLU, as
 //                     implicit GEMMs on v_mfma_f32_16x16x32_bf16
 //
+// The back of the hop (the last three decoder levels with their skips, the
+// mask, the masked spectrum's irFFT-512 and the overlap-add) is a second
+// launch of the same form (crn_stream_dec_kernel):
+//
+//   decoder cl = 3..1 dccrn2.py:83-111 / dccrn.py:480-509: ComplexConvTranspose2d
+//                     on complex_cat(dec, enc skip) (both output parities per GEMM)
+//   mask + ConviSTFT  dccrn2.py:185-215, dccrn.py:80-100
+//
 // Each level is the batch path's GEMM restated: the same packed weights, the
 // same 32-k chunks accumulated in the same order from zero, the same epilogue
 // (v >= 0 ? v : alpha v, then bf16), so its outputs equal the row-GEMM
-// kernel's (tests/test_gpu_crn.py::test_fused_stream_front_bit_exact).
+// kernel's, and the transforms are the batch kernels' code
+// (tests/test_gpu_crn.py::test_fused_stream_bit_exact).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -27,6 +36,7 @@
 #include "crn_launch.h"
 
 namespace crn {
+
 
 namespace {
 
@@ -240,6 +250,253 @@ hipError_t launch_stream_enc(const StreamEncArgs& a, int taps, hipStream_t st) {
         CRN_ENC_CASE(0) CRN_ENC_CASE(1) CRN_ENC_CASE(2) CRN_ENC_CASE(3) CRN_ENC_CASE(4)
         CRN_ENC_CASE(5) CRN_ENC_CASE(6) CRN_ENC_CASE(7) CRN_ENC_CASE(8)
 #undef CRN_ENC_CASE
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// --------------------------------------------------------------------------
+// Fused back: decoder levels cl = 3, 2, 1 + mask + irFFT + overlap-add, one block per stream
+// --------------------------------------------------------------------------
+namespace {
+
+// one decoder level: 8 output tiles of 16 input bins x 16 columns, two per wave (N tile nt =
+// wave % NT, M tiles m0 = wave / NT, m0 + 4 / NT); A rows: input bins i - 1 + j (j = k / Cin),
+// zero outside [0, Fin); the 32-k chunks accumulated in order from zero
+template <int NC>
+__device__ __forceinline__ void dec_tiles(f32x4 (&acc)[2], const bf16_t* in, int Fin, int cs, int nchunk,
+                                          const u32x4 (&bw)[NC], int m0, int m1, int lane) {
+    acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        if (c >= nchunk) break;
+        const int k0 = 32 * c + 8 * (lane >> 4);
+        const int j = k0 >> cs, q0 = k0 & ((1 << cs) - 1);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int i = (t ? m1 : m0) * 16 + (lane & 15);
+            const int ib = i - 1 + j;
+            u32x4 a = {0u, 0u, 0u, 0u};
+            if (j < 3 && ib >= 0 && ib < Fin) a = *reinterpret_cast<const u32x4*>(in + (ib << cs) + q0);
+            mma_chunk(acc[t], a, bw[c], bf16_t{});
+        }
+    }
+}
+
+template <int NC>
+__device__ __forceinline__ void load_bw(u32x4 (&bw)[NC], const StreamDecLevel& L, int n) {
+    const bf16_t* wr = L.w + (int64_t)n * L.kpad + 8 * ((threadIdx.x & 63) >> 4);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) bw[c] = c < L.nchunk ? *reinterpret_cast<const u32x4*>(wr + 32 * c) : u32x4{0u, 0u, 0u, 0u};
+}
+
+}  // namespace
+
+template <int MODE>
+__global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
+    constexpr int kMap = 4096;                    // bf16 elements of a level's input map (Fin x Cin)
+    __shared__ __attribute__((aligned(16))) bf16_t sIn[3][kMap];
+    __shared__ __attribute__((aligned(16))) float2 sMask[256];
+    __shared__ __attribute__((aligned(16))) float2 sRow[256];
+    __shared__ __attribute__((aligned(16))) float2 sS[260];
+    __shared__ __attribute__((aligned(16))) float sTab[258 * 2 + 256 * 2 + 512 + 256];
+    __shared__ __attribute__((aligned(16))) float sGrp[aec::kGroupFloats];
+    float2* sTw512 = reinterpret_cast<float2*>(sTab);
+    float2* sTwT = sTw512 + 258;
+    float* sHann = reinterpret_cast<float*>(sTwT + 256);
+    float* sCoff = sHann + 512;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int b = blockIdx.x;
+
+    // 1. independent loads: level 0's whole input map, the encoder halves of the later maps, the
+    //    spectrum source (E row or the mic frame), the OLA tail, tables, weight fragments, biases
+    {
+        const StreamDecLevel& L0 = p.lev[0];
+        const int n16 = 32 * (1 << L0.cin_shift) / 8;                 // 16-B pieces of the map (Fin0 = 32 rows)
+        const u32x4* src = reinterpret_cast<const u32x4*>(L0.src + (int64_t)b * (32 << L0.cin_shift));
+        for (int i = tid; i < n16; i += 256) reinterpret_cast<u32x4*>(sIn[0])[i] = src[i];
+#pragma unroll
+        for (int l = 1; l < 3; ++l) {            // encoder half: channels [C/2, C) of Fin rows
+            const StreamDecLevel& L = p.lev[l];
+            const int Fin = 32 << l, C = 1 << L.cin_shift, half = C / 2;
+            const int per = half / 8;             // 16-B pieces per row
+            const bf16_t* sb = L.src + (int64_t)b * Fin * C + half;
+            for (int i = tid; i < Fin * per; i += 256) {
+                const int r = i / per, q = i % per;
+                *reinterpret_cast<u32x4*>(sIn[l] + r * C + half + 8 * q) = *reinterpret_cast<const u32x4*>(sb + (int64_t)r * C + 8 * q);
+            }
+        }
+    }
+    if (p.espec) {
+        sRow[tid] = p.espec[(int64_t)b * 256 + tid];
+    } else {
+        const int h = tid >> 6, i = tid & 63;
+        if (h < 2)
+            reinterpret_cast<float4*>(sGrp + h * aec::kHopStride)[i] =
+                reinterpret_cast<const float4*>((h ? p.cur_mic : p.prev_mic) + (int64_t)b * 256)[i];
+    }
+    const float tl = p.tail[(int64_t)b * 256 + tid];
+    sTw512[tid] = p.tab->tw512[tid];
+    if (tid < 2) sTw512[256 + tid] = p.tab->tw512[256 + tid];
+    sTwT[tid] = p.tab->twT[tid];
+    sHann[tid] = p.tab->hann[tid];
+    sHann[tid + 256] = p.tab->hann[tid + 256];
+    sCoff[tid] = p.tab->inv_coff[tid];
+    u32x4 bw0[kStreamDecChunks0], bw1[kStreamDecChunks1], bw2[kStreamDecChunks2];
+    int nt[3], m0[3], m1[3];
+    float bias[3];
+#pragma unroll
+    for (int l = 0; l < 3; ++l) {
+        const int NT = (p.lev[l].N + 15) >> 4;
+        nt[l] = wave % NT;
+        m0[l] = wave / NT;
+        m1[l] = m0[l] + 4 / NT;
+        const int n = nt[l] * 16 + (lane & 15);
+        bias[l] = n < p.lev[l].N ? p.lev[l].bias[n] : 0.f;
+    }
+    load_bw(bw0, p.lev[0], nt[0] * 16 + (lane & 15));
+    load_bw(bw1, p.lev[1], nt[1] * 16 + (lane & 15));
+    load_bw(bw2, p.lev[2], nt[2] * 16 + (lane & 15));
+    __syncthreads();
+
+    // 2. decoder levels cl = 3, 2: output bins 2 i + parity, channel n -> the next map's decoder half
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+        const StreamDecLevel& L = p.lev[l];
+        const int Fin = 32 << l, Co = L.N >> 1, Cn = 1 << p.lev[l + 1].cin_shift;
+        f32x4 acc[2];
+        if (l == 0) dec_tiles(acc, sIn[0], Fin, L.cin_shift, L.nchunk, bw0, m0[0], m1[0], lane);
+        else dec_tiles(acc, sIn[1], Fin, L.cin_shift, L.nchunk, bw1, m0[1], m1[1], lane);
+        const int n = nt[l] * 16 + (lane & 15), par = n >= Co, ch = n - par * Co;
+        bf16_t* next = sIn[l + 1];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = (t ? m1[l] : m0[l]) * 16 + 4 * (lane >> 4) + r;
+                float v = acc[t][r] + bias[l];
+                v = v >= 0.f ? v : L.alpha * v;
+                next[(2 * i + par) * Cn + ch] = f2bf(v);
+            }
+        __syncthreads();
+    }
+    // 3. the mask level (cl = 1): columns (parity, re / im), f32, act none (v2) / tanh (v1)
+    {
+        const StreamDecLevel& L = p.lev[2];
+        f32x4 acc[2];
+        dec_tiles(acc, sIn[2], 128, L.cin_shift, L.nchunk, bw2, m0[2], m1[2], lane);
+        const int n = lane & 15;
+        if (n < 4) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = (t ? m1[2] : m0[2]) * 16 + 4 * (lane >> 4) + r;
+                    float v = acc[t][r] + bias[2];
+                    if (L.act == 2) v = tanhf(v);              // the batch epilogue's apply_act<2>
+                    reinterpret_cast<float*>(sMask)[(2 * i + (n >> 1)) * 2 + (n & 1)] = v;
+                }
+        }
+    }
+    // the mic spectrum (no NLMS): the batch front's transform of [prev | cur]
+    if (!p.espec && wave == 0 && lane < 16) {
+        float2 v[16];
+        float2 xa[8], xb[8], x128;
+        aec::load_frame(v, sGrp, sHann, 0, lane);
+        aec::wave_fence();
+        aec::fft256<false>(v, lane, sGrp, sTwT);
+        aec::rfft_unpack(v, lane, sTw512, xa, xb, x128);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const int kk = lane + 16 * m;
+            if (kk == 0) {
+                sRow[0] = make_float2(xa[0].x, xb[0].x);
+            } else {
+                sRow[kk] = xa[m];
+                sRow[256 - kk] = xb[m];
+            }
+        }
+        if (lane == 0) sRow[128] = x128;
+    }
+    __syncthreads();
+    // 4. the mask on every bin (thread k: bin k; thread 0 also the Nyquist bin; DC's mask is 0)
+    {
+        const int k = tid;
+        const float2 x = sRow[k];
+        if (k == 0) {
+            sS[0] = apply_mask<MODE>(make_float2(x.x, 0.f), make_float2(0.f, 0.f));
+            sS[256] = apply_mask<MODE>(make_float2(x.y, 0.f), sMask[255]);
+        } else {
+            sS[k] = apply_mask<MODE>(x, sMask[k - 1]);
+        }
+    }
+    __syncthreads();
+    // 5. inverse pack, irFFT-256, window, overlap-add (crn_stream_back_kernel's code), wave 0 lanes 0-15
+    if (wave == 0 && lane < 16) {
+        const int lb = lane;
+        float2 xa[8], xb[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const int kk = lb + 16 * m;
+            xa[m] = sS[kk];
+            xb[m] = sS[256 - kk];
+        }
+        const float2 x128 = sS[128];
+        float2 Zk[8], Zmk[8], v[16];
+        aec::static_for<0, 8>([&](auto mi) {
+            constexpr int m = decltype(mi)::value;
+            const int kk = lb + 16 * m;
+            float2 zk, zmk;
+            aec::irfft_pair(xa[m], xb[m], sTw512[kk], zk, zmk);
+            const float s0 = xa[m].x, s256 = xb[m].x;
+            Zk[m] = aec::csel(kk == 0, make_float2(s0 + s256, s0 - s256), zk);
+            Zmk[m] = aec::csel(kk == 0, Zk[m], zmk);
+        });
+        float2 z128 = make_float2(0.f, 0.f);
+        if (lb == 0) z128 = make_float2(2.f * x128.x, -2.f * x128.y);
+#pragma unroll
+        for (int a = 0; a < 8; ++a) v[a] = Zk[a];
+        aec::static_for<8, 16>([&](auto ai) {
+            constexpr int a = decltype(ai)::value;
+            const float2 mir = aec::mirror16(Zmk[15 - a]);
+            v[a] = aec::csel(lb != 0, mir, a == 8 ? z128 : Zmk[(16 - a) & 7]);
+        });
+        aec::wave_fence();
+        aec::fft256<true>(v, lb, sGrp, sTwT);
+        float2* s2 = reinterpret_cast<float2*>(sGrp);
+        const float2* h2 = reinterpret_cast<const float2*>(sHann);
+#pragma unroll
+        for (int m2 = 0; m2 < 16; ++m2) {
+            const float2 zz = v[aec::kP(m2)];
+            const float2 w = h2[lb + 16 * m2];
+            s2[lb + 16 * m2] = make_float2(zz.x * (w.x * (1.f / 512.f)), zz.y * (w.y * (1.f / 512.f)));
+        }
+    }
+    __syncthreads();
+    {
+        const int r = tid;
+        p.out[(int64_t)b * p.ld_out + r] = (tl + sGrp[r]) * sCoff[r];
+        p.tail[(int64_t)b * 256 + r] = sGrp[256 + r];
+    }
+}
+
+hipError_t launch_stream_dec(const StreamDecArgs& a, int mode, hipStream_t st) {
+    if (a.B <= 0) return hipSuccess;
+    const int caps[3] = {kStreamDecChunks0, kStreamDecChunks1, kStreamDecChunks2};
+    for (int l = 0; l < 3; ++l) {
+        const StreamDecLevel& L = a.lev[l];
+        const int Fin = 32 << l, NT = (L.N + 15) / 16;
+        if (!L.w || !L.bias || !L.src || L.nchunk < 1 || L.nchunk > caps[l] || L.kpad < 32 * L.nchunk ||
+            (Fin / 16) * NT != 8 || 4 % NT || (Fin << L.cin_shift) > 4096 || L.cin_shift < 4 ||
+            (l < 2 && (L.N % 32 || L.act != 1 || L.N != (1 << a.lev[l + 1].cin_shift))) ||   // Co = next map's half
+            (l == 2 && (L.N != 4 || L.act == 1)))
+            return hipErrorInvalidValue;
+    }
+    switch (mode) {
+        case 0: hipLaunchKernelGGL(crn_stream_dec_kernel<0>, dim3((unsigned)a.B), dim3(256), 0, st, a); break;
+        case 1: hipLaunchKernelGGL(crn_stream_dec_kernel<1>, dim3((unsigned)a.B), dim3(256), 0, st, a); break;
+        case 2: hipLaunchKernelGGL(crn_stream_dec_kernel<2>, dim3((unsigned)a.B), dim3(256), 0, st, a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
