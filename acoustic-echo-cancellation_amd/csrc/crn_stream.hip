@@ -37,10 +37,28 @@
 
 namespace crn {
 
+#ifdef AEC_STREAM_PROF
+// timing experiments only (tools/stream_prof.py): s_memtime at the phase boundaries of block 0 of
+// the fused kernels (wave 0, lane 0): [kernel 0 = enc, 1 = dec][phase]
+__device__ unsigned long long g_sprof[2][16];
+#define SPROF(kern, ph)                                                                               \
+    do {                                                                                              \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_sprof[kern][ph] = __builtin_amdgcn_s_memtime();   \
+    } while (0)
+#else
+#define SPROF(kern, ph) do {} while (0)
+#endif
+
 
 namespace {
 
-constexpr int kMapElems = 2048;    // bf16 elements of one level's output map (Fo x N = 8 tiles of 16 x 16)
+constexpr int kMapElems = 2048;
+
+// block barrier that drains LDS only: the global stores of the level outputs (read by a later
+// launch) and the register loads of weight fragments stay in flight across it
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}    // bf16 elements of one level's output map (Fo x N = 8 tiles of 16 x 16)
 
 // X0 bin k (1..256) as 8 bf16: (mic.re, far.re, mic.im, far.im, 0, 0, 0, 0) (dccrn.py:559-561)
 __device__ __forceinline__ void x0_put(bf16_t* x0, int k, float2 m, float2 f) {
@@ -66,6 +84,7 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
     float* sHann = reinterpret_cast<float*>(sTw512 + 258);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int b = blockIdx.x;
+    SPROF(0, 0);
 
     // 1. every independent load first: the two hops of both signals (one float4 per thread;
     //    the current hop also saved to the ring), the tables, the NLMS state and the weight
@@ -127,7 +146,8 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
     if (tid < 2) sTw512[256 + tid] = t2;
     sHann[tid] = h0;
     sHann[tid + 256] = h1;
-    __syncthreads();
+    lds_barrier();
+    SPROF(0, 1);
 
     // 2. the two transforms on waves 0 (mic) and 1 (far), lanes 0-15: the batch front's
     //    transform code (bit-identical frames) -> packed spectrum rows (slot 0 = (X[0], X[256]))
@@ -153,7 +173,8 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
         }
         if (lb == 0) row[128] = x128;
     }
-    __syncthreads();
+    lds_barrier();
+    SPROF(0, 2);
 
     // 3. bin slot k = tid: the NLMS step (crn_stream_nlms_kernel's arithmetic) and X0
     {
@@ -184,7 +205,8 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
         else   // slot 0 holds (X[0], X[256]): the Nyquist bin 256; DC is not an encoder input
             x0_put(sX0, 256, make_float2(e.y, 0.f), make_float2(rf.y, 0.f));
     }
-    __syncthreads();
+    lds_barrier();
+    SPROF(0, 3);
 
     // 4. encoder levels: 8 output tiles of 16 bins x 16 channels per level, two per wave (N tile
     //    nt = wave % NT, M tiles m0 = wave / NT and m0 + 4 / NT); the implicit A rows read the
@@ -201,7 +223,7 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
         f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
         for (int c = 0; c < kStreamEncChunks; ++c) {
-            if (c >= L.nchunk) break;
+            if (c >= L.nchunk) continue;
             const int k0 = 32 * c + 8 * (lane >> 4);
             const int tap = k0 >> cs, q0 = k0 & ((1 << cs) - 1);
 #pragma unroll
@@ -228,7 +250,8 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
                 if (keep) map[row * L.N + n] = o;
                 out[(int64_t)row * L.ldo + n] = o;
             }
-        __syncthreads();
+        lds_barrier();
+        SPROF(0, 4 + i);
         in = map;
     }
 }
@@ -268,27 +291,31 @@ __device__ __forceinline__ void dec_tiles(f32x4 (&acc)[2], const bf16_t* in, int
                                           const u32x4 (&bw)[NC], int m0, int m1, int lane) {
     acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
     acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // compile-time chunk indices (a runtime-bounded loop would leave bw[] in scratch)
+    aec::static_for<0, NC>([&](auto ci) {
+        constexpr int c = decltype(ci)::value;
+        if (c < nchunk) {
+            const int k0 = 32 * c + 8 * (lane >> 4);
+            const int j = k0 >> cs, q0 = k0 & ((1 << cs) - 1);
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-        if (c >= nchunk) break;
-        const int k0 = 32 * c + 8 * (lane >> 4);
-        const int j = k0 >> cs, q0 = k0 & ((1 << cs) - 1);
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int i = (t ? m1 : m0) * 16 + (lane & 15);
-            const int ib = i - 1 + j;
-            u32x4 a = {0u, 0u, 0u, 0u};
-            if (j < 3 && ib >= 0 && ib < Fin) a = *reinterpret_cast<const u32x4*>(in + (ib << cs) + q0);
-            mma_chunk(acc[t], a, bw[c], bf16_t{});
+            for (int t = 0; t < 2; ++t) {
+                const int i = (t ? m1 : m0) * 16 + (lane & 15);
+                const int ib = i - 1 + j;
+                u32x4 a = {0u, 0u, 0u, 0u};
+                if (j < 3 && ib >= 0 && ib < Fin) a = *reinterpret_cast<const u32x4*>(in + (ib << cs) + q0);
+                mma_chunk(acc[t], a, bw[c], bf16_t{});
+            }
         }
-    }
+    });
 }
 
 template <int NC>
 __device__ __forceinline__ void load_bw(u32x4 (&bw)[NC], const StreamDecLevel& L, int n) {
     const bf16_t* wr = L.w + (int64_t)n * L.kpad + 8 * ((threadIdx.x & 63) >> 4);
-#pragma unroll
-    for (int c = 0; c < NC; ++c) bw[c] = c < L.nchunk ? *reinterpret_cast<const u32x4*>(wr + 32 * c) : u32x4{0u, 0u, 0u, 0u};
+    aec::static_for<0, NC>([&](auto ci) {
+        constexpr int c = decltype(ci)::value;
+        bw[c] = c < L.nchunk ? *reinterpret_cast<const u32x4*>(wr + 32 * c) : u32x4{0u, 0u, 0u, 0u};
+    });
 }
 
 }  // namespace
@@ -308,25 +335,25 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
     float* sCoff = sHann + 512;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int b = blockIdx.x;
+    SPROF(1, 0);
 
     // 1. independent loads: level 0's whole input map, the encoder halves of the later maps, the
     //    spectrum source (E row or the mic frame), the OLA tail, tables, weight fragments, biases
-    {
-        const StreamDecLevel& L0 = p.lev[0];
-        const int n16 = 32 * (1 << L0.cin_shift) / 8;                 // 16-B pieces of the map (Fin0 = 32 rows)
-        const u32x4* src = reinterpret_cast<const u32x4*>(L0.src + (int64_t)b * (32 << L0.cin_shift));
-        for (int i = tid; i < n16; i += 256) reinterpret_cast<u32x4*>(sIn[0])[i] = src[i];
+    // (the map pieces are loaded into registers first, all in flight together, then stored:
+    //  kDecPieces 16-B pieces per thread for level 0 (32 x 128 bf16) and one each for the two
+    //  encoder halves (launch_stream_dec checks the shapes))
+    constexpr int kDecPieces = 2;
+    u32x4 mp[kDecPieces + 2];
+    const StreamDecLevel& L0 = p.lev[0];
+    const u32x4* src0 = reinterpret_cast<const u32x4*>(L0.src + (int64_t)b * (32 << L0.cin_shift));
 #pragma unroll
-        for (int l = 1; l < 3; ++l) {            // encoder half: channels [C/2, C) of Fin rows
-            const StreamDecLevel& L = p.lev[l];
-            const int Fin = 32 << l, C = 1 << L.cin_shift, half = C / 2;
-            const int per = half / 8;             // 16-B pieces per row
-            const bf16_t* sb = L.src + (int64_t)b * Fin * C + half;
-            for (int i = tid; i < Fin * per; i += 256) {
-                const int r = i / per, q = i % per;
-                *reinterpret_cast<u32x4*>(sIn[l] + r * C + half + 8 * q) = *reinterpret_cast<const u32x4*>(sb + (int64_t)r * C + 8 * q);
-            }
-        }
+    for (int i = 0; i < kDecPieces; ++i) mp[i] = src0[tid + 256 * i];
+#pragma unroll
+    for (int l = 1; l < 3; ++l) {                // encoder half: channels [C/2, C) of Fin rows, one piece per thread
+        const StreamDecLevel& L = p.lev[l];
+        const int Fin = 32 << l, C = 1 << L.cin_shift, half = C / 2, per = half / 8;
+        const int r = tid / per, q = tid % per;
+        mp[kDecPieces + l - 1] = *reinterpret_cast<const u32x4*>(L.src + ((int64_t)b * Fin + r) * C + half + 8 * q);
     }
     if (p.espec) {
         sRow[tid] = p.espec[(int64_t)b * 256 + tid];
@@ -358,7 +385,16 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
     load_bw(bw0, p.lev[0], nt[0] * 16 + (lane & 15));
     load_bw(bw1, p.lev[1], nt[1] * 16 + (lane & 15));
     load_bw(bw2, p.lev[2], nt[2] * 16 + (lane & 15));
-    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kDecPieces; ++i) reinterpret_cast<u32x4*>(sIn[0])[tid + 256 * i] = mp[i];
+#pragma unroll
+    for (int l = 1; l < 3; ++l) {
+        const int C = 1 << p.lev[l].cin_shift, half = C / 2, per = half / 8;
+        const int r = tid / per, q = tid % per;
+        *reinterpret_cast<u32x4*>(sIn[l] + r * C + half + 8 * q) = mp[kDecPieces + l - 1];
+    }
+    lds_barrier();
+    SPROF(1, 1);
 
     // 2. decoder levels cl = 3, 2: output bins 2 i + parity, channel n -> the next map's decoder half
 #pragma unroll
@@ -379,7 +415,8 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
                 v = v >= 0.f ? v : L.alpha * v;
                 next[(2 * i + par) * Cn + ch] = f2bf(v);
             }
-        __syncthreads();
+        lds_barrier();
+        SPROF(1, 2 + l);
     }
     // 3. the mask level (cl = 1): columns (parity, re / im), f32, act none (v2) / tanh (v1)
     {
@@ -419,7 +456,8 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
         }
         if (lane == 0) sRow[128] = x128;
     }
-    __syncthreads();
+    lds_barrier();
+    SPROF(1, 4);
     // 4. the mask on every bin (thread k: bin k; thread 0 also the Nyquist bin; DC's mask is 0)
     {
         const int k = tid;
@@ -431,7 +469,8 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
             sS[k] = apply_mask<MODE>(x, sMask[k - 1]);
         }
     }
-    __syncthreads();
+    lds_barrier();
+    SPROF(1, 5);
     // 5. inverse pack, irFFT-256, window, overlap-add (crn_stream_back_kernel's code), wave 0 lanes 0-15
     if (wave == 0 && lane < 16) {
         const int lb = lane;
@@ -473,12 +512,14 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
             s2[lb + 16 * m2] = make_float2(zz.x * (w.x * (1.f / 512.f)), zz.y * (w.y * (1.f / 512.f)));
         }
     }
-    __syncthreads();
+    lds_barrier();
+    SPROF(1, 6);
     {
         const int r = tid;
         p.out[(int64_t)b * p.ld_out + r] = (tl + sGrp[r]) * sCoff[r];
         p.tail[(int64_t)b * 256 + r] = sGrp[256 + r];
     }
+    SPROF(1, 7);
 }
 
 hipError_t launch_stream_dec(const StreamDecArgs& a, int mode, hipStream_t st) {
@@ -492,6 +533,8 @@ hipError_t launch_stream_dec(const StreamDecArgs& a, int mode, hipStream_t st) {
             (l < 2 && (L.N % 32 || L.act != 1 || L.N != (1 << a.lev[l + 1].cin_shift))) ||   // Co = next map's half
             (l == 2 && (L.N != 4 || L.act == 1)))
             return hipErrorInvalidValue;
+        const int C = 1 << L.cin_shift;
+        if (l == 0 ? Fin * C != 2 * 256 * 8 : Fin * (C / 2) != 256 * 8) return hipErrorInvalidValue;   // the load's piece counts
     }
     switch (mode) {
         case 0: hipLaunchKernelGGL(crn_stream_dec_kernel<0>, dim3((unsigned)a.B), dim3(256), 0, st, a); break;
@@ -503,3 +546,10 @@ hipError_t launch_stream_dec(const StreamDecArgs& a, int mode, hipStream_t st) {
 }
 
 }  // namespace crn
+
+#ifdef AEC_STREAM_PROF
+extern "C" int aec_debug_stream_prof(void* host, size_t bytes) {
+    if (bytes < sizeof(crn::g_sprof)) return -1;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(crn::g_sprof), sizeof(crn::g_sprof)) == hipSuccess ? 0 : -2;
+}
+#endif

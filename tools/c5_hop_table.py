@@ -10,7 +10,7 @@ import sys
 def hops(d):
     rows = list(csv.DictReader(open(os.path.join(d, 'trace', 'run_kernel_trace.csv'))))
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
-    idx = [i for i, r in enumerate(rows) if 'stream_front' in r['Kernel_Name']]
+    idx = [i for i, r in enumerate(rows) if 'stream_front' in r['Kernel_Name'] or 'stream_enc' in r['Kernel_Name']]
     out = []
     for a, b in zip(idx[5:-1], idx[6:]):
         seq = rows[a:b]

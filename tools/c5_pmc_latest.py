@@ -11,7 +11,7 @@ import sys
 
 summ = json.load(open(sys.argv[1]))
 tag = sys.argv[2]
-front = [v['launches'] for k, v in summ.items() if 'stream_front' in k]
+front = [v['launches'] for k, v in summ.items() if 'stream_front' in k or 'stream_enc' in k]
 hops = max(front)
 per_hop = {k: v for k, v in summ.items()
            if v['launches'] >= hops and not k.startswith(('__amd_rocclr', 'at::native'))}
