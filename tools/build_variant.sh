@@ -9,7 +9,9 @@ NAME=$1; shift
 REV=${1:-tree}; [ $# -gt 0 ] && shift
 SRC=$R/acoustic-echo-cancellation_amd/csrc
 W=$(mktemp -d)
-if [ "$REV" != tree ]; then
+if [ -d "$REV" ]; then
+  SRC=$(cd "$REV" && pwd)
+elif [ "$REV" != tree ]; then
   git -C "$R" archive "$REV" acoustic-echo-cancellation_amd/csrc include | tar -x -C "$W"
   SRC=$W/acoustic-echo-cancellation_amd/csrc
 fi

@@ -1,3 +1,7 @@
+#!/usr/bin/env python3
+"""Where the fused per-hop kernels (crn_stream.hip) differ from the separate
+launches: the C5 step at AEC_CRN_STREAM_FUSE = 0 / 1 (front) / 2 (back) / 3,
+37 streams x 14 hops, max abs difference and the hops it appears in."""
 import os, sys, copy, json
 import numpy as np, torch
 sys.path.insert(0, 'acoustic-echo-cancellation_amd'); sys.path.insert(0, 'oracle'); sys.path.insert(0,'tests')
