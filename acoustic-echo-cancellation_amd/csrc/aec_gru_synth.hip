@@ -9,19 +9,20 @@
 // step on one wave), so gru_kernel leaves its CU mostly idle while the
 // separate synthesis kernel then streams the error spectrum back in.  Here
 // the synthesis waves of the stream run inside the GRU's own tick pipeline,
-// two chunks behind the recurrence:
+// two chunks behind the recurrence, and a block carries NS = 2 streams (one
+// recurrence wave each, on different SIMDs; 8 frames of each per tick):
 //
-//   wave 0       recurrence, chunk c                     (gru_kernel's code)
-//   waves 1..3   stage feats of chunk c+2, load chunk c+3, gi = W_ih x + b of chunk c+1
-//   waves 4..6   head / mask / est_erb / loss of chunk c-1 -> est (HBM + LDS ring);
-//                OLA + WOLA of chunk c-3 from the frame ring -> out
-//   waves 7..10  synthesis (gains, irFFT, window) of chunk c-2 into the LDS
-//                frame ring;  E rows of chunk c-1 into registers
+//   waves 0..NS-1  recurrence of stream s, chunk c          (gru_kernel's code)
+//   3 gi waves     stage feats of chunk c+2, load chunk c+3, gi = W_ih x + b of chunk c+1
+//   3 head waves   head / mask / est_erb / loss of chunk c-1 -> est (HBM + LDS ring);
+//                  OLA + WOLA of chunk c-3 from the frame ring -> out
+//   4 synth waves  synthesis (gains, irFFT, window) of chunk c-2 into the LDS
+//                  frame ring;  E rows of chunk c-1 into registers
 //
-// one block barrier per tick of 16 frames.  The arithmetic of every output
-// sample is the unfused path's (synth_frame, the same OLA expression), so
-// the result is bit-identical to gru_kernel + synthesis_kernel
-// (tests/test_gpu_parity.py::test_fused_synthesis_bit_exact).
+// one block barrier per tick of 16 frame slots.  The arithmetic of every
+// output sample is the unfused path's (synth_frame, the same OLA expression),
+// so the result is bit-identical to gru_kernel + synthesis_kernel
+// (tests/test_gpu_nlms.py::test_fused_synthesis_bit_exact) for any NS.
 #ifndef AEC_OUT_NT
 #define AEC_OUT_NT 1   // waveform stores nt: written once, never re-read on the device (fused kernel -1 %)
 #endif
@@ -30,6 +31,7 @@
 #endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "aec_fft.h"
 #include "aec_frame.h"
@@ -40,32 +42,34 @@ namespace aec {
 
 namespace {
 constexpr int kGiWaves = 3, kHeadWaves = 3, kSynWaves = 4;
-constexpr int kFusedWaves = 1 + kGiWaves + kHeadWaves + kSynWaves;    // 11
-constexpr int kFusedThreads = 64 * kFusedWaves;
+constexpr int kHelperWaves = kGiWaves + kHeadWaves + kSynWaves;      // 10
 constexpr int kGiLanes = 64 * kGiWaves;                               // 192
 constexpr int kHeadLanes = 64 * kHeadWaves;                           // 192
 constexpr int kHeadGrp = kHeadLanes / 32;                             // 6 groups of 32 lanes
 constexpr int kEstS = 33;                                             // est ring row stride
+constexpr int kMaxNS = 2;                                             // streams per block
 
-// LDS carve (floats)
+// LDS carve (floats).  A tick holds kCH = 16 frame slots: NS streams x kCH / NS frames
+// (slot q = stream q / TF, frame q % TF of the stream's chunk)
 constexpr int oX = 0;                                   // [2][16][64]
 constexpr int oGi = oX + 2 * kCH * 64;                  // [2][16][96]
 constexpr int oH = oGi + 2 * kCH * 96;                  // [2][16][32]
 constexpr int oMic = oH + 2 * kCH * 32;                 // [4][16][32]
 constexpr int oNear = oMic + 4 * kCH * 32;              // [4][16][32]
 constexpr int oO = oNear + 4 * kCH * 32;                // [6][32]
-constexpr int oLoss = oO + kHeadGrp * 32;               // [8]
-constexpr int oHb = oLoss + 8;                          // [32]
-constexpr int oEst = oHb + 32;                          // [2][16][33] (+2 pad)
+constexpr int oLoss = oO + kHeadGrp * 32;               // [kHeadWaves][NS]
+constexpr int oHb = oLoss + 8;                          // [NS][32]
+constexpr int oEst = oHb + 32 * kMaxNS;                 // [2][16][33] (+2 pad)
 constexpr int oBin = (oEst + 2 * kCH * kEstS + 2 + 3) & ~3;   // float4[257] (+3)
 constexpr int oTw512 = oBin + 260 * 4;                  // float2[258]
 constexpr int oTwT = oTw512 + 258 * 2;                  // float2[256]
 constexpr int oHann = oTwT + 256 * 2;                   // [512]
 constexpr int oCoff = oHann + 512;                      // [256]
-constexpr int oTail = oCoff + 256;                      // [2][256]
-constexpr int oOut = oTail + 2 * 256;                   // [2][4 waves][4 groups][576] frame ring
+constexpr int oTail = oCoff + 256;                      // [2][NS][256]
+constexpr int oOut = oTail + 2 * kMaxNS * 256;          // [2][4 waves][4 groups][576] frame ring
 constexpr int kFusedFloats = oOut + 2 * kSynWaves * 4 * kGroupFloats;
 static_assert(oOut % 4 == 0 && oBin % 4 == 0, "16-B alignment");
+static_assert(kHeadWaves * kMaxNS <= 8, "loss slots");
 }  // namespace
 
 size_t gru_synth_smem_bytes() { return (size_t)kFusedFloats * 4; }
@@ -82,7 +86,15 @@ __device__ __forceinline__ void tick_barrier() {
     asm volatile("" ::: "memory");
 }
 
-__global__ __launch_bounds__(kFusedThreads, 1) void gru_synth_kernel(GruArgs p, SynthArgs y) {
+// NS streams per block (one recurrence wave each, waves 0 .. NS-1), TF = 16 / NS frames of
+// every stream per tick, so the helper roles see 16 frame slots per tick whatever NS is.
+// With NS = 2 the block holds two independent recurrence chains on two SIMDs (the chain of
+// one stream leaves its CU mostly idle) and half the blocks occupy half the CUs for about
+// the same time: the CUs the other half frees run the next batch's analysis kernel.
+template <int NS>
+__global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(GruArgs p, SynthArgs y, int nb) {
+    constexpr int TF = kCH / NS;
+    constexpr int kThreads = 64 * (NS + kHelperWaves);
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* sX = smem + oX;
     float* sGi = smem + oGi;
@@ -101,11 +113,22 @@ __global__ __launch_bounds__(kFusedThreads, 1) void gru_synth_kernel(GruArgs p, 
     float* sTail = smem + oTail;
     float* sOut = smem + oOut;
 
-    const int b = p.b0 + blockIdx.x;
-    const int64_t n = p.lens[b];
-    const int T = (int)(n / kHop + 1);
-    const int64_t nhop = n / kHop;                       // output hops (T - 1)
-    const int nch = (T + kCH - 1) / kCH;
+    // the block's streams (an odd last block: stream 1 absent, its addresses those of stream 0)
+    int bs[NS], Ts[NS], nchs[NS];
+    int64_t nhops[NS];
+    bool vs[NS];
+    int nchmax = 0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const int i = NS * blockIdx.x + s;
+        vs[s] = i < nb;
+        bs[s] = p.b0 + (vs[s] ? i : NS * blockIdx.x);
+        const int64_t n = p.lens[bs[s]];
+        Ts[s] = vs[s] ? (int)(n / kHop + 1) : 0;
+        nhops[s] = vs[s] ? n / kHop : 0;                  // output hops (T - 1)
+        nchs[s] = (Ts[s] + TF - 1) / TF;
+        nchmax = max(nchmax, nchs[s]);
+    }
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const float* W_ih = p.w;                  // [96][64]
@@ -116,28 +139,27 @@ __global__ __launch_bounds__(kFusedThreads, 1) void gru_synth_kernel(GruArgs p, 
     const float* b1 = W1 + 32 * 64;           // [32]
     const float* W2 = b1 + 32;                // [32][32]
     const float* b2 = W2 + 32 * 32;           // [32]
-    const float* fb = p.feats + (int64_t)b * p.Tmax * 96;
 
     // synthesis tables (read after the first tick barrier)
     {
         const DevTables* tb = reinterpret_cast<const DevTables*>(y.tables);
         const float4* bt = reinterpret_cast<const float4*>(y.bintab);
-        for (int i = tid; i < 257; i += kFusedThreads) sBin[i] = bt[i];
-        for (int i = tid; i < 258; i += kFusedThreads) sTw512[i] = tb->tw512[i];
-        for (int i = tid; i < 256; i += kFusedThreads) {
+        for (int i = tid; i < 257; i += kThreads) sBin[i] = bt[i];
+        for (int i = tid; i < 258; i += kThreads) sTw512[i] = tb->tw512[i];
+        for (int i = tid; i < 256; i += kThreads) {
             sTwT[i] = tb->twT[i];
             sCoff[i] = tb->inv_coff[i];
-            sTail[i] = 0.f;
-            sTail[256 + i] = 0.f;
         }
-        for (int i = tid; i < 512; i += kFusedThreads) sHann[i] = tb->hann[i];
+        for (int i = tid; i < 2 * NS * 256; i += kThreads) sTail[i] = 0.f;
+        for (int i = tid; i < 512; i += kThreads) sHann[i] = tb->hann[i];
     }
 
     {
         // role priorities (AEC_FUSED_MODE bits 3-4 synthesis, 5-6 head, 7-8 gi; timing experiments;
         // bits 9 / 10 / 11 skip the recurrence / head / gi, tools/modes_r03.sh)
-        const int role_prio = wave == 0 ? 0 : (wave <= kGiWaves ? (y.fmode >> 7) & 3
-                              : (wave <= kGiWaves + kHeadWaves ? (y.fmode >> 5) & 3 : (y.fmode >> 3) & 3));
+        const int hw = wave - NS;
+        const int role_prio = hw < 0 ? 0 : (hw < kGiWaves ? (y.fmode >> 7) & 3
+                              : (hw < kGiWaves + kHeadWaves ? (y.fmode >> 5) & 3 : (y.fmode >> 3) & 3));
         switch (role_prio) {
             case 1: __builtin_amdgcn_s_setprio(1); break;
             case 2: __builtin_amdgcn_s_setprio(2); break;
@@ -145,9 +167,11 @@ __global__ __launch_bounds__(kFusedThreads, 1) void gru_synth_kernel(GruArgs p, 
             default: break;
         }
     }
-    if (wave == 0) {
-        // ---------------- recurrence wave (gru_kernel wave 0) ----------------
+    if (wave < NS) {
+        // ---------------- recurrence wave of stream `wave` (gru_kernel wave 0) ----------------
         __builtin_amdgcn_s_setprio(3);
+        const int s = wave;
+        const int T = Ts[s], nch = nchs[s];
         const int j = lane & 31, kh = lane >> 5;
         f2v wrz[16], wn[8];
         {
@@ -161,12 +185,13 @@ __global__ __launch_bounds__(kFusedThreads, 1) void gru_synth_kernel(GruArgs p, 
         }
         const float bhn = b_hh[64 + j];
         float hj = 0.f;
-        float* hb = sHb;
+        float* hb = sHb + 32 * s;
         if (lane < 32) hb[lane] = 0.f;
-        for (int c = -3; c <= nch + 2; ++c) {
+        for (int c = -3; c <= nchmax + 2; ++c) {
             if (c >= 0 && c < nch && !(y.fmode & 512)) {
-                const int f_end = min(kCH, T - c * kCH);
-                const float* gi = sGi + (c & 1) * kCH * 96;
+                const int f_end = min(TF, T - c * TF);
+                const float* gi = sGi + ((c & 1) * kCH + s * TF) * 96;
+                float* hrow = sH + ((c & 1) * kCH + s * TF) * 32;
                 float gr = gi[j], gz = gi[32 + j], gn = gi[64 + j];
                 for (int f = 0; f < f_end; ++f) {
                     const int fn = f + 1 < f_end ? f + 1 : f;
@@ -174,17 +199,17 @@ __global__ __launch_bounds__(kFusedThreads, 1) void gru_synth_kernel(GruArgs p, 
                     hj = gru_step(wrz, wn, hb, kh, gr, gz, gn, bhn, hj);
                     if (kh == 0) {
                         hb[j] = hj;
-                        sH[((c & 1) * kCH + f) * 32 + j] = hj;
+                        hrow[f * 32 + j] = hj;
                     }
                     gr = ngr; gz = ngz; gn = ngn;
                 }
             }
             tick_barrier();
         }
-    } else if (wave <= kGiWaves) {
+    } else if (wave < NS + kGiWaves) {
         // ---------------- feats staging + input projection ----------------
-        const int hl = tid - 64;                              // 0..191
-        const int grow = hl % 96, fq = hl / 96;               // frames fq, fq + 2, ...
+        const int hl = tid - 64 * NS;                         // 0..191
+        const int grow = hl % 96, fq = hl / 96;               // slots fq, fq + 2, ...
         float wih[64];
 #pragma unroll
         for (int k = 0; k < 64; ++k) wih[k] = W_ih[grow * 64 + k];
@@ -195,9 +220,14 @@ __global__ __launch_bounds__(kFusedThreads, 1) void gru_synth_kernel(GruArgs p, 
 #pragma unroll
             for (int u = 0; u < kStU; ++u) {
                 const int e = hl + u * kGiLanes;
-                const int t = cc * kCH + (e >> 5);
-                const bool ok = e < kCH * 32 && t < T;
-                const float* f = fb + (int64_t)t * 96 + (e & 31);
+                const int q = e >> 5, s = q / TF;
+                const int t = cc * TF + q % TF;
+                int Tq = 0, bq = bs[0];
+#pragma unroll
+                for (int z = 0; z < NS; ++z)
+                    if (s == z) Tq = Ts[z], bq = bs[z];
+                const bool ok = e < kCH * 32 && t < Tq;
+                const float* f = p.feats + ((int64_t)bq * p.Tmax + t) * 96 + (e & 31);
                 pm[u] = ok ? f[0] : 0.f;
                 pr[u] = ok ? f[32] : 0.f;
                 pn[u] = ok && p.has_near ? f[64] : 0.f;
@@ -205,129 +235,151 @@ __global__ __launch_bounds__(kFusedThreads, 1) void gru_synth_kernel(GruArgs p, 
         };
 #pragma unroll
         for (int u = 0; u < kStU; ++u) pm[u] = pr[u] = pn[u] = 0.f;
-        for (int c = -3; c <= nch + 2; ++c) {
+        for (int c = -3; c <= nchmax + 2; ++c) {
             const int cs = c + 2;
-            if (cs >= 0 && cs < nch) {
+            if (cs >= 0 && cs < nchmax) {
 #pragma unroll
                 for (int u = 0; u < kStU; ++u) {
                     const int e = hl + u * kGiLanes;
                     if (e < kCH * 32) {
-                        const int f = e >> 5, jj = e & 31;
-                        sX[((cs & 1) * kCH + f) * 64 + jj] = pm[u];
-                        sX[((cs & 1) * kCH + f) * 64 + 32 + jj] = fabsf(pm[u] - pr[u]);
-                        sMic[((cs & 3) * kCH + f) * 32 + jj] = pm[u];
-                        sNear[((cs & 3) * kCH + f) * 32 + jj] = pn[u];
+                        const int q = e >> 5, jj = e & 31;
+                        sX[((cs & 1) * kCH + q) * 64 + jj] = pm[u];
+                        sX[((cs & 1) * kCH + q) * 64 + 32 + jj] = fabsf(pm[u] - pr[u]);
+                        sMic[((cs & 3) * kCH + q) * 32 + jj] = pm[u];
+                        sNear[((cs & 3) * kCH + q) * 32 + jj] = pn[u];
                     }
                 }
             }
-            if (c + 3 < nch) load_chunk(c + 3);
+            if (c + 3 < nchmax) load_chunk(c + 3);
             const int cg = c + 1;
-            if (cg >= 0 && cg < nch && !(y.fmode & 2048)) {
+            if (cg >= 0 && cg < nchmax && !(y.fmode & 2048)) {
 #pragma unroll 2
                 for (int i = 0; i < kCH / 2; ++i) {
-                    const int f = fq + 2 * i;
-                    sGi[((cg & 1) * kCH + f) * 96 + grow] = gru_gi(wih, sX + ((cg & 1) * kCH + f) * 64, gbias);
+                    const int q = fq + 2 * i;
+                    sGi[((cg & 1) * kCH + q) * 96 + grow] = gru_gi(wih, sX + ((cg & 1) * kCH + q) * 64, gbias);
                 }
             }
             tick_barrier();
         }
-    } else if (wave <= kGiWaves + kHeadWaves) {
+    } else if (wave < NS + kGiWaves + kHeadWaves) {
         // ---------------- head / mask / est_erb / loss ----------------
-        const int hh = tid - 64 * (1 + kGiWaves);             // 0..191
-        const int hj_ = hh & 31, fg = hh >> 5;                // frames fg, fg + 6, fg + 12
+        const int hh = tid - 64 * (NS + kGiWaves);            // 0..191
+        const int hj_ = hh & 31, fg = hh >> 5;                // slots fg, fg + 6, fg + 12
         float w1[64], w2[32];
 #pragma unroll
         for (int k = 0; k < 64; ++k) w1[k] = W1[hj_ * 64 + k];
 #pragma unroll
         for (int k = 0; k < 32; ++k) w2[k] = W2[hj_ * 32 + k];
         const float b1j = b1[hj_], b2j = b2[hj_];
-        float lacc = 0.f;
-        float* orow = y.out + (int64_t)b * y.ld_out;
+        float lacc[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) lacc[s] = 0.f;
         const bool oal = ((y.ld_out & 3) == 0) && ((reinterpret_cast<uintptr_t>(y.out) & 15) == 0);
-        for (int c = -3; c <= nch + 2; ++c) {
+        for (int c = -3; c <= nchmax + 2; ++c) {
             const int ch = c - 1;
-            if (ch >= 0 && ch < nch && !(y.fmode & 1024)) {
-                for (int f = fg; f < kCH; f += kHeadGrp) {
-                    const int t = ch * kCH + f;
+            if (ch >= 0 && ch < nchmax && !(y.fmode & 1024)) {
+                for (int q = fg; q < kCH; q += kHeadGrp) {
+                    const int s = q / TF, t = ch * TF + q % TF;
+                    int Tq = 0, bq = bs[0];
+#pragma unroll
+                    for (int z = 0; z < NS; ++z)
+                        if (s == z) Tq = Ts[z], bq = bs[z];
                     float est = 0.f;
-                    if (t < T) {                              // uniform within the 32-lane group
-                        const float mask = head_mask(w1, w2, b1j, b2j, sH + ((ch & 1) * kCH + f) * 32,
-                                                     sMic + ((ch & 3) * kCH + f) * 32, sO + fg * 32, hj_);
-                        const float me = sMic[((ch & 3) * kCH + f) * 32 + hj_];
+                    if (t < Tq) {                             // uniform within the 32-lane group
+                        const float mask = head_mask(w1, w2, b1j, b2j, sH + ((ch & 1) * kCH + q) * 32,
+                                                     sMic + ((ch & 3) * kCH + q) * 32, sO + fg * 32, hj_);
+                        const float me = sMic[((ch & 3) * kCH + q) * 32 + hj_];
                         est = mask * me;
-                        const int64_t o_idx = ((int64_t)b * p.Tmax + t) * 32 + hj_;
+                        const int64_t o_idx = ((int64_t)bq * p.Tmax + t) * 32 + hj_;
                         p.est[o_idx] = est;
-                        if (p.dbg_h) p.dbg_h[o_idx] = sH[((ch & 1) * kCH + f) * 32 + hj_];
+                        if (p.dbg_h) p.dbg_h[o_idx] = sH[((ch & 1) * kCH + q) * 32 + hj_];
                         if (p.dbg_mask) p.dbg_mask[o_idx] = mask;
                         if (p.has_near) {
-                            const float d = sqrtf(sNear[((ch & 3) * kCH + f) * 32 + hj_]) - sqrtf(est);
-                            lacc += d * d;
+                            const float d = sqrtf(sNear[((ch & 3) * kCH + q) * 32 + hj_]) - sqrtf(est);
+#pragma unroll
+                            for (int z = 0; z < NS; ++z)
+                                if (s == z) lacc[z] += d * d;
                         }
                     }
-                    sEst[((ch & 1) * kCH + f) * kEstS + hj_] = est;   // frames past the end: gain 0
+                    sEst[((ch & 1) * kCH + q) * kEstS + hj_] = est;   // frames past the end: gain 0
                 }
             }
-            // OLA + WOLA of chunk k = c - 3 (frames 16k .. 16k+15 in ring k & 1):
-            //     hops 16k-1 .. 16k+14; hop 16k-1 uses the tail of frame 16k-1
+            // OLA + WOLA of chunk k = c - 3 of every stream (its TF frames in ring k & 1, slots
+            // s TF ..): hops TF k - 1 .. TF k + TF - 2; hop TF k - 1 uses the tail of frame TF k - 1
             const int k = c - 3;
-            if (k >= 0 && k < nch && !(y.fmode & 2)) {
-                const float* ring = sOut + (k & 1) * (kSynWaves * 4 * kGroupFloats);
-                const float* tail_in = sTail + (k & 1) * 256;
-                const int64_t j0 = (int64_t)k * kCH - 1;
-                const int nh = (int)min((int64_t)kCH, nhop - j0);       // hops j0 .. j0 + nh - 1 below nhop
-                if (oal) {
-                    for (int e = hh; e < kCH * (kHop / 4); e += kHeadLanes) {
-                        const int i = e >> 6, r = (e & 63) * 4;         // hop j0 + i = frame i-1 (2nd half) + frame i
-                        if (i >= nh || j0 + i < 0) continue;
-                        const float4 a = i == 0 ? *reinterpret_cast<const float4*>(tail_in + r)
-                                                : *reinterpret_cast<const float4*>(ring + (i - 1) * kGroupFloats + 256 + r);
-                        const float4 cv = *reinterpret_cast<const float4*>(ring + i * kGroupFloats + r);
-                        const float4 cf = *reinterpret_cast<const float4*>(sCoff + r);
-                        float4 o;
-                        o.x = (a.x + cv.x) * cf.x + 1e-9f;
-                        o.y = (a.y + cv.y) * cf.y + 1e-9f;
-                        o.z = (a.z + cv.z) * cf.z + 1e-9f;
-                        o.w = (a.w + cv.w) * cf.w + 1e-9f;
+            if (k >= 0 && k < nchmax && !(y.fmode & 2)) {
+#pragma unroll
+                for (int s = 0; s < NS; ++s) {
+                    if (k >= nchs[s]) continue;
+                    const float* ring = sOut + (k & 1) * (kSynWaves * 4 * kGroupFloats) + s * TF * kGroupFloats;
+                    const float* tail_in = sTail + ((k & 1) * NS + s) * 256;
+                    const int64_t j0 = (int64_t)k * TF - 1;
+                    const int nh = (int)min((int64_t)TF, nhops[s] - j0);    // hops j0 .. j0 + nh - 1 below nhop
+                    float* orow = y.out + (int64_t)bs[s] * y.ld_out;
+                    if (oal) {
+                        for (int e = hh; e < TF * (kHop / 4); e += kHeadLanes) {
+                            const int i = e >> 6, r = (e & 63) * 4;     // hop j0 + i = frame i-1 (2nd half) + frame i
+                            if (i >= nh || j0 + i < 0) continue;
+                            const float4 a = i == 0 ? *reinterpret_cast<const float4*>(tail_in + r)
+                                                    : *reinterpret_cast<const float4*>(ring + (i - 1) * kGroupFloats + 256 + r);
+                            const float4 cv = *reinterpret_cast<const float4*>(ring + i * kGroupFloats + r);
+                            const float4 cf = *reinterpret_cast<const float4*>(sCoff + r);
+                            float4 o;
+                            o.x = (a.x + cv.x) * cf.x + 1e-9f;
+                            o.y = (a.y + cv.y) * cf.y + 1e-9f;
+                            o.z = (a.z + cv.z) * cf.z + 1e-9f;
+                            o.w = (a.w + cv.w) * cf.w + 1e-9f;
 #if AEC_OUT_NT
-                        typedef float f4v __attribute__((ext_vector_type(4)));
-                        __builtin_nontemporal_store(f4v{o.x, o.y, o.z, o.w},
-                                                    reinterpret_cast<f4v*>(orow + (j0 + i) * kHop + r));
+                            typedef float f4v __attribute__((ext_vector_type(4)));
+                            __builtin_nontemporal_store(f4v{o.x, o.y, o.z, o.w},
+                                                        reinterpret_cast<f4v*>(orow + (j0 + i) * kHop + r));
 #else
-                        *reinterpret_cast<float4*>(orow + (j0 + i) * kHop + r) = o;
+                            *reinterpret_cast<float4*>(orow + (j0 + i) * kHop + r) = o;
 #endif
+                        }
+                    } else {
+                        for (int e = hh; e < TF * kHop; e += kHeadLanes) {
+                            const int i = e >> 8, r = e & 255;
+                            if (i >= nh || j0 + i < 0) continue;
+                            const float a = i == 0 ? tail_in[r] : ring[(i - 1) * kGroupFloats + 256 + r];
+                            const float cv = ring[i * kGroupFloats + r];
+                            orow[(j0 + i) * kHop + r] = (a + cv) * sCoff[r] + 1e-9f;
+                        }
                     }
-                } else {
-                    for (int e = hh; e < kCH * kHop; e += kHeadLanes) {
-                        const int i = e >> 8, r = e & 255;
-                        if (i >= nh || j0 + i < 0) continue;
-                        const float a = i == 0 ? tail_in[r] : ring[(i - 1) * kGroupFloats + 256 + r];
-                        const float cv = ring[i * kGroupFloats + r];
-                        orow[(j0 + i) * kHop + r] = (a + cv) * sCoff[r] + 1e-9f;
-                    }
+                    for (int r = hh; r < 256; r += kHeadLanes)
+                        sTail[(((k + 1) & 1) * NS + s) * 256 + r] = ring[(TF - 1) * kGroupFloats + 256 + r];
                 }
-                for (int r = hh; r < 256; r += kHeadLanes)
-                    sTail[((k + 1) & 1) * 256 + r] = ring[(kCH - 1) * kGroupFloats + 256 + r];
             }
             tick_barrier();
         }
         if (p.loss) {
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) lacc += __shfl_xor(lacc, o);
-            if (lane == 0) sLoss[wave - 1 - kGiWaves] = lacc;
+            for (int s = 0; s < NS; ++s) {
+                float l = lacc[s];
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o);
+                if (lane == 0) sLoss[(wave - NS - kGiWaves) * NS + s] = l;
+            }
         }
     } else {
         // ---------------- synthesis waves ----------------
-        const int sw = wave - (1 + kGiWaves + kHeadWaves);    // 0..3
+        const int sw = wave - (NS + kGiWaves + kHeadWaves);   // 0..3
         const int gg = lane >> 4, lb = lane & 15;
-        const int fl = 4 * sw + gg;                           // frame of the chunk this group synthesises
-        const float2* spec = y.spec + (int64_t)b * y.Tmax * 256;
+        const int fl = 4 * sw + gg;                           // slot this group synthesises
+        const int s = fl / TF, fs = fl % TF;
+        int64_t nhop = 0;
+        int bq = bs[0];
+#pragma unroll
+        for (int z = 0; z < NS; ++z)
+            if (s == z) nhop = nhops[z], bq = bs[z];
+        const float2* spec = y.spec + (int64_t)bq * y.Tmax * 256;
         float2 xa[8] = {}, xb[8] = {}, x128 = {};
         auto load_rows = [&](int cc) {
             // E rows of chunk cc.  A frame past the last one (t > nhop) feeds no
             // written hop (hop j reads frames j and j + 1 <= nhop), so it may
             // read any valid row: the index is clamped, the loads stay plain
             // global loads with no per-lane select.
-            const int64_t t = min((int64_t)cc * kCH + fl, nhop);
+            const int64_t t = min((int64_t)cc * TF + fs, nhop);
             const float2* row = spec + t * 256;
 #pragma unroll
             for (int m = 0; m < 8; ++m) {
@@ -346,13 +398,13 @@ __global__ __launch_bounds__(kFusedThreads, 1) void gru_synth_kernel(GruArgs p, 
             }
             x128 = row[128];
         };
-        for (int c = -3; c <= nch + 2; ++c) {
+        for (int c = -3; c <= nchmax + 2; ++c) {
             // (2) synthesis of chunk c - 2 into ring (c - 2) & 1 (rows loaded last tick); the
             // E rows of chunk c - 1 for the next tick are requested as soon as the inverse pack
             // has consumed this tick's rows, so their load runs under the inverse transform
             const int cs = c - 2;
-            const bool next = c - 1 >= 0 && c - 1 < nch && !(y.fmode & 4);
-            if (cs >= 0 && cs < nch && !(y.fmode & 1)) {
+            const bool next = c - 1 >= 0 && c - 1 < nchmax && !(y.fmode & 4);
+            if (cs >= 0 && cs < nchmax && !(y.fmode & 1)) {
                 float* scr = sOut + (cs & 1) * (kSynWaves * 4 * kGroupFloats) + fl * kGroupFloats;
                 float2 v[16];
                 synth_pack(xa, xb, x128, sEst + ((cs & 1) * kCH + fl) * kEstS, sBin, sTw512, lb, v);
@@ -366,21 +418,38 @@ __global__ __launch_bounds__(kFusedThreads, 1) void gru_synth_kernel(GruArgs p, 
     }
     if (p.loss) {
         __syncthreads();
-        if (tid == 0) {
-            float s = 0.f;
-            for (int w = 0; w < kHeadWaves; ++w) s += sLoss[w];
-            p.loss[b] = s / (float)(T * 32);
+        if (tid < NS) {
+            float sum = 0.f;
+            for (int w = 0; w < kHeadWaves; ++w) sum += sLoss[w * NS + tid];
+            int Tq = 0, bq = 0;
+            bool v = false;
+#pragma unroll
+            for (int z = 0; z < NS; ++z)
+                if (tid == z) Tq = Ts[z], bq = bs[z], v = vs[z];
+            if (v) p.loss[bq] = sum / (float)(Tq * 32);
         }
     }
 }
 
+// streams per block: AEC_GRU_NS (1 or 2, default 2), read per launch
 hipError_t launch_gru_synth(const GruArgs& g, const SynthArgs& y, int B, hipStream_t st) {
     if (B <= 0) return hipSuccess;
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gru_synth_kernel),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       (int)gru_synth_smem_bytes());
-    if (attr != hipSuccess) return attr;
-    hipLaunchKernelGGL(gru_synth_kernel, dim3(B), dim3(kFusedThreads), gru_synth_smem_bytes(), st, g, y);
+    const char* env = getenv("AEC_GRU_NS");
+    const int ns = env && atoi(env) == 1 ? 1 : 2;
+#define AEC_GRU_SYNTH(NS_)                                                                                     \
+    do {                                                                                                       \
+        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gru_synth_kernel<NS_>), \
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize,         \
+                                                           (int)gru_synth_smem_bytes());                       \
+        if (attr != hipSuccess) return attr;                                                                   \
+        hipLaunchKernelGGL(gru_synth_kernel<NS_>, dim3((B + NS_ - 1) / NS_), dim3(64 * (NS_ + kHelperWaves)),   \
+                           gru_synth_smem_bytes(), st, g, y, B);                                               \
+    } while (0)
+    if (ns == 1)
+        AEC_GRU_SYNTH(1);
+    else
+        AEC_GRU_SYNTH(2);
+#undef AEC_GRU_SYNTH
     return hipGetLastError();
 }
 

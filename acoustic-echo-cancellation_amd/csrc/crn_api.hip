@@ -1065,13 +1065,27 @@ static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int
     s = persist_copy(h, st);
     if (s != AEC_OK) return s;
     mark(h, st);
-    s = run_decoder<T>(h, bf, BT, st);
+    // bf16: the mask level runs inside the back kernel (no f32 mask round trip) unless the
+    // caller wants the mask itself (AEC_CRN_BACK_MASK=0: the row GEMM, A/B and bit-equality)
+    const char* bm_env = getenv("AEC_CRN_BACK_MASK");
+    const Packed& pm = h->decf[h->L - 1];
+    const bool mask_in_back = sizeof(T) == 2 && !(bm_env && atoi(bm_env) == 0) && pm.w && !mask_out &&
+                              (out || spec) && pm.N == 4 && pm.kpad <= 128 && pm.kpad % 32 == 0 && pm.act != 1;
+    s = run_decoder<T>(h, bf, BT, st, mask_in_back ? h->L - 1 : -1);
     if (s != AEC_OK) return s;
     mark(h, st);
     if (out || spec) {
         crn::BackArgs ba{mic, ld, h->d_len, Tmax, h->d_tab, reinterpret_cast<const float2*>(h->mask), out, ld_out,
                          reinterpret_cast<float2*>(spec)};
         if (c.nlms_taps > 0) ba.espec = h->espec;
+        if (mask_in_back) {
+            ba.dm_in = reinterpret_cast<const bf16_t*>(h->cat[1]);
+            ba.dm_w = reinterpret_cast<const bf16_t*>(pm.w);
+            ba.dm_bias = pm.bias;
+            ba.dm_kpad = pm.kpad;
+            ba.dm_cin_shift = ilog2(2 * h->cfg.conv_channels[1]);
+            ba.dm_act = pm.act;
+        }
         CRN_TRY(h, crn::launch_back(ba, B, mask_mode(h), st));
     }
     if (mask_out)   // internal frames are t-major ([Tmax][B]); the ABI's mask is [B][Tmax]

@@ -208,6 +208,52 @@ __global__ __launch_bounds__(256) void crn_back_kernel(BackArgs p) {
 
     // mask row of frame t (bins 1..256 -> index bin-1); DC has mask 0 (F.pad, dccrn.py:577-578)
     const float2* mrow = p.mask + ((int64_t)(live ? t : 0) * gridDim.y + b) * 256;   // frame f = t*B + b
+    if (p.dm_in) {
+        // the mask level here: each wave computes the mask rows of its 4 frames (M = 128 input bins
+        // i, N = 4 columns (parity, re / im), K = 3 taps x Cin: input bins i - 1 .. i + 1) into its
+        // LDS region (free between the forward transform and the inverse one)
+        aec::wave_fence();
+        const int cs = p.dm_cin_shift, nch = p.dm_kpad >> 5;
+        const int n = lane & 15;
+        u32x4 bw[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            bw[c] = c < nch ? *reinterpret_cast<const u32x4*>(p.dm_w + (int64_t)n * p.dm_kpad + 32 * c + 8 * gg)
+                            : u32x4{0u, 0u, 0u, 0u};
+        const float bias = n < 4 ? p.dm_bias[n] : 0.f;
+        for (int fi = 0; fi < 4; ++fi) {
+            const int64_t tf = h0 + kWaveFrames * wave + fi;
+            if (!(tf <= nhop && tf < p.Tmax)) continue;                  // wave-uniform
+            const bf16_t* src = p.dm_in + ((tf * gridDim.y + b) * 128 << cs);
+            float* mo = sWave + wave * kWaveFloats + fi * kGroupFloats;
+#pragma unroll
+            for (int mt = 0; mt < 8; ++mt) {
+                const int i = mt * 16 + lb;
+                u32x4 a[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int k0 = 32 * c + 8 * gg, j = k0 >> cs, ib = i - 1 + j;
+                    a[c] = (c < nch && j < 3 && ib >= 0 && ib < 128)
+                               ? *reinterpret_cast<const u32x4*>(src + ((int64_t)ib << cs) + (k0 & ((1 << cs) - 1)))
+                               : u32x4{0u, 0u, 0u, 0u};
+                }
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if (c < nch) mma_chunk(acc, a[c], bw[c], bf16_t{});
+                if (n < 4)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int ii = mt * 16 + 4 * gg + r;
+                        float v = acc[r] + bias;
+                        if (p.dm_act == 2) v = tanhf(v);                // apply_act<2>
+                        mo[(2 * ii + (n >> 1)) * 2 + (n & 1)] = v;
+                    }
+            }
+        }
+        aec::wave_fence();
+        mrow = reinterpret_cast<const float2*>(sWave + wave * kWaveFloats + gg * kGroupFloats);
+    }
     const float2 z = make_float2(0.f, 0.f);
     auto mk = [&](int bin) { return (live && bin > 0) ? mrow[bin - 1] : z; };
 #pragma unroll

@@ -51,6 +51,13 @@ struct BackArgs {
     int64_t ld_out;
     float2* spec;               // nullable
     const float2* espec = nullptr;   // non-null (NLMS): mask the error rows E [B][Tmax][256] (packed) instead
+    // bf16: the mask level (decoder cl = 1, pack_decoder_fused, N = 4) computed in the kernel from
+    // cat[1] [Tmax*B][128][2 ch1] instead of reading `mask` (the per-frame GEMM of the row kernel:
+    // same 32-k chunks from zero, same epilogue)
+    const bf16_t* dm_in = nullptr;
+    const bf16_t* dm_w = nullptr;    // packed [16][kpad]
+    const float* dm_bias = nullptr;
+    int32_t dm_kpad = 0, dm_cin_shift = 0, dm_act = 0;
 };
 
 // Row-GEMM epilogue: out[(m >> oshift)*o_hi + (m & mask)*o_lo + o_add + n] =

@@ -515,3 +515,52 @@ def test_fused_stream_bit_exact(monkeypatch, name, dtype, nlms):
     assert np.abs(res['3']).max() > 0
     assert np.array_equal(res['1'], res['0'])
     assert rel(res['3'], res['0']) <= 1e-6
+
+
+@pytest.mark.parametrize('name,dtype,nlms', [('v2E_16000', 'bf16', False), ('v2E_16000', 'fp8', True),
+                                             ('v1_2125', 'bf16', True), ('v1_2125', 'bf16', False),
+                                             ('v2C_bn_2125', 'fp8', False), ('v2R_1000', 'bf16', False)])
+def test_back_mask_level_matches_gemm(monkeypatch, name, dtype, nlms):
+    """Batch path, bf16 storage: the mask level (the last decoder level, 2
+    output channels x 2 parities) computed inside the back kernel from cat[1]
+    against the row GEMM writing the f32 mask to HBM (AEC_CRN_BACK_MASK=0, read
+    per call): the same 32-k bf16 MFMA chunks from zero, the same bias / tanh
+    epilogue, so out_wav and out_spec agree bit for bit.  Ragged lengths (dead
+    frames of short rows are never computed) and the caller-wants-the-mask
+    case (want_mask: the GEMM path, the mask equal to the fused run's)."""
+    from aec_amd import synth
+    m = META[name]
+    conf = copy.deepcopy(aec_amd.net_conf)
+    conf.update(m['overrides'])
+    nl = dict(taps=4, mu=0.3, beta=0.5, delta=1e-4) if nlms else None
+    net = (aec_amd.dccrn if m['version'] == 1 else aec_amd.dccrn2).DCCRN(conf, dtype=dtype, nlms=nl).eval()
+    sd = net.state_dict()
+    for k, v in C.make_weights(conf, m['version'], m['weight_seed']).items():
+        sd[k] = torch.from_numpy(v)
+    net.load_state_dict(sd, strict=True)
+    net = net.to('cuda:0')
+    B, n = 23, 9000
+    lens = [n - 317 * b for b in range(B)]
+    M = torch.zeros(B, n, device='cuda:0')
+    F = torch.zeros_like(M)
+    for b in range(B):
+        s = synth.scene(lens[b], 3100 + b)
+        M[b, :lens[b]] = torch.from_numpy(s[0]).cuda()
+        F[b, :lens[b]] = torch.from_numpy(s[1]).cuda()
+    res = {}
+    for flag in ('0', '1'):
+        monkeypatch.setenv('AEC_CRN_BACK_MASK', flag)
+        with torch.no_grad():
+            out, spec, _ = net.forward_ragged(M, F, lens, want_spec=True)
+        torch.cuda.synchronize()
+        res[flag] = (out.cpu().numpy(), spec.cpu().numpy())
+    with torch.no_grad():
+        out_m, _, mask = net.forward_ragged(M, F, lens, want_spec=False, want_mask=True)
+    torch.cuda.synchronize()
+    assert np.isfinite(res['1'][0]).all() and np.abs(res['1'][0]).max() > 0
+    for b in range(B):
+        nb, tb = 256 * (lens[b] // 256), lens[b] // 256 + 1
+        assert np.array_equal(res['1'][0][b, :nb], res['0'][0][b, :nb]), b
+        assert np.array_equal(res['1'][1][b, :, :tb], res['0'][1][b, :, :tb]), b
+        assert np.array_equal(out_m.cpu().numpy()[b, :nb], res['1'][0][b, :nb]), b
+    assert np.isfinite(mask.cpu().numpy()).all()

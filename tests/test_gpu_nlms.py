@@ -156,10 +156,11 @@ def test_nlms_erle_delta_vs_oracle(nlms_net, golden_weights, golden_erb):
 def test_fused_synthesis_bit_exact(golden_weights, golden_erb, monkeypatch):
     """The fused GRU + synthesis kernel (aec_gru_synth.hip, default on the
     NLMS path) against the separate gru_kernel + synthesis_kernel
-    (AEC_FUSED_SYNTH=0): the same per-sample arithmetic, so the waveform and
-    est_erb are bit-identical; the loss is summed in a different order
-    (<= 1e-6 relative).  Ragged lengths cover partial last chunks and a
-    stream shorter than one chunk."""
+    (AEC_FUSED_SYNTH=0), with one and with two streams per fused block
+    (AEC_GRU_NS; B = 5 leaves the last block one stream): the same per-sample
+    arithmetic, so the waveform and est_erb are bit-identical; the loss is
+    summed in a different order (<= 1e-6 relative).  Ragged lengths cover
+    partial last chunks and a stream shorter than one chunk."""
     from aec_amd import synth
     lens = [33333, 4097, 255, 16000, 256]
     L = max(lens)
@@ -171,20 +172,23 @@ def test_fused_synthesis_bit_exact(golden_weights, golden_erb, monkeypatch):
     erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
     M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
     res = {}
-    for fused in ('0', '1'):
+    for fused, ns in (('0', '2'), ('1', '1'), ('1', '2')):
         monkeypatch.setenv('AEC_FUSED_SYNTH', fused)            # read when the handle is created
+        monkeypatch.setenv('AEC_GRU_NS', ns)                    # streams per fused block, read per launch
         net = _net(golden_weights, NLMS)
         net.set_debug(True)
         with torch.no_grad():
             out, loss = net.forward_ragged(M, R, N, erb_t, lens)
         est = net.debug_intermediate('est_erb', len(lens), L // 256 + 1)
         torch.cuda.synchronize()
-        res[fused] = (out.cpu().numpy(), loss.cpu().numpy(), est.cpu().numpy())
-    (o0, l0, e0), (o1, l1, e1) = res['0'], res['1']
-    assert np.array_equal(o0, o1)
-    for i, n in enumerate(lens):
-        assert np.array_equal(e0[i, :n // 256 + 1], e1[i, :n // 256 + 1])
-    np.testing.assert_allclose(l1, l0, rtol=1e-6)
+        res[fused + ns] = (out.cpu().numpy(), loss.cpu().numpy(), est.cpu().numpy())
+    o0, l0, e0 = res['02']
+    for key in ('11', '12'):                                     # one and two streams per block (B = 5: odd)
+        o1, l1, e1 = res[key]
+        assert np.array_equal(o0, o1), key
+        for i, n in enumerate(lens):
+            assert np.array_equal(e0[i, :n // 256 + 1], e1[i, :n // 256 + 1]), (key, i)
+        np.testing.assert_allclose(l1, l0, rtol=1e-6)
 
 
 def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatch):
