@@ -1297,6 +1297,10 @@ static crn::StreamEncArgs stream_enc_args(aec_crn_handle* h, int B) {
         L.out = reinterpret_cast<bf16_t*>(ss.cat[i + 1]);
         L.ldo = 2 * ch[i + 1];
         L.choff = ch[i + 1];
+        if (shadow_level(h, i + 1)) {
+            L.q8 = ss.cat8[i + 1];
+            L.qs = ss.cats[i + 1];
+        }
     }
     return ea;
 }
@@ -1364,6 +1368,14 @@ static int stream_enc_levels(const aec_crn_handle* h) {
             shadow_level(h, i + 1))
             break;
         ++n;
+    }
+    // level 3 (16 x 128 from the 32 x 64 map; its MX shadow written in the kernel): AEC_CRN_STREAM_FUSE bit 2
+    if (n == 3 && h->L > 4 && (!v || (atoi(v) & 4))) {
+        const Packed& pk = h->enc[3];
+        const int nc = (pk.K + 31) / 32;
+        if (!pk.wq && pk.act == 1 && pk.N == 128 && ch[3] == 64 && ch[4] == 128 && nc <= crn::kStreamEncChunks3 &&
+            pk.kpad >= 32 * nc)
+            ++n;
     }
     return n;
 }

@@ -713,43 +713,6 @@ __device__ __forceinline__ float apply_act(float v, float alpha) {
     else return v;
 }
 
-// MX-fp8 shadow of one 16-B output chunk (8 bf16, columns n .. n+7) whose
-// 32-column group's 4 chunks sit in lanes 4j .. 4j+3: the group's E8M0 scale
-// (amax over the 4 lanes) and the chunk's 8 e4m3 bytes, by mx8_quant_kernel's
-// rule on the same bf16 values (so an MX GEMM reading the shadow in place sees
-// the bytes the separate quantisation pass would have written).  ok: the
-// chunk is a real output (its bytes / scale are stored); every lane of the
-// wave must call it (cross-lane reduction).
-__device__ __forceinline__ void mx8_chunk(const u32x4& v, bool ok, uint8_t* q8, uint8_t* qs, int64_t eo, bool lead) {
-    float x[8];
-    float amax = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        x[2 * i] = __uint_as_float(v[i] << 16);
-        x[2 * i + 1] = __uint_as_float(v[i] & 0xFFFF0000u);
-        amax = fmaxf(amax, fmaxf(fabsf(x[2 * i]), fabsf(x[2 * i + 1])));
-    }
-    if (!ok) amax = 0.f;
-    amax = fmaxf(amax, __shfl_xor(amax, 1));
-    amax = fmaxf(amax, __shfl_xor(amax, 2));
-    const int ebits = (int)((__float_as_uint(amax) >> 23) & 0xFF);     // floor(log2 amax) + 127
-    const int code = ebits > 8 ? ebits - 8 : 0;                          // E8M0: 2^(code - 127)
-    uint32_t pk[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        float y[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) y[j] = fminf(fmaxf(ldexpf(x[4 * i + j], 127 - code), -448.f), 448.f);
-        int w = __builtin_amdgcn_cvt_pk_fp8_f32(y[0], y[1], 0, false);
-        w = __builtin_amdgcn_cvt_pk_fp8_f32(y[2], y[3], w, true);
-        pk[i] = (uint32_t)w;
-    }
-    if (ok) {
-        *reinterpret_cast<uint2*>(q8 + eo) = make_uint2(pk[0], pk[1]);
-        if (lead) qs[eo >> 5] = (uint8_t)code;
-    }
-}
-
 // Row-GEMM epilogue: bias (loaded once per column fragment), activation,
 // store.  Rows / columns beyond M / N are skipped.
 template <typename OutT, int FM, int FN, int ACT>

@@ -180,7 +180,8 @@ struct StreamBackArgs {
 // Fused per-hop front (crn_stream.hip): frame -> rFFT of mic and far -> [FD-NLMS step] -> X0 ->
 // encoder levels 0 .. nlev-1 (bf16 implicit-GEMM MFMA, 8 tiles of 16 x 16 per level), one block
 // per stream; replaces launch_stream_front + launch_stream_nlms + those levels' row GEMMs.
-constexpr int kStreamEncChunks = 5;   // 32-k chunks per level (K <= 160)
+constexpr int kStreamEncChunks = 5;   // 32-k chunks per level 0-2 (K <= 160)
+constexpr int kStreamEncChunks3 = 10; // level 3 (K <= 320)
 struct StreamEncLevel {
     const bf16_t* w;            // packed [npad][kpad] (pack_encoder)
     const float* bias;
@@ -190,6 +191,8 @@ struct StreamEncLevel {
     bf16_t* out;                // cat[l + 1] [B][Fo][ldo]: the encoder half at channel offset choff
     int64_t ldo;
     int32_t choff;
+    uint8_t* q8 = nullptr;      // level 3: the output's MX-fp8 shadow (RowEpi::q8 / qs layout) or null
+    uint8_t* qs = nullptr;
 };
 struct StreamEncArgs {
     const float* prev_mic;      // [B][256] hop ring
@@ -204,8 +207,8 @@ struct StreamEncArgs {
     float2* state;              // NLMS (taps > 0): [B][2 taps][256] (StreamNlmsArgs layout)
     float2* espec;              //   E rows [B][256]
     float mu, beta, delta;
-    int32_t nlev;               // 1..3
-    StreamEncLevel lev[3];
+    int32_t nlev;               // 1..4 (level 3: 16 output bins x 128 channels, K <= 320)
+    StreamEncLevel lev[4];
 };
 hipError_t launch_stream_enc(const StreamEncArgs& a, int taps, hipStream_t st);
 

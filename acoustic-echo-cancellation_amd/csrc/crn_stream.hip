@@ -28,6 +28,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "aec_fft.h"
 #include "aec_frame.h"
 #include "aec_stft.h"
@@ -140,6 +142,22 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
 #pragma unroll
         for (int c = 0; c < kStreamEncChunks; ++c)
             bw[i][c] = c < L.nchunk ? *reinterpret_cast<const u32x4*>(wr + 32 * c) : u32x4{0u, 0u, 0u, 0u};
+    }
+    // level 3 (16 output bins x 128 channels): this wave's N tiles wave and wave + 4
+    u32x4 bw3[2][kStreamEncChunks3];
+    float bias3[2] = {0.f, 0.f};
+    if (p.nlev > 3) {
+        const StreamEncLevel& L = p.lev[3];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int n = (wave + 4 * t) * 16 + (lane & 15);
+            bias3[t] = L.bias[n];
+            const bf16_t* wr = L.w + (int64_t)n * L.kpad + 8 * (lane >> 4);
+            aec::static_for<0, kStreamEncChunks3>([&](auto ci) {
+                constexpr int c = decltype(ci)::value;
+                bw3[t][c] = c < L.nchunk ? *reinterpret_cast<const u32x4*>(wr + 32 * c) : u32x4{0u, 0u, 0u, 0u};
+            });
+        }
     }
     sTwT[tid] = t0;
     sTw512[tid] = t1;
@@ -254,12 +272,56 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
         SPROF(0, 4 + i);
         in = map;
     }
+    // 5. level 3: one M tile (the 16 output bins) x N tiles wave, wave + 4; the outputs staged in
+    //    LDS, then stored as 16-B row chunks with their MX-fp8 shadow (the row GEMM epilogue's
+    //    mx8_chunk: a 32-column group's 4 chunks in 4 adjacent lanes)
+    if (p.nlev > 3) {
+        const StreamEncLevel& L = p.lev[3];
+        const int cs = L.cin_shift;
+        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        aec::static_for<0, kStreamEncChunks3>([&](auto ci) {
+            constexpr int c = decltype(ci)::value;
+            if (c < L.nchunk) {
+                const int k0 = 32 * c + 8 * (lane >> 4);
+                const int tap = k0 >> cs, q0 = k0 & ((1 << cs) - 1);
+                const int ib = 2 * (lane & 15) - 2 + tap;
+                u32x4 a = {0u, 0u, 0u, 0u};
+                if (tap < 5 && ib >= 0 && ib < 32) a = *reinterpret_cast<const u32x4*>(in + (ib << cs) + q0);
+                mma_chunk(acc[0], a, bw3[0][c], bf16_t{});
+                mma_chunk(acc[1], a, bw3[1][c], bf16_t{});
+            }
+        });
+        bf16_t* stage = sMap[1];                      // level 1's map, consumed by level 2
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 4 * (lane >> 4) + r, n = (wave + 4 * t) * 16 + (lane & 15);
+                float v = acc[t][r] + bias3[t];
+                v = v >= 0.f ? v : L.alpha * v;
+                stage[row * 128 + n] = f2bf(v);
+            }
+        lds_barrier();
+        const int row = tid >> 4, chn = tid & 15;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(stage + row * 128 + 8 * chn);
+        const int64_t eo = ((int64_t)b * 16 + row) * L.ldo + L.choff + 8 * chn;
+        *reinterpret_cast<u32x4*>(L.out + eo) = v;
+        if (L.q8) mx8_chunk(v, true, L.q8, L.qs, eo, (chn & 3) == 0);
+        SPROF(0, 7);
+    }
 }
 
 hipError_t launch_stream_enc(const StreamEncArgs& a, int taps, hipStream_t st) {
     if (a.B <= 0) return hipSuccess;
-    if (a.nlev < 1 || a.nlev > 3) return hipErrorInvalidValue;
-    for (int i = 0; i < a.nlev; ++i) {
+    if (a.nlev < 1 || a.nlev > 4) return hipErrorInvalidValue;
+    if (a.nlev > 3) {
+        const StreamEncLevel& L = a.lev[3];
+        if (L.N != 128 || L.cin_shift != 6 || a.lev[2].N != 64 || L.nchunk < 1 || L.nchunk > kStreamEncChunks3 ||
+            L.kpad < 32 * L.nchunk || L.kpad % 8 || L.ldo % 8 || L.choff % 8 || !L.w || !L.bias || !L.out ||
+            (L.q8 && (L.ldo % 32 || L.choff % 32 || !L.qs)))
+            return hipErrorInvalidValue;
+    }
+    for (int i = 0; i < std::min(a.nlev, 3); ++i) {
         const StreamEncLevel& L = a.lev[i];
         const int Fo = 128 >> i;
         if (L.N % 16 || (Fo / 16) * (L.N / 16) != 8 || 4 % (L.N / 16) || L.nchunk < 1 ||

@@ -472,12 +472,14 @@ def test_fused_stream_bit_exact(monkeypatch, name, dtype, nlms):
     """The per-hop step's fused kernels (crn_stream.hip) against the separate
     launches (AEC_CRN_STREAM_FUSE=0, read at stream_open):
     * front: frame -> rFFT -> FD-NLMS step -> X0 -> encoder levels 0-2 in one
-      launch (vs the front kernel, the NLMS kernel and three row GEMMs);
+      launch (vs the front kernel, the NLMS kernel and three row GEMMs), with
+      bit 2 level 3 as well (16 x 128, its MX-fp8 shadow written in the
+      kernel for the fp8 level 4 that reads it);
     * back: decoder levels 3-1 with their skips, the mask (E / C / R), irFFT
       and overlap-add in one launch (vs three row GEMMs and the back kernel).
     The same transform code, NLMS arithmetic, 32-k MFMA chunks in the same
-    order and epilogues: with the fused front alone (AEC_CRN_STREAM_FUSE=1)
-    37 streams over 14 hops agree bit for bit; with the fused back as well the
+    order and epilogues: with the fused front alone (AEC_CRN_STREAM_FUSE=1,
+    5) 37 streams over 14 hops agree bit for bit; with the fused back as well the
     masked spectrum reaches the inverse transform through LDS (the separate
     back kernel keeps its chain group's bins in registers, where the compiler
     contracts the mask's last product into the inverse pack), so the output
@@ -503,7 +505,7 @@ def test_fused_stream_bit_exact(monkeypatch, name, dtype, nlms):
     M[:, :n] = torch.from_numpy(np.stack([s[0] for s in sig])).cuda()
     F[:, :n] = torch.from_numpy(np.stack([s[1] for s in sig])).cuda()
     res = {}
-    for flag in ('0', '1', '3'):
+    for flag in ('0', '1', '5', '3', '7'):
         monkeypatch.setenv('AEC_CRN_STREAM_FUSE', flag)
         net.stream_open(B)
         with torch.no_grad():
@@ -514,7 +516,9 @@ def test_fused_stream_bit_exact(monkeypatch, name, dtype, nlms):
     assert np.isfinite(res['3']).all()
     assert np.abs(res['3']).max() > 0
     assert np.array_equal(res['1'], res['0'])
+    assert np.array_equal(res['5'], res['0'])
     assert rel(res['3'], res['0']) <= 1e-6
+    assert rel(res['7'], res['0']) <= 1e-6
 
 
 @pytest.mark.parametrize('name,dtype,nlms', [('v2E_16000', 'bf16', False), ('v2E_16000', 'fp8', True),
