@@ -54,6 +54,33 @@ __device__ __forceinline__ void mma_chunk(f32x4& acc, const u32x4& a, const u32x
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[3]), __uint_as_float(b[3]), acc, 0, 0, 0);
 }
 
+// Output tile (mt, nt) of block `bid` in a 1-D grid of nbm x nbn tiles (a speed choice only: every
+// tile is computed the same way wherever it runs).  gm == 0: row tiles in order, column tiles
+// fastest.  gm > 0: blocks b, b + 8, ... are dealt to one XCD (MI355X_MICROARCH.md §Workgroup
+// dispatch, observed placement); the bijective remap of cdna_hip_programming.md §5.5 T1 gives
+// each such set a contiguous range of tile ids, so an XCD owns 1/8 of the rows and A is fetched
+// into one L2 instead of all eight; inside that range gm row tiles are walked per column step,
+// so the tiles an XCD runs together share gm A panels and 32 / gm B panels.
+__device__ __forceinline__ void tile_order(int bid, int nwg, int nbm, int nbn, int gm, int64_t& mt, int& nt) {
+    if (gm <= 0) {
+        mt = bid / nbn;
+        nt = bid % nbn;
+        return;
+    }
+    const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+    const int id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+    if (id >= nbm * nbn) {                          // a padded grid's spare blocks: rows past M
+        mt = nbm;
+        nt = 0;
+        return;
+    }
+    const int per = gm * nbn;                       // tile ids per group of gm row tiles
+    const int g = id / per, in = id - g * per;
+    const int rows = min(gm, nbm - g * gm);
+    mt = (int64_t)g * gm + in % rows;
+    nt = in / rows;
+}
+
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 __device__ __forceinline__ float tanhf_(float x) {
     // tanh(x) = 1 - 2 / (exp(2x) + 1): saturates cleanly for |x| large

@@ -943,8 +943,11 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(RowSrc a, const T* __res
     // 1-D grid, column blocks fastest: the column tiles of one row tile run
     // together (the A rows are read once from HBM and re-used through L2/MALL)
     const int nbn = (e.N + BN - 1) / BN;
-    const int64_t m0 = (int64_t)(blockIdx.x / nbn) * BM;
-    const int n0 = (int)(blockIdx.x % nbn) * BN;
+    int64_t mt;
+    int nt;
+    tile_order((int)blockIdx.x, (int)gridDim.x, (int)((e.M + BM - 1) / BM), nbn, e.xcd_gm, mt, nt);
+    const int64_t m0 = mt * BM;
+    const int n0 = nt * BN;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wr0 = (wave / WN) * FM * 16, wc0 = (wave % WN) * FN * 16;
     f32x4 acc[FM][FN];
@@ -981,8 +984,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_rows_dma_kernel(RowSrc a, c
     // 1-D grid, column blocks fastest: the column tiles of one row tile run
     // together (the A rows are read once from HBM and re-used through L2/MALL)
     const int nbn = (e.N + BN - 1) / BN;
-    const int64_t m0 = (int64_t)(blockIdx.x / nbn) * BM;
-    const int n0 = (int)(blockIdx.x % nbn) * BN;
+    int64_t mt;
+    int nt;
+    tile_order((int)blockIdx.x, (int)gridDim.x, (int)((e.M + BM - 1) / BM), nbn, e.xcd_gm, mt, nt);
+    const int64_t m0 = mt * BM;
+    const int n0 = nt * BN;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wr0 = (wave / WN) * FM * 16, wc0 = (wave % WN) * FN * 16;
     constexpr int ES = (int)sizeof(T);
@@ -1064,6 +1070,12 @@ static int env_int(const char* name, int dflt) {
     return v ? atoi(v) : dflt;
 }
 
+// tile order of the row / MX GEMMs (RowEpi::xcd_gm): CRN_GEMM_XCD
+static int gemm_xcd_gm() {
+    static const int g = env_int("CRN_GEMM_XCD", 0);
+    return g;
+}
+
 template <typename T, typename OutT>
 hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstages, const RowEpi& e, int npad,
                             hipStream_t st) {
@@ -1104,6 +1116,7 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
     static const int pipe = env_int("CRN_GEMM_PIPE", 3);
     RowEpi ee = e;
     ee.mode = gmode;
+    ee.xcd_gm = gemm_xcd_gm();
     switch (bn) {
         // few rows (the per-hop step): quarter-height tiles, 4x the blocks
         case 16:
@@ -1238,8 +1251,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mx8_kernel(const uint8_t* _
     const int nbn = (e.N + BN - 1) / BN;
     const int ntiles = (int)(gridDim.x / (unsigned)ksplit);
     const int tile = (int)(blockIdx.x % (unsigned)ntiles), slice = (int)(blockIdx.x / (unsigned)ntiles);
-    const int64_t m0 = (int64_t)(tile / nbn) * BM;
-    const int n0 = (int)(tile % nbn) * BN;
+    int64_t mt;
+    int nt;
+    tile_order(tile, ntiles, (int)((e.M + BM - 1) / BM), nbn, ksplit == 1 ? e.xcd_gm : 0, mt, nt);
+    const int64_t m0 = mt * BM;
+    const int n0 = nt * BN;
     const int nst = K / 128;
     const int s0 = slice * nst / ksplit, s1 = (slice + 1) * nst / ksplit;
     const int kb0 = s0 * 128;
@@ -1388,7 +1404,9 @@ static hipError_t launch_mx8_cfg(const uint8_t* aq, const uint8_t* as, const uin
     if (ksplit > 1 && (!e.skp || !e.skc || tiles > e.skc_n || K / 128 < ksplit ||
                        tiles * ksplit * BM * BN * 4 > e.sk_bytes))
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(kern, dim3((unsigned)(tiles * ksplit)), dim3(64 * WM * WN), lds, st, aq, as, bq, bs, K, e, ia,
+    RowEpi ee = e;
+    ee.xcd_gm = gemm_xcd_gm();
+    hipLaunchKernelGGL(kern, dim3((unsigned)(tiles * ksplit)), dim3(64 * WM * WN), lds, st, aq, as, bq, bs, K, ee, ia,
                        ksplit);
     return hipGetLastError();
 }

@@ -72,6 +72,10 @@ struct RowEpi {
     float alpha;
     int32_t act;
     int32_t mode = 0;           // timing experiments only (CRN_GEMM_MODE): bit0 skip the epilogue
+    // tile order (speed only, never the result): 0 = row tiles in order, column tiles fastest;
+    // g > 0 = XCD-aware: each set of blocks sharing an XCD gets a contiguous range of tile ids,
+    // walked g row tiles per column step (crn_gemm.h tile_order)
+    int32_t xcd_gm = 0;
     // column split (the decoder's fused parities): columns n >= nsplit are
     // stored at element offset split_add + (n - nsplit) instead of n
     int32_t nsplit = 0x7fffffff;
