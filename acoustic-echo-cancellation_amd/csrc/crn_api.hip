@@ -753,12 +753,74 @@ static void splitk_need(const aec_crn_handle* h, int64_t B, int64_t* bytes, int6
     }
 }
 
+// Batch forward: encoder levels 0-3 in one launch (crn_enc_batch_kernel) when the handle's
+// levels have its shapes (bf16 storage, bf16 GEMMs on those levels); AEC_CRN_BATCH_ENC=0
+// restores the four row GEMMs (A/B and the bit-equality test), =2 makes a handle whose levels do
+// not fit fail with AEC_ERR_UNSUPPORTED (the test's proof that the fused path ran).  Returns the
+// levels it ran.
 template <typename T>
-static aec_status run_encoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipStream_t st, int first = 0) {
+static int run_enc_batch_try(aec_crn_handle* h, const Bufs& bf, int64_t F, hipStream_t st, aec_status* s);
+template <typename T>
+static int run_enc_batch(aec_crn_handle* h, const Bufs& bf, int64_t F, hipStream_t st, aec_status* s) {
+    *s = AEC_OK;
+    const char* v = getenv("AEC_CRN_BATCH_ENC");
+    const int mode = v ? atoi(v) : 1;
+    if (mode == 0) return 0;
+    const int n = run_enc_batch_try<T>(h, bf, F, st, s);
+    if (n == 0 && *s == AEC_OK && mode == 2) {
+        h->err = "AEC_CRN_BATCH_ENC=2: the encoder levels do not fit crn_enc_batch_kernel";
+        *s = AEC_ERR_UNSUPPORTED;
+    }
+    return n;
+}
+template <typename T>
+static int run_enc_batch_try(aec_crn_handle* h, const Bufs& bf, int64_t F, hipStream_t st, aec_status* s) {
+    if (sizeof(T) != 2 || h->es != 2 || h->L < 5) return 0;
+    const int* ch = h->cfg.conv_channels;
+    crn::EncBatchArgs ea{};
+    ea.x0 = reinterpret_cast<const bf16_t*>(bf.x0);
+    ea.F = F;
+    for (int i = 0; i < 4; ++i) {
+        const Packed& pk = h->enc[i];
+        if (pk.wq || pk.act != 1) return 0;
+        crn::StreamEncLevel& L = ea.lev[i];
+        L.w = reinterpret_cast<const bf16_t*>(pk.w);
+        L.bias = pk.bias;
+        L.alpha = pk.alpha;
+        L.kpad = pk.kpad;
+        L.N = pk.N;
+        L.nchunk = (pk.K + 31) / 32;
+        L.cin_shift = ilog2(i == 0 ? 8 : ch[i]);
+        L.out = reinterpret_cast<bf16_t*>(bf.cat[i + 1]);
+        L.ldo = 2 * ch[i + 1];
+        L.choff = ch[i + 1];
+        if (bf.cat8 && bf.cat8[i + 1] && pk.N % 128 == 0) {   // set_shadow's rule
+            L.q8 = bf.cat8[i + 1];
+            L.qs = bf.cats[i + 1];
+        }
+        if (pk.N != ch[i + 1]) return 0;
+    }
+    if (!crn::enc_batch_ok(ea)) return 0;
+    const hipError_t e = crn::launch_enc_batch(ea, st);
+    if (e != hipSuccess) {
+        h->err = std::string("launch_enc_batch: ") + hipGetErrorString(e);
+        *s = e == hipErrorOutOfMemory ? AEC_ERR_OOM : AEC_ERR_HIP;
+        return 0;
+    }
+    return 4;
+}
+
+template <typename T>
+static aec_status run_encoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipStream_t st, int first = 0,
+                              bool batch = false) {
     using crn::RowEpi;
     using crn::RowSrc;
     aec_status s = AEC_OK;
     const int* ch = h->cfg.conv_channels;
+    if (batch && first == 0) {
+        first = run_enc_batch<T>(h, bf, F, st, &s);
+        if (s != AEC_OK) return s;
+    }
     for (int i = first; i < h->L; ++i) {
         const int Fin = 256 >> i, Fo = Fin / 2;
         const int cin = i == 0 ? 8 : ch[i];
@@ -852,12 +914,12 @@ static aec_status run_lstm_combine(aec_crn_handle* h, const Bufs& bf, int l, con
 }
 
 template <typename T>
-static aec_status run_decoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipStream_t st, int nd = -1) {
+static aec_status run_decoder(aec_crn_handle* h, const Bufs& bf, int64_t F, hipStream_t st, int nd = -1, int d0 = 0) {
     using crn::RowEpi;
     using crn::RowSrc;
     const int* ch = h->cfg.conv_channels;
     const int L = h->L;
-    for (int d = 0; d < (nd < 0 ? L : nd); ++d) {
+    for (int d = d0; d < (nd < 0 ? L : nd); ++d) {
         const int cl = L - d;
         const int Fin = 256 >> cl, Fo = 2 * Fin;
         const int64_t ld_in = 2 * ch[cl];
@@ -1018,6 +1080,55 @@ static aec_status persist_wait(aec_crn_handle* h) {
     return AEC_OK;
 }
 
+// Batch forward, bf16 storage: decoder levels cl = 3, 2 in one launch (crn_dec_batch_kernel) when
+// their shapes fit; AEC_CRN_BATCH_DEC=0 restores the two row GEMMs, =2 fails the call unless the
+// fused kernel ran (the bit-equality test).  Returns true when it ran.
+template <typename T>
+static bool run_dec_batch(aec_crn_handle* h, const Bufs& bf, int64_t F, hipStream_t st, aec_status* s) {
+    *s = AEC_OK;
+    const char* v = getenv("AEC_CRN_BATCH_DEC");
+    const int mode = v ? atoi(v) : 1;
+    if (mode == 0) return false;
+    bool ok = sizeof(T) == 2 && h->es == 2 && h->L >= 4;
+    crn::DecBatchArgs da{};
+    if (ok) {
+        const int* ch = h->cfg.conv_channels;
+        da.F = F;
+        for (int l = 0; l < 2; ++l) {
+            const int cl = 3 - l, d = h->L - cl;
+            const Packed& pk = h->decf[d];
+            crn::StreamDecLevel& L = da.lev[l];
+            if (!pk.w || pk.wq || pk.N != 2 * ch[cl - 1]) ok = false;
+            L.w = reinterpret_cast<const bf16_t*>(pk.w);
+            L.bias = pk.bias;
+            L.alpha = pk.alpha;
+            L.act = pk.act;
+            L.kpad = pk.kpad;
+            L.N = pk.N;
+            L.nchunk = (pk.K + 31) / 32;
+            L.cin_shift = ilog2(2 * ch[cl]);
+            L.src = reinterpret_cast<const bf16_t*>(bf.cat[cl]);
+        }
+        da.out = reinterpret_cast<bf16_t*>(bf.cat[1]);
+        da.ldo1 = 2 * ch[1];
+        ok = ok && crn::dec_batch_ok(da);
+    }
+    if (!ok) {
+        if (mode == 2) {
+            h->err = "AEC_CRN_BATCH_DEC=2: decoder levels 3, 2 do not fit crn_dec_batch_kernel";
+            *s = AEC_ERR_UNSUPPORTED;
+        }
+        return false;
+    }
+    const hipError_t e = crn::launch_dec_batch(da, st);
+    if (e != hipSuccess) {
+        h->err = std::string("launch_dec_batch: ") + hipGetErrorString(e);
+        *s = e == hipErrorOutOfMemory ? AEC_ERR_OOM : AEC_ERR_HIP;
+        return false;
+    }
+    return true;
+}
+
 template <typename T>
 static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int32_t B, int64_t ld, int64_t Tmax,
                       float* out, int64_t ld_out, float* spec, float* mask_out, hipStream_t st) {
@@ -1039,7 +1150,7 @@ static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int
         CRN_TRY(h, crn::launch_rows_x0<T>(xa, st));
     }
     mark(h, st);
-    aec_status s = run_encoder<T>(h, bf, BT, st);
+    aec_status s = run_encoder<T>(h, bf, BT, st, 0, true);
     if (s != AEC_OK) return s;
     mark(h, st);
     for (int l = 0; l < h->nrnn; ++l) {
@@ -1071,8 +1182,17 @@ static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int
     const Packed& pm = h->decf[h->L - 1];
     const bool mask_in_back = sizeof(T) == 2 && !(bm_env && atoi(bm_env) == 0) && pm.w && !mask_out &&
                               (out || spec) && pm.N == 4 && pm.kpad <= 128 && pm.kpad % 32 == 0 && pm.act != 1;
-    s = run_decoder<T>(h, bf, BT, st, mask_in_back ? h->L - 1 : -1);
-    if (s != AEC_OK) return s;
+    {
+        // decoder levels cl = L .. 4 as row GEMMs, cl = 3, 2 fused when they fit, then the mask
+        // level (cl = 1) as a GEMM unless the back kernel computes it
+        const int Ld = h->L, d3 = std::max(0, Ld - 3);
+        s = run_decoder<T>(h, bf, BT, st, d3);
+        if (s != AEC_OK) return s;
+        const bool fused = run_dec_batch<T>(h, bf, BT, st, &s);
+        if (s != AEC_OK) return s;
+        s = run_decoder<T>(h, bf, BT, st, mask_in_back ? Ld - 1 : Ld, fused ? Ld - 1 : d3);
+        if (s != AEC_OK) return s;
+    }
     mark(h, st);
     if (out || spec) {
         crn::BackArgs ba{mic, ld, h->d_len, Tmax, h->d_tab, reinterpret_cast<const float2*>(h->mask), out, ld_out,

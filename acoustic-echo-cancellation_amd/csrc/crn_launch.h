@@ -216,6 +216,17 @@ struct StreamEncArgs {
 };
 hipError_t launch_stream_enc(const StreamEncArgs& a, int taps, hipStream_t st);
 
+// Batch encoder front (crn_stream.hip): encoder levels 0-3 of F frames from X0 [F][256][8]
+// (frame f's level-i map at lev[i].out + f * Fo_i * ldo + choff), the four levels' shapes as
+// launch_stream_enc's; replaces the four row GEMMs of the batch forward's encoder front.
+struct EncBatchArgs {
+    const bf16_t* x0;
+    int64_t F;
+    StreamEncLevel lev[4];
+};
+bool enc_batch_ok(const EncBatchArgs& a);
+hipError_t launch_enc_batch(const EncBatchArgs& a, hipStream_t st);
+
 // Fused per-hop back (crn_stream.hip): the last three decoder levels (ComplexConvTranspose2d +
 // skip, both parities per GEMM: pack_decoder_fused) with the maps in LDS, the mask, the masked
 // spectrum's irFFT and the overlap-add, one block per stream; replaces those levels' row GEMMs
@@ -244,6 +255,19 @@ struct StreamDecArgs {
     int32_t B;
 };
 hipError_t launch_stream_dec(const StreamDecArgs& a, int mode, hipStream_t st);
+
+// Batch decoder levels cl = 3, 2 (crn_stream.hip): per frame, cat[3] (whole map, 32 bins x 128)
+// -> level cl = 3 -> cat[2]'s decoder half (LDS only) + its encoder half from HBM -> level cl = 2
+// -> cat[1]'s decoder half (out, 128 bins x 16 at row stride ldo1).  lev[0..1] as the per-hop
+// back's first two levels (src = cat[3] / cat[2]); replaces those two row GEMMs of the batch forward.
+struct DecBatchArgs {
+    int64_t F;
+    StreamDecLevel lev[2];
+    bf16_t* out;                // cat[1] [F][128][ldo1], channels [0, 16)
+    int64_t ldo1;
+};
+bool dec_batch_ok(const DecBatchArgs& a);
+hipError_t launch_dec_batch(const DecBatchArgs& a, hipStream_t st);
 
 template <typename T>
 hipError_t launch_stream_front(const StreamFrontArgs& a, hipStream_t st);

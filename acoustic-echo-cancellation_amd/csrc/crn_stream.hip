@@ -55,6 +55,10 @@ __device__ unsigned long long g_sprof[2][16];
 namespace {
 
 constexpr int kMapElems = 2048;
+// The level maps in LDS keep one bin per row, padded by 16 B: a level's A fragment reads the 16
+// lanes' bins two apart (encoder) or adjacent (decoder), which unpadded land on 4 to 16 copies of
+// the same bank slots (32- to 256-B rows); padded, a 16-lane group spreads over 8 or 16 slots.
+constexpr int kPadMapElems = 128 * (16 + 8);   // the largest padded encoder map: level 0's 128 x (16 + 8)
 
 // block barrier that drains LDS only: the global stores of the level outputs (read by a later
 // launch) and the register loads of weight fragments stay in flight across it
@@ -80,7 +84,7 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
     __shared__ __attribute__((aligned(16))) float sGrp[2][aec::kGroupFloats];
     __shared__ __attribute__((aligned(16))) float2 sRow[2][256];
     __shared__ __attribute__((aligned(16))) bf16_t sX0[256 * 8];
-    __shared__ __attribute__((aligned(16))) bf16_t sMap[2][kMapElems];
+    __shared__ __attribute__((aligned(16))) bf16_t sMap[2][kPadMapElems];
     float2* sTwT = reinterpret_cast<float2*>(sTab);
     float2* sTw512 = sTwT + 256;
     float* sHann = reinterpret_cast<float*>(sTw512 + 258);
@@ -244,12 +248,13 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
             if (c >= L.nchunk) continue;
             const int k0 = 32 * c + 8 * (lane >> 4);
             const int tap = k0 >> cs, q0 = k0 & ((1 << cs) - 1);
+            const int rs = i == 0 ? 8 : (1 << cs) + 8;             // row stride (X0: 16-B rows, unpadded)
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
                 const int j = (t ? m1 : m0) * 16 + (lane & 15);
                 const int ib = 2 * j - 2 + tap;
                 u32x4 a = {0u, 0u, 0u, 0u};
-                if (tap < 5 && ib >= 0 && ib < Fin) a = *reinterpret_cast<const u32x4*>(in + (ib << cs) + q0);
+                if (tap < 5 && ib >= 0 && ib < Fin) a = *reinterpret_cast<const u32x4*>(in + ib * rs + q0);
                 mma_chunk(acc[t], a, bw[i][c], bf16_t{});
             }
         }
@@ -265,7 +270,7 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
                 float v = acc[t][r] + bias[i];
                 v = v >= 0.f ? v : L.alpha * v;
                 const bf16_t o = f2bf(v);
-                if (keep) map[row * L.N + n] = o;
+                if (keep) map[row * (L.N + 8) + n] = o;
                 out[(int64_t)row * L.ldo + n] = o;
             }
         lds_barrier();
@@ -286,7 +291,7 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
                 const int tap = k0 >> cs, q0 = k0 & ((1 << cs) - 1);
                 const int ib = 2 * (lane & 15) - 2 + tap;
                 u32x4 a = {0u, 0u, 0u, 0u};
-                if (tap < 5 && ib >= 0 && ib < 32) a = *reinterpret_cast<const u32x4*>(in + (ib << cs) + q0);
+                if (tap < 5 && ib >= 0 && ib < 32) a = *reinterpret_cast<const u32x4*>(in + ib * ((1 << cs) + 8) + q0);
                 mma_chunk(acc[0], a, bw3[0][c], bf16_t{});
                 mma_chunk(acc[1], a, bw3[1][c], bf16_t{});
             }
@@ -341,6 +346,219 @@ hipError_t launch_stream_enc(const StreamEncArgs& a, int taps, hipStream_t st) {
 }
 
 // --------------------------------------------------------------------------
+// Batch encoder front (the batch forward of C3 / C4 and its fp8 form): encoder levels 0-3 of
+// every frame from X0 in HBM, the per-hop front's level arithmetic over FR frames per block at
+// once, the maps in LDS.  A persistent frame loop keeps the weight fragments of all four levels
+// in registers for the whole launch; X0 of the next FR frames is fetched into registers while
+// the current ones run.  Each level's map leaves LDS as 16-B rows (the encoder half of
+// cat[l + 1]); level 3 also writes its MX-fp8 shadow.  Same packed weights, the same 32-k
+// chunks in the same order from zero and the same epilogue as the row GEMMs these four
+// launches replace, so the maps are bit-identical (tests/test_gpu_crn.py::test_batch_enc_fused_bit_exact).
+// The LDS maps are padded as the per-hop kernels' (kPadMapElems).
+// --------------------------------------------------------------------------
+template <int FR>
+__global__ __launch_bounds__(256, 1) void crn_enc_batch_kernel(EncBatchArgs p) {
+    __shared__ __attribute__((aligned(16))) bf16_t sX0[FR][256 * 8];
+    __shared__ __attribute__((aligned(16))) bf16_t sMap[2][FR][kPadMapElems];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    // weight fragments (crn_stream_enc_kernel's map): levels 0-2, this wave's N tile wave % NT;
+    // level 3, N tiles wave and wave + 4
+    u32x4 bw[3][kStreamEncChunks];
+    float bias[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const StreamEncLevel& L = p.lev[i];
+        const int NT = L.N >> 4;
+        const int n = (wave % NT) * 16 + (lane & 15);
+        bias[i] = L.bias[n];
+        const bf16_t* wr = L.w + (int64_t)n * L.kpad + 8 * (lane >> 4);
+#pragma unroll
+        for (int c = 0; c < kStreamEncChunks; ++c)
+            bw[i][c] = c < L.nchunk ? *reinterpret_cast<const u32x4*>(wr + 32 * c) : u32x4{0u, 0u, 0u, 0u};
+    }
+    u32x4 bw3[2][kStreamEncChunks3];
+    float bias3[2];
+    {
+        const StreamEncLevel& L = p.lev[3];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int n = (wave + 4 * t) * 16 + (lane & 15);
+            bias3[t] = L.bias[n];
+            const bf16_t* wr = L.w + (int64_t)n * L.kpad + 8 * (lane >> 4);
+            aec::static_for<0, kStreamEncChunks3>([&](auto ci) {
+                constexpr int c = decltype(ci)::value;
+                bw3[t][c] = c < L.nchunk ? *reinterpret_cast<const u32x4*>(wr + 32 * c) : u32x4{0u, 0u, 0u, 0u};
+            });
+        }
+    }
+    const int64_t F = p.F, step = (int64_t)gridDim.x * FR;
+    // X0 of frames fb .. fb + FR - 1: 4 KB each = one 16-B piece per thread
+    u32x4 nx[FR];
+    auto fetch = [&](int64_t fb) {
+#pragma unroll
+        for (int fr = 0; fr < FR; ++fr) {
+            const int64_t f = fb + fr;
+            nx[fr] = f < F ? reinterpret_cast<const u32x4*>(p.x0 + f * 2048)[tid] : u32x4{0u, 0u, 0u, 0u};
+        }
+    };
+    fetch((int64_t)blockIdx.x * FR);
+    for (int64_t f0 = (int64_t)blockIdx.x * FR; f0 < F; f0 += step) {
+#pragma unroll
+        for (int fr = 0; fr < FR; ++fr) reinterpret_cast<u32x4*>(sX0[fr])[tid] = nx[fr];
+        lds_barrier();
+        fetch(f0 + step);
+        // levels 0-2: 8 output tiles of 16 bins x 16 channels per frame, two per wave
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const StreamEncLevel& L = p.lev[i];
+            const int Fin = 256 >> i, Fo = Fin >> 1;
+            const int NT = L.N >> 4;
+            const int nt = wave % NT, m0 = wave / NT, m1 = m0 + 4 / NT;
+            const int cs = L.cin_shift;
+            f32x4 acc[FR][2];
+#pragma unroll
+            for (int fr = 0; fr < FR; ++fr) acc[fr][0] = acc[fr][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < kStreamEncChunks; ++c) {
+                if (c >= L.nchunk) continue;
+                const int k0 = 32 * c + 8 * (lane >> 4);
+                const int tap = k0 >> cs, q0 = k0 & ((1 << cs) - 1);
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const int j = (t ? m1 : m0) * 16 + (lane & 15);
+                    const int ib = 2 * j - 2 + tap;
+                    const bool ok = tap < 5 && ib >= 0 && ib < Fin;
+#pragma unroll
+                    for (int fr = 0; fr < FR; ++fr) {
+                        const bf16_t* in = i == 0 ? sX0[fr] : sMap[(i - 1) & 1][fr];
+                        const int rs = i == 0 ? 8 : (1 << cs) + 8;       // row stride (elements)
+                        u32x4 a = {0u, 0u, 0u, 0u};
+                        if (ok) a = *reinterpret_cast<const u32x4*>(in + ib * rs + q0);
+                        mma_chunk(acc[fr][t], a, bw[i][c], bf16_t{});
+                    }
+                }
+            }
+            const int n = nt * 16 + (lane & 15);
+#pragma unroll
+            for (int fr = 0; fr < FR; ++fr)
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = (t ? m1 : m0) * 16 + 4 * (lane >> 4) + r;
+                        float v = acc[fr][t][r] + bias[i];
+                        v = v >= 0.f ? v : L.alpha * v;
+                        sMap[i & 1][fr][row * (L.N + 8) + n] = f2bf(v);
+                    }
+            lds_barrier();
+            // the map -> the encoder half of cat[i + 1]: map row `row` (N channels) is contiguous
+            const int e0 = 8 * tid, row = e0 / L.N, ch0 = e0 % L.N;
+#pragma unroll
+            for (int fr = 0; fr < FR; ++fr) {
+                const int64_t f = f0 + fr;
+                if (f < F)
+                    *reinterpret_cast<u32x4*>(L.out + (f * Fo + row) * L.ldo + L.choff + ch0) =
+                        *reinterpret_cast<const u32x4*>(sMap[i & 1][fr] + row * (L.N + 8) + ch0);
+            }
+        }
+        // level 3: the 16 output bins x N tiles wave, wave + 4, staged in level 1's map
+        {
+            const StreamEncLevel& L = p.lev[3];
+            const int cs = L.cin_shift;
+            f32x4 acc[FR][2];
+#pragma unroll
+            for (int fr = 0; fr < FR; ++fr) acc[fr][0] = acc[fr][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            aec::static_for<0, kStreamEncChunks3>([&](auto ci) {
+                constexpr int c = decltype(ci)::value;
+                if (c < L.nchunk) {
+                    const int k0 = 32 * c + 8 * (lane >> 4);
+                    const int tap = k0 >> cs, q0 = k0 & ((1 << cs) - 1);
+                    const int ib = 2 * (lane & 15) - 2 + tap;
+                    const bool ok = tap < 5 && ib >= 0 && ib < 32;
+#pragma unroll
+                    for (int fr = 0; fr < FR; ++fr) {
+                        u32x4 a = {0u, 0u, 0u, 0u};
+                        if (ok) a = *reinterpret_cast<const u32x4*>(sMap[0][fr] + ib * ((1 << cs) + 8) + q0);
+                        mma_chunk(acc[fr][0], a, bw3[0][c], bf16_t{});
+                        mma_chunk(acc[fr][1], a, bw3[1][c], bf16_t{});
+                    }
+                }
+            });
+#pragma unroll
+            for (int fr = 0; fr < FR; ++fr)
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = 4 * (lane >> 4) + r, n = (wave + 4 * t) * 16 + (lane & 15);
+                        float v = acc[fr][t][r] + bias3[t];
+                        v = v >= 0.f ? v : L.alpha * v;
+                        sMap[1][fr][row * 128 + n] = f2bf(v);
+                    }
+            lds_barrier();
+            const int row = tid >> 4, chn = tid & 15;
+#pragma unroll
+            for (int fr = 0; fr < FR; ++fr) {
+                const int64_t f = f0 + fr;
+                const bool ok = f < F;
+                const u32x4 v = *reinterpret_cast<const u32x4*>(sMap[1][fr] + row * 128 + 8 * chn);
+                const int64_t eo = ((ok ? f : 0) * 16 + row) * L.ldo + L.choff + 8 * chn;
+                if (ok) *reinterpret_cast<u32x4*>(L.out + eo) = v;
+                if (L.q8) mx8_chunk(v, ok, L.q8, L.qs, eo, (chn & 3) == 0);
+            }
+        }
+    }
+}
+
+// the shapes crn_enc_batch_kernel takes (those of crn_stream_enc_kernel's four levels)
+bool enc_batch_ok(const EncBatchArgs& a) {
+    if (a.F <= 0 || !a.x0) return false;
+    for (int i = 0; i < 4; ++i) {
+        const StreamEncLevel& L = a.lev[i];
+        if (!L.w || !L.bias || !L.out || L.kpad % 8 || L.ldo % 8 || L.choff % 8 || L.nchunk < 1 ||
+            L.kpad < 32 * L.nchunk)
+            return false;
+        if (i < 3) {
+            const int Fo = 128 >> i;
+            if (L.N % 16 || (Fo / 16) * (L.N / 16) != 8 || 4 % (L.N / 16) || L.nchunk > kStreamEncChunks ||
+                L.cin_shift < 3 || (i > 0 && (1 << L.cin_shift) != a.lev[i - 1].N) || (i == 0 && L.cin_shift != 3) ||
+                L.q8)
+                return false;
+        } else if (L.N != 128 || L.cin_shift != 6 || a.lev[2].N != 64 || L.nchunk > kStreamEncChunks3 ||
+                   (L.q8 && (L.ldo % 32 || L.choff % 32 || !L.qs))) {
+            return false;
+        }
+    }
+    return true;
+}
+
+template <int FR>
+static hipError_t launch_enc_batch_fr(const EncBatchArgs& a, hipStream_t st) {
+    static const int grid = [] {
+        int dev = 0, ncu = 0, per = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(crn_enc_batch_kernel<FR>),
+                                                           256, 0);
+        return std::max(1, ncu) * std::max(1, per);
+    }();
+    const int64_t need = (a.F + FR - 1) / FR;
+    hipLaunchKernelGGL(crn_enc_batch_kernel<FR>, dim3((unsigned)std::min<int64_t>(grid, need)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_enc_batch(const EncBatchArgs& a, hipStream_t st) {
+    if (a.F <= 0) return hipSuccess;
+    if (!enc_batch_ok(a)) return hipErrorInvalidValue;
+    static const int fr = [] { const char* v = getenv("AEC_CRN_ENC_FR"); return v ? atoi(v) : 4; }();   // A/B only
+    switch (fr) {
+        case 2: return launch_enc_batch_fr<2>(a, st);
+        case 8: return launch_enc_batch_fr<8>(a, st);
+        default: return launch_enc_batch_fr<4>(a, st);
+    }
+}
+
+// --------------------------------------------------------------------------
 // Fused back: decoder levels cl = 3, 2, 1 + mask + irFFT + overlap-add, one block per stream
 // --------------------------------------------------------------------------
 namespace {
@@ -364,7 +582,7 @@ __device__ __forceinline__ void dec_tiles(f32x4 (&acc)[2], const bf16_t* in, int
                 const int i = (t ? m1 : m0) * 16 + (lane & 15);
                 const int ib = i - 1 + j;
                 u32x4 a = {0u, 0u, 0u, 0u};
-                if (j < 3 && ib >= 0 && ib < Fin) a = *reinterpret_cast<const u32x4*>(in + (ib << cs) + q0);
+                if (j < 3 && ib >= 0 && ib < Fin) a = *reinterpret_cast<const u32x4*>(in + ib * ((1 << cs) + 8) + q0);
                 mma_chunk(acc[t], a, bw[c], bf16_t{});
             }
         }
@@ -384,7 +602,7 @@ __device__ __forceinline__ void load_bw(u32x4 (&bw)[NC], const StreamDecLevel& L
 
 template <int MODE>
 __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
-    constexpr int kMap = 4096;                    // bf16 elements of a level's input map (Fin x Cin)
+    constexpr int kMap = 5120;                    // bf16 elements of a level's padded input map (Fin x (Cin + 8))
     __shared__ __attribute__((aligned(16))) bf16_t sIn[3][kMap];
     __shared__ __attribute__((aligned(16))) float2 sMask[256];
     __shared__ __attribute__((aligned(16))) float2 sRow[256];
@@ -447,13 +665,19 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
     load_bw(bw0, p.lev[0], nt[0] * 16 + (lane & 15));
     load_bw(bw1, p.lev[1], nt[1] * 16 + (lane & 15));
     load_bw(bw2, p.lev[2], nt[2] * 16 + (lane & 15));
+    {
+        const int C = 1 << L0.cin_shift, per = C / 8;   // 16-B pieces per map row
 #pragma unroll
-    for (int i = 0; i < kDecPieces; ++i) reinterpret_cast<u32x4*>(sIn[0])[tid + 256 * i] = mp[i];
+        for (int i = 0; i < kDecPieces; ++i) {
+            const int pc = tid + 256 * i, r = pc / per, q = pc % per;
+            *reinterpret_cast<u32x4*>(sIn[0] + r * (C + 8) + 8 * q) = mp[i];
+        }
+    }
 #pragma unroll
     for (int l = 1; l < 3; ++l) {
         const int C = 1 << p.lev[l].cin_shift, half = C / 2, per = half / 8;
         const int r = tid / per, q = tid % per;
-        *reinterpret_cast<u32x4*>(sIn[l] + r * C + half + 8 * q) = mp[kDecPieces + l - 1];
+        *reinterpret_cast<u32x4*>(sIn[l] + r * (C + 8) + half + 8 * q) = mp[kDecPieces + l - 1];
     }
     lds_barrier();
     SPROF(1, 1);
@@ -475,7 +699,7 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
                 const int i = (t ? m1[l] : m0[l]) * 16 + 4 * (lane >> 4) + r;
                 float v = acc[t][r] + bias[l];
                 v = v >= 0.f ? v : L.alpha * v;
-                next[(2 * i + par) * Cn + ch] = f2bf(v);
+                next[(2 * i + par) * (Cn + 8) + ch] = f2bf(v);
             }
         lds_barrier();
         SPROF(1, 2 + l);
@@ -582,6 +806,136 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
         p.tail[(int64_t)b * 256 + r] = sGrp[256 + r];
     }
     SPROF(1, 7);
+}
+
+// --------------------------------------------------------------------------
+// Batch decoder levels cl = 3, 2 (the batch forward of C3 / C4): FR frames per block in a
+// persistent frame loop, the per-hop back's level arithmetic (dec_tiles, both parities per
+// GEMM, the PReLU epilogue) with the maps in padded LDS rows; cat[2]'s decoder half never
+// leaves LDS, cat[1]'s leaves as 16-B rows for crn_back_kernel's mask level.  The inputs of
+// the next FR frames (cat[3] whole, cat[2]'s encoder half) are fetched into registers while
+// the current ones run.  Bit-identical to the two row GEMMs (test_batch_dec_fused_bit_exact).
+// --------------------------------------------------------------------------
+template <int FR>
+__global__ __launch_bounds__(256, 1) void crn_dec_batch_kernel(DecBatchArgs p) {
+    constexpr int kA = 32 * (128 + 8), kB = 64 * (64 + 8), kO = 128 * 16;
+    __shared__ __attribute__((aligned(16))) bf16_t sA[FR][kA];
+    __shared__ __attribute__((aligned(16))) bf16_t sB[FR][kB];
+    __shared__ __attribute__((aligned(16))) bf16_t sO[FR][kO];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const StreamDecLevel& LA = p.lev[0];
+    const StreamDecLevel& LB = p.lev[1];
+    u32x4 bw0[kStreamDecChunks0], bw1[kStreamDecChunks1];
+    const int nt0 = wave % 4, nt1 = wave % 2, mb0 = wave / 2;      // level A: 4 N tiles x M tiles 0, 1
+    const int n0 = nt0 * 16 + (lane & 15), n1 = nt1 * 16 + (lane & 15);
+    load_bw(bw0, LA, n0);
+    load_bw(bw1, LB, n1);
+    const float bias0 = LA.bias[n0], bias1 = LB.bias[n1];
+    const int64_t F = p.F, step = (int64_t)gridDim.x * FR;
+    // cat[3]: 512 16-B pieces per frame (2 per thread); cat[2]'s encoder half: 64 rows x 4 pieces
+    u32x4 na[FR][2], nb[FR];
+    auto fetch = [&](int64_t fb) {
+#pragma unroll
+        for (int fr = 0; fr < FR; ++fr) {
+            const int64_t f = fb + fr;
+            const bool ok = f < F;
+            const u32x4* a3 = reinterpret_cast<const u32x4*>(LA.src + (ok ? f : 0) * 4096);
+            na[fr][0] = ok ? a3[tid] : u32x4{0u, 0u, 0u, 0u};
+            na[fr][1] = ok ? a3[tid + 256] : u32x4{0u, 0u, 0u, 0u};
+            nb[fr] = ok ? *reinterpret_cast<const u32x4*>(LB.src + ((ok ? f : 0) * 64 + (tid >> 2)) * 64 + 32 + 8 * (tid & 3))
+                        : u32x4{0u, 0u, 0u, 0u};
+        }
+    };
+    fetch((int64_t)blockIdx.x * FR);
+    for (int64_t f0 = (int64_t)blockIdx.x * FR; f0 < F; f0 += step) {
+#pragma unroll
+        for (int fr = 0; fr < FR; ++fr) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int pc = tid + 256 * h, r = pc >> 4, q = pc & 15;
+                *reinterpret_cast<u32x4*>(sA[fr] + r * 136 + 8 * q) = na[fr][h];
+            }
+            *reinterpret_cast<u32x4*>(sB[fr] + (tid >> 2) * 72 + 32 + 8 * (tid & 3)) = nb[fr];
+        }
+        lds_barrier();
+        fetch(f0 + step);
+        // level cl = 3: M = 32 input bins (tiles 0, 1), N = 64 (parity x 32 channels) -> sB's decoder half
+        {
+            f32x4 acc[FR][2];
+#pragma unroll
+            for (int fr = 0; fr < FR; ++fr) dec_tiles(acc[fr], sA[fr], 32, 7, LA.nchunk, bw0, 0, 1, lane);
+            const int par = n0 >= 32, ch = n0 - 32 * par;
+#pragma unroll
+            for (int fr = 0; fr < FR; ++fr)
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = t * 16 + 4 * (lane >> 4) + r;
+                        float v = acc[fr][t][r] + bias0;
+                        v = v >= 0.f ? v : LA.alpha * v;
+                        sB[fr][(2 * i + par) * 72 + ch] = f2bf(v);
+                    }
+        }
+        lds_barrier();
+        // level cl = 2: M = 64 input bins (tiles mb0, mb0 + 2), N = 32 (parity x 16 channels) -> sO
+        {
+            f32x4 acc[FR][2];
+#pragma unroll
+            for (int fr = 0; fr < FR; ++fr) dec_tiles(acc[fr], sB[fr], 64, 6, LB.nchunk, bw1, mb0, mb0 + 2, lane);
+            const int par = n1 >= 16, ch = n1 - 16 * par;
+#pragma unroll
+            for (int fr = 0; fr < FR; ++fr)
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = (mb0 + 2 * t) * 16 + 4 * (lane >> 4) + r;
+                        float v = acc[fr][t][r] + bias1;
+                        v = v >= 0.f ? v : LB.alpha * v;
+                        sO[fr][(2 * i + par) * 16 + ch] = f2bf(v);
+                    }
+        }
+        lds_barrier();
+        // cat[1]'s decoder half: 128 rows x 32 B (two 16-B pieces per row, one per thread)
+#pragma unroll
+        for (int fr = 0; fr < FR; ++fr) {
+            const int64_t f = f0 + fr;
+            if (f < F)
+                *reinterpret_cast<u32x4*>(p.out + (f * 128 + (tid >> 1)) * p.ldo1 + 8 * (tid & 1)) =
+                    *reinterpret_cast<const u32x4*>(sO[fr] + tid * 8);
+        }
+    }
+}
+
+bool dec_batch_ok(const DecBatchArgs& a) {
+    if (a.F <= 0 || !a.out || a.ldo1 % 8 || a.ldo1 < 16) return false;
+    const int caps[2] = {kStreamDecChunks0, kStreamDecChunks1};
+    const int cs[2] = {7, 6}, N[2] = {64, 32};
+    for (int l = 0; l < 2; ++l) {
+        const StreamDecLevel& L = a.lev[l];
+        if (!L.w || !L.bias || !L.src || L.nchunk < 1 || L.nchunk > caps[l] || L.kpad < 32 * L.nchunk || L.kpad % 8 ||
+            L.act != 1 || L.cin_shift != cs[l] || L.N != N[l])
+            return false;
+    }
+    return true;
+}
+
+hipError_t launch_dec_batch(const DecBatchArgs& a, hipStream_t st) {
+    if (a.F <= 0) return hipSuccess;
+    if (!dec_batch_ok(a)) return hipErrorInvalidValue;
+    constexpr int FR = 4;
+    static const int grid = [] {
+        int dev = 0, ncu = 0, per = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(crn_dec_batch_kernel<FR>),
+                                                           256, 0);
+        return std::max(1, ncu) * std::max(1, per);
+    }();
+    const int64_t need = (a.F + FR - 1) / FR;
+    hipLaunchKernelGGL(crn_dec_batch_kernel<FR>, dim3((unsigned)std::min<int64_t>(grid, need)), dim3(256), 0, st, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_stream_dec(const StreamDecArgs& a, int mode, hipStream_t st) {

@@ -568,3 +568,54 @@ def test_back_mask_level_matches_gemm(monkeypatch, name, dtype, nlms):
         assert np.array_equal(res['1'][1][b, :, :tb], res['0'][1][b, :, :tb]), b
         assert np.array_equal(out_m.cpu().numpy()[b, :nb], res['1'][0][b, :nb]), b
     assert np.isfinite(mask.cpu().numpy()).all()
+
+
+@pytest.mark.parametrize('knob', ['AEC_CRN_BATCH_ENC', 'AEC_CRN_BATCH_DEC'])
+@pytest.mark.parametrize('name,dtype,nlms', [('v2E_16000', 'bf16', False), ('v2E_16000', 'fp8', False),
+                                             ('v2E_16000', 'bf16', True), ('v1_2125', 'bf16', False),
+                                             ('v2C_bn_2125', 'fp8', True)])
+def test_batch_fused_levels_bit_exact(monkeypatch, knob, name, dtype, nlms):
+    """Batch path, bf16 storage, the fused conv levels against the row GEMMs
+    they replace (knob=0, read per call; knob=2 fails the call unless the
+    fused kernel ran):
+    * AEC_CRN_BATCH_ENC: encoder levels 0-3 in one persistent launch
+      (crn_enc_batch_kernel: X0 -> the four maps in LDS, four frames per
+      block, level 3's MX-fp8 shadow written in the kernel);
+    * AEC_CRN_BATCH_DEC: decoder levels cl = 3, 2 in one persistent launch
+      (crn_dec_batch_kernel: cat[3] -> cat[2]'s decoder half in LDS ->
+      cat[1]'s decoder half).
+    The same packed weights, 32-k bf16 MFMA chunks from zero and PReLU
+    epilogue, so out_wav and out_spec agree bit for bit.  Ragged lengths;
+    F = 23 rows x 36 frames is not a multiple of the block's four frames
+    (the tail iteration)."""
+    from aec_amd import synth
+    m = META[name]
+    conf = copy.deepcopy(aec_amd.net_conf)
+    conf.update(m['overrides'])
+    nl = dict(taps=4, mu=0.3, beta=0.5, delta=1e-4) if nlms else None
+    net = (aec_amd.dccrn if m['version'] == 1 else aec_amd.dccrn2).DCCRN(conf, dtype=dtype, nlms=nl).eval()
+    sd = net.state_dict()
+    for k, v in C.make_weights(conf, m['version'], m['weight_seed']).items():
+        sd[k] = torch.from_numpy(v)
+    net.load_state_dict(sd, strict=True)
+    net = net.to('cuda:0')
+    B, n = 23, 9000
+    lens = [n - 317 * b for b in range(B)]
+    M = torch.zeros(B, n, device='cuda:0')
+    F = torch.zeros_like(M)
+    for b in range(B):
+        s = synth.scene(lens[b], 3300 + b)
+        M[b, :lens[b]] = torch.from_numpy(s[0]).cuda()
+        F[b, :lens[b]] = torch.from_numpy(s[1]).cuda()
+    res = {}
+    for flag in ('0', '2'):
+        monkeypatch.setenv(knob, flag)
+        with torch.no_grad():
+            out, spec, _ = net.forward_ragged(M, F, lens, want_spec=True)
+        torch.cuda.synchronize()
+        res[flag] = (out.cpu().numpy(), spec.cpu().numpy())
+    assert np.isfinite(res['2'][0]).all() and np.abs(res['2'][0]).max() > 0
+    for b in range(B):
+        nb, tb = 256 * (lens[b] // 256), lens[b] // 256 + 1
+        assert np.array_equal(res['2'][0][b, :nb], res['0'][0][b, :nb]), b
+        assert np.array_equal(res['2'][1][b, :, :tb], res['0'][1][b, :, :tb]), b
