@@ -1463,8 +1463,8 @@ static bool stream_dec_ok(const aec_crn_handle* h) {
         const int cl = 3 - l, d = h->L - cl, Fin = 256 >> cl;
         const Packed& pk = h->decf[d];
         const int NT = (pk.N + 15) / 16;
-        if (!pk.w || pk.wq || (pk.K + 31) / 32 > caps[l] || pk.kpad < 32 * ((pk.K + 31) / 32) || (Fin / 16) * NT != 8 ||
-            4 % NT || Fin * 2 * ch[cl] > 4096 || ilog2(2 * ch[cl]) < 4)
+        if (!pk.w || pk.wq || (pk.K + 31) / 32 != caps[l] || pk.kpad < 32 * ((pk.K + 31) / 32) || (Fin / 16) * NT != 8 ||
+            4 % NT || Fin * 2 * ch[cl] > 4096 || ilog2(2 * ch[cl]) != 7 - l)
             return false;
         if (l < 2 && (pk.act != 1 || pk.N != 2 * ch[cl - 1] || pk.N % 32)) return false;
         if (l == 2 && (pk.N != 4 || pk.act == 1)) return false;
@@ -1480,20 +1480,22 @@ static int stream_enc_levels(const aec_crn_handle* h) {
     if (v && !(atoi(v) & 1)) return 0;
     const int* ch = h->cfg.conv_channels;
     int n = 0;
+    // levels 0-2 together, at net_conf's shapes (crn_stream_enc_kernel's compile-time chunk counts)
+    const int nc[3] = {2, 3, 5};
     for (int i = 0; i < std::min(3, h->L); ++i) {
         const Packed& pk = h->enc[i];
-        const int Fo = 128 >> i, cin = i == 0 ? 8 : ch[i];
-        if (pk.wq || pk.act != 1 || pk.N % 16 || (Fo / 16) * (pk.N / 16) != 8 || 4 % (pk.N / 16) ||
-            (pk.K + 31) / 32 > crn::kStreamEncChunks || ilog2(cin) < 3 || pk.kpad < 32 * ((pk.K + 31) / 32) ||
-            shadow_level(h, i + 1))
-            break;
+        const int cin = i == 0 ? 8 : ch[i];
+        if (pk.wq || pk.act != 1 || pk.N != (16 << i) || cin != (8 << i) || (pk.K + 31) / 32 != nc[i] ||
+            pk.kpad < 32 * nc[i] || shadow_level(h, i + 1))
+            return 0;
         ++n;
     }
+    if (n < 3) return 0;
     // level 3 (16 x 128 from the 32 x 64 map; its MX shadow written in the kernel): AEC_CRN_STREAM_FUSE bit 2
     if (n == 3 && h->L > 4 && (!v || (atoi(v) & 4))) {
         const Packed& pk = h->enc[3];
         const int nc = (pk.K + 31) / 32;
-        if (!pk.wq && pk.act == 1 && pk.N == 128 && ch[3] == 64 && ch[4] == 128 && nc <= crn::kStreamEncChunks3 &&
+        if (!pk.wq && pk.act == 1 && pk.N == 128 && ch[3] == 64 && ch[4] == 128 && nc == crn::kStreamEncChunks3 &&
             pk.kpad >= 32 * nc)
             ++n;
     }

@@ -66,6 +66,73 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }    // bf16 elements of one level's output map (Fo x N = 8 tiles of 16 x 16)
 
+// A 16-B piece of an implicit A row from an LDS map, zero when !ok.  The read always happens, at
+// row 0 when !ok (every map has one), and the zero is selected afterwards: a guarded read compiled
+// to a branch and an lgkmcnt(0) wait per MFMA, where branch-free reads of a chunk stay in flight
+// together.
+__device__ __forceinline__ u32x4 lds_frag(const bf16_t* map, int row, int rs, int q0, bool ok) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(map + (ok ? row : 0) * rs + q0);
+    return ok ? v : u32x4{0u, 0u, 0u, 0u};
+}
+
+// FR frames' two 16 x 16 output tiles (M tiles m0, m1) of one conv level over NC 32-k chunks:
+// implicit A rows from the LDS maps (input bin ST * j + OFF + tap of output row j, TAPS taps,
+// 2^CS channels per bin, RS elements per map row), B fragments in registers.  Compile-time chunk
+// count and shapes: the reads of a chunk for every frame go out together and the chunk loop
+// carries no branch (a runtime-bounded one compiled to a branch and an lgkmcnt(0) wait per chunk).
+// Per accumulator the chunks run in order from zero: the row GEMM's sum.
+template <int FR, int NC, int CS, int RS, int ST, int OFF, int TAPS, int FIN, int NCAP>
+__device__ __forceinline__ void conv_tiles(f32x4 (&acc)[FR][2], const bf16_t* const (&in)[FR], const u32x4 (&bw)[NCAP],
+                                           int m0, int m1, int lane) {
+#pragma unroll
+    for (int fr = 0; fr < FR; ++fr) acc[fr][0] = acc[fr][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    aec::static_for<0, NC>([&](auto ci) {
+        constexpr int c = decltype(ci)::value;
+        const int k0 = 32 * c + 8 * (lane >> 4);
+        const int tap = k0 >> CS, q0 = k0 & ((1 << CS) - 1);
+        u32x4 a[FR][2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int ib = ST * ((t ? m1 : m0) * 16 + (lane & 15)) + OFF + tap;
+            const bool ok = tap < TAPS && ib >= 0 && ib < FIN;
+#pragma unroll
+            for (int fr = 0; fr < FR; ++fr) a[fr][t] = lds_frag(in[fr], ib, RS, q0, ok);
+        }
+#pragma unroll
+        for (int fr = 0; fr < FR; ++fr)
+#pragma unroll
+            for (int t = 0; t < 2; ++t) mma_chunk(acc[fr][t], a[fr][t], bw[c], bf16_t{});
+    });
+}
+
+// conv_tiles' form for one M tile (m0) and two N tiles (weights bwa, bwb): one A piece per frame
+// and chunk feeds both (encoder level 3: 16 output bins)
+template <int FR, int NC, int CS, int RS, int ST, int OFF, int TAPS, int FIN, int NCAP>
+__device__ __forceinline__ void conv_tiles_n2(f32x4 (&acc)[FR][2], const bf16_t* const (&in)[FR],
+                                              const u32x4 (&bwa)[NCAP], const u32x4 (&bwb)[NCAP], int m0, int lane) {
+#pragma unroll
+    for (int fr = 0; fr < FR; ++fr) acc[fr][0] = acc[fr][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    aec::static_for<0, NC>([&](auto ci) {
+        constexpr int c = decltype(ci)::value;
+        const int k0 = 32 * c + 8 * (lane >> 4);
+        const int tap = k0 >> CS, q0 = k0 & ((1 << CS) - 1);
+        const int ib = ST * (m0 * 16 + (lane & 15)) + OFF + tap;
+        const bool ok = tap < TAPS && ib >= 0 && ib < FIN;
+        u32x4 a[FR];
+#pragma unroll
+        for (int fr = 0; fr < FR; ++fr) a[fr] = lds_frag(in[fr], ib, RS, q0, ok);
+#pragma unroll
+        for (int fr = 0; fr < FR; ++fr) {
+            mma_chunk(acc[fr][0], a[fr], bwa[c], bf16_t{});
+            mma_chunk(acc[fr][1], a[fr], bwb[c], bf16_t{});
+        }
+    });
+}
+
+// net_conf's encoder levels 0-3 (conv_channels 4, 16, 32, 64, 128: N = 16 << i, K = 5 taps x
+// 8 / 16 / 32 / 64 input channels): the shapes the batch kernels are compiled for
+constexpr int kEncNC[4] = {2, 3, 5, 10};
+
 // X0 bin k (1..256) as 8 bf16: (mic.re, far.re, mic.im, far.im, 0, 0, 0, 0) (dccrn.py:559-561)
 __device__ __forceinline__ void x0_put(bf16_t* x0, int k, float2 m, float2 f) {
     u32x4 v;
@@ -230,36 +297,15 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
     lds_barrier();
     SPROF(0, 3);
 
-    // 4. encoder levels: 8 output tiles of 16 bins x 16 channels per level, two per wave (N tile
-    //    nt = wave % NT, M tiles m0 = wave / NT and m0 + 4 / NT); the implicit A rows read the
-    //    input map in LDS (input bin 2 j - 2 + tap, zero outside [0, Fin))
-    const bf16_t* in = sX0;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        if (i >= p.nlev) break;
+    // 4. encoder levels 0-2 (net_conf's shapes, checked by launch_stream_enc): 8 output tiles of 16
+    //    bins x 16 channels per level, two per wave (N tile nt = wave % NT, M tiles m0 = wave / NT and
+    //    m0 + 4 / NT); the implicit A rows read the input map in LDS (input bin 2 j - 2 + tap, zero
+    //    outside [0, Fin))
+    f32x4 acc[1][2];
+    auto level_out = [&](auto Ic, int nt, int m0, int m1, bool keep) {
+        constexpr int i = decltype(Ic)::value, N = 16 << i, Fo = 128 >> i;
         const StreamEncLevel& L = p.lev[i];
-        const int Fin = 256 >> i, Fo = Fin >> 1;
-        const int NT = L.N >> 4;
-        const int nt = wave % NT, m0 = wave / NT, m1 = m0 + 4 / NT;
-        const int cs = L.cin_shift;
-        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-        for (int c = 0; c < kStreamEncChunks; ++c) {
-            if (c >= L.nchunk) continue;
-            const int k0 = 32 * c + 8 * (lane >> 4);
-            const int tap = k0 >> cs, q0 = k0 & ((1 << cs) - 1);
-            const int rs = i == 0 ? 8 : (1 << cs) + 8;             // row stride (X0: 16-B rows, unpadded)
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const int j = (t ? m1 : m0) * 16 + (lane & 15);
-                const int ib = 2 * j - 2 + tap;
-                u32x4 a = {0u, 0u, 0u, 0u};
-                if (tap < 5 && ib >= 0 && ib < Fin) a = *reinterpret_cast<const u32x4*>(in + ib * rs + q0);
-                mma_chunk(acc[t], a, bw[i][c], bf16_t{});
-            }
-        }
         bf16_t* map = sMap[i & 1];
-        const bool keep = i + 1 < p.nlev;
         bf16_t* out = L.out + (int64_t)b * Fo * L.ldo + L.choff;
         const int n = nt * 16 + (lane & 15);
 #pragma unroll
@@ -267,42 +313,44 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = (t ? m1 : m0) * 16 + 4 * (lane >> 4) + r;
-                float v = acc[t][r] + bias[i];
+                float v = acc[0][t][r] + bias[i];
                 v = v >= 0.f ? v : L.alpha * v;
                 const bf16_t o = f2bf(v);
-                if (keep) map[row * (L.N + 8) + n] = o;
+                if (keep) map[row * (N + 8) + n] = o;
                 out[(int64_t)row * L.ldo + n] = o;
             }
         lds_barrier();
         SPROF(0, 4 + i);
-        in = map;
+    };
+    {
+        const bf16_t* in[1] = {sX0};
+        conv_tiles<1, kEncNC[0], 3, 8, 2, -2, 5, 256>(acc, in, bw[0], wave, wave + 4, lane);
+        level_out(std::integral_constant<int, 0>{}, 0, wave, wave + 4, true);
+    }
+    {
+        const bf16_t* in[1] = {sMap[0]};
+        conv_tiles<1, kEncNC[1], 4, 16 + 8, 2, -2, 5, 128>(acc, in, bw[1], wave / 2, wave / 2 + 2, lane);
+        level_out(std::integral_constant<int, 1>{}, wave % 2, wave / 2, wave / 2 + 2, true);
+    }
+    {
+        const bf16_t* in[1] = {sMap[1]};
+        conv_tiles<1, kEncNC[2], 5, 32 + 8, 2, -2, 5, 64>(acc, in, bw[2], 0, 1, lane);
+        level_out(std::integral_constant<int, 2>{}, wave, 0, 1, p.nlev > 3);
     }
     // 5. level 3: one M tile (the 16 output bins) x N tiles wave, wave + 4; the outputs staged in
     //    LDS, then stored as 16-B row chunks with their MX-fp8 shadow (the row GEMM epilogue's
     //    mx8_chunk: a 32-column group's 4 chunks in 4 adjacent lanes)
     if (p.nlev > 3) {
         const StreamEncLevel& L = p.lev[3];
-        const int cs = L.cin_shift;
-        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-        aec::static_for<0, kStreamEncChunks3>([&](auto ci) {
-            constexpr int c = decltype(ci)::value;
-            if (c < L.nchunk) {
-                const int k0 = 32 * c + 8 * (lane >> 4);
-                const int tap = k0 >> cs, q0 = k0 & ((1 << cs) - 1);
-                const int ib = 2 * (lane & 15) - 2 + tap;
-                u32x4 a = {0u, 0u, 0u, 0u};
-                if (tap < 5 && ib >= 0 && ib < 32) a = *reinterpret_cast<const u32x4*>(in + ib * ((1 << cs) + 8) + q0);
-                mma_chunk(acc[0], a, bw3[0][c], bf16_t{});
-                mma_chunk(acc[1], a, bw3[1][c], bf16_t{});
-            }
-        });
+        const bf16_t* in[1] = {sMap[0]};
+        conv_tiles_n2<1, kEncNC[3], 6, 64 + 8, 2, -2, 5, 32>(acc, in, bw3[0], bw3[1], 0, lane);
         bf16_t* stage = sMap[1];                      // level 1's map, consumed by level 2
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = 4 * (lane >> 4) + r, n = (wave + 4 * t) * 16 + (lane & 15);
-                float v = acc[t][r] + bias3[t];
+                float v = acc[0][t][r] + bias3[t];
                 v = v >= 0.f ? v : L.alpha * v;
                 stage[row * 128 + n] = f2bf(v);
             }
@@ -318,10 +366,10 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
 
 hipError_t launch_stream_enc(const StreamEncArgs& a, int taps, hipStream_t st) {
     if (a.B <= 0) return hipSuccess;
-    if (a.nlev < 1 || a.nlev > 4) return hipErrorInvalidValue;
+    if (a.nlev < 3 || a.nlev > 4) return hipErrorInvalidValue;
     if (a.nlev > 3) {
         const StreamEncLevel& L = a.lev[3];
-        if (L.N != 128 || L.cin_shift != 6 || a.lev[2].N != 64 || L.nchunk < 1 || L.nchunk > kStreamEncChunks3 ||
+        if (L.N != 128 || L.cin_shift != 6 || a.lev[2].N != 64 || L.nchunk != kEncNC[3] ||
             L.kpad < 32 * L.nchunk || L.kpad % 8 || L.ldo % 8 || L.choff % 8 || !L.w || !L.bias || !L.out ||
             (L.q8 && (L.ldo % 32 || L.choff % 32 || !L.qs)))
             return hipErrorInvalidValue;
@@ -329,9 +377,8 @@ hipError_t launch_stream_enc(const StreamEncArgs& a, int taps, hipStream_t st) {
     for (int i = 0; i < std::min(a.nlev, 3); ++i) {
         const StreamEncLevel& L = a.lev[i];
         const int Fo = 128 >> i;
-        if (L.N % 16 || (Fo / 16) * (L.N / 16) != 8 || 4 % (L.N / 16) || L.nchunk < 1 ||
-            L.nchunk > kStreamEncChunks || L.cin_shift < 3 || (i > 0 && (1 << L.cin_shift) != a.lev[i - 1].N) ||
-            (i == 0 && L.cin_shift != 3) || L.kpad < 32 * L.nchunk || L.kpad % 8 || !L.w || !L.bias || !L.out)
+        if (L.N != (16 << i) || (Fo / 16) * (L.N / 16) != 8 || L.nchunk != kEncNC[i] || L.cin_shift != 3 + i ||
+            L.kpad < 32 * L.nchunk || L.kpad % 8 || !L.w || !L.bias || !L.out)
             return hipErrorInvalidValue;
     }
     switch (taps) {
@@ -363,34 +410,28 @@ __global__ __launch_bounds__(256, 1) void crn_enc_batch_kernel(EncBatchArgs p) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     // weight fragments (crn_stream_enc_kernel's map): levels 0-2, this wave's N tile wave % NT;
     // level 3, N tiles wave and wave + 4
-    u32x4 bw[3][kStreamEncChunks];
+    u32x4 bw0[kEncNC[0]], bw1[kEncNC[1]], bw2[kEncNC[2]], bw3a[kEncNC[3]], bw3b[kEncNC[3]];
     float bias[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const StreamEncLevel& L = p.lev[i];
-        const int NT = L.N >> 4;
-        const int n = (wave % NT) * 16 + (lane & 15);
-        bias[i] = L.bias[n];
+    auto load_w = [&](auto& bw, const StreamEncLevel& L, int n) {
         const bf16_t* wr = L.w + (int64_t)n * L.kpad + 8 * (lane >> 4);
-#pragma unroll
-        for (int c = 0; c < kStreamEncChunks; ++c)
-            bw[i][c] = c < L.nchunk ? *reinterpret_cast<const u32x4*>(wr + 32 * c) : u32x4{0u, 0u, 0u, 0u};
-    }
-    u32x4 bw3[2][kStreamEncChunks3];
-    float bias3[2];
+        aec::static_for<0, (int)(sizeof(bw) / sizeof(bw[0]))>([&](auto ci) {
+            constexpr int c = decltype(ci)::value;
+            bw[c] = *reinterpret_cast<const u32x4*>(wr + 32 * c);
+        });
+    };
     {
-        const StreamEncLevel& L = p.lev[3];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int n = (wave + 4 * t) * 16 + (lane & 15);
-            bias3[t] = L.bias[n];
-            const bf16_t* wr = L.w + (int64_t)n * L.kpad + 8 * (lane >> 4);
-            aec::static_for<0, kStreamEncChunks3>([&](auto ci) {
-                constexpr int c = decltype(ci)::value;
-                bw3[t][c] = c < L.nchunk ? *reinterpret_cast<const u32x4*>(wr + 32 * c) : u32x4{0u, 0u, 0u, 0u};
-            });
-        }
+        const int n0 = (wave % 1) * 16 + (lane & 15), n1 = (wave % 2) * 16 + (lane & 15), n2 = (wave % 4) * 16 + (lane & 15);
+        load_w(bw0, p.lev[0], n0);
+        load_w(bw1, p.lev[1], n1);
+        load_w(bw2, p.lev[2], n2);
+        bias[0] = p.lev[0].bias[n0];
+        bias[1] = p.lev[1].bias[n1];
+        bias[2] = p.lev[2].bias[n2];
     }
+    const int n3a = wave * 16 + (lane & 15), n3b = (wave + 4) * 16 + (lane & 15);
+    load_w(bw3a, p.lev[3], n3a);
+    load_w(bw3b, p.lev[3], n3b);
+    const float bias3[2] = {p.lev[3].bias[n3a], p.lev[3].bias[n3b]};
     const int64_t F = p.F, step = (int64_t)gridDim.x * FR;
     // X0 of frames fb .. fb + FR - 1: 4 KB each = one 16-B piece per thread
     u32x4 nx[FR];
@@ -401,89 +442,69 @@ __global__ __launch_bounds__(256, 1) void crn_enc_batch_kernel(EncBatchArgs p) {
             nx[fr] = f < F ? reinterpret_cast<const u32x4*>(p.x0 + f * 2048)[tid] : u32x4{0u, 0u, 0u, 0u};
         }
     };
+    // level i's epilogue: PReLU, bf16 into the padded map, then the map -> cat[i + 1]'s encoder half
+    // (map row `row` = N contiguous channels)
+    auto level_out = [&](auto Ic, const f32x4 (&acc)[FR][2], int nt, int m0, int m1, int64_t f0) {
+        constexpr int i = decltype(Ic)::value, N = 16 << i;
+        const StreamEncLevel& L = p.lev[i];
+        const int n = nt * 16 + (lane & 15);
+#pragma unroll
+        for (int fr = 0; fr < FR; ++fr)
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = (t ? m1 : m0) * 16 + 4 * (lane >> 4) + r;
+                    float v = acc[fr][t][r] + bias[i];
+                    v = v >= 0.f ? v : L.alpha * v;
+                    sMap[i & 1][fr][row * (N + 8) + n] = f2bf(v);
+                }
+        lds_barrier();
+        constexpr int Fo = 128 >> i;
+        const int e0 = 8 * tid, row = e0 / N, ch0 = e0 % N;
+#pragma unroll
+        for (int fr = 0; fr < FR; ++fr) {
+            const int64_t f = f0 + fr;
+            if (f < F)
+                *reinterpret_cast<u32x4*>(L.out + (f * Fo + row) * L.ldo + L.choff + ch0) =
+                    *reinterpret_cast<const u32x4*>(sMap[i & 1][fr] + row * (N + 8) + ch0);
+        }
+    };
     fetch((int64_t)blockIdx.x * FR);
     for (int64_t f0 = (int64_t)blockIdx.x * FR; f0 < F; f0 += step) {
 #pragma unroll
         for (int fr = 0; fr < FR; ++fr) reinterpret_cast<u32x4*>(sX0[fr])[tid] = nx[fr];
         lds_barrier();
         fetch(f0 + step);
-        // levels 0-2: 8 output tiles of 16 bins x 16 channels per frame, two per wave
+        f32x4 acc[FR][2];
+        {   // level 0: 128 output bins x 16 channels (8 M tiles, 1 N tile) from X0 (16-B rows)
+            const bf16_t* in[FR];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const StreamEncLevel& L = p.lev[i];
-            const int Fin = 256 >> i, Fo = Fin >> 1;
-            const int NT = L.N >> 4;
-            const int nt = wave % NT, m0 = wave / NT, m1 = m0 + 4 / NT;
-            const int cs = L.cin_shift;
-            f32x4 acc[FR][2];
+            for (int fr = 0; fr < FR; ++fr) in[fr] = sX0[fr];
+            conv_tiles<FR, kEncNC[0], 3, 8, 2, -2, 5, 256>(acc, in, bw0, wave, wave + 4, lane);
+            level_out(std::integral_constant<int, 0>{}, acc, 0, wave, wave + 4, f0);
+        }
+        {   // level 1: 64 x 32 (4 M tiles x 2 N tiles)
+            const bf16_t* in[FR];
 #pragma unroll
-            for (int fr = 0; fr < FR; ++fr) acc[fr][0] = acc[fr][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int fr = 0; fr < FR; ++fr) in[fr] = sMap[0][fr];
+            conv_tiles<FR, kEncNC[1], 4, 16 + 8, 2, -2, 5, 128>(acc, in, bw1, wave / 2, wave / 2 + 2, lane);
+            level_out(std::integral_constant<int, 1>{}, acc, wave % 2, wave / 2, wave / 2 + 2, f0);
+        }
+        {   // level 2: 32 x 64 (2 M tiles x 4 N tiles)
+            const bf16_t* in[FR];
 #pragma unroll
-            for (int c = 0; c < kStreamEncChunks; ++c) {
-                if (c >= L.nchunk) continue;
-                const int k0 = 32 * c + 8 * (lane >> 4);
-                const int tap = k0 >> cs, q0 = k0 & ((1 << cs) - 1);
-#pragma unroll
-                for (int t = 0; t < 2; ++t) {
-                    const int j = (t ? m1 : m0) * 16 + (lane & 15);
-                    const int ib = 2 * j - 2 + tap;
-                    const bool ok = tap < 5 && ib >= 0 && ib < Fin;
-#pragma unroll
-                    for (int fr = 0; fr < FR; ++fr) {
-                        const bf16_t* in = i == 0 ? sX0[fr] : sMap[(i - 1) & 1][fr];
-                        const int rs = i == 0 ? 8 : (1 << cs) + 8;       // row stride (elements)
-                        u32x4 a = {0u, 0u, 0u, 0u};
-                        if (ok) a = *reinterpret_cast<const u32x4*>(in + ib * rs + q0);
-                        mma_chunk(acc[fr][t], a, bw[i][c], bf16_t{});
-                    }
-                }
-            }
-            const int n = nt * 16 + (lane & 15);
-#pragma unroll
-            for (int fr = 0; fr < FR; ++fr)
-#pragma unroll
-                for (int t = 0; t < 2; ++t)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int row = (t ? m1 : m0) * 16 + 4 * (lane >> 4) + r;
-                        float v = acc[fr][t][r] + bias[i];
-                        v = v >= 0.f ? v : L.alpha * v;
-                        sMap[i & 1][fr][row * (L.N + 8) + n] = f2bf(v);
-                    }
-            lds_barrier();
-            // the map -> the encoder half of cat[i + 1]: map row `row` (N channels) is contiguous
-            const int e0 = 8 * tid, row = e0 / L.N, ch0 = e0 % L.N;
-#pragma unroll
-            for (int fr = 0; fr < FR; ++fr) {
-                const int64_t f = f0 + fr;
-                if (f < F)
-                    *reinterpret_cast<u32x4*>(L.out + (f * Fo + row) * L.ldo + L.choff + ch0) =
-                        *reinterpret_cast<const u32x4*>(sMap[i & 1][fr] + row * (L.N + 8) + ch0);
-            }
+            for (int fr = 0; fr < FR; ++fr) in[fr] = sMap[1][fr];
+            conv_tiles<FR, kEncNC[2], 5, 32 + 8, 2, -2, 5, 64>(acc, in, bw2, 0, 1, lane);
+            level_out(std::integral_constant<int, 2>{}, acc, wave, 0, 1, f0);
         }
         // level 3: the 16 output bins x N tiles wave, wave + 4, staged in level 1's map
         {
             const StreamEncLevel& L = p.lev[3];
-            const int cs = L.cin_shift;
-            f32x4 acc[FR][2];
+            const bf16_t* in[FR];
 #pragma unroll
-            for (int fr = 0; fr < FR; ++fr) acc[fr][0] = acc[fr][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-            aec::static_for<0, kStreamEncChunks3>([&](auto ci) {
-                constexpr int c = decltype(ci)::value;
-                if (c < L.nchunk) {
-                    const int k0 = 32 * c + 8 * (lane >> 4);
-                    const int tap = k0 >> cs, q0 = k0 & ((1 << cs) - 1);
-                    const int ib = 2 * (lane & 15) - 2 + tap;
-                    const bool ok = tap < 5 && ib >= 0 && ib < 32;
-#pragma unroll
-                    for (int fr = 0; fr < FR; ++fr) {
-                        u32x4 a = {0u, 0u, 0u, 0u};
-                        if (ok) a = *reinterpret_cast<const u32x4*>(sMap[0][fr] + ib * ((1 << cs) + 8) + q0);
-                        mma_chunk(acc[fr][0], a, bw3[0][c], bf16_t{});
-                        mma_chunk(acc[fr][1], a, bw3[1][c], bf16_t{});
-                    }
-                }
-            });
+            for (int fr = 0; fr < FR; ++fr) in[fr] = sMap[0][fr];
+            conv_tiles_n2<FR, kEncNC[3], 6, 64 + 8, 2, -2, 5, 32>(acc, in, bw3a, bw3b, 0, lane);
 #pragma unroll
             for (int fr = 0; fr < FR; ++fr)
 #pragma unroll
@@ -515,8 +536,8 @@ bool enc_batch_ok(const EncBatchArgs& a) {
     if (a.F <= 0 || !a.x0) return false;
     for (int i = 0; i < 4; ++i) {
         const StreamEncLevel& L = a.lev[i];
-        if (!L.w || !L.bias || !L.out || L.kpad % 8 || L.ldo % 8 || L.choff % 8 || L.nchunk < 1 ||
-            L.kpad < 32 * L.nchunk)
+        if (!L.w || !L.bias || !L.out || L.kpad % 8 || L.ldo % 8 || L.choff % 8 || L.nchunk != kEncNC[i] ||
+            L.kpad < 32 * L.nchunk || L.N != (16 << i) || L.cin_shift != 3 + i)
             return false;
         if (i < 3) {
             const int Fo = 128 >> i;
@@ -563,32 +584,9 @@ hipError_t launch_enc_batch(const EncBatchArgs& a, hipStream_t st) {
 // --------------------------------------------------------------------------
 namespace {
 
-// one decoder level: 8 output tiles of 16 input bins x 16 columns, two per wave (N tile nt =
-// wave % NT, M tiles m0 = wave / NT, m0 + 4 / NT); A rows: input bins i - 1 + j (j = k / Cin),
-// zero outside [0, Fin); the 32-k chunks accumulated in order from zero
-template <int NC>
-__device__ __forceinline__ void dec_tiles(f32x4 (&acc)[2], const bf16_t* in, int Fin, int cs, int nchunk,
-                                          const u32x4 (&bw)[NC], int m0, int m1, int lane) {
-    acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // compile-time chunk indices (a runtime-bounded loop would leave bw[] in scratch)
-    aec::static_for<0, NC>([&](auto ci) {
-        constexpr int c = decltype(ci)::value;
-        if (c < nchunk) {
-            const int k0 = 32 * c + 8 * (lane >> 4);
-            const int j = k0 >> cs, q0 = k0 & ((1 << cs) - 1);
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const int i = (t ? m1 : m0) * 16 + (lane & 15);
-                const int ib = i - 1 + j;
-                u32x4 a = {0u, 0u, 0u, 0u};
-                if (j < 3 && ib >= 0 && ib < Fin) a = *reinterpret_cast<const u32x4*>(in + ib * ((1 << cs) + 8) + q0);
-                mma_chunk(acc[t], a, bw[c], bf16_t{});
-            }
-        }
-    });
-}
-
+// A decoder level (conv_tiles with ST = 1, OFF = -1, 3 taps): 8 output tiles of 16 input bins x 16
+// columns, two per wave (N tile nt = wave % NT, M tiles m0 = wave / NT, m0 + 4 / NT); A rows:
+// input bins i - 1 + j (j = k / Cin), zero outside [0, Fin).  load_bw: a wave's B fragments.
 template <int NC>
 __device__ __forceinline__ void load_bw(u32x4 (&bw)[NC], const StreamDecLevel& L, int n) {
     const bf16_t* wr = L.w + (int64_t)n * L.kpad + 8 * ((threadIdx.x & 63) >> 4);
@@ -686,10 +684,12 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
 #pragma unroll
     for (int l = 0; l < 2; ++l) {
         const StreamDecLevel& L = p.lev[l];
-        const int Fin = 32 << l, Co = L.N >> 1, Cn = 1 << p.lev[l + 1].cin_shift;
-        f32x4 acc[2];
-        if (l == 0) dec_tiles(acc, sIn[0], Fin, L.cin_shift, L.nchunk, bw0, m0[0], m1[0], lane);
-        else dec_tiles(acc, sIn[1], Fin, L.cin_shift, L.nchunk, bw1, m0[1], m1[1], lane);
+        const int Co = L.N >> 1, Cn = 1 << p.lev[l + 1].cin_shift;
+        f32x4 acc2[1][2];
+        const bf16_t* in[1] = {sIn[l]};
+        if (l == 0) conv_tiles<1, kStreamDecChunks0, 7, 128 + 8, 1, -1, 3, 32>(acc2, in, bw0, m0[0], m1[0], lane);
+        else conv_tiles<1, kStreamDecChunks1, 6, 64 + 8, 1, -1, 3, 64>(acc2, in, bw1, m0[1], m1[1], lane);
+        const f32x4 (&acc)[2] = acc2[0];
         const int n = nt[l] * 16 + (lane & 15), par = n >= Co, ch = n - par * Co;
         bf16_t* next = sIn[l + 1];
 #pragma unroll
@@ -707,8 +707,10 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
     // 3. the mask level (cl = 1): columns (parity, re / im), f32, act none (v2) / tanh (v1)
     {
         const StreamDecLevel& L = p.lev[2];
-        f32x4 acc[2];
-        dec_tiles(acc, sIn[2], 128, L.cin_shift, L.nchunk, bw2, m0[2], m1[2], lane);
+        f32x4 acc2[1][2];
+        const bf16_t* in[1] = {sIn[2]};
+        conv_tiles<1, kStreamDecChunks2, 5, 32 + 8, 1, -1, 3, 128>(acc2, in, bw2, m0[2], m1[2], lane);
+        const f32x4 (&acc)[2] = acc2[0];
         const int n = lane & 15;
         if (n < 4) {
 #pragma unroll
@@ -810,7 +812,7 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
 
 // --------------------------------------------------------------------------
 // Batch decoder levels cl = 3, 2 (the batch forward of C3 / C4): FR frames per block in a
-// persistent frame loop, the per-hop back's level arithmetic (dec_tiles, both parities per
+// persistent frame loop, the per-hop back's level arithmetic (conv_tiles, both parities per
 // GEMM, the PReLU epilogue) with the maps in padded LDS rows; cat[2]'s decoder half never
 // leaves LDS, cat[1]'s leaves as 16-B rows for crn_back_kernel's mask level.  The inputs of
 // the next FR frames (cat[3] whole, cat[2]'s encoder half) are fetched into registers while
@@ -862,8 +864,10 @@ __global__ __launch_bounds__(256, 1) void crn_dec_batch_kernel(DecBatchArgs p) {
         // level cl = 3: M = 32 input bins (tiles 0, 1), N = 64 (parity x 32 channels) -> sB's decoder half
         {
             f32x4 acc[FR][2];
+            const bf16_t* in[FR];
 #pragma unroll
-            for (int fr = 0; fr < FR; ++fr) dec_tiles(acc[fr], sA[fr], 32, 7, LA.nchunk, bw0, 0, 1, lane);
+            for (int fr = 0; fr < FR; ++fr) in[fr] = sA[fr];
+            conv_tiles<FR, kStreamDecChunks0, 7, 136, 1, -1, 3, 32>(acc, in, bw0, 0, 1, lane);
             const int par = n0 >= 32, ch = n0 - 32 * par;
 #pragma unroll
             for (int fr = 0; fr < FR; ++fr)
@@ -881,8 +885,10 @@ __global__ __launch_bounds__(256, 1) void crn_dec_batch_kernel(DecBatchArgs p) {
         // level cl = 2: M = 64 input bins (tiles mb0, mb0 + 2), N = 32 (parity x 16 channels) -> sO
         {
             f32x4 acc[FR][2];
+            const bf16_t* in[FR];
 #pragma unroll
-            for (int fr = 0; fr < FR; ++fr) dec_tiles(acc[fr], sB[fr], 64, 6, LB.nchunk, bw1, mb0, mb0 + 2, lane);
+            for (int fr = 0; fr < FR; ++fr) in[fr] = sB[fr];
+            conv_tiles<FR, kStreamDecChunks1, 6, 72, 1, -1, 3, 64>(acc, in, bw1, mb0, mb0 + 2, lane);
             const int par = n1 >= 16, ch = n1 - 16 * par;
 #pragma unroll
             for (int fr = 0; fr < FR; ++fr)
@@ -914,7 +920,7 @@ bool dec_batch_ok(const DecBatchArgs& a) {
     const int cs[2] = {7, 6}, N[2] = {64, 32};
     for (int l = 0; l < 2; ++l) {
         const StreamDecLevel& L = a.lev[l];
-        if (!L.w || !L.bias || !L.src || L.nchunk < 1 || L.nchunk > caps[l] || L.kpad < 32 * L.nchunk || L.kpad % 8 ||
+        if (!L.w || !L.bias || !L.src || L.nchunk != caps[l] || L.kpad < 32 * L.nchunk || L.kpad % 8 ||
             L.act != 1 || L.cin_shift != cs[l] || L.N != N[l])
             return false;
     }
@@ -944,8 +950,8 @@ hipError_t launch_stream_dec(const StreamDecArgs& a, int mode, hipStream_t st) {
     for (int l = 0; l < 3; ++l) {
         const StreamDecLevel& L = a.lev[l];
         const int Fin = 32 << l, NT = (L.N + 15) / 16;
-        if (!L.w || !L.bias || !L.src || L.nchunk < 1 || L.nchunk > caps[l] || L.kpad < 32 * L.nchunk ||
-            (Fin / 16) * NT != 8 || 4 % NT || (Fin << L.cin_shift) > 4096 || L.cin_shift < 4 ||
+        if (!L.w || !L.bias || !L.src || L.nchunk != caps[l] || L.kpad < 32 * L.nchunk || L.cin_shift != 7 - l ||
+            (Fin / 16) * NT != 8 || 4 % NT || (Fin << L.cin_shift) > 4096 ||
             (l < 2 && (L.N % 32 || L.act != 1 || L.N != (1 << a.lev[l + 1].cin_shift))) ||   // Co = next map's half
             (l == 2 && (L.N != 4 || L.act == 1)))
             return hipErrorInvalidValue;
