@@ -81,7 +81,10 @@ __device__ __forceinline__ u32x4 lds_frag(const bf16_t* map, int row, int rs, in
 // count and shapes: the reads of a chunk for every frame go out together and the chunk loop
 // carries no branch (a runtime-bounded one compiled to a branch and an lgkmcnt(0) wait per chunk).
 // Per accumulator the chunks run in order from zero: the row GEMM's sum.
-template <int FR, int NC, int CS, int RS, int ST, int OFF, int TAPS, int FIN, int NCAP>
+// TR: transposed accumulators (the operands swapped: a lane holds 4 adjacent columns 4 (lane >> 4)
+// .. + 3 of row lane & 15, so the epilogue writes 8 B at a time); the same products summed the same
+// way per element.
+template <int FR, int NC, int CS, int RS, int ST, int OFF, int TAPS, int FIN, int NCAP, bool TR = false>
 __device__ __forceinline__ void conv_tiles(f32x4 (&acc)[FR][2], const bf16_t* const (&in)[FR], const u32x4 (&bw)[NCAP],
                                            int m0, int m1, int lane) {
 #pragma unroll
@@ -101,13 +104,16 @@ __device__ __forceinline__ void conv_tiles(f32x4 (&acc)[FR][2], const bf16_t* co
 #pragma unroll
         for (int fr = 0; fr < FR; ++fr)
 #pragma unroll
-            for (int t = 0; t < 2; ++t) mma_chunk(acc[fr][t], a[fr][t], bw[c], bf16_t{});
+            for (int t = 0; t < 2; ++t) {
+                if constexpr (TR) mma_chunk(acc[fr][t], bw[c], a[fr][t], bf16_t{});
+                else mma_chunk(acc[fr][t], a[fr][t], bw[c], bf16_t{});
+            }
     });
 }
 
 // conv_tiles' form for one M tile (m0) and two N tiles (weights bwa, bwb): one A piece per frame
 // and chunk feeds both (encoder level 3: 16 output bins)
-template <int FR, int NC, int CS, int RS, int ST, int OFF, int TAPS, int FIN, int NCAP>
+template <int FR, int NC, int CS, int RS, int ST, int OFF, int TAPS, int FIN, int NCAP, bool TR = false>
 __device__ __forceinline__ void conv_tiles_n2(f32x4 (&acc)[FR][2], const bf16_t* const (&in)[FR],
                                               const u32x4 (&bwa)[NCAP], const u32x4 (&bwb)[NCAP], int m0, int lane) {
 #pragma unroll
@@ -123,10 +129,28 @@ __device__ __forceinline__ void conv_tiles_n2(f32x4 (&acc)[FR][2], const bf16_t*
         for (int fr = 0; fr < FR; ++fr) a[fr] = lds_frag(in[fr], ib, RS, q0, ok);
 #pragma unroll
         for (int fr = 0; fr < FR; ++fr) {
-            mma_chunk(acc[fr][0], a[fr], bwa[c], bf16_t{});
-            mma_chunk(acc[fr][1], a[fr], bwb[c], bf16_t{});
+            if constexpr (TR) {
+                mma_chunk(acc[fr][0], bwa[c], a[fr], bf16_t{});
+                mma_chunk(acc[fr][1], bwb[c], a[fr], bf16_t{});
+            } else {
+                mma_chunk(acc[fr][0], a[fr], bwa[c], bf16_t{});
+                mma_chunk(acc[fr][1], a[fr], bwb[c], bf16_t{});
+            }
         }
     });
+}
+
+// the PReLU epilogue of 4 adjacent columns (v + bias, then v >= 0 ? v : alpha v) as 4 bf16 in 8 B
+__device__ __forceinline__ uint2 prelu4_bf16(const f32x4& v, const float4& bias, float alpha) {
+    const float b[4] = {bias.x, bias.y, bias.z, bias.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        float x = v[r] + b[r];
+        x = x >= 0.f ? x : alpha * x;
+        o[r] = f2bf(x);
+    }
+    return make_uint2(o[0] | (o[1] << 16), o[2] | (o[3] << 16));
 }
 
 // net_conf's encoder levels 0-3 (conv_channels 4, 16, 32, 64, 128: N = 16 << i, K = 5 taps x
@@ -411,7 +435,7 @@ __global__ __launch_bounds__(256, 1) void crn_enc_batch_kernel(EncBatchArgs p) {
     // weight fragments (crn_stream_enc_kernel's map): levels 0-2, this wave's N tile wave % NT;
     // level 3, N tiles wave and wave + 4
     u32x4 bw0[kEncNC[0]], bw1[kEncNC[1]], bw2[kEncNC[2]], bw3a[kEncNC[3]], bw3b[kEncNC[3]];
-    float bias[3];
+    float4 bias[3];
     auto load_w = [&](auto& bw, const StreamEncLevel& L, int n) {
         const bf16_t* wr = L.w + (int64_t)n * L.kpad + 8 * (lane >> 4);
         aec::static_for<0, (int)(sizeof(bw) / sizeof(bw[0]))>([&](auto ci) {
@@ -424,14 +448,17 @@ __global__ __launch_bounds__(256, 1) void crn_enc_batch_kernel(EncBatchArgs p) {
         load_w(bw0, p.lev[0], n0);
         load_w(bw1, p.lev[1], n1);
         load_w(bw2, p.lev[2], n2);
-        bias[0] = p.lev[0].bias[n0];
-        bias[1] = p.lev[1].bias[n1];
-        bias[2] = p.lev[2].bias[n2];
+        // TR epilogue: the lane's 4 columns nt * 16 + 4 (lane >> 4) .. + 3
+        const int g4 = 4 * (lane >> 4);
+        bias[0] = *reinterpret_cast<const float4*>(p.lev[0].bias + g4);
+        bias[1] = *reinterpret_cast<const float4*>(p.lev[1].bias + (wave % 2) * 16 + g4);
+        bias[2] = *reinterpret_cast<const float4*>(p.lev[2].bias + (wave % 4) * 16 + g4);
     }
     const int n3a = wave * 16 + (lane & 15), n3b = (wave + 4) * 16 + (lane & 15);
     load_w(bw3a, p.lev[3], n3a);
     load_w(bw3b, p.lev[3], n3b);
-    const float bias3[2] = {p.lev[3].bias[n3a], p.lev[3].bias[n3b]};
+    const float4 bias3[2] = {*reinterpret_cast<const float4*>(p.lev[3].bias + wave * 16 + 4 * (lane >> 4)),
+                             *reinterpret_cast<const float4*>(p.lev[3].bias + (wave + 4) * 16 + 4 * (lane >> 4))};
     const int64_t F = p.F, step = (int64_t)gridDim.x * FR;
     // X0 of frames fb .. fb + FR - 1: 4 KB each = one 16-B piece per thread
     u32x4 nx[FR];
@@ -447,18 +474,14 @@ __global__ __launch_bounds__(256, 1) void crn_enc_batch_kernel(EncBatchArgs p) {
     auto level_out = [&](auto Ic, const f32x4 (&acc)[FR][2], int nt, int m0, int m1, int64_t f0) {
         constexpr int i = decltype(Ic)::value, N = 16 << i;
         const StreamEncLevel& L = p.lev[i];
-        const int n = nt * 16 + (lane & 15);
+        const int n0 = nt * 16 + 4 * (lane >> 4);
 #pragma unroll
         for (int fr = 0; fr < FR; ++fr)
 #pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = (t ? m1 : m0) * 16 + 4 * (lane >> 4) + r;
-                    float v = acc[fr][t][r] + bias[i];
-                    v = v >= 0.f ? v : L.alpha * v;
-                    sMap[i & 1][fr][row * (N + 8) + n] = f2bf(v);
-                }
+            for (int t = 0; t < 2; ++t) {
+                const int row = (t ? m1 : m0) * 16 + (lane & 15);
+                *reinterpret_cast<uint2*>(sMap[i & 1][fr] + row * (N + 8) + n0) = prelu4_bf16(acc[fr][t], bias[i], L.alpha);
+            }
         lds_barrier();
         constexpr int Fo = 128 >> i;
         const int e0 = 8 * tid, row = e0 / N, ch0 = e0 % N;
@@ -481,21 +504,21 @@ __global__ __launch_bounds__(256, 1) void crn_enc_batch_kernel(EncBatchArgs p) {
             const bf16_t* in[FR];
 #pragma unroll
             for (int fr = 0; fr < FR; ++fr) in[fr] = sX0[fr];
-            conv_tiles<FR, kEncNC[0], 3, 8, 2, -2, 5, 256>(acc, in, bw0, wave, wave + 4, lane);
+            conv_tiles<FR, kEncNC[0], 3, 8, 2, -2, 5, 256, kEncNC[0], true>(acc, in, bw0, wave, wave + 4, lane);
             level_out(std::integral_constant<int, 0>{}, acc, 0, wave, wave + 4, f0);
         }
         {   // level 1: 64 x 32 (4 M tiles x 2 N tiles)
             const bf16_t* in[FR];
 #pragma unroll
             for (int fr = 0; fr < FR; ++fr) in[fr] = sMap[0][fr];
-            conv_tiles<FR, kEncNC[1], 4, 16 + 8, 2, -2, 5, 128>(acc, in, bw1, wave / 2, wave / 2 + 2, lane);
+            conv_tiles<FR, kEncNC[1], 4, 16 + 8, 2, -2, 5, 128, kEncNC[1], true>(acc, in, bw1, wave / 2, wave / 2 + 2, lane);
             level_out(std::integral_constant<int, 1>{}, acc, wave % 2, wave / 2, wave / 2 + 2, f0);
         }
         {   // level 2: 32 x 64 (2 M tiles x 4 N tiles)
             const bf16_t* in[FR];
 #pragma unroll
             for (int fr = 0; fr < FR; ++fr) in[fr] = sMap[1][fr];
-            conv_tiles<FR, kEncNC[2], 5, 32 + 8, 2, -2, 5, 64>(acc, in, bw2, 0, 1, lane);
+            conv_tiles<FR, kEncNC[2], 5, 32 + 8, 2, -2, 5, 64, kEncNC[2], true>(acc, in, bw2, 0, 1, lane);
             level_out(std::integral_constant<int, 2>{}, acc, wave, 0, 1, f0);
         }
         // level 3: the 16 output bins x N tiles wave, wave + 4, staged in level 1's map
@@ -504,18 +527,14 @@ __global__ __launch_bounds__(256, 1) void crn_enc_batch_kernel(EncBatchArgs p) {
             const bf16_t* in[FR];
 #pragma unroll
             for (int fr = 0; fr < FR; ++fr) in[fr] = sMap[0][fr];
-            conv_tiles_n2<FR, kEncNC[3], 6, 64 + 8, 2, -2, 5, 32>(acc, in, bw3a, bw3b, 0, lane);
+            conv_tiles_n2<FR, kEncNC[3], 6, 64 + 8, 2, -2, 5, 32, kEncNC[3], true>(acc, in, bw3a, bw3b, 0, lane);
 #pragma unroll
             for (int fr = 0; fr < FR; ++fr)
 #pragma unroll
-                for (int t = 0; t < 2; ++t)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int row = 4 * (lane >> 4) + r, n = (wave + 4 * t) * 16 + (lane & 15);
-                        float v = acc[fr][t][r] + bias3[t];
-                        v = v >= 0.f ? v : L.alpha * v;
-                        sMap[1][fr][row * 128 + n] = f2bf(v);
-                    }
+                for (int t = 0; t < 2; ++t) {
+                    const int row = lane & 15, n0 = (wave + 4 * t) * 16 + 4 * (lane >> 4);
+                    *reinterpret_cast<uint2*>(sMap[1][fr] + row * 128 + n0) = prelu4_bf16(acc[fr][t], bias3[t], L.alpha);
+                }
             lds_barrier();
             const int row = tid >> 4, chn = tid & 15;
 #pragma unroll
@@ -832,7 +851,10 @@ __global__ __launch_bounds__(256, 1) void crn_dec_batch_kernel(DecBatchArgs p) {
     const int n0 = nt0 * 16 + (lane & 15), n1 = nt1 * 16 + (lane & 15);
     load_bw(bw0, LA, n0);
     load_bw(bw1, LB, n1);
-    const float bias0 = LA.bias[n0], bias1 = LB.bias[n1];
+    // TR epilogue: the lane's 4 columns nt * 16 + 4 (lane >> 4) .. + 3 (one parity: Co % 4 == 0)
+    const int c0 = nt0 * 16 + 4 * (lane >> 4), c1 = nt1 * 16 + 4 * (lane >> 4);
+    const float4 bias0 = *reinterpret_cast<const float4*>(LA.bias + c0);
+    const float4 bias1 = *reinterpret_cast<const float4*>(LB.bias + c1);
     const int64_t F = p.F, step = (int64_t)gridDim.x * FR;
     // cat[3]: 512 16-B pieces per frame (2 per thread); cat[2]'s encoder half: 64 rows x 4 pieces
     u32x4 na[FR][2], nb[FR];
@@ -867,19 +889,15 @@ __global__ __launch_bounds__(256, 1) void crn_dec_batch_kernel(DecBatchArgs p) {
             const bf16_t* in[FR];
 #pragma unroll
             for (int fr = 0; fr < FR; ++fr) in[fr] = sA[fr];
-            conv_tiles<FR, kStreamDecChunks0, 7, 136, 1, -1, 3, 32>(acc, in, bw0, 0, 1, lane);
-            const int par = n0 >= 32, ch = n0 - 32 * par;
+            conv_tiles<FR, kStreamDecChunks0, 7, 136, 1, -1, 3, 32, kStreamDecChunks0, true>(acc, in, bw0, 0, 1, lane);
+            const int par = c0 >= 32, ch = c0 - 32 * par;
 #pragma unroll
             for (int fr = 0; fr < FR; ++fr)
 #pragma unroll
-                for (int t = 0; t < 2; ++t)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int i = t * 16 + 4 * (lane >> 4) + r;
-                        float v = acc[fr][t][r] + bias0;
-                        v = v >= 0.f ? v : LA.alpha * v;
-                        sB[fr][(2 * i + par) * 72 + ch] = f2bf(v);
-                    }
+                for (int t = 0; t < 2; ++t) {
+                    const int i = t * 16 + (lane & 15);
+                    *reinterpret_cast<uint2*>(sB[fr] + (2 * i + par) * 72 + ch) = prelu4_bf16(acc[fr][t], bias0, LA.alpha);
+                }
         }
         lds_barrier();
         // level cl = 2: M = 64 input bins (tiles mb0, mb0 + 2), N = 32 (parity x 16 channels) -> sO
@@ -888,19 +906,15 @@ __global__ __launch_bounds__(256, 1) void crn_dec_batch_kernel(DecBatchArgs p) {
             const bf16_t* in[FR];
 #pragma unroll
             for (int fr = 0; fr < FR; ++fr) in[fr] = sB[fr];
-            conv_tiles<FR, kStreamDecChunks1, 6, 72, 1, -1, 3, 64>(acc, in, bw1, mb0, mb0 + 2, lane);
-            const int par = n1 >= 16, ch = n1 - 16 * par;
+            conv_tiles<FR, kStreamDecChunks1, 6, 72, 1, -1, 3, 64, kStreamDecChunks1, true>(acc, in, bw1, mb0, mb0 + 2, lane);
+            const int par = c1 >= 16, ch = c1 - 16 * par;
 #pragma unroll
             for (int fr = 0; fr < FR; ++fr)
 #pragma unroll
-                for (int t = 0; t < 2; ++t)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int i = (mb0 + 2 * t) * 16 + 4 * (lane >> 4) + r;
-                        float v = acc[fr][t][r] + bias1;
-                        v = v >= 0.f ? v : LB.alpha * v;
-                        sO[fr][(2 * i + par) * 16 + ch] = f2bf(v);
-                    }
+                for (int t = 0; t < 2; ++t) {
+                    const int i = (mb0 + 2 * t) * 16 + (lane & 15);
+                    *reinterpret_cast<uint2*>(sO[fr] + (2 * i + par) * 16 + ch) = prelu4_bf16(acc[fr][t], bias1, LB.alpha);
+                }
         }
         lds_barrier();
         // cat[1]'s decoder half: 128 rows x 32 B (two 16-B pieces per row, one per thread)
