@@ -1269,6 +1269,7 @@ struct StreamState {
     // bf16 / fp8: the last three decoder levels, the mask, irFFT and overlap-add as one launch
     // (crn_stream_dec_kernel); its graph node is back_node (AEC_CRN_STREAM_FUSE=0: off)
     bool dec_fused = false;
+    bool dec_mx = false;                 // + decoder cl = 4 (MX-fp8) inside it (AEC_CRN_STREAM_FUSE bit 3)
     crn::StreamDecArgs dec_args[2];
     hipStream_t cap = nullptr;           // capture stream
 };
@@ -1472,6 +1473,20 @@ static bool stream_dec_ok(const aec_crn_handle* h) {
     return true;
 }
 
+// decoder cl = 4 inside the fused back (MX-fp8 step, AEC_CRN_STREAM_FUSE bit 3, default on): its
+// fused-parity MX GEMM at net_conf's shape (16 input bins x 256 channels -> 2 x 64 columns, K = 768)
+// reading cat[4]'s shadow, split into 1 or 2 K slices
+static bool stream_dec_mx_ok(const aec_crn_handle* h) {
+    const char* v = getenv("AEC_CRN_STREAM_FUSE");
+    if (v && !(atoi(v) & 8)) return false;
+    if (h->L < 5 || !h->ss) return false;
+    const int* ch = h->cfg.conv_channels;
+    const Packed& pk = h->decf[h->L - 4];
+    const int ks = conv_ksplit(pk.kpad);
+    return pk.wq && pk.wsc && pk.act == 1 && pk.N == 128 && pk.K == 768 && pk.kpad == 768 && ch[4] == 128 &&
+           ch[3] == 64 && shadow_level(h, 4) && h->ss->cat8.size() > 4 && h->ss->cat8[4] && h->ss->cats[4] && (ks == 1 || ks == 2);
+}
+
 // leading encoder levels crn_stream_enc_kernel can take: bf16 GEMM (not MX), PReLU, 8 output tiles
 // of 16 bins x 16 channels, K <= 160, no MX shadow on the output
 static int stream_enc_levels(const aec_crn_handle* h) {
@@ -1561,9 +1576,13 @@ static aec_status stream_launches(aec_crn_handle* h, int par, const StreamIo& io
         if (s != AEC_OK) return s;
     }
     if (ss.dec_fused) {
-        s = run_decoder<T>(h, bf, B, st, h->L - 3);
+        s = run_decoder<T>(h, bf, B, st, h->L - (ss.dec_mx ? 4 : 3));
         if (s != AEC_OK) return s;
         crn::StreamDecArgs da = stream_dec_args(h, B);
+        if (ss.dec_mx) {
+            const Packed& pk = h->decf[h->L - 4];
+            da.mx = crn::StreamDecMxLevel{pk.wq, pk.wsc, pk.bias, pk.alpha, ss.cat8[4], ss.cats[4], conv_ksplit(pk.kpad)};
+        }
         da.prev_mic = prev_mic;
         da.cur_mic = cur_mic;
         da.out = io.out;
@@ -1892,6 +1911,7 @@ aec_status aec_crn_stream_open(aec_crn_handle* h, int32_t B) {
     }
     ss.enc_nlev = stream_enc_levels(h);
     ss.dec_fused = stream_dec_ok(h);
+    ss.dec_mx = ss.dec_fused && stream_dec_mx_ok(h);
     CRN_TRY(h, hipStreamCreateWithFlags(&ss.cap, hipStreamNonBlocking));
     CRN_TRY(h, hipDeviceSynchronize());
     ss.k = 0;

@@ -243,8 +243,23 @@ struct StreamDecLevel {
     int32_t cin_shift;          // log2 of the input map's channels per bin (2 ch[cl])
     const bf16_t* src;          // cat[cl] [B][Fin][2 ch[cl]]: the whole map (level 0) or its encoder half (later levels)
 };
+// Optional first level of the fused back (fp8 step, AEC_CRN_STREAM_FUSE bit 3): decoder cl = 4 as
+// its MX-fp8 GEMM (scaled MFMA on cat[4]'s e4m3 shadow and the e4m3 weights, 16 input bins x 128
+// columns = both parities of 64 channels, K = 3 taps x 256), its output cat[3]'s decoder half kept
+// in LDS.  The K slices (ksplit 1 or 2) summed as gemm_mx8_kernel's split-K reducer sums them.
+constexpr int kStreamMxStages = 6;   // 128-k stages of cl = 4 (K = 768)
+struct StreamDecMxLevel {
+    const uint8_t* wq;          // [npad8][768] e4m3 (pack_decoder_fused order, MX)
+    const uint8_t* wsc;         // [npad8][24] E8M0
+    const float* bias;
+    float alpha;
+    const uint8_t* q8;          // cat[4]'s shadow [B][16][256] e4m3
+    const uint8_t* qs;          //   and its E8M0 per 32 [B][16][8]
+    int32_t ksplit;             // the row GEMM's split (conv_ksplit), 1 or 2
+};
 struct StreamDecArgs {
     StreamDecLevel lev[3];      // cl = 3, 2, 1 (the last is the mask level)
+    StreamDecMxLevel mx;        // mx.wq non-null: cl = 4 first (then lev[0].src supplies only the encoder half)
     const aec::DevTables* tab;
     const float2* espec;        // NLMS: E rows [B][256] (the masked spectrum), else the mic frame:
     const float* prev_mic;      //   [prev hop | cur hop] from the ring

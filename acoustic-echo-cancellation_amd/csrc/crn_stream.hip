@@ -642,9 +642,36 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
     constexpr int kDecPieces = 2;
     u32x4 mp[kDecPieces + 2];
     const StreamDecLevel& L0 = p.lev[0];
+    const bool mx = p.mx.wq != nullptr;                         // uniform
     const u32x4* src0 = reinterpret_cast<const u32x4*>(L0.src + (int64_t)b * (32 << L0.cin_shift));
+    // cl = 4 (MX): cat[4]'s shadow row pieces (16 bins x 256 B, one per thread), its scales (16 x 8
+    // B, threads < 32), this wave's B fragments of N tiles wave, wave + 4 (stage st: bytes 128 st +
+    // 16 g and + 64; the MX GEMM core's operand map) and their scale words
+    u32x4 xq = {0u, 0u, 0u, 0u};
+    uint32_t xs = 0;
+    u32x4 mb[2][kStreamMxStages][2];
+    uint32_t msw[2][kStreamMxStages];
+    if (mx) {
+        // level 0's encoder half only (channels 64 .. 127 of 32 bins: one piece per thread)
+        mp[0] = src0[(tid >> 3) * 16 + 8 + (tid & 7)];
+        xq = reinterpret_cast<const u32x4*>(p.mx.q8 + (int64_t)b * 4096)[tid];
+        if (tid < 32) xs = reinterpret_cast<const uint32_t*>(p.mx.qs + (int64_t)b * 128)[tid];
 #pragma unroll
-    for (int i = 0; i < kDecPieces; ++i) mp[i] = src0[tid + 256 * i];
+        for (int t = 0; t < 2; ++t) {
+            const int n = (wave + 4 * t) * 16 + (lane & 15);
+            const uint8_t* wr = p.mx.wq + (int64_t)n * 768 + 16 * (lane >> 4);
+            const uint32_t* sr = reinterpret_cast<const uint32_t*>(p.mx.wsc + (int64_t)n * 24);
+#pragma unroll
+            for (int st = 0; st < kStreamMxStages; ++st) {
+                mb[t][st][0] = *reinterpret_cast<const u32x4*>(wr + 128 * st);
+                mb[t][st][1] = *reinterpret_cast<const u32x4*>(wr + 128 * st + 64);
+                msw[t][st] = sr[st];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < kDecPieces; ++i) mp[i] = src0[tid + 256 * i];
+    }
 #pragma unroll
     for (int l = 1; l < 3; ++l) {                // encoder half: channels [C/2, C) of Fin rows, one piece per thread
         const StreamDecLevel& L = p.lev[l];
@@ -682,7 +709,13 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
     load_bw(bw0, p.lev[0], nt[0] * 16 + (lane & 15));
     load_bw(bw1, p.lev[1], nt[1] * 16 + (lane & 15));
     load_bw(bw2, p.lev[2], nt[2] * 16 + (lane & 15));
-    {
+    __shared__ __attribute__((aligned(16))) uint8_t sX4[16 * (256 + 16)];   // cat[4]'s shadow, rows padded
+    __shared__ uint32_t sX4s[32];
+    if (mx) {
+        *reinterpret_cast<u32x4*>(sIn[0] + (tid >> 3) * (128 + 8) + 64 + 8 * (tid & 7)) = mp[0];
+        *reinterpret_cast<u32x4*>(sX4 + (tid >> 4) * (256 + 16) + 16 * (tid & 15)) = xq;
+        if (tid < 32) sX4s[tid] = xs;
+    } else {
         const int C = 1 << L0.cin_shift, per = C / 8;   // 16-B pieces per map row
 #pragma unroll
         for (int i = 0; i < kDecPieces; ++i) {
@@ -698,6 +731,61 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
     }
     lds_barrier();
     SPROF(1, 1);
+
+    // 1b. cl = 4 (MX): 16 input bins i (one M tile) x N tiles wave, wave + 4 (parity n >= 64,
+    //     channel n % 64) -> level 0's decoder half; input bin i - 1 + tap, tap = stage / 2
+    if (mx) {
+        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        const int g = lane >> 4, r = lane & 15;
+        auto run = [&](auto S0, auto S1, f32x4 (&part)[2]) {
+            aec::static_for<decltype(S0)::value, decltype(S1)::value>([&](auto si) {
+                constexpr int st = decltype(si)::value, tap = st >> 1, kb = (st & 1) * 128;
+                const int ib = r - 1 + tap;
+                const bool ok = ib >= 0 && ib < 16;
+                const uint8_t* row = sX4 + (ok ? ib : 0) * (256 + 16) + kb;
+                const u32x4 lo = *reinterpret_cast<const u32x4*>(row + 16 * g);
+                const u32x4 hi = *reinterpret_cast<const u32x4*>(row + 64 + 16 * g);
+                const u32x4 z = {0u, 0u, 0u, 0u};
+                const u32x4 l2 = ok ? lo : z, h2 = ok ? hi : z;
+                const i32x8 af = i32x8{(int)l2[0], (int)l2[1], (int)l2[2], (int)l2[3], (int)h2[0], (int)h2[1], (int)h2[2], (int)h2[3]};
+                const int sa = ok ? (int)((sX4s[(ok ? ib : 0) * 2 + (st & 1)] >> (8 * g)) & 0xFFu) : 0;
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const i32x8 bf = i32x8{(int)mb[t][st][0][0], (int)mb[t][st][0][1], (int)mb[t][st][0][2], (int)mb[t][st][0][3],
+                                           (int)mb[t][st][1][0], (int)mb[t][st][1][1], (int)mb[t][st][1][2], (int)mb[t][st][1][3]};
+                    const int sb = (int)((msw[t][st] >> (8 * g)) & 0xFFu);
+                    part[t] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bf, part[t], 0, 0, 0, sa, 0, sb);
+                }
+            });
+        };
+        if (p.mx.ksplit == 2) {   // gemm_mx8_kernel's reducer: 0 + slice 0 + slice 1
+            f32x4 p0[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+            f32x4 p1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+            run(std::integral_constant<int, 0>{}, std::integral_constant<int, 3>{}, p0);
+            run(std::integral_constant<int, 3>{}, std::integral_constant<int, 6>{}, p1);
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                acc[t] += p0[t];
+                acc[t] += p1[t];
+            }
+        } else {
+            run(std::integral_constant<int, 0>{}, std::integral_constant<int, 6>{}, acc);
+        }
+        // epilogue (rows_epilogue_lds's: + bias, PReLU, bf16): acc[t][rr] = row 4 g + rr, column n
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int n = (wave + 4 * t) * 16 + r, par = n >= 64, ch = n - 64 * par;
+            const float bn = p.mx.bias[n];
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int i = 4 * g + rr;
+                float v = acc[t][rr] + bn;
+                v = v >= 0.f ? v : p.mx.alpha * v;
+                sIn[0][(2 * i + par) * (128 + 8) + ch] = f2bf(v);
+            }
+        }
+        lds_barrier();
+    }
 
     // 2. decoder levels cl = 3, 2: output bins 2 i + parity, channel n -> the next map's decoder half
 #pragma unroll

@@ -775,6 +775,15 @@ def main():
     if os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path))
     roof = roofline(args.pipeline, dom, per_launch_ms[dom], int(round(B * T / calls_per_step)), pmc)
+    # every kernel of the step against its own roofline (the fused GRU + synthesis kernel runs two
+    # streams per block on half the CUs, so the longest launch is not the one holding the most CU
+    # time): the same figures as `roofline`, per kernel
+    kernel_rooflines = {}
+    for k in per_launch_ms:
+        if per_launch_ms[k] > 0 and k in ALG[args.pipeline]:
+            r = roofline(args.pipeline, k, per_launch_ms[k], int(round(B * T / calls_per_step)), pmc)
+            kernel_rooflines[k] = {x: r[x] for x in ('bound', 'frac', 'hbm_frac', 'fp32_frac', 'ms_per_launch',
+                                                     'traffic', 'traffic_alg_bytes_per_launch')}
     pipe_t = ms_step * 1e-3
     pipe_gbs = PIPE['bytes'] * B * T / pipe_t / 1e9
     pipe_tfl = path_flops(args.pipeline) * B * T / pipe_t / 1e12
@@ -868,6 +877,7 @@ def main():
             'kernels_per_step': kernels_per_call,
             'launches_per_step': launches_per_step,
             'roofline': roof,
+            'kernel_rooflines': kernel_rooflines,
             'pipeline_roofline': {'alg_bytes_per_frame': PIPE['bytes'],
                                   'alg_flops_per_frame': path_flops(args.pipeline),
                                   'hbm_frac': round(pipe_gbs / HBM_PEAK_GBS, 4),
