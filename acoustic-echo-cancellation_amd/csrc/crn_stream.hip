@@ -225,14 +225,14 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
     // weight fragments: level i, this wave's N tile nt = wave % NT, chunk c: row nt*16 + (lane & 15),
     // k = 32 c + 8 (lane >> 4) .. + 7 (the 16x16x32 B operand)
     u32x4 bw[3][kStreamEncChunks];
-    float bias[3];
+    float4 bias[3];                               // the TR epilogue's 4 columns nt * 16 + 4 (lane >> 4) .. + 3
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         if (i >= p.nlev) break;
         const StreamEncLevel& L = p.lev[i];
         const int NT = L.N >> 4;
         const int n = (wave % NT) * 16 + (lane & 15);
-        bias[i] = L.bias[n];
+        bias[i] = *reinterpret_cast<const float4*>(L.bias + (wave % NT) * 16 + 4 * (lane >> 4));
         const bf16_t* wr = L.w + (int64_t)n * L.kpad + 8 * (lane >> 4);
 #pragma unroll
         for (int c = 0; c < kStreamEncChunks; ++c)
@@ -240,13 +240,13 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
     }
     // level 3 (16 output bins x 128 channels): this wave's N tiles wave and wave + 4
     u32x4 bw3[2][kStreamEncChunks3];
-    float bias3[2] = {0.f, 0.f};
+    float4 bias3[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
     if (p.nlev > 3) {
         const StreamEncLevel& L = p.lev[3];
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             const int n = (wave + 4 * t) * 16 + (lane & 15);
-            bias3[t] = L.bias[n];
+            bias3[t] = *reinterpret_cast<const float4*>(L.bias + (wave + 4 * t) * 16 + 4 * (lane >> 4));
             const bf16_t* wr = L.w + (int64_t)n * L.kpad + 8 * (lane >> 4);
             aec::static_for<0, kStreamEncChunks3>([&](auto ci) {
                 constexpr int c = decltype(ci)::value;
@@ -331,34 +331,30 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
         const StreamEncLevel& L = p.lev[i];
         bf16_t* map = sMap[i & 1];
         bf16_t* out = L.out + (int64_t)b * Fo * L.ldo + L.choff;
-        const int n = nt * 16 + (lane & 15);
+        const int n0 = nt * 16 + 4 * (lane >> 4);   // transposed accumulators: 4 adjacent columns
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = (t ? m1 : m0) * 16 + 4 * (lane >> 4) + r;
-                float v = acc[0][t][r] + bias[i];
-                v = v >= 0.f ? v : L.alpha * v;
-                const bf16_t o = f2bf(v);
-                if (keep) map[row * (N + 8) + n] = o;
-                out[(int64_t)row * L.ldo + n] = o;
-            }
+        for (int t = 0; t < 2; ++t) {
+            const int row = (t ? m1 : m0) * 16 + (lane & 15);
+            const uint2 o = prelu4_bf16(acc[0][t], bias[i], L.alpha);
+            if (keep) *reinterpret_cast<uint2*>(map + row * (N + 8) + n0) = o;
+            *reinterpret_cast<uint2*>(out + (int64_t)row * L.ldo + n0) = o;
+        }
         lds_barrier();
         SPROF(0, 4 + i);
     };
     {
         const bf16_t* in[1] = {sX0};
-        conv_tiles<1, kEncNC[0], 3, 8, 2, -2, 5, 256>(acc, in, bw[0], wave, wave + 4, lane);
+        conv_tiles<1, kEncNC[0], 3, 8, 2, -2, 5, 256, kStreamEncChunks, true>(acc, in, bw[0], wave, wave + 4, lane);
         level_out(std::integral_constant<int, 0>{}, 0, wave, wave + 4, true);
     }
     {
         const bf16_t* in[1] = {sMap[0]};
-        conv_tiles<1, kEncNC[1], 4, 16 + 8, 2, -2, 5, 128>(acc, in, bw[1], wave / 2, wave / 2 + 2, lane);
+        conv_tiles<1, kEncNC[1], 4, 16 + 8, 2, -2, 5, 128, kStreamEncChunks, true>(acc, in, bw[1], wave / 2, wave / 2 + 2, lane);
         level_out(std::integral_constant<int, 1>{}, wave % 2, wave / 2, wave / 2 + 2, true);
     }
     {
         const bf16_t* in[1] = {sMap[1]};
-        conv_tiles<1, kEncNC[2], 5, 32 + 8, 2, -2, 5, 64>(acc, in, bw[2], 0, 1, lane);
+        conv_tiles<1, kEncNC[2], 5, 32 + 8, 2, -2, 5, 64, kStreamEncChunks, true>(acc, in, bw[2], 0, 1, lane);
         level_out(std::integral_constant<int, 2>{}, wave, 0, 1, p.nlev > 3);
     }
     // 5. level 3: one M tile (the 16 output bins) x N tiles wave, wave + 4; the outputs staged in
@@ -367,17 +363,13 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
     if (p.nlev > 3) {
         const StreamEncLevel& L = p.lev[3];
         const bf16_t* in[1] = {sMap[0]};
-        conv_tiles_n2<1, kEncNC[3], 6, 64 + 8, 2, -2, 5, 32>(acc, in, bw3[0], bw3[1], 0, lane);
+        conv_tiles_n2<1, kEncNC[3], 6, 64 + 8, 2, -2, 5, 32, kStreamEncChunks3, true>(acc, in, bw3[0], bw3[1], 0, lane);
         bf16_t* stage = sMap[1];                      // level 1's map, consumed by level 2
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = 4 * (lane >> 4) + r, n = (wave + 4 * t) * 16 + (lane & 15);
-                float v = acc[0][t][r] + bias3[t];
-                v = v >= 0.f ? v : L.alpha * v;
-                stage[row * 128 + n] = f2bf(v);
-            }
+        for (int t = 0; t < 2; ++t) {
+            const int row = lane & 15, n0 = (wave + 4 * t) * 16 + 4 * (lane >> 4);
+            *reinterpret_cast<uint2*>(stage + row * 128 + n0) = prelu4_bf16(acc[0][t], bias3[t], L.alpha);
+        }
         lds_barrier();
         const int row = tid >> 4, chn = tid & 15;
         const u32x4 v = *reinterpret_cast<const u32x4*>(stage + row * 128 + 8 * chn);
@@ -696,7 +688,7 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
     sCoff[tid] = p.tab->inv_coff[tid];
     u32x4 bw0[kStreamDecChunks0], bw1[kStreamDecChunks1], bw2[kStreamDecChunks2];
     int nt[3], m0[3], m1[3];
-    float bias[3];
+    f32x4 bias[3];
 #pragma unroll
     for (int l = 0; l < 3; ++l) {
         const int NT = (p.lev[l].N + 15) >> 4;
@@ -704,7 +696,10 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
         m0[l] = wave / NT;
         m1[l] = m0[l] + 4 / NT;
         const int n = nt[l] * 16 + (lane & 15);
-        bias[l] = n < p.lev[l].N ? p.lev[l].bias[n] : 0.f;
+        // transposed accumulators: the lane's 4 columns nt * 16 + 4 (lane >> 4) .. + 3
+        const int c4 = nt[l] * 16 + 4 * (lane >> 4);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bias[l][q] = c4 + q < p.lev[l].N ? p.lev[l].bias[c4 + q] : 0.f;
     }
     load_bw(bw0, p.lev[0], nt[0] * 16 + (lane & 15));
     load_bw(bw1, p.lev[1], nt[1] * 16 + (lane & 15));
@@ -794,20 +789,17 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
         const int Co = L.N >> 1, Cn = 1 << p.lev[l + 1].cin_shift;
         f32x4 acc2[1][2];
         const bf16_t* in[1] = {sIn[l]};
-        if (l == 0) conv_tiles<1, kStreamDecChunks0, 7, 128 + 8, 1, -1, 3, 32>(acc2, in, bw0, m0[0], m1[0], lane);
-        else conv_tiles<1, kStreamDecChunks1, 6, 64 + 8, 1, -1, 3, 64>(acc2, in, bw1, m0[1], m1[1], lane);
+        if (l == 0) conv_tiles<1, kStreamDecChunks0, 7, 128 + 8, 1, -1, 3, 32, kStreamDecChunks0, true>(acc2, in, bw0, m0[0], m1[0], lane);
+        else conv_tiles<1, kStreamDecChunks1, 6, 64 + 8, 1, -1, 3, 64, kStreamDecChunks1, true>(acc2, in, bw1, m0[1], m1[1], lane);
         const f32x4 (&acc)[2] = acc2[0];
-        const int n = nt[l] * 16 + (lane & 15), par = n >= Co, ch = n - par * Co;
+        const int c4 = nt[l] * 16 + 4 * (lane >> 4), par = c4 >= Co, ch = c4 - par * Co;
         bf16_t* next = sIn[l + 1];
+        const float4 b4 = make_float4(bias[l][0], bias[l][1], bias[l][2], bias[l][3]);
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int i = (t ? m1[l] : m0[l]) * 16 + 4 * (lane >> 4) + r;
-                float v = acc[t][r] + bias[l];
-                v = v >= 0.f ? v : L.alpha * v;
-                next[(2 * i + par) * (Cn + 8) + ch] = f2bf(v);
-            }
+        for (int t = 0; t < 2; ++t) {
+            const int i = (t ? m1[l] : m0[l]) * 16 + (lane & 15);
+            *reinterpret_cast<uint2*>(next + (2 * i + par) * (Cn + 8) + ch) = prelu4_bf16(acc[t], b4, L.alpha);
+        }
         lds_barrier();
         SPROF(1, 2 + l);
     }
@@ -816,19 +808,21 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
         const StreamDecLevel& L = p.lev[2];
         f32x4 acc2[1][2];
         const bf16_t* in[1] = {sIn[2]};
-        conv_tiles<1, kStreamDecChunks2, 5, 32 + 8, 1, -1, 3, 128>(acc2, in, bw2, m0[2], m1[2], lane);
+        conv_tiles<1, kStreamDecChunks2, 5, 32 + 8, 1, -1, 3, 128, kStreamDecChunks2, true>(acc2, in, bw2, m0[2], m1[2], lane);
         const f32x4 (&acc)[2] = acc2[0];
-        const int n = lane & 15;
-        if (n < 4) {
+        // the 4 columns (parity, re / im) of input bin i sit in the lanes with lane >> 4 == 0
+        if ((lane >> 4) == 0) {
 #pragma unroll
-            for (int t = 0; t < 2; ++t)
+            for (int t = 0; t < 2; ++t) {
+                const int i = (t ? m1[2] : m0[2]) * 16 + (lane & 15);
+                float v[4];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int i = (t ? m1[2] : m0[2]) * 16 + 4 * (lane >> 4) + r;
-                    float v = acc[t][r] + bias[2];
-                    if (L.act == 2) v = tanhf(v);              // the batch epilogue's apply_act<2>
-                    reinterpret_cast<float*>(sMask)[(2 * i + (n >> 1)) * 2 + (n & 1)] = v;
+                for (int q = 0; q < 4; ++q) {
+                    v[q] = acc[t][q] + bias[2][q];
+                    if (L.act == 2) v[q] = tanhf(v[q]);            // the batch epilogue's apply_act<2>
                 }
+                *reinterpret_cast<float4*>(reinterpret_cast<float*>(sMask) + 4 * i) = make_float4(v[0], v[1], v[2], v[3]);
+            }
         }
     }
     // the mic spectrum (no NLMS): the batch front's transform of [prev | cur]
