@@ -1270,6 +1270,7 @@ struct StreamState {
     // (crn_stream_dec_kernel); its graph node is back_node (AEC_CRN_STREAM_FUSE=0: off)
     bool dec_fused = false;
     bool dec_mx = false;                 // + decoder cl = 4 (MX-fp8) inside it (AEC_CRN_STREAM_FUSE bit 3)
+    bool enc_mx = false;                 // + encoder level 4 (MX-fp8) inside the fused front (bit 4)
     crn::StreamDecArgs dec_args[2];
     hipStream_t cap = nullptr;           // capture stream
 };
@@ -1405,6 +1406,18 @@ static crn::StreamEncArgs stream_enc_args(aec_crn_handle* h, int B) {
         ea.delta = h->cfg.nlms_delta;
     }
     ea.nlev = ss.enc_nlev;
+    if (ss.enc_mx) {
+        const Packed& pk = h->enc[4];
+        ea.mx4.wq = pk.wq;
+        ea.mx4.wsc = pk.wsc;
+        ea.mx4.bias = pk.bias;
+        ea.mx4.alpha = pk.alpha;
+        ea.mx4.out = reinterpret_cast<bf16_t*>(ss.cat[5]);
+        ea.mx4.ldo = 2 * ch[5];
+        ea.mx4.choff = ch[5];
+        ea.mx4.q8 = ss.cat8[5];
+        ea.mx4.qs = ss.cats[5];
+    }
     for (int i = 0; i < ss.enc_nlev; ++i) {
         const Packed& pk = h->enc[i];
         crn::StreamEncLevel& L = ea.lev[i];
@@ -1487,6 +1500,21 @@ static bool stream_dec_mx_ok(const aec_crn_handle* h) {
            ch[3] == 64 && shadow_level(h, 4) && h->ss->cat8.size() > 4 && h->ss->cat8[4] && h->ss->cats[4] && (ks == 1 || ks == 2);
 }
 
+// encoder level 4 inside the fused front (MX-fp8 step, AEC_CRN_STREAM_FUSE bit 4, default on): its
+// MX GEMM at net_conf's shape (8 output bins x 256 channels, K = 5 taps x 128, one K slice) on level
+// 3's shadow, its output with a shadow for level 5
+static bool stream_enc_mx_ok(const aec_crn_handle* h) {
+    const char* v = getenv("AEC_CRN_STREAM_FUSE");
+    if (v && !(atoi(v) & 16)) return false;
+    if (h->L < 6 || !h->ss) return false;
+    const int* ch = h->cfg.conv_channels;
+    const Packed& pk = h->enc[4];
+    const StreamState& ss = *h->ss;
+    return pk.wq && pk.wsc && pk.act == 1 && pk.N == 256 && pk.K == 640 && pk.kpad == 640 && ch[4] == 128 &&
+           ch[5] == 256 && conv_ksplit(pk.kpad) == 1 && ss.cat8.size() > 5 && ss.cat8[4] && ss.cats[4] &&
+           ss.cat8[5] && ss.cats[5];
+}
+
 // leading encoder levels crn_stream_enc_kernel can take: bf16 GEMM (not MX), PReLU, 8 output tiles
 // of 16 bins x 16 channels, K <= 160, no MX shadow on the output
 static int stream_enc_levels(const aec_crn_handle* h) {
@@ -1543,7 +1571,9 @@ static aec_status stream_launches(aec_crn_handle* h, int par, const StreamIo& io
         CRN_TRY(h, crn::launch_stream_enc(ea, c.nlms_taps, st));
         ss.front_node[par] = last_node(st);
         ss.enc_args[par] = ea;
-        first = ss.enc_nlev;
+        // AEC_CRN_ENC_MX_RERUN=1 (debugging only): the level-4 GEMM runs after the fused front anyway
+        static const bool rerun = [] { const char* v = getenv("AEC_CRN_ENC_MX_RERUN"); return v && atoi(v); }();
+        first = ss.enc_nlev + (ss.enc_mx && !rerun ? 1 : 0);
     } else {
         crn::StreamFrontArgs fa{prev_mic, io.mic, prev_far, io.far, h->d_tab, ss.x0, B};
         fa.ld_cur = io.ld_in;
@@ -1912,6 +1942,7 @@ aec_status aec_crn_stream_open(aec_crn_handle* h, int32_t B) {
     ss.enc_nlev = stream_enc_levels(h);
     ss.dec_fused = stream_dec_ok(h);
     ss.dec_mx = ss.dec_fused && stream_dec_mx_ok(h);
+    ss.enc_mx = ss.enc_nlev == 4 && stream_enc_mx_ok(h);
     CRN_TRY(h, hipStreamCreateWithFlags(&ss.cap, hipStreamNonBlocking));
     CRN_TRY(h, hipDeviceSynchronize());
     ss.k = 0;

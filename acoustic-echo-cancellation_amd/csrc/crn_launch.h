@@ -198,6 +198,21 @@ struct StreamEncLevel {
     uint8_t* q8 = nullptr;      // level 3: the output's MX-fp8 shadow (RowEpi::q8 / qs layout) or null
     uint8_t* qs = nullptr;
 };
+// Optional last level of the fused front (fp8 step, AEC_CRN_STREAM_FUSE bit 4): encoder level 4
+// as its MX-fp8 GEMM (scaled MFMA, 8 output bins x 256 channels, K = 5 taps x 128) on level 3's
+// e4m3 shadow kept in LDS; its output (and the output's MX-fp8 shadow) -> cat[5]'s encoder half.
+constexpr int kStreamEncMxStages = 5;   // 128-k stages of level 4 (K = 640)
+struct StreamEncMxLevel {
+    const uint8_t* wq = nullptr;  // [npad8][640] e4m3
+    const uint8_t* wsc = nullptr; // [npad8][20] E8M0
+    const float* bias = nullptr;
+    float alpha = 0.f;
+    bf16_t* out = nullptr;        // cat[5] [B][8][ldo] at channel offset choff
+    int64_t ldo = 0;
+    int32_t choff = 0;
+    uint8_t* q8 = nullptr;        // its shadow (RowEpi::q8 / qs layout)
+    uint8_t* qs = nullptr;
+};
 struct StreamEncArgs {
     const float* prev_mic;      // [B][256] hop ring
     const float* cur_mic;       // [B][ld_cur] this call's hop (caller's buffer)
@@ -211,8 +226,9 @@ struct StreamEncArgs {
     float2* state;              // NLMS (taps > 0): [B][2 taps][256] (StreamNlmsArgs layout)
     float2* espec;              //   E rows [B][256]
     float mu, beta, delta;
-    int32_t nlev;               // 1..4 (level 3: 16 output bins x 128 channels, K <= 320)
+    int32_t nlev;               // 3 or 4 (level 3: 16 output bins x 128 channels, K = 320)
     StreamEncLevel lev[4];
+    StreamEncMxLevel mx4;       // mx4.wq non-null (nlev == 4): level 4 as well
 };
 hipError_t launch_stream_enc(const StreamEncArgs& a, int taps, hipStream_t st);
 

@@ -153,6 +153,43 @@ __device__ __forceinline__ uint2 prelu4_bf16(const f32x4& v, const float4& bias,
     return make_uint2(o[0] | (o[1] << 16), o[2] | (o[3] << 16));
 }
 
+// A scaled-MFMA operand kept live past the instruction that reads it: the B fragment of a first
+// stage (C = 0) is otherwise dead after the MFMA, and under register pressure the allocator gave
+// its registers to the MFMA's own destination (vdst = a[56:59] with srcB = a[56:63]), which read
+// back corrupted operands (NaN outputs); the scale registers were rewritten two cycles after the
+// issue.  An empty asm that reads them after the MFMA forbids both reuses.
+__device__ __forceinline__ void keep_live(const i32x8& b) { asm volatile("" ::"v"(b)); }
+__device__ __forceinline__ void keep_live(int x) { asm volatile("" ::"v"(x)); }
+
+// mx8_chunk's arithmetic (crn_gemm.h) returning the chunk's 8 e4m3 bytes and its group's E8M0 code
+// instead of storing them (the fused front keeps level 3's shadow in LDS for level 4 as well)
+__device__ __forceinline__ uint2 mx8_pack_chunk(const u32x4& v, int& code_out) {
+    float x[8];
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        x[2 * i] = __uint_as_float(v[i] << 16);
+        x[2 * i + 1] = __uint_as_float(v[i] & 0xFFFF0000u);
+        amax = fmaxf(amax, fmaxf(fabsf(x[2 * i]), fabsf(x[2 * i + 1])));
+    }
+    amax = fmaxf(amax, __shfl_xor(amax, 1));
+    amax = fmaxf(amax, __shfl_xor(amax, 2));
+    const int ebits = (int)((__float_as_uint(amax) >> 23) & 0xFF);
+    const int code = ebits > 8 ? ebits - 8 : 0;
+    uint32_t pk[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        float y[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y[j] = fminf(fmaxf(ldexpf(x[4 * i + j], 127 - code), -448.f), 448.f);
+        int w = __builtin_amdgcn_cvt_pk_fp8_f32(y[0], y[1], 0, false);
+        w = __builtin_amdgcn_cvt_pk_fp8_f32(y[2], y[3], w, true);
+        pk[i] = (uint32_t)w;
+    }
+    code_out = code;
+    return make_uint2(pk[0], pk[1]);
+}
+
 // net_conf's encoder levels 0-3 (conv_channels 4, 16, 32, 64, 128: N = 16 << i, K = 5 taps x
 // 8 / 16 / 32 / 64 input channels): the shapes the batch kernels are compiled for
 constexpr int kEncNC[4] = {2, 3, 5, 10};
@@ -176,6 +213,8 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
     __shared__ __attribute__((aligned(16))) float2 sRow[2][256];
     __shared__ __attribute__((aligned(16))) bf16_t sX0[256 * 8];
     __shared__ __attribute__((aligned(16))) bf16_t sMap[2][kPadMapElems];
+    __shared__ __attribute__((aligned(16))) uint8_t sQ3[16 * (128 + 16)];   // level 3's e4m3 shadow (level 4)
+    __shared__ uint8_t sQ3s[16 * 4];
     float2* sTwT = reinterpret_cast<float2*>(sTab);
     float2* sTw512 = sTwT + 256;
     float* sHann = reinterpret_cast<float*>(sTw512 + 258);
@@ -252,6 +291,28 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
                 constexpr int c = decltype(ci)::value;
                 bw3[t][c] = c < L.nchunk ? *reinterpret_cast<const u32x4*>(wr + 32 * c) : u32x4{0u, 0u, 0u, 0u};
             });
+        }
+    }
+    // level 4 (MX, optional): this wave's B fragments of N tiles wave + 4 t (t = 0..3), stage st =
+    // tap st: bytes 128 st + 16 g and + 64 (the MX GEMM core's operand map), their scale words, and
+    // the lane's bias per tile (the non-transposed accumulator: column (lane & 15) of the tile)
+    const bool mx4 = p.mx4.wq != nullptr;                        // uniform
+    u32x4 mb4[4][kStreamEncMxStages][2];
+    uint32_t msw4[4][kStreamEncMxStages];
+    float mbias4[4];
+    if (mx4) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int n = (wave + 4 * t) * 16 + (lane & 15);
+            const uint8_t* wr = p.mx4.wq + (int64_t)n * 640 + 16 * (lane >> 4);
+            const uint32_t* sr = reinterpret_cast<const uint32_t*>(p.mx4.wsc + (int64_t)n * 20);
+#pragma unroll
+            for (int st = 0; st < kStreamEncMxStages; ++st) {
+                mb4[t][st][0] = *reinterpret_cast<const u32x4*>(wr + 128 * st);
+                mb4[t][st][1] = *reinterpret_cast<const u32x4*>(wr + 128 * st + 64);
+                msw4[t][st] = (sr[st] >> (8 * (lane >> 4))) & 0xFFu;   // this lane's scale byte
+            }
+            mbias4[t] = p.mx4.bias[n];
         }
     }
     sTwT[tid] = t0;
@@ -375,14 +436,94 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
         const u32x4 v = *reinterpret_cast<const u32x4*>(stage + row * 128 + 8 * chn);
         const int64_t eo = ((int64_t)b * 16 + row) * L.ldo + L.choff + 8 * chn;
         *reinterpret_cast<u32x4*>(L.out + eo) = v;
-        if (L.q8) mx8_chunk(v, true, L.q8, L.qs, eo, (chn & 3) == 0);
+        if (mx4) {
+            // the shadow to HBM (decoder level 4 reads it) and into LDS for level 4: rows of 128 e4m3
+            // (+16 B pad), 4 E8M0 per row
+            int code;
+            const uint2 pk = mx8_pack_chunk(v, code);
+            *reinterpret_cast<uint2*>(L.q8 + eo) = pk;
+            if ((chn & 3) == 0) L.qs[eo >> 5] = (uint8_t)code;
+            *reinterpret_cast<uint2*>(sQ3 + row * (128 + 16) + 8 * chn) = pk;
+            if ((chn & 3) == 0) sQ3s[row * 4 + (chn >> 2)] = (uint8_t)code;
+        } else if (L.q8) {
+            mx8_chunk(v, true, L.q8, L.qs, eo, (chn & 3) == 0);
+        }
         SPROF(0, 7);
+    }
+    // 6. level 4 (MX-fp8, optional): 8 output bins j (rows 8..15 of the M tile unused) x N tiles
+    //    wave + 4 t; input bin 2 j - 2 + tap, tap = stage; then + bias, PReLU, bf16, staged in LDS
+    //    (level 2's map, consumed) and stored as 16-B row chunks with the output's MX-fp8 shadow
+    if (mx4) {
+        lds_barrier();
+        const int g = lane >> 4, r = lane & 15;
+        f32x4 acc4[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
+                         f32x4{0.f, 0.f, 0.f, 0.f}};
+        // every stage's A fragment and scale first, then the MFMAs, then every operand kept live to the
+        // end of the level (see keep_live: no operand register is rewritten while an MFMA may read it)
+        i32x8 af[kStreamEncMxStages];
+        int sa[kStreamEncMxStages];
+        aec::static_for<0, kStreamEncMxStages>([&](auto si) {
+            constexpr int st = decltype(si)::value;
+            const int ib = 2 * r - 2 + st;
+            const bool ok = r < 8 && ib >= 0 && ib < 16;
+            const uint8_t* rowp = sQ3 + (ok ? ib : 0) * (128 + 16);
+            const u32x4 lo = *reinterpret_cast<const u32x4*>(rowp + 16 * g);
+            const u32x4 hi = *reinterpret_cast<const u32x4*>(rowp + 64 + 16 * g);
+            const u32x4 z = {0u, 0u, 0u, 0u};
+            const u32x4 l2 = ok ? lo : z, h2 = ok ? hi : z;
+            af[st] = i32x8{(int)l2[0], (int)l2[1], (int)l2[2], (int)l2[3], (int)h2[0], (int)h2[1], (int)h2[2], (int)h2[3]};
+            sa[st] = ok ? (int)sQ3s[(ok ? ib : 0) * 4 + g] : 0;
+        });
+        auto bfrag = [&](int t, auto Sc) {
+            constexpr int st = decltype(Sc)::value;
+            return i32x8{(int)mb4[t][st][0][0], (int)mb4[t][st][0][1], (int)mb4[t][st][0][2], (int)mb4[t][st][0][3],
+                         (int)mb4[t][st][1][0], (int)mb4[t][st][1][1], (int)mb4[t][st][1][2], (int)mb4[t][st][1][3]};
+        };
+        aec::static_for<0, kStreamEncMxStages>([&](auto si) {
+            constexpr int st = decltype(si)::value;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                acc4[t] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[st], bfrag(t, si), acc4[t], 0, 0, 0, sa[st], 0,
+                                                                           (int)msw4[t][st]);
+        });
+        aec::static_for<0, kStreamEncMxStages>([&](auto si) {
+            constexpr int st = decltype(si)::value;
+            keep_live(af[st]);
+            keep_live(sa[st]);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                keep_live(bfrag(t, si));
+                keep_live((int)msw4[t][st]);
+            }
+        });
+        bf16_t* st4 = sMap[0];                                      // [8 rows][256 channels]
+        if (g < 2) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int n = (wave + 4 * t) * 16 + r;
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    float v = acc4[t][rr] + mbias4[t];
+                    v = v >= 0.f ? v : p.mx4.alpha * v;
+                    st4[(4 * g + rr) * 256 + n] = f2bf(v);
+                }
+            }
+        }
+        lds_barrier();
+        const int row = tid >> 5, chn = tid & 31;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(st4 + row * 256 + 8 * chn);
+        const int64_t eo = ((int64_t)b * 8 + row) * p.mx4.ldo + p.mx4.choff + 8 * chn;
+        *reinterpret_cast<u32x4*>(p.mx4.out + eo) = v;
+        if (p.mx4.q8) mx8_chunk(v, true, p.mx4.q8, p.mx4.qs, eo, (chn & 3) == 0);
     }
 }
 
 hipError_t launch_stream_enc(const StreamEncArgs& a, int taps, hipStream_t st) {
     if (a.B <= 0) return hipSuccess;
     if (a.nlev < 3 || a.nlev > 4) return hipErrorInvalidValue;
+    if (a.mx4.wq && (a.nlev != 4 || !a.lev[3].q8 || !a.lev[3].qs || !a.mx4.wsc || !a.mx4.bias || !a.mx4.out ||
+                     a.mx4.ldo % 8 || a.mx4.choff % 32 || (a.mx4.q8 && (!a.mx4.qs || a.mx4.ldo % 32))))
+        return hipErrorInvalidValue;
     if (a.nlev > 3) {
         const StreamEncLevel& L = a.lev[3];
         if (L.N != 128 || L.cin_shift != 6 || a.lev[2].N != 64 || L.nchunk != kEncNC[3] ||
@@ -750,7 +891,11 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
                                            (int)mb[t][st][1][0], (int)mb[t][st][1][1], (int)mb[t][st][1][2], (int)mb[t][st][1][3]};
                     const int sb = (int)((msw[t][st] >> (8 * g)) & 0xFFu);
                     part[t] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bf, part[t], 0, 0, 0, sa, 0, sb);
+                    keep_live(bf);
+                    keep_live(sb);
                 }
+                keep_live(af);
+                keep_live(sa);
             });
         };
         if (p.mx.ksplit == 2) {   // gemm_mx8_kernel's reducer: 0 + slice 0 + slice 1

@@ -478,7 +478,9 @@ def test_fused_stream_bit_exact(monkeypatch, name, dtype, nlms):
     * back: decoder levels 3-1 with their skips, the mask (E / C / R), irFFT
       and overlap-add in one launch (vs three row GEMMs and the back kernel);
       with bit 3 (fp8) decoder level 4's MX-fp8 GEMM as well (scaled MFMA on
-      cat[4]'s shadow, its split-K sum restated): bit-identical to bit 3 off.
+      cat[4]'s shadow, its split-K sum restated), and with bit 4 encoder
+      level 4's in the front (on level 3's shadow kept in LDS): bit-identical
+      to bits 3 and 4 off.
     The same transform code, NLMS arithmetic, 32-k MFMA chunks in the same
     order and epilogues: with the fused front alone (AEC_CRN_STREAM_FUSE=1,
     5) 37 streams over 14 hops agree bit for bit; with the fused back as well the
@@ -507,7 +509,7 @@ def test_fused_stream_bit_exact(monkeypatch, name, dtype, nlms):
     M[:, :n] = torch.from_numpy(np.stack([s[0] for s in sig])).cuda()
     F[:, :n] = torch.from_numpy(np.stack([s[1] for s in sig])).cuda()
     res = {}
-    for flag in ('0', '1', '5', '3', '7', '15'):
+    for flag in ('0', '1', '5', '3', '7', '15', '31'):
         monkeypatch.setenv('AEC_CRN_STREAM_FUSE', flag)
         net.stream_open(B)
         with torch.no_grad():
@@ -522,6 +524,7 @@ def test_fused_stream_bit_exact(monkeypatch, name, dtype, nlms):
     assert rel(res['3'], res['0']) <= 1e-6
     assert rel(res['7'], res['0']) <= 1e-6
     assert np.array_equal(res['15'], res['7'])
+    assert np.array_equal(res['31'], res['7'])
 
 
 @pytest.mark.parametrize('name,dtype,nlms', [('v2E_16000', 'bf16', False), ('v2E_16000', 'fp8', True),
