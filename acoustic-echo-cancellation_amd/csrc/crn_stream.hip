@@ -160,6 +160,17 @@ __device__ __forceinline__ uint2 prelu4_bf16(const f32x4& v, const float4& bias,
 // issue.  An empty asm that reads them after the MFMA forbids both reuses.
 __device__ __forceinline__ void keep_live(const i32x8& b) { asm volatile("" ::"v"(b)); }
 __device__ __forceinline__ void keep_live(int x) { asm volatile("" ::"v"(x)); }
+// After a run of scaled MFMAs: no instruction is scheduled into the run (sched_barrier) and ~48
+// cycles pass before any later instruction may rewrite an operand or scale register.  With the
+// epilogue's register reads ten cycles after the last MFMA, the level's outputs differed from the
+// MX GEMM's in the last bits for a few columns; the scale operands are evidently still read after
+// the issue, and the compiler's hazard recognizer does not pad for it.
+__device__ __forceinline__ void mx_drain() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+static_assert(2 * kPadMapElems >= 16 * 256, "level 4 staging spans both maps");
 
 // mx8_chunk's arithmetic (crn_gemm.h) returning the chunk's 8 e4m3 bytes and its group's E8M0 code
 // instead of storing them (the fused front keeps level 3's shadow in LDS for level 4 as well)
@@ -293,28 +304,6 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
             });
         }
     }
-    // level 4 (MX, optional): this wave's B fragments of N tiles wave + 4 t (t = 0..3), stage st =
-    // tap st: bytes 128 st + 16 g and + 64 (the MX GEMM core's operand map), their scale words, and
-    // the lane's bias per tile (the non-transposed accumulator: column (lane & 15) of the tile)
-    const bool mx4 = p.mx4.wq != nullptr;                        // uniform
-    u32x4 mb4[4][kStreamEncMxStages][2];
-    uint32_t msw4[4][kStreamEncMxStages];
-    float mbias4[4];
-    if (mx4) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int n = (wave + 4 * t) * 16 + (lane & 15);
-            const uint8_t* wr = p.mx4.wq + (int64_t)n * 640 + 16 * (lane >> 4);
-            const uint32_t* sr = reinterpret_cast<const uint32_t*>(p.mx4.wsc + (int64_t)n * 20);
-#pragma unroll
-            for (int st = 0; st < kStreamEncMxStages; ++st) {
-                mb4[t][st][0] = *reinterpret_cast<const u32x4*>(wr + 128 * st);
-                mb4[t][st][1] = *reinterpret_cast<const u32x4*>(wr + 128 * st + 64);
-                msw4[t][st] = (sr[st] >> (8 * (lane >> 4))) & 0xFFu;   // this lane's scale byte
-            }
-            mbias4[t] = p.mx4.bias[n];
-        }
-    }
     sTwT[tid] = t0;
     sTw512[tid] = t1;
     if (tid < 2) sTw512[256 + tid] = t2;
@@ -382,6 +371,30 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
     lds_barrier();
     SPROF(0, 3);
 
+    // level 4 (MX, optional): this wave's B fragments of N tiles wave + 4 t (t = 0..3), stage st =
+    // tap st: bytes 128 st + 16 g and + 64 (the MX GEMM core's operand map), their scale bytes, and
+    // the lane's bias per tile (the non-transposed accumulator: column (lane & 15) of the tile).
+    // Requested here, after the transforms and the NLMS step (180 VGPRs fewer live through them),
+    // so their L2 latency runs under levels 0-3.
+    const bool mx4 = p.mx4.wq != nullptr;                        // uniform
+    u32x4 mb4[4][kStreamEncMxStages][2];
+    uint32_t msw4[4][kStreamEncMxStages];
+    float mbias4[4];
+    if (mx4) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int n = (wave + 4 * t) * 16 + (lane & 15);
+            const uint8_t* wr = p.mx4.wq + (int64_t)n * 640 + 16 * (lane >> 4);
+            const uint32_t* sr = reinterpret_cast<const uint32_t*>(p.mx4.wsc + (int64_t)n * 20);
+#pragma unroll
+            for (int st = 0; st < kStreamEncMxStages; ++st) {
+                mb4[t][st][0] = *reinterpret_cast<const u32x4*>(wr + 128 * st);
+                mb4[t][st][1] = *reinterpret_cast<const u32x4*>(wr + 128 * st + 64);
+                msw4[t][st] = (sr[st] >> (8 * (lane >> 4))) & 0xFFu;   // this lane's scale byte
+            }
+            mbias4[t] = p.mx4.bias[n];
+        }
+    }
     // 4. encoder levels 0-2 (net_conf's shapes, checked by launch_stream_enc): 8 output tiles of 16
     //    bins x 16 channels per level, two per wave (N tile nt = wave % NT, M tiles m0 = wave / NT and
     //    m0 + 4 / NT); the implicit A rows read the input map in LDS (input bin 2 j - 2 + tap, zero
@@ -486,6 +499,7 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
                 acc4[t] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[st], bfrag(t, si), acc4[t], 0, 0, 0, sa[st], 0,
                                                                            (int)msw4[t][st]);
         });
+        mx_drain();
         aec::static_for<0, kStreamEncMxStages>([&](auto si) {
             constexpr int st = decltype(si)::value;
             keep_live(af[st]);
@@ -496,17 +510,18 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
                 keep_live((int)msw4[t][st]);
             }
         });
-        bf16_t* st4 = sMap[0];                                      // [8 rows][256 channels]
-        if (g < 2) {
+        // every lane writes its rows, the unused 8 .. 15 included: with a `g < 2` guard the compiler
+        // sank the MFMAs (pure, used only there) into the lanes-0..31 region, where the operand moves
+        // of lanes 32..63 (k bytes 32..63, 96..127 of every row) did not run
+        bf16_t* st4 = &sMap[0][0];                                  // [16 rows][256 channels] (both maps)
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int n = (wave + 4 * t) * 16 + r;
+        for (int t = 0; t < 4; ++t) {
+            const int n = (wave + 4 * t) * 16 + r;
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr) {
-                    float v = acc4[t][rr] + mbias4[t];
-                    v = v >= 0.f ? v : p.mx4.alpha * v;
-                    st4[(4 * g + rr) * 256 + n] = f2bf(v);
-                }
+            for (int rr = 0; rr < 4; ++rr) {
+                float v = acc4[t][rr] + mbias4[t];
+                v = v >= 0.f ? v : p.mx4.alpha * v;
+                st4[(4 * g + rr) * 256 + n] = f2bf(v);
             }
         }
         lds_barrier();
@@ -903,6 +918,7 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
             f32x4 p1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
             run(std::integral_constant<int, 0>{}, std::integral_constant<int, 3>{}, p0);
             run(std::integral_constant<int, 3>{}, std::integral_constant<int, 6>{}, p1);
+            mx_drain();
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
                 acc[t] += p0[t];
@@ -910,6 +926,7 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
             }
         } else {
             run(std::integral_constant<int, 0>{}, std::integral_constant<int, 6>{}, acc);
+            mx_drain();
         }
         // epilogue (rows_epilogue_lds's: + bias, PReLU, bf16): acc[t][rr] = row 4 g + rr, column n
 #pragma unroll
@@ -955,6 +972,9 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
         const bf16_t* in[1] = {sIn[2]};
         conv_tiles<1, kStreamDecChunks2, 5, 32 + 8, 1, -1, 3, 128, kStreamDecChunks2, true>(acc2, in, bw2, m0[2], m1[2], lane);
         const f32x4 (&acc)[2] = acc2[0];
+        // materialised in every lane before the lane-divergent store (else the compiler may sink the
+        // MFMAs into it, where the other lanes' operand reads do not run; see the level-4 epilogue)
+        asm volatile("" ::"v"(acc[0]), "v"(acc[1]));
         // the 4 columns (parity, re / im) of input bin i sit in the lanes with lane >> 4 == 0
         if ((lane >> 4) == 0) {
 #pragma unroll
