@@ -1941,8 +1941,14 @@ aec_status aec_crn_stream_open(aec_crn_handle* h, int32_t B) {
     }
     ss.enc_nlev = stream_enc_levels(h);
     ss.dec_fused = stream_dec_ok(h);
-    ss.dec_mx = ss.dec_fused && stream_dec_mx_ok(h);
-    ss.enc_mx = ss.enc_nlev == 4 && stream_enc_mx_ok(h);
+    // the MX folds (one block per stream, 1 wave per SIMD) win while every stream has a CU of its own;
+    // past that the unfolded kernels' occupancy (2-3 waves per SIMD) wins: 4,096 streams 4.08 M vs
+    // 3.35 M frames/s with both folds, 256 streams 0.1134 vs 0.1204 ms per hop (profiles/r04v_c5_fold_sweep.txt)
+    int ncu = 256;
+    CRN_TRY(h, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
+    const bool fold = B <= ncu;
+    ss.dec_mx = fold && ss.dec_fused && stream_dec_mx_ok(h);
+    ss.enc_mx = fold && ss.enc_nlev == 4 && stream_enc_mx_ok(h);
     CRN_TRY(h, hipStreamCreateWithFlags(&ss.cap, hipStreamNonBlocking));
     CRN_TRY(h, hipDeviceSynchronize());
     ss.k = 0;

@@ -217,8 +217,11 @@ __device__ __forceinline__ void x0_put(bf16_t* x0, int k, float2 m, float2 f) {
 
 }  // namespace
 
-template <int TAPS>
-__global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
+// MX4: encoder level 4 folded in (its weight fragments hold ~180 VGPRs, so the kernel without it is
+// a separate instantiation: at many streams per CU its occupancy, not the extra launch, decides;
+// without the fold and with <= 4 taps it fits 2 waves per SIMD with no scratch)
+template <int TAPS, bool MX4>
+__global__ __launch_bounds__(256, MX4 || TAPS > 4 ? 1 : 2) void crn_stream_enc_kernel(StreamEncArgs p) {
     __shared__ __attribute__((aligned(16))) float sTab[256 * 2 + 258 * 2 + 512];
     __shared__ __attribute__((aligned(16))) float sGrp[2][aec::kGroupFloats];
     __shared__ __attribute__((aligned(16))) float2 sRow[2][256];
@@ -376,7 +379,7 @@ __global__ __launch_bounds__(256) void crn_stream_enc_kernel(StreamEncArgs p) {
     // the lane's bias per tile (the non-transposed accumulator: column (lane & 15) of the tile).
     // Requested here, after the transforms and the NLMS step (180 VGPRs fewer live through them),
     // so their L2 latency runs under levels 0-3.
-    const bool mx4 = p.mx4.wq != nullptr;                        // uniform
+    constexpr bool mx4 = MX4;                                    // launch_stream_enc: == (p.mx4.wq != nullptr)
     u32x4 mb4[4][kStreamEncMxStages][2];
     uint32_t msw4[4][kStreamEncMxStages];
     float mbias4[4];
@@ -555,7 +558,12 @@ hipError_t launch_stream_enc(const StreamEncArgs& a, int taps, hipStream_t st) {
     }
     switch (taps) {
 #define CRN_ENC_CASE(N)                                                                               \
-    case N: hipLaunchKernelGGL((crn_stream_enc_kernel<N>), dim3((unsigned)a.B), dim3(256), 0, st, a); break;
+    case N:                                                                                           \
+        if (a.mx4.wq)                                                                                 \
+            hipLaunchKernelGGL((crn_stream_enc_kernel<N, true>), dim3((unsigned)a.B), dim3(256), 0, st, a); \
+        else                                                                                          \
+            hipLaunchKernelGGL((crn_stream_enc_kernel<N, false>), dim3((unsigned)a.B), dim3(256), 0, st, a); \
+        break;
         CRN_ENC_CASE(0) CRN_ENC_CASE(1) CRN_ENC_CASE(2) CRN_ENC_CASE(3) CRN_ENC_CASE(4)
         CRN_ENC_CASE(5) CRN_ENC_CASE(6) CRN_ENC_CASE(7) CRN_ENC_CASE(8)
 #undef CRN_ENC_CASE
@@ -765,7 +773,8 @@ __device__ __forceinline__ void load_bw(u32x4 (&bw)[NC], const StreamDecLevel& L
 
 }  // namespace
 
-template <int MODE>
+// MX: decoder level cl = 4 folded in (a separate instantiation, as crn_stream_enc_kernel's MX4)
+template <int MODE, bool MX>
 __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
     constexpr int kMap = 5120;                    // bf16 elements of a level's padded input map (Fin x (Cin + 8))
     __shared__ __attribute__((aligned(16))) bf16_t sIn[3][kMap];
@@ -790,7 +799,7 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
     constexpr int kDecPieces = 2;
     u32x4 mp[kDecPieces + 2];
     const StreamDecLevel& L0 = p.lev[0];
-    const bool mx = p.mx.wq != nullptr;                         // uniform
+    constexpr bool mx = MX;                                     // launch_stream_dec: == (p.mx.wq != nullptr)
     const u32x4* src0 = reinterpret_cast<const u32x4*>(L0.src + (int64_t)b * (32 << L0.cin_shift));
     // cl = 4 (MX): cat[4]'s shadow row pieces (16 bins x 256 B, one per thread), its scales (16 x 8
     // B, threads < 32), this wave's B fragments of N tiles wave, wave + 4 (stage st: bytes 128 st +
@@ -1219,12 +1228,17 @@ hipError_t launch_stream_dec(const StreamDecArgs& a, int mode, hipStream_t st) {
         const int C = 1 << L.cin_shift;
         if (l == 0 ? Fin * C != 2 * 256 * 8 : Fin * (C / 2) != 256 * 8) return hipErrorInvalidValue;   // the load's piece counts
     }
-    switch (mode) {
-        case 0: hipLaunchKernelGGL(crn_stream_dec_kernel<0>, dim3((unsigned)a.B), dim3(256), 0, st, a); break;
-        case 1: hipLaunchKernelGGL(crn_stream_dec_kernel<1>, dim3((unsigned)a.B), dim3(256), 0, st, a); break;
-        case 2: hipLaunchKernelGGL(crn_stream_dec_kernel<2>, dim3((unsigned)a.B), dim3(256), 0, st, a); break;
-        default: return hipErrorInvalidValue;
+    if (mode < 0 || mode > 2) return hipErrorInvalidValue;
+    const bool mx = a.mx.wq != nullptr;
+#define CRN_DEC_CASE(M)                                                                                     \
+    if (mode == M) {                                                                                        \
+        if (mx)                                                                                             \
+            hipLaunchKernelGGL((crn_stream_dec_kernel<M, true>), dim3((unsigned)a.B), dim3(256), 0, st, a);  \
+        else                                                                                                \
+            hipLaunchKernelGGL((crn_stream_dec_kernel<M, false>), dim3((unsigned)a.B), dim3(256), 0, st, a); \
     }
+    CRN_DEC_CASE(0) CRN_DEC_CASE(1) CRN_DEC_CASE(2)
+#undef CRN_DEC_CASE
     return hipGetLastError();
 }
 

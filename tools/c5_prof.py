@@ -10,5 +10,5 @@ sys.argv = ['bench.py']
 import bench  # noqa: E402
 import torch  # noqa: E402
 
-r = bench.run_c5_stream(torch.device('cuda', 0), hops=int(os.environ.get('HOPS', '200')), sweep=())
+r = bench.run_c5_stream(torch.device('cuda', 0), B=int(os.environ.get('STREAMS', '256')), hops=int(os.environ.get('HOPS', '200')), sweep=())
 print(json.dumps(r))
