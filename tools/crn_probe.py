@@ -7,6 +7,7 @@ the per-stage HIP-event breakdown.  Run on the GPU box:
 """
 import argparse
 import copy
+import hashlib
 import json
 import os
 import sys
@@ -85,7 +86,8 @@ def main():
     print(json.dumps(dict(B=a.B, N=a.N, dtype=a.dtype, ms_per_call=dt * 1e3, frames_per_s=frames / dt,
                           stage_ms={k: v / max(calls, 1) for k, v in
                                     zip(['front', 'encoder', 'lstm', 'decoder', 'back'], ms)},
-                          finite=bool(torch.isfinite(out).all()))), flush=True)
+                          finite=bool(torch.isfinite(out).all()),
+                          out_sha1=hashlib.sha1(out.cpu().numpy().tobytes()).hexdigest()[:16])), flush=True)
 
 
 if __name__ == '__main__':
