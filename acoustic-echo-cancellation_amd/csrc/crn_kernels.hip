@@ -1987,7 +1987,7 @@ __global__ __launch_bounds__(256) void lstm_step_mx8_kernel(StepMxArgs p) {
     for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int st = 0; st < nst; ++st) {
+    for (int st = 0; st < ((p.mode & 1) ? 0 : nst); ++st) {
         if (st + NBUF - 2 < nst)
             wait_vm<(NBUF - 2) * (LA + LB)>();
         else
@@ -2046,6 +2046,7 @@ __global__ __launch_bounds__(256) void lstm_step_mx8_kernel(StepMxArgs p) {
             sH[r * HS + j] = h;
         }
     __syncthreads();
+    if (p.mode & 2) return;
     // 3a. h_t as e4m3 + E8M0 (4 threads per row, 8 units each), and f32 -> hx for the partner block
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.hx, (uint64_t)p.B * C * S * H * 4);
 #pragma unroll
@@ -2083,7 +2084,7 @@ __global__ __launch_bounds__(256) void lstm_step_mx8_kernel(StepMxArgs p) {
     // 3b. the combination of stream bl, units jj .. jj + 3 (8 threads per stream): own cell's h
     //     from LDS, the partner's from hx
 #pragma unroll
-    for (int bp = 0; bp < (SB + 31) / 32; ++bp) {
+    for (int bp = 0; bp < ((p.mode & 4) ? 0 : (SB + 31) / 32); ++bp) {
         const int bl = bp * 32 + (tid >> 3), jj = (tid & 7) * 4, b = b0 + bl;
         if (SB % 32 && bl >= SB) break;                 // SB = 16: threads 128.. idle here (8-lane groups intact)
         const int oc = 1 - cell;
@@ -2146,8 +2147,11 @@ hipError_t launch_lstm_step_mx8(const StepMxArgs& a, hipStream_t st) {
                                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
         if (attr != hipSuccess) return attr;                                                                      \
         const int nsb = (a.B + SB_ - 1) / SB_;                                                                    \
-        hipLaunchKernelGGL(kern, dim3(a.H / 32, 2 * nsb), dim3(256), lds, st, a);                                 \
+        hipLaunchKernelGGL(kern, dim3(a.H / 32, 2 * nsb), dim3(256), lds, st, a2);                                \
     } while (0)
+    static const int smode = env_int("CRN_MX_STEP_MODE", 0);
+    StepMxArgs a2 = a;
+    a2.mode = smode;
     const char* sreg_env = getenv("AEC_CRN_MX_SREG");  // read per launch (captured once per stream open)
     const int sreg = sreg_env ? atoi(sreg_env) : 1;
     if (a.H == 1024 && sreg)

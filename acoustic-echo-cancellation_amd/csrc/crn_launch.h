@@ -137,6 +137,7 @@ struct StepMxArgs {
     uint8_t* q8;                // their MX-fp8 shadow (RowEpi::q8 layout), nullable
     uint8_t* qs;
     int32_t B, H;
+    int32_t mode = 0;           // timing experiments only (CRN_MX_STEP_MODE; results invalid unless 0)
 };
 hipError_t launch_lstm_step_mx8(const StepMxArgs& a, hipStream_t st);
 // the layout preconditions of lstm_step_mx8_kernel (H % 256, 128-k stages inside one x tap, 32-unit
