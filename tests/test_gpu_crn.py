@@ -527,6 +527,49 @@ def test_fused_stream_bit_exact(monkeypatch, name, dtype, nlms):
     assert np.array_equal(res['31'], res['7'])
 
 
+def test_fp8_stream_fold_policy_bit_exact():
+    """The per-hop step folds the MX-fp8 encoder level 4 / decoder level cl = 4 into the fused front
+    / back only while every stream has a CU of its own (aec_crn_stream_open: streams <= CUs; past
+    that the unfolded kernels' occupancy wins, profiles/r04v_c5_fold_sweep.txt).  Both forms run
+    the same MFMA chains and epilogues and every stream's rows are independent of the others, so
+    37 streams (folds on) and the same 37 streams inside a CUs + 44 stream handle (folds off) agree
+    bit for bit over 13 hops: net_conf, fp8, 4-tap FD-NLMS (BASELINE config 5's step)."""
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+    from aec_amd import synth
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    m = META['v2E_16000']
+    conf = copy.deepcopy(aec_amd.net_conf)
+    conf.update(m['overrides'])
+    net = aec_amd.dccrn2.DCCRN(conf, dtype='fp8', nlms=dict(taps=4, mu=0.3, beta=0.5, delta=1e-4)).eval()
+    sd = net.state_dict()
+    for k, v in C.make_weights(conf, 2, m['weight_seed']).items():
+        sd[k] = torch.from_numpy(v)
+    net.load_state_dict(sd, strict=True)
+    net = net.to('cuda:0')
+    n, Bs, Bb = 3072, 37, ncu + 44
+    nh = n // 256 + 1
+    sig = [synth.scene(n, 3100 + b) for b in range(Bs)]
+    M = torch.zeros(Bb, 256 * (nh + 1), device='cuda:0')
+    F = torch.zeros_like(M)
+    M[:Bs, :n] = torch.from_numpy(np.stack([s[0] for s in sig])).cuda()
+    F[:Bs, :n] = torch.from_numpy(np.stack([s[1] for s in sig])).cuda()
+    g = torch.Generator(device='cuda:0').manual_seed(7)
+    M[Bs:, :n] = 0.1 * torch.randn(Bb - Bs, n, device='cuda:0', generator=g)
+    F[Bs:, :n] = 0.1 * torch.randn(Bb - Bs, n, device='cuda:0', generator=g)
+    res = {}
+    for B in (Bs, Bb):
+        net.stream_open(B)
+        with torch.no_grad():
+            outs = [net.stream_step(M[:B, 256 * k:256 * (k + 1)], F[:B, 256 * k:256 * (k + 1)]).clone()
+                    for k in range(nh)]
+        torch.cuda.synchronize()
+        res[B] = torch.cat(outs, dim=1).cpu().numpy()
+    assert np.isfinite(res[Bb]).all()
+    assert np.abs(res[Bs]).max() > 0
+    assert np.array_equal(res[Bb][:Bs], res[Bs])
+
+
 @pytest.mark.parametrize('name,dtype,nlms', [('v2E_16000', 'bf16', False), ('v2E_16000', 'fp8', True),
                                              ('v1_2125', 'bf16', True), ('v1_2125', 'bf16', False),
                                              ('v2C_bn_2125', 'fp8', False), ('v2R_1000', 'bf16', False)])
