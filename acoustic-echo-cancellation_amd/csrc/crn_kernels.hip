@@ -1766,12 +1766,78 @@ __global__ __launch_bounds__(256) void lstm_combine_kernel(const T* __restrict__
     }
 }
 
+// bf16, 2 cells x 2 sequences: the same per-element arithmetic, 8 adjacent units per thread (16-B
+// loads of the four rows, 16-B stores of real and imag; the MX shadow's 32-unit group = 4 adjacent
+// lanes, its 8 bytes per lane in one store), launch_lstm_combine checks the alignment
+__global__ __launch_bounds__(256) void lstm_combine8_kernel(const bf16_t* __restrict__ y, bf16_t* __restrict__ dst,
+                                                            int64_t nframes, int H, int dshift, int64_t ldf, int64_t ldd,
+                                                            uint8_t* __restrict__ q8, uint8_t* __restrict__ qs) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;    // (frame, j / 8)
+    const int H8 = H >> 3;
+    if (idx >= nframes * H8) return;                                 // wave-uniform (H % 512 == 0)
+    const int64_t f = idx / H8;
+    const int j = (int)(idx - f * H8) * 8;
+    const bf16_t* row = y + f * 4 * (int64_t)H + j;
+    u32x4 v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = *reinterpret_cast<const u32x4*>(row + (int64_t)r * H);
+    auto el = [](const u32x4& w, int i) { return __uint_as_float(i & 1 ? (w[i >> 1] & 0xFFFF0000u) : (w[i >> 1] << 16)); };
+    float xr[8], xi[8];
+    u32x4 orr, oi;
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+        const bf16_t r0 = f2bf(el(v[0], i) - el(v[3], i)), r1 = f2bf(el(v[0], i + 1) - el(v[3], i + 1));
+        const bf16_t i0 = f2bf(el(v[1], i) + el(v[2], i)), i1 = f2bf(el(v[1], i + 1) + el(v[2], i + 1));
+        orr[i >> 1] = (uint32_t)r0 | ((uint32_t)r1 << 16);
+        oi[i >> 1] = (uint32_t)i0 | ((uint32_t)i1 << 16);
+        xr[i] = bf2f(r0), xr[i + 1] = bf2f(r1), xi[i] = bf2f(i0), xi[i + 1] = bf2f(i1);
+    }
+    const int64_t o = f * ldf + (int64_t)(j >> dshift) * ldd + (j & ((1 << dshift) - 1));
+    *reinterpret_cast<u32x4*>(dst + o) = orr;
+    *reinterpret_cast<u32x4*>(dst + o + (1 << dshift)) = oi;
+    if (q8) {
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+            const float* x = h2 ? xi : xr;
+            float amax = 0.f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(x[i]));
+            amax = fmaxf(amax, __shfl_xor(amax, 1));
+            amax = fmaxf(amax, __shfl_xor(amax, 2));
+            const int ebits = (int)((__float_as_uint(amax) >> 23) & 0xFF);
+            const int code = ebits > 8 ? ebits - 8 : 0;
+            uint32_t pk[2];
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+                float q[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) q[i] = fminf(fmaxf(ldexpf(x[4 * w + i], 127 - code), -448.f), 448.f);
+                int t = __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], 0, false);
+                t = __builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], t, true);
+                pk[w] = (uint32_t)t;
+            }
+            const int64_t oo = o + (h2 ? (1 << dshift) : 0);
+            *reinterpret_cast<uint2*>(q8 + oo) = make_uint2(pk[0], pk[1]);
+            if ((j & 31) == 0) qs[oo >> 5] = (uint8_t)code;
+        }
+    }
+}
+
 template <typename T>
 hipError_t launch_lstm_combine(const T* y, T* dst, int64_t nframes, int H, int cells, int seqs, int dshift,
                                int64_t ldf, int64_t ldd, hipStream_t st, uint8_t* q8, uint8_t* qs) {
     const int64_t n = nframes * H;
     if (n <= 0) return hipSuccess;
     if (q8 && (H % 64 || (1 << dshift) % 32 || cells * seqs != 4)) return hipErrorInvalidValue;
+    const int vec = env_int("CRN_COMBINE_VEC", 1);             // read per call (tests compare both forms)
+    if constexpr (sizeof(T) == 2) {
+        if (vec && cells == 2 && seqs == 2 && H % 512 == 0 && dshift >= 5 && ldf % 8 == 0 && ldd % 8 == 0 &&
+            ((reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0) {
+            const dim3 g8((unsigned)((n / 8 + 255) / 256));
+            hipLaunchKernelGGL(lstm_combine8_kernel, g8, dim3(256), 0, st, y, dst, nframes, H, dshift, ldf, ldd, q8, qs);
+            return hipGetLastError();
+        }
+    }
     const dim3 grid((unsigned)((n + 255) / 256));
     if (cells == 2 && seqs == 2)
         hipLaunchKernelGGL((lstm_combine_kernel<T, 2, 2>), grid, dim3(256), 0, st, y, dst, nframes, H, dshift, ldf,

@@ -527,6 +527,32 @@ def test_fused_stream_bit_exact(monkeypatch, name, dtype, nlms):
     assert np.array_equal(res['31'], res['7'])
 
 
+@pytest.mark.parametrize('dtype', ['bf16', 'fp8'])
+def test_lstm_combine_vector_form_bit_exact(monkeypatch, dtype):
+    """NavieComplexLSTM's real / imag combination (dccrn.py:443-446) in its 8-units-per-thread form
+    (16-B row loads and stores, the MX shadow's 32-unit group over 4 lanes) against the one-unit
+    form (CRN_COMBINE_VEC=0, read per call): the same per-element bf16 arithmetic and E8M0 rule, so
+    the batch forward's output is bit-identical (5 ragged streams of net_conf)."""
+    from aec_amd import synth
+    net, m, conf = build('v2E_16000', dtype)
+    lens = [16000, 12345, 9000, 16000, 4100]
+    sig = [synth.scene(n, 4200 + b) for b, n in enumerate(lens)]
+    mic = torch.zeros(len(lens), max(lens), device='cuda:0')
+    far = torch.zeros_like(mic)
+    for b, sc in enumerate(sig):
+        mic[b, :lens[b]] = torch.from_numpy(sc[0])
+        far[b, :lens[b]] = torch.from_numpy(sc[1])
+    res = {}
+    for flag in ('0', '1'):
+        monkeypatch.setenv('CRN_COMBINE_VEC', flag)
+        with torch.no_grad():
+            out, _, _ = net.forward_ragged(mic, far, lens, want_spec=False)
+        torch.cuda.synchronize()
+        res[flag] = out.cpu().numpy()
+    assert np.isfinite(res['1']).all() and np.abs(res['1']).max() > 0
+    assert np.array_equal(res['1'], res['0'])
+
+
 def test_fp8_stream_fold_policy_bit_exact():
     """The per-hop step folds the MX-fp8 encoder level 4 / decoder level cl = 4 into the fused front
     / back only while every stream has a CU of its own (aec_crn_stream_open: streams <= CUs; past
