@@ -1469,7 +1469,11 @@ static crn::StreamDecArgs stream_dec_args(aec_crn_handle* h, int B) {
 // map shapes of configs.net_conf's narrow levels)
 static bool stream_dec_ok(const aec_crn_handle* h) {
     if (h->es != 2 || h->L < 3) return false;
-    const char* v = getenv("AEC_CRN_STREAM_FUSE");   // bit 0: fused front, bit 1: fused back (default 3)
+    // AEC_CRN_STREAM_FUSE (A/B knob; unset = every bit on, i.e. 31): bit 0 fused front (encoder
+    // levels 0-2), bit 1 fused back (decoder cl = 3..1 + mask + irFFT), bit 2 encoder level 3 in the
+    // front, bit 3 decoder cl = 4 (MX) in the back, bit 4 encoder level 4 (MX) in the front; the MX
+    // folds (bits 3, 4) are further limited to streams <= CUs at stream_open
+    const char* v = getenv("AEC_CRN_STREAM_FUSE");
     if (v && !(atoi(v) & 2)) return false;
     const int* ch = h->cfg.conv_channels;
     const int caps[3] = {crn::kStreamDecChunks0, crn::kStreamDecChunks1, crn::kStreamDecChunks2};

@@ -241,6 +241,9 @@ __global__ __launch_bounds__(256) void crn_back_kernel(BackArgs p) {
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
                     if (c < nch) mma_chunk(acc, a[c], bw[c], bf16_t{});
+                // pin the accumulators in all lanes: otherwise the compiler may sink the MFMAs and
+                // their operand loads into the lane-divergent store region below
+                asm volatile("" ::"v"(acc));
                 if (n < 4)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {

@@ -158,17 +158,26 @@ __device__ __forceinline__ uint2 prelu4_bf16(const f32x4& v, const float4& bias,
 // its registers to the MFMA's own destination (vdst = a[56:59] with srcB = a[56:63]), which read
 // back corrupted operands (NaN outputs); the scale registers were rewritten two cycles after the
 // issue.  An empty asm that reads them after the MFMA forbids both reuses.
+// CRN_NO_CODEGEN_GUARDS (tests/test_isa_guard.py only, never a product build): every workaround of
+// this file compiled out, so the CPU-side code-object check can show that it catches their absence.
+#ifndef CRN_NO_CODEGEN_GUARDS
 __device__ __forceinline__ void keep_live(const i32x8& b) { asm volatile("" ::"v"(b)); }
 __device__ __forceinline__ void keep_live(int x) { asm volatile("" ::"v"(x)); }
+#else
+__device__ __forceinline__ void keep_live(const i32x8&) {}
+__device__ __forceinline__ void keep_live(int) {}
+#endif
 // After a run of scaled MFMAs: no instruction is scheduled into the run (sched_barrier) and ~48
 // cycles pass before any later instruction may rewrite an operand or scale register.  With the
 // epilogue's register reads ten cycles after the last MFMA, the level's outputs differed from the
 // MX GEMM's in the last bits for a few columns; the scale operands are evidently still read after
 // the issue, and the compiler's hazard recognizer does not pad for it.
 __device__ __forceinline__ void mx_drain() {
+#ifndef CRN_NO_CODEGEN_GUARDS
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+#endif
 }
 static_assert(2 * kPadMapElems >= 16 * 256, "level 4 staging spans both maps");
 
@@ -728,16 +737,27 @@ bool enc_batch_ok(const EncBatchArgs& a) {
     return true;
 }
 
+// Grid of a persistent frame-loop kernel: CUs x resident 256-thread blocks, cached per device id
+// (handles on different devices of one process each get their own device's figure).
+template <typename K>
+static int persistent_grid(K* kern) {
+    constexpr int kMaxDev = 64;
+    static int cache[kMaxDev] = {};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= kMaxDev) dev = 0;
+    if (cache[dev] == 0) {
+        int ncu = 0, per = 0;
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(kern), 256, 0);
+        cache[dev] = std::max(1, ncu) * std::max(1, per);
+    }
+    return cache[dev];
+}
+
 template <int FR>
 static hipError_t launch_enc_batch_fr(const EncBatchArgs& a, hipStream_t st) {
-    static const int grid = [] {
-        int dev = 0, ncu = 0, per = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(crn_enc_batch_kernel<FR>),
-                                                           256, 0);
-        return std::max(1, ncu) * std::max(1, per);
-    }();
+    const int grid = persistent_grid(crn_enc_batch_kernel<FR>);
     const int64_t need = (a.F + FR - 1) / FR;
     hipLaunchKernelGGL(crn_enc_batch_kernel<FR>, dim3((unsigned)std::min<int64_t>(grid, need)), dim3(256), 0, st, a);
     return hipGetLastError();
@@ -983,7 +1003,9 @@ __global__ __launch_bounds__(256) void crn_stream_dec_kernel(StreamDecArgs p) {
         const f32x4 (&acc)[2] = acc2[0];
         // materialised in every lane before the lane-divergent store (else the compiler may sink the
         // MFMAs into it, where the other lanes' operand reads do not run; see the level-4 epilogue)
+#ifndef CRN_NO_CODEGEN_GUARDS
         asm volatile("" ::"v"(acc[0]), "v"(acc[1]));
+#endif
         // the 4 columns (parity, re / im) of input bin i sit in the lanes with lane >> 4 == 0
         if ((lane >> 4) == 0) {
 #pragma unroll
@@ -1201,14 +1223,7 @@ hipError_t launch_dec_batch(const DecBatchArgs& a, hipStream_t st) {
     if (a.F <= 0) return hipSuccess;
     if (!dec_batch_ok(a)) return hipErrorInvalidValue;
     constexpr int FR = 4;
-    static const int grid = [] {
-        int dev = 0, ncu = 0, per = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(crn_dec_batch_kernel<FR>),
-                                                           256, 0);
-        return std::max(1, ncu) * std::max(1, per);
-    }();
+    const int grid = persistent_grid(crn_dec_batch_kernel<FR>);
     const int64_t need = (a.F + FR - 1) / FR;
     hipLaunchKernelGGL(crn_dec_batch_kernel<FR>, dim3((unsigned)std::min<int64_t>(grid, need)), dim3(256), 0, st, a);
     return hipGetLastError();

@@ -126,6 +126,8 @@ def roofline(pipeline, kernel, ms_per_launch, frames_per_launch, pmc):
     path = dict(alg_bytes_per_frame=PIPE['bytes'], alg_flops_per_frame=fl, achieved_gbs=round(pg, 1),
                 achieved_tflops=round(pt, 3), frac=round(max(pg / HBM_PEAK_GBS, pt / FP32_PEAK_TFLOPS), 4))
     common = dict(traffic=traffic, traffic_alg_bytes_per_launch=a['bytes'] * frames_per_launch, kernel=kernel,
+                  frac_basis='kernel_share: this kernel\'s own algorithmic bytes / FLOPs (DESIGN.md §5); '
+                             'path_priced.frac charges the whole path to it (the pre-round-4 definition)',
                   alg_bytes_per_frame=a['bytes'], alg_flops_per_frame=a['flops'],
                   frames_per_launch=frames_per_launch, ms_per_launch=round(ms_per_launch, 4),
                   hbm_frac=round(gbs / HBM_PEAK_GBS, 4), fp32_frac=round(tfl / FP32_PEAK_TFLOPS, 4),
@@ -175,6 +177,7 @@ def cpu_baseline(seconds, B=256, n=160000):
 
 
 BF16_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
+FP8_PEAK_TFLOPS = 5000.0      # MI355X_MICROARCH.md: dense FP8 (block-scaled e4m3: 2x the bf16 rate)
 CRN_STAGES = ['front', 'encoder', 'lstm', 'decoder', 'back']
 
 
@@ -194,15 +197,16 @@ def crn_flops_per_frame(conf, version):
     return dict(encoder=enc, decoder=dec, lstm=rnn, total=enc + dec + rnn)
 
 
-def cpu_baseline_crn(seconds, conf, version, n=160000, B=1):
+def cpu_baseline_crn(seconds, conf, version, n=160000, B=1, nlms=None):
     """The reference op mix (oracle/torch_crn_port.py: conv2d / conv_transpose2d /
-    nn.LSTM, float32) on host cores, bounded sample."""
+    nn.LSTM, float32; with nlms, the FD-NLMS front end in front) on host cores,
+    bounded sample."""
     import torch
     sys.path.insert(0, os.path.join(REPO, 'oracle'))
     import crn_oracle
     from torch_crn_port import TorchCrnPort
     from aec_amd import synth
-    port = TorchCrnPort(crn_oracle.make_weights(conf, version, 1), conf, version)
+    port = TorchCrnPort(crn_oracle.make_weights(conf, version, 1), conf, version, nlms=nlms)
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     mic, far, _ = (torch.from_numpy(a) for a in synth.batch(B, n, seed0=7000))
@@ -218,7 +222,8 @@ def cpu_baseline_crn(seconds, conf, version, n=160000, B=1):
             break
     return dict(value=round(frames / el, 1), unit='frames/s', cores=threads, kind='port',
                 sample=f'{reps} x [{B} stream x {n} samples] through oracle/torch_crn_port.py '
-                       f'(reference op mix: conv2d / conv_transpose2d / nn.LSTM, float32), {el:.1f} s wall')
+                       f'(reference op mix: conv2d / conv_transpose2d / nn.LSTM, float32'
+                       f'{", FD-NLMS front end" if nlms else ""}), {el:.1f} s wall')
 
 
 def erle_check(run_gpu, run_ref, n, streams=2):
@@ -255,7 +260,7 @@ def _init_dist(torch, dist, world, local):
     return local
 
 
-def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu, nlms=None):
+def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu, nlms=None, with_erle=None):
     """BASELINE config 3: the DCCRN post-filter (dccrn2.py, configs.net_conf) on
     B streams x n samples; returns the measurements (timing = max over ranks).
     nlms: the FD-NLMS front end (C5: NLMS -> CRN, include/aec_crn.h), timed
@@ -265,6 +270,8 @@ def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu, nlms=N
     import torch.distributed as dist
     import aec_amd
     from aec_amd import shard, synth
+    if with_erle is None:
+        with_erle = with_cpu
     conf = dict(aec_amd.net_conf)
     T = n // 256 + 1
     torch.manual_seed(0)                         # the reference's own init (random weights, no checkpoint ships)
@@ -331,6 +338,14 @@ def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu, nlms=N
     dom = max(stage_ms, key=stage_ms.get)
     dom_fl = fl.get(dom, 0)
     ach = dom_fl * B * T / (stage_ms[dom] * 1e-3) / 1e12 if dom_fl else 0.0
+    dom_peak, peak_note = peak, None
+    if dtype == 'fp8' and dom == 'lstm':
+        # the fp8 LSTM stage: the input projections (half the stage's FLOPs: W_ih x) run on the scaled
+        # MX-fp8 MFMA (dense fp8 peak), the batch recurrence (W_hh h, the other half) stays bf16
+        t_pk = (dom_fl / 2) / FP8_PEAK_TFLOPS + (dom_fl / 2) / BF16_PEAK_TFLOPS
+        dom_peak = round(dom_fl / t_pk, 1)
+        peak_note = ('blended: input-projection half (MX-fp8) at %.0f TF/s, recurrence half (bf16) at %.0f TF/s'
+                     % (FP8_PEAK_TFLOPS, BF16_PEAK_TFLOPS))
     whole = fl['total'] * B * T / (ms_step * 1e-3) / 1e12
     # HBM bytes of the LSTM stage per batch from the committed PMC passes
     # (profiles/pmc_latest_crn.json, tools/crn_pmc.sh + tools/crn_pmc_latest.py), same shape and dtype only
@@ -343,19 +358,20 @@ def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu, nlms=N
     res = dict(value=round(value, 1), value_per_gpu=round(value / world, 1), ms_per_step=round(ms_step, 3),
                batches_in_flight=inflight,
                rtf_batch1=rtf1, stage_ms_per_step={k: round(v, 3) for k, v in stage_ms.items()},
-               roofline={'bound': 'mfma', 'achieved': round(ach, 1), 'peak': peak, 'unit': 'TFLOP/s',
-                         'frac': round(ach / peak, 4), 'traffic': traffic,
+               roofline={'bound': 'mfma', 'achieved': round(ach, 1), 'peak': dom_peak, 'unit': 'TFLOP/s',
+                         'frac': round(ach / dom_peak, 4), 'traffic': traffic, 'peak_note': peak_note,
                          'kernel': f'{dom} stage ({"input GEMM + per-frame recurrence steps + combine per layer" if dom == "lstm" else "GEMM launches"})',
                          'alg_flops_per_frame': dom_fl, 'frames_per_launch': B * T},
                pipeline_roofline={'alg_flops_per_frame': fl['total'], 'achieved_tflops': round(whole, 1),
                                   'mfma_frac': round(whole / peak, 4)},
                erle=None, cpu_baseline=None)
-    if with_cpu and rank == 0 and world == 1 and not nlms:
-        res['cpu_baseline'] = cpu_baseline_crn(args.cpu_seconds, conf, args.crn_version, n=n)
+    if with_erle and rank == 0 and world == 1:
+        if with_cpu:
+            res['cpu_baseline'] = cpu_baseline_crn(args.cpu_seconds, conf, args.crn_version, n=n, nlms=nlms)
         sys.path.insert(0, os.path.join(REPO, 'oracle'))
         from torch_crn_port import TorchCrnPort
         wref = {k: v.detach().cpu().numpy() for k, v in net.state_dict().items()}
-        port = TorchCrnPort(wref, conf, args.crn_version)
+        port = TorchCrnPort(wref, conf, args.crn_version, nlms=nlms)
 
         def gpu1(m_, f_, _n):
             with torch.no_grad():
@@ -365,12 +381,13 @@ def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu, nlms=N
 
         res['erle'] = erle_check(gpu1, lambda m_, f_, _n: port(torch.from_numpy(m_)[None],
                                                                torch.from_numpy(f_)[None])[0].numpy(), n)
+        res['erle']['reference'] = ('oracle/torch_crn_port.py TorchCrnPort (the reference op mix, f32' +
+                                    (', with the same FD-NLMS front end' if nlms else '') + ')')
     del net, nets
     torch.cuda.empty_cache()
     return res
 
 
-FP8_PEAK_TFLOPS = 5000.0      # MI355X_MICROARCH.md: dense FP8 (block-scaled e4m3: 2x the bf16 rate)
 
 
 def c5_flop_split(conf):
@@ -442,8 +459,42 @@ def cpu_baseline_c5(seconds, net, conf, nlms, B=256):
                        f'state, FD-NLMS per bin, float32), {el:.1f} s wall')
 
 
+def c5_erle(net, dev, conf, nlms, streams=2, n=160000):
+    """ERLE of the per-hop step (10 s far-end single-talk scenes stepped one hop
+    per call, step k emitting hop k-1) against the reference op mix on the
+    same signals (oracle/torch_crn_port.py TorchCrnPort with the same FD-NLMS
+    front end, f32 CPU)."""
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.join(REPO, 'oracle'))
+    from aec_oracle import erle_db
+    from torch_crn_port import TorchCrnPort
+    from aec_amd import synth
+    sc = [synth.scene(n, 90000 + i, double_talk=False) for i in range(streams)]
+    nh = n // 256 + 1
+    M = torch.zeros(streams, 256 * (nh + 1), device=dev)
+    F = torch.zeros_like(M)
+    M[:, :n] = torch.from_numpy(np.stack([s[0] for s in sc])).to(dev)
+    F[:, :n] = torch.from_numpy(np.stack([s[1] for s in sc])).to(dev)
+    net.stream_open(streams, device=dev)
+    with torch.no_grad():
+        outs = [net.stream_step(M[:, 256 * k:256 * (k + 1)], F[:, 256 * k:256 * (k + 1)]).clone() for k in range(nh)]
+    torch.cuda.synchronize(dev)
+    got = torch.cat(outs[1:], dim=1)[:, :256 * (n // 256)].cpu().numpy()
+    w = {k: v.detach().cpu().numpy() for k, v in net.state_dict().items()}
+    port = TorchCrnPort(w, conf, 2, nlms=nlms)
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    ref = port(torch.from_numpy(np.stack([s[0] for s in sc])), torch.from_numpy(np.stack([s[1] for s in sc]))).numpy()
+    g = [erle_db(sc[i][0], got[i]) for i in range(streams)]
+    r = [erle_db(sc[i][0], ref[i]) for i in range(streams)]
+    return dict(gpu_db=round(float(np.mean(g)), 4), reference_db=round(float(np.mean(r)), 4),
+                delta_db=round(float(np.mean(g) - np.mean(r)), 5), streams=streams,
+                scene='far-end single talk (near = 0), 10 s, synthetic RIR echo, stepped one hop per call',
+                reference='oracle/torch_crn_port.py TorchCrnPort (reference op mix, f32, same FD-NLMS front end)')
+
+
 def run_c5_stream(dev, B=256, hops=200, dtype='fp8', world=1, with_cpu=False, sweep=(1024, 4096),
-                  cpu_seconds=10.0):
+                  cpu_seconds=10.0, with_erle=False):
     """BASELINE config 5: the hipGraph-captured per-hop step of the DCCRN
     (MX-fp8 LSTM input projections, recurrence and wide conv layers) fed by the FD-NLMS,
     B concurrent streams per GPU, one 256-sample hop per stream per step
@@ -484,12 +535,37 @@ def run_c5_stream(dev, B=256, hops=200, dtype='fp8', world=1, with_cpu=False, sw
 
     dt = time_hops(B, hops, True)
     streams_sweep = None
+    lat_b1 = None
+    if world == 1:
+        # the drop-in's own operating point is one stream (test.py:139): per-hop latency of a single
+        # stream, host-synchronous per hop (submit, wait) and back-to-back (the graph replay rate)
+        lat_b1 = dict(ms_per_hop_back_to_back=round(time_hops(1, hops, False) * 1e3, 4))
+        net.stream_open(1, device=dev)
+        g1 = torch.Generator(device=dev).manual_seed(6)
+        m1 = 0.1 * torch.randn(1, 256, device=dev, generator=g1)
+        f1 = 0.1 * torch.randn(1, 256, device=dev, generator=g1)
+        o1 = torch.empty(1, 256, device=dev)
+        sync_lat = []
+        with torch.no_grad():
+            for k in range(60):
+                torch.cuda.synchronize(dev)
+                t1 = time.perf_counter()
+                net.stream_step(m1, f1, o1)
+                torch.cuda.synchronize(dev)
+                if k >= 10:
+                    sync_lat.append(time.perf_counter() - t1)
+        sync_lat.sort()
+        lat_b1['ms_per_hop_synchronous_median'] = round(sync_lat[len(sync_lat) // 2] * 1e3, 4)
+        lat_b1['rtf'] = round(lat_b1['ms_per_hop_synchronous_median'] / 16.0, 6)
     if world == 1 and sweep:
-        streams_sweep = {str(B): round(B / dt, 1)}
+        streams_sweep = {'1': round(1e3 / lat_b1['ms_per_hop_back_to_back'], 1), str(B): round(B / dt, 1)}
         for bb in sweep:
             d2 = time_hops(bb, max(20, hops // 4), False)
             streams_sweep[str(bb)] = round(bb / d2, 1)
-        time_hops(B, 1, False)                       # leave the bench shape's streams open
+    erle = None
+    if with_erle and world == 1:
+        erle = c5_erle(net, dev, conf, aec_amd.nlms_conf)
+    time_hops(B, 1, False)                           # leave the bench shape's streams open
     pmc = None
     pp = os.path.join(REPO, 'profiles', 'pmc_latest_c5.json')
     if os.path.exists(pp):
@@ -503,7 +579,8 @@ def run_c5_stream(dev, B=256, hops=200, dtype='fp8', world=1, with_cpu=False, sw
                dtype=dtype, n_gpus=world, streams=B * world, hops=hops, ms_per_hop=round(dt * 1e3, 4),
                frames_per_s=round(world * B / dt, 1), frames_per_s_per_gpu=round(B / dt, 1),
                rtf=round(dt / 0.016, 5), roofline=c5_roofline(conf, B, dt * 1e3, pmc),
-               streams_sweep_frames_per_s_per_gpu=streams_sweep, cpu_baseline=None)
+               latency_ms_per_hop_b1=lat_b1['ms_per_hop_synchronous_median'] if lat_b1 else None,
+               batch1=lat_b1, streams_sweep_frames_per_s_per_gpu=streams_sweep, erle=erle, cpu_baseline=None)
     if with_cpu and world == 1:
         res['cpu_baseline'] = cpu_baseline_c5(cpu_seconds, net, conf, aec_amd.nlms_conf, B)
     del net
@@ -803,26 +880,36 @@ def main():
     if world == 1 and not args.no_c3:
         # the same C3 batch with dtype fp8 (MX-fp8 LSTM input projections and wide conv layers,
         # e4m3 operands written by the producing epilogues)
-        c3f = run_crn(args, dev, rank, world, 'fp8', args.c3_steps, 2, 256, 160000, False)
+        c3f = run_crn(args, dev, rank, world, 'fp8', args.c3_steps, 2, 256, 160000, False,
+                      with_erle=not args.no_cpu)
+        if c3 and c3.get('cpu_baseline'):
+            # the CPU reference path is the same f32 op mix whatever the GPU dtype: C3's sample, reported here too
+            c3f['cpu_baseline'] = dict(c3['cpu_baseline'], note='same CPU sample as c3_crn_bf16.cpu_baseline (the '
+                                                                 'reference op mix is f32 for every GPU dtype)')
         c3f = dict(workload=crn_workload(args, 'fp8', 256), dtype='fp8', steps=args.c3_steps,
                    batches_in_flight=c3f['batches_in_flight'], frames_per_s=c3f['value'],
-                   ms_per_step=c3f['ms_per_step'], stage_ms_per_step=c3f['stage_ms_per_step'])
+                   ms_per_step=c3f['ms_per_step'], stage_ms_per_step=c3f['stage_ms_per_step'],
+                   roofline=c3f['roofline'], pipeline_roofline=c3f['pipeline_roofline'], erle=c3f['erle'],
+                   cpu_baseline=c3f['cpu_baseline'])
     c4 = None
     if world == 1 and not args.no_c3:
         # C4's per-GPU leg: FD-NLMS + DCCRN post-filter (bf16) on one GPU's shard of utterances
-        c4 = run_crn(args, dev, rank, world, 'bf16', args.c3_steps, 2, 256, 160000, False, aec_amd.nlms_conf)
+        c4 = run_crn(args, dev, rank, world, 'bf16', args.c3_steps, 2, 256, 160000, False, aec_amd.nlms_conf,
+                     with_erle=not args.no_cpu)
         c4 = dict(workload='C4 (BASELINE configs[3]) per-GPU leg: end-to-end STFT -> FD-NLMS (4 taps) -> DCCRN v2 '
                            'post-filter (dccrn2.py, configs.net_conf, bf16 MFMA) -> iSTFT on one GPU\'s shard of 256 '
                            'concurrent 10 s 16 kHz utterances (the 8-GPU job runs this per rank, no data-path '
                            'collective)',
                   dtype='bf16', steps=args.c3_steps, batches_in_flight=c4['batches_in_flight'],
                   frames_per_s=c4['value'], ms_per_step=c4['ms_per_step'],
-                  stage_ms_per_step=c4['stage_ms_per_step'])
+                  stage_ms_per_step=c4['stage_ms_per_step'], roofline=c4['roofline'],
+                  pipeline_roofline=c4['pipeline_roofline'], erle=c4['erle'])
     c5s = None
     if not args.no_c3:
         # C5 is quoted on 8 GPUs: the per-hop step runs on every rank (streams sharded, weak scaling)
         c5s = run_c5_stream(dev, world=world, with_cpu=rank == 0 and world == 1 and not args.no_cpu,
-                            sweep=() if args.no_sweep else (1024, 4096))
+                            sweep=() if args.no_sweep else (1024, 4096),
+                            with_erle=rank == 0 and world == 1 and not args.no_cpu)
     tr = None
     if world == 1 and not args.no_train:
         tr = run_train(dev, 16, 160000, args.train_steps, with_cpu=not args.no_cpu)

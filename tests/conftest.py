@@ -48,3 +48,34 @@ def gpu_net(golden_weights):
         sd[k] = torch.from_numpy(golden_weights[k])
     net.load_state_dict(sd, strict=True)
     return net.to('cuda:0')
+
+
+# ---------------------------------------------------------------------------
+# Parity margins: every reduced-precision bar goes through margin(), which
+# asserts the bar and records the observed value, so a run leaves the
+# observed-error vs bar table (gpurun_out/parity_margins.json) that the bars
+# are sized from (about 1.5-2x the largest observed error).
+# ---------------------------------------------------------------------------
+_MARGINS = []
+
+
+def margin(name, value, bar):
+    value = float(value)
+    test = os.environ.get('PYTEST_CURRENT_TEST', '').split(' ')[0]
+    _MARGINS.append(dict(test=test, check=name, observed=value, bar=float(bar),
+                         headroom=(float(bar) / value) if value > 0 else None))
+    print(f'[margin] {name}: observed {value:.4g} bar {bar:.4g}')
+    assert value <= bar, f'{name}: {value} > bar {bar}'
+
+
+def pytest_sessionfinish(session, exitstatus):
+    if not _MARGINS:
+        return
+    import json
+    out = os.path.join(REPO, 'gpurun_out')
+    try:
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, 'parity_margins.json'), 'w') as f:
+            json.dump(_MARGINS, f, indent=1)
+    except OSError:
+        pass
