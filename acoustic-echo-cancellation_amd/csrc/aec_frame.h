@@ -61,59 +61,84 @@ __device__ __forceinline__ v2f vrot(v2f a) { return v2f{-a.y, a.x}; }       // i
 
 // One lane's NLMS.  A lane runs either one complex bin or, on the lane that
 // owns row slot 0, the two real bins 0 and 256 side by side (x, y halves).
-// Both cases are the same instruction stream over per-tap operands
-//   complex: A = h, B = i h              dual real: A = (h.x, 0), B = (0, h.y)
-//   y  = sum_l w.x A + w.y B             (complex W h  /  (w.x h.x, w.y h.y))
-//   W += ge.x conj(A) + ge.y (-B.x, B.y) (ge conj(h)   /  (ge.x h.x, ge.y h.y))
-//   pw = sum_l A*A + B*B                 (|h|^2 in both halves / (h.x^2, h.y^2))
-// with ge = e * mu / (P + delta) per half.
+// Both cases are the same scalar instruction stream over per-tap operands
+// derived once when R[t] enters the history (hist()):
+//   complex bin:  p1 = r.x, p2 = -r.y, p4 = r.x      dual real:  p1 = r.x, p2 = 0, p4 = r.y
+//   y.x = sum_l w.x p1 + w.y p2        y.y = sum_l w.y p4 - w.x p2
+//         (complex: W R;  dual: (w.x r.x, w.y r.y))
+//   W.x += ge.x p1 - ge.y p2           W.y += ge.y p4 + ge.x p2
+//         (complex: W += ge conj(R);  dual: per half)
+//   q  = (p1^2 + p2^2, p4^2 + p2^2)    (|R|^2 in both halves / (r.x^2, r.y^2))
+// with ge = e * mu / (P + delta) per half.  Plain f32 FMAs: on gfx950 a
+// v_pk_fma_f32 costs at least two v_fma_f32 issue slots, so the packed form of
+// this recursion (one complex value per VGPR pair, operand masks) issued ~100
+// slot-equivalents per step against ~60 here, on a chain of dependent packed
+// ops; the recursion's waves share their SIMDs with the transforms.
 template <int TAPS>
 struct NlmsBin {
-    v2f w[TAPS];
-    v2f a[TAPS], bq[TAPS], qq[TAPS];   // operands A, B and A*A + B*B of R[t], R[t-1], ...
-    v2f p;
-    v2f ma, mb, mc;                    // operand masks: complex (1,1), (-1,1), (0,0); dual (1,0), (0,0), (0,1)
-    __device__ __forceinline__ void reset(bool dual) {
-#pragma unroll
-        for (int l = 0; l < TAPS; ++l) w[l] = a[l] = bq[l] = qq[l] = vsplat(0.f);
-        p = vsplat(0.f);
-        ma = dual ? v2f{1.f, 0.f} : v2f{1.f, 1.f};
-        mb = dual ? v2f{0.f, 0.f} : v2f{-1.f, 1.f};
-        mc = dual ? v2f{0.f, 1.f} : v2f{0.f, 0.f};
-    }
-    // One frame: returns E = D - sum_l W[l] R[t-l] and adapts W.
-    __device__ __forceinline__ float2 step(float2 d2, float2 r2, float mu, float beta, float delta) {
-        const v2f d{d2.x, d2.y}, r{r2.x, r2.y};
-#pragma unroll
-        for (int l = TAPS - 1; l >= 1; --l) {
-            a[l] = a[l - 1];
-            bq[l] = bq[l - 1];
-            qq[l] = qq[l - 1];
-        }
-        a[0] = r * ma;
-        bq[0] = vfma(v2f{r.y, r.x}, mb, r * mc);
-        qq[0] = vfma(a[0], a[0], bq[0] * bq[0]);
-        // independent per-tap products summed as a tree (short dependency chain)
-        v2f pr[TAPS];
-        v2f pw = qq[0];
-#pragma unroll
-        for (int l = 0; l < TAPS; ++l) pr[l] = vfma(vsplat(w[l].y), bq[l], vsplat(w[l].x) * a[l]);
-#pragma unroll
-        for (int l = 1; l < TAPS; ++l) pw = pw + qq[l];
-#pragma unroll
-        for (int s = 1; s < TAPS; s *= 2)
-#pragma unroll
-            for (int l = 0; l + s < TAPS; l += 2 * s) pr[l] = pr[l] + pr[l + s];
-        const v2f e = d - pr[0];
-        p = vfma(vsplat(beta), p, vsplat(1.f - beta) * pw);
-        const v2f g = v2f{__builtin_amdgcn_rcpf(p.x + delta), __builtin_amdgcn_rcpf(p.y + delta)} * vsplat(mu);
-        const v2f ge = e * g;
+    float2 w[TAPS];
+    float p1[TAPS], p2[TAPS], p4[TAPS];   // operands of R[t], R[t-1], ...
+    float qx[TAPS], qy[TAPS];             // per-half |R|^2 of the same entries
+    float2 p;                             // smoothed power per half
+    bool dual;
+    __device__ __forceinline__ void reset(bool dual_) {
+        dual = dual_;
 #pragma unroll
         for (int l = 0; l < TAPS; ++l) {
-            w[l] = vfma(vsplat(ge.x), v2f{a[l].x, -a[l].y}, w[l]);
-            w[l] = vfma(vsplat(ge.y), v2f{-bq[l].x, bq[l].y}, w[l]);
+            w[l] = make_float2(0.f, 0.f);
+            p1[l] = p2[l] = p4[l] = qx[l] = qy[l] = 0.f;
         }
-        return make_float2(e.x, e.y);
+        p = make_float2(0.f, 0.f);
+    }
+    // history slot l <- the operands of far-end bin value r (step() uses the
+    // same expressions for slot 0; the streaming steps restore their saved
+    // history through this)
+    __device__ __forceinline__ void hist(int l, float2 r) {
+        p1[l] = r.x;
+        p2[l] = dual ? 0.f : -r.y;
+        p4[l] = dual ? r.y : r.x;
+        const float s = p2[l] * p2[l];
+        qx[l] = fmaf(p1[l], p1[l], s);
+        qy[l] = fmaf(p4[l], p4[l], s);
+    }
+    // One frame: returns E = D - sum_l W[l] R[t-l] and adapts W.
+    __device__ __forceinline__ float2 step(float2 d, float2 r, float mu, float beta, float delta) {
+#pragma unroll
+        for (int l = TAPS - 1; l >= 1; --l) {
+            p1[l] = p1[l - 1];
+            p2[l] = p2[l - 1];
+            p4[l] = p4[l - 1];
+            qx[l] = qx[l - 1];
+            qy[l] = qy[l - 1];
+        }
+        hist(0, r);
+        // y: two partial chains per half (taps [0, H) and [H, TAPS)), then one add
+        constexpr int H = (TAPS + 1) / 2;
+        float yx[2], yy[2], px[2], py[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int l0 = h ? H : 0, l1 = h ? TAPS : H;
+            yx[h] = yy[h] = px[h] = py[h] = 0.f;
+#pragma unroll
+            for (int l = l0; l < l1; ++l) {
+                yx[h] = fmaf(w[l].x, p1[l], fmaf(w[l].y, p2[l], yx[h]));
+                yy[h] = fmaf(w[l].y, p4[l], fmaf(-w[l].x, p2[l], yy[h]));
+                px[h] += qx[l];
+                py[h] += qy[l];
+            }
+        }
+        const float ex = d.x - (yx[0] + yx[1]);
+        const float ey = d.y - (yy[0] + yy[1]);
+        p.x = fmaf(beta, p.x, (1.f - beta) * (px[0] + px[1]));
+        p.y = fmaf(beta, p.y, (1.f - beta) * (py[0] + py[1]));
+        const float gx = ex * (__builtin_amdgcn_rcpf(p.x + delta) * mu);
+        const float gy = ey * (__builtin_amdgcn_rcpf(p.y + delta) * mu);
+#pragma unroll
+        for (int l = 0; l < TAPS; ++l) {
+            w[l].x = fmaf(gx, p1[l], fmaf(-gy, p2[l], w[l].x));
+            w[l].y = fmaf(gy, p4[l], fmaf(gx, p2[l], w[l].y));
+        }
+        return make_float2(ex, ey);
     }
 };
 

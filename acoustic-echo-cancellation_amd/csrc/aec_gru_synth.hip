@@ -74,6 +74,19 @@ static_assert(kHeadWaves * kMaxNS <= 8, "loss slots");
 
 size_t gru_synth_smem_bytes() { return (size_t)kFusedFloats * 4; }
 
+#ifdef AEC_TICK_PROF
+// timing experiments only (tools/gru_tick_prof.py): s_memtime stamps of blocks 0 and 64 per wave and
+// tick: loop top, work done (before the tick barrier)
+__device__ unsigned long long g_gtick[2][12][96][2];
+#define GTICK(slot)                                                                                    \
+    do {                                                                                               \
+        if ((blockIdx.x == 0 || blockIdx.x == 64) && lane == 0 && c + 3 < 96)                          \
+            g_gtick[blockIdx.x ? 1 : 0][wave][c + 3][slot] = __builtin_amdgcn_s_memtime();             \
+    } while (0)
+#else
+#define GTICK(slot) do {} while (0)
+#endif
+
 // The tick barrier: LDS traffic drained (lgkmcnt(0)), global loads and
 // stores left in flight.  __syncthreads would also drain vmcnt, exposing the
 // HBM latency of the loads issued for the NEXT tick (feats, E rows) once per
@@ -188,6 +201,7 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
         float* hb = sHb + 32 * s;
         if (lane < 32) hb[lane] = 0.f;
         for (int c = -3; c <= nchmax + 2; ++c) {
+            GTICK(0);
             if (c >= 0 && c < nch && !(y.fmode & 512)) {
                 const int f_end = min(TF, T - c * TF);
                 const float* gi = sGi + ((c & 1) * kCH + s * TF) * 96;
@@ -204,6 +218,7 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
                     gr = ngr; gz = ngz; gn = ngn;
                 }
             }
+            GTICK(1);
             tick_barrier();
         }
     } else if (wave < NS + kGiWaves) {
@@ -236,6 +251,7 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
 #pragma unroll
         for (int u = 0; u < kStU; ++u) pm[u] = pr[u] = pn[u] = 0.f;
         for (int c = -3; c <= nchmax + 2; ++c) {
+            GTICK(0);
             const int cs = c + 2;
             if (cs >= 0 && cs < nchmax) {
 #pragma unroll
@@ -259,6 +275,7 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
                     sGi[((cg & 1) * kCH + q) * 96 + grow] = gru_gi(wih, sX + ((cg & 1) * kCH + q) * 64, gbias);
                 }
             }
+            GTICK(1);
             tick_barrier();
         }
     } else if (wave < NS + kGiWaves + kHeadWaves) {
@@ -276,6 +293,7 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
         for (int s = 0; s < NS; ++s) lacc[s] = 0.f;
         const bool oal = ((y.ld_out & 3) == 0) && ((reinterpret_cast<uintptr_t>(y.out) & 15) == 0);
         for (int c = -3; c <= nchmax + 2; ++c) {
+            GTICK(0);
             const int ch = c - 1;
             if (ch >= 0 && ch < nchmax && !(y.fmode & 1024)) {
                 for (int q = fg; q < kCH; q += kHeadGrp) {
@@ -350,6 +368,7 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
                         sTail[(((k + 1) & 1) * NS + s) * 256 + r] = ring[(TF - 1) * kGroupFloats + 256 + r];
                 }
             }
+            GTICK(1);
             tick_barrier();
         }
         if (p.loss) {
@@ -399,6 +418,7 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
             x128 = row[128];
         };
         for (int c = -3; c <= nchmax + 2; ++c) {
+            GTICK(0);
             // (2) synthesis of chunk c - 2 into ring (c - 2) & 1 (rows loaded last tick); the
             // E rows of chunk c - 1 for the next tick are requested as soon as the inverse pack
             // has consumed this tick's rows, so their load runs under the inverse transform
@@ -413,6 +433,7 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
             } else if (next) {
                 load_rows(c - 1);
             }
+            GTICK(1);
             tick_barrier();
         }
     }
@@ -454,3 +475,10 @@ hipError_t launch_gru_synth(const GruArgs& g, const SynthArgs& y, int B, hipStre
 }
 
 }  // namespace aec
+
+#ifdef AEC_TICK_PROF
+extern "C" int aec_debug_gru_tick_prof(void* host, size_t bytes) {
+    if (bytes < sizeof(aec::g_gtick)) return -1;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(aec::g_gtick), sizeof(aec::g_gtick)) == hipSuccess ? 0 : -2;
+}
+#endif

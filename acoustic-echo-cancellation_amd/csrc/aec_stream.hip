@@ -113,20 +113,17 @@ __global__ __launch_bounds__(kStreamThreads) void stream_step_kernel(StreamStepA
 #pragma unroll
         for (int l = 0; l < TAPS; ++l) {
             const float2 w = nst[l * 256 + tid];
-            nb.w[l] = v2f{w.x, w.y};
+            nb.w[l] = w;
         }
 #pragma unroll
         for (int l = 0; l + 1 < TAPS; ++l) {
             // the operands step() derived from r when r entered (same expressions)
             const float2 r2 = nst[(TAPS + l) * 256 + tid];
             rh[l] = r2;
-            const v2f r{r2.x, r2.y};
-            nb.a[l] = r * nb.ma;
-            nb.bq[l] = vfma(v2f{r.y, r.x}, nb.mb, r * nb.mc);
-            nb.qq[l] = vfma(nb.a[l], nb.a[l], nb.bq[l] * nb.bq[l]);
+            nb.hist(l, r2);
         }
         const float2 pp = nst[(2 * TAPS - 1) * 256 + tid];
-        nb.p = v2f{pp.x, pp.y};
+        nb.p = pp;
     }
 
     // role weights: wave 0 the recurrence (W_hh k-halves, as gru_kernel's
@@ -183,13 +180,13 @@ __global__ __launch_bounds__(kStreamThreads) void stream_step_kernel(StreamStepA
         const float2 e = nb.step(sRow[0][tid], sRow[1][tid], p.mu, p.beta, p.delta);
         sRow[2][tid] = e;
 #pragma unroll
-        for (int l = 0; l < TAPS; ++l) nst[l * 256 + tid] = make_float2(nb.w[l].x, nb.w[l].y);
+        for (int l = 0; l < TAPS; ++l) nst[l * 256 + tid] = nb.w[l];
         if constexpr (TAPS > 1) {
             nst[TAPS * 256 + tid] = sRow[1][tid];
 #pragma unroll
             for (int l = 1; l + 1 < TAPS; ++l) nst[(TAPS + l) * 256 + tid] = rh[l - 1];
         }
-        nst[(2 * TAPS - 1) * 256 + tid] = make_float2(nb.p.x, nb.p.y);
+        nst[(2 * TAPS - 1) * 256 + tid] = nb.p;
         __syncthreads();
     }
 

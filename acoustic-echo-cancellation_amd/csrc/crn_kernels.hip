@@ -582,7 +582,6 @@ __global__ __launch_bounds__(256) void crn_rows_x0_kernel(RowsX0Args p) {
 
 template <typename T, int TAPS>
 __global__ __launch_bounds__(256) void crn_stream_nlms_kernel(StreamNlmsArgs p) {
-    using aec::v2f;
     const int b = blockIdx.x, k = threadIdx.x;
     float2* nst = p.state + (int64_t)b * (2 * TAPS) * 256;
     // restore (aec_stream.hip's layout: taps, raw far history, power); the
@@ -593,30 +592,27 @@ __global__ __launch_bounds__(256) void crn_stream_nlms_kernel(StreamNlmsArgs p) 
 #pragma unroll
     for (int l = 0; l < TAPS; ++l) {
         const float2 w = nst[l * 256 + k];
-        nb.w[l] = v2f{w.x, w.y};
+        nb.w[l] = w;
     }
 #pragma unroll
     for (int l = 0; l + 1 < TAPS; ++l) {
         const float2 r2 = nst[(TAPS + l) * 256 + k];
         rh[l] = r2;
-        const v2f r{r2.x, r2.y};
-        nb.a[l] = r * nb.ma;
-        nb.bq[l] = aec::vfma(v2f{r.y, r.x}, nb.mb, r * nb.mc);
-        nb.qq[l] = aec::vfma(nb.a[l], nb.a[l], nb.bq[l] * nb.bq[l]);
+        nb.hist(l, r2);
     }
     const float2 pp = nst[(2 * TAPS - 1) * 256 + k];
-    nb.p = v2f{pp.x, pp.y};
+    nb.p = pp;
     const float2* rows = p.rows + (int64_t)b * 512;
     const float2 r = rows[256 + k];
     const float2 e = nb.step(rows[k], r, p.mu, p.beta, p.delta);
 #pragma unroll
-    for (int l = 0; l < TAPS; ++l) nst[l * 256 + k] = make_float2(nb.w[l].x, nb.w[l].y);
+    for (int l = 0; l < TAPS; ++l) nst[l * 256 + k] = nb.w[l];
     if constexpr (TAPS > 1) {
         nst[TAPS * 256 + k] = r;
 #pragma unroll
         for (int l = 1; l + 1 < TAPS; ++l) nst[(TAPS + l) * 256 + k] = rh[l - 1];
     }
-    nst[(2 * TAPS - 1) * 256 + k] = make_float2(nb.p.x, nb.p.y);
+    nst[(2 * TAPS - 1) * 256 + k] = nb.p;
     float2* erow = p.espec + (int64_t)b * 256;
     erow[k] = e;
     // X0 bin k (k >= 1) or, on lane 0, the Nyquist bin: from this lane's own

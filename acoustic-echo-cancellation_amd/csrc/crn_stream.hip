@@ -277,12 +277,12 @@ __global__ __launch_bounds__(256, MX4 || TAPS > 4 ? 1 : 2) void crn_stream_enc_k
 #pragma unroll
         for (int l = 0; l < TAPS; ++l) {
             const float2 w = nst[l * 256 + k];
-            nb.w[l] = aec::v2f{w.x, w.y};
+            nb.w[l] = w;
         }
 #pragma unroll
         for (int l = 0; l + 1 < TAPS; ++l) rh[l] = nst[(TAPS + l) * 256 + k];
         const float2 pp = nst[(2 * TAPS - 1) * 256 + k];
-        nb.p = aec::v2f{pp.x, pp.y};
+        nb.p = pp;
     }
     // weight fragments: level i, this wave's N tile nt = wave % NT, chunk c: row nt*16 + (lane & 15),
     // k = 32 c + 8 (lane >> 4) .. + 7 (the 16x16x32 B operand)
@@ -358,21 +358,16 @@ __global__ __launch_bounds__(256, MX4 || TAPS > 4 ? 1 : 2) void crn_stream_enc_k
         float2 e = rm;
         if constexpr (TAPS > 0) {
 #pragma unroll
-            for (int l = 0; l + 1 < TAPS; ++l) {
-                const aec::v2f r{rh[l].x, rh[l].y};
-                nb.a[l] = r * nb.ma;
-                nb.bq[l] = aec::vfma(aec::v2f{r.y, r.x}, nb.mb, r * nb.mc);
-                nb.qq[l] = aec::vfma(nb.a[l], nb.a[l], nb.bq[l] * nb.bq[l]);
-            }
+            for (int l = 0; l + 1 < TAPS; ++l) nb.hist(l, rh[l]);
             e = nb.step(rm, rf, p.mu, p.beta, p.delta);
 #pragma unroll
-            for (int l = 0; l < TAPS; ++l) nst[l * 256 + k] = make_float2(nb.w[l].x, nb.w[l].y);
+            for (int l = 0; l < TAPS; ++l) nst[l * 256 + k] = nb.w[l];
             if constexpr (TAPS > 1) {
                 nst[TAPS * 256 + k] = rf;
 #pragma unroll
                 for (int l = 1; l + 1 < TAPS; ++l) nst[(TAPS + l) * 256 + k] = rh[l - 1];
             }
-            nst[(2 * TAPS - 1) * 256 + k] = make_float2(nb.p.x, nb.p.y);
+            nst[(2 * TAPS - 1) * 256 + k] = nb.p;
             p.espec[(int64_t)b * 256 + k] = e;
         }
         if (k > 0)

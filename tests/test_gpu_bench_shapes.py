@@ -11,7 +11,7 @@ and the MX layer step's config coverage (include/aec_crn.h).
   ERLE_DB dB.
 * C5's per-GPU unit (`c5_stream_fp8`): the hipGraph per-hop NLMS -> DCCRN fp8
   step at 256 streams (8 MX stream blocks, 512 blocks per layer step) over
-  201 hops: every stream within FP8_WAV_TOL of the fp8 batch forward of the
+  201 hops: every stream within STREAM_VS_BATCH_TOL of the fp8 batch forward of the
   same signal, three within FP8_WAV_TOL of the reference op mix.
 * The MX layer step (lstm_step_mx8_kernel) with rnn_layers = 3 (a middle layer
   reads one xn set and writes the other) against the bf16 step + combine
@@ -32,10 +32,14 @@ from conftest import margin
 pytestmark = pytest.mark.gpu
 
 NLMS = dict(taps=4, mu=0.3, beta=0.5, delta=1e-4)
-BF16_WAV_TOL = 1e-2
-FP8_WAV_TOL = 2e-2
+# bars ~1.5-2x the errors observed on MI355X (round 5, profiles/r05a_parity_margins.json):
+# C4 rows 0.0042, C5 rows vs the op mix 0.0050, C5 stream vs batch 0.0017, 3-layer MX vs
+# bf16 0.0017 / vs the op mix 0.0044; ERLE deltas <= 0.0071 dB against north_star's 0.1 dB
+BF16_WAV_TOL = 7e-3
+FP8_WAV_TOL = 1e-2
 ERLE_DB = 0.1
-STREAM_VS_BATCH_TOL = FP8_WAV_TOL
+STREAM_VS_BATCH_TOL = 3.5e-3
+MX_VS_BF16_TOL = 3.5e-3
 WEIGHT_SEED = 1
 
 
@@ -153,7 +157,7 @@ def test_fp8_stream_three_lstm_layers(monkeypatch):
     assert np.isfinite(res['1']).all()
     assert not np.array_equal(res['1'], res['0'])
     errs = [rel(res['1'][b], res['0'][b]) for b in range(B)]
-    margin('3 LSTM layers: MX vs bf16 recurrence', max(errs), FP8_WAV_TOL / 2)
+    margin('3 LSTM layers: MX vs bf16 recurrence', max(errs), MX_VS_BF16_TOL)
     ref = port_out(w, conf, [sig[b] for b in (0, 39)], nlms=None)
     for i, b in enumerate((0, 39)):
         margin(f'3 LSTM layers: stream {b} vs reference op mix', rel(res['1'][b], ref[i]), FP8_WAV_TOL)

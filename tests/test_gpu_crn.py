@@ -8,7 +8,7 @@ Tolerances (relative RMS, written here):
 * bf16 path (bf16 storage / MFMA, f32 accumulate): out_wav <= BF16_WAV_TOL,
   mask <= BF16_MASK_TOL (reduced precision; the f32 path is the parity gate;
   observed out_wav relative RMS vs the reference 0.0018-0.0034 on the
-  goldens, so the bar is ~3x the observed error);
+  goldens, so the bar is ~1.8x the observed error);
 * fp8 path (bf16 + MX-fp8 GEMMs for the LSTM input projections and the
   wide conv layers, encoder 4-5 / decoder levels 5-6: e4m3 weights and
   activations, E8M0 scale per 32 k): out_wav <= FP8_WAV_TOL, mask <=
@@ -38,15 +38,20 @@ pytestmark = pytest.mark.gpu
 
 GOLD = os.path.join(os.path.dirname(__file__), 'golden')
 META = json.load(open(os.path.join(GOLD, 'crn_meta.json')))
+# Reduced-precision bars: ~1.5-2x the largest error observed on MI355X (round 5,
+# gpurun_out/parity_margins.json -> profiles/r05a_parity_margins.json), so a change
+# that doubles an error fails.  Observed maxima: bf16 out_wav 0.0034 / mask 0.0032,
+# fp8 out_wav 0.0051 / mask 0.0104, fp8 vs bf16 0.0038, persistent vs step 0.00026,
+# MX vs bf16 recurrence 0.0018, ERLE delta 0.0073 dB (the 0.1 dB bar is north_star's).
 F32_TOL = 1e-4
-BF16_WAV_TOL = 1e-2
-BF16_MASK_TOL = 1e-2
-FP8_WAV_TOL = 2e-2
-FP8_MASK_TOL = 2e-2
-FP8_VS_BF16_TOL = 2e-2
+BF16_WAV_TOL = 6e-3
+BF16_MASK_TOL = 6e-3
+FP8_WAV_TOL = 1e-2
+FP8_MASK_TOL = 1.6e-2
+FP8_VS_BF16_TOL = 7e-3
 C3_ERLE_DB = 0.1
-PERSIST_TOL = 1e-2
-MX_VS_BF16_STEP_TOL = FP8_WAV_TOL / 2
+PERSIST_TOL = 5e-4
+MX_VS_BF16_STEP_TOL = 3.5e-3
 
 
 def rel(a, b):
@@ -401,7 +406,7 @@ def test_fp8_stream_mx_recurrence(monkeypatch):
     NavieComplexLSTM combination fused into its epilogue (lstm_step_mx8_kernel)
     against the bf16 step + combine kernels (AEC_CRN_STEP_MX=0, read at
     stream_open) on 80 streams (three step blocks, the last one partial) of
-    the full net_conf: within FP8_WAV_TOL / 2 relative RMS of each other per
+    the full net_conf: within MX_VS_BF16_STEP_TOL relative RMS of each other per
     stream (observed 0.003-0.005: the e4m3 rounding of W_hh and h against
     bf16), and not identical (the MX recurrence really ran); three streams
     within the fp8 bar of the reference op mix (oracle/torch_crn_port), the

@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Per-tick role timing of gru_synth_kernel (a -DAEC_TICK_PROF build loaded via
+AEC_HIP_LIB): the full pipeline at 256 x 10 s, then per wave the median over
+ticks of the work time (loop top -> before the tick barrier) and of the tick
+period, blocks 0 and 64 (s_memtime cycles).
+  AEC_HIP_LIB=.../ab/tick.so python tools/gru_tick_prof.py"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, 'acoustic-echo-cancellation_amd'))
+import aec_amd  # noqa: E402
+from aec_amd import _lib, synth  # noqa: E402
+
+dev = torch.device('cuda', 0)
+w = dict(np.load(os.path.join(REPO, 'tests', 'golden', 'weights.npz')))
+net = aec_amd.Little_net(aec_amd.speech_conf, 32, nlms=aec_amd.nlms_conf).eval()
+sd = net.state_dict()
+for k in ['gru1.weight_ih_l0', 'gru1.weight_hh_l0', 'gru1.bias_ih_l0', 'gru1.bias_hh_l0',
+          'linear1.weight', 'linear1.bias', 'linear2.weight', 'linear2.bias']:
+    sd[k] = torch.from_numpy(w[k])
+net.load_state_dict(sd)
+net = net.to(dev)
+erb = torch.tensor(aec_amd.erb_matrix(), dtype=torch.float32, device=dev)
+B, n = 256, 160000
+mic, ref, near = (torch.from_numpy(a).to(dev) for a in synth.batch(B, n, seed0=0))
+with torch.no_grad():
+    for _ in range(3):
+        net.forward_ragged(mic, ref, near, erb, [n] * B)
+torch.cuda.synchronize()
+lib = _lib.load()
+buf = np.zeros((2, 12, 96, 2), np.uint64)
+rc = lib.aec_debug_gru_tick_prof(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes))
+assert rc == 0, rc
+ns = int(os.environ.get('AEC_GRU_NS', '2'))
+roles = ['rec'] * ns + ['gi'] * 3 + ['head'] * 3 + ['synth'] * 4
+for blk in range(2):
+    b = buf[blk].astype(np.int64)
+    ticks = range(6, 80)
+    per = [b[0, c + 1, 0] - b[0, c, 0] for c in ticks]
+    print(f'block {blk * 64}: tick period median {np.median(per):.0f} cycles')
+    for wv in range(len(roles)):
+        work = np.median([b[wv, c, 1] - b[wv, c, 0] for c in ticks])
+        print(f'  {roles[wv]:5s} wave {wv:2d}: work {work:7.0f}')
