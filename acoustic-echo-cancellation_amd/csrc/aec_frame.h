@@ -22,6 +22,7 @@ __device__ __forceinline__ float mag(float2 x) {
 // partial sums, pieces of split bands combined through comb.  fo = the
 // frame's 32-float feature row, or null (frame beyond the stream: compute
 // nothing visible).  Leaves the wave fenced.
+template <int PART = 512>
 __device__ __forceinline__ void erb_project(float* scr, const float4* sSched, const int2* sComb, int L, int lb,
                                             int sw, float* fo) {
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
@@ -35,7 +36,7 @@ __device__ __forceinline__ void erb_project(float* scr, const float4* sSched, co
             a2 = fmaf(en.w, mg, a2);
         }
     }
-    float* part = scr + 512;
+    float* part = scr + PART;                      // 48 partials after the magnitudes
     part[3 * lb + 0] = a0;
     part[3 * lb + 1] = a1;
     part[3 * lb + 2] = a2;

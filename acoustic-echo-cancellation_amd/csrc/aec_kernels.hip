@@ -288,7 +288,15 @@ __device__ unsigned long long g_tick[2][kNlmsWavesProf][48][4];
 #endif
 constexpr int kSpecRow = 256;          // float2 per spectrum row
 constexpr int kNlmsWaves = 12;
-constexpr int kERow = 512 + 48;        // floats per LDS error row: 256 float2, then ERB partials
+constexpr int kERow = 512 + 48;        // floats per LDS error row (split path): 256 float2, then ERB partials
+#ifndef AEC_NLMS_MAGROW
+#define AEC_NLMS_MAGROW 1              // K2n: the nlms waves write |E| rows (0: E rows, mags on the ref waves)
+#endif
+// K2n LDS row per frame of a chunk: with AEC_NLMS_MAGROW the nlms waves store |E[k]| at k ^ sw (the
+// swizzle of the group that projects the frame, sw = 16 (i & 1) for frame i), bins 0..256 -> 273
+// floats, then erb_project's 48 partials at kMagPart; otherwise the E row (256 float2) as before
+constexpr int kMagPart = 288;
+constexpr int kNRow = AEC_NLMS_MAGROW ? kMagPart + 48 : kERow;
 
 // One transform pass of a wave: commit the prefetched samples of (signal,
 // 4 frames at wt), prefetch the next task, window + rFFT -> xa / xb / x128.
@@ -319,7 +327,7 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
     float2* sTwT = sTw512 + 258;                                      // 256
     float* sHann = reinterpret_cast<float*>(sTwT + 256);              // 512
     float* sWave = sHann + 512;                                       // 8 * kWaveFloats (mic, ref waves)
-    float* sE = sWave + 8 * kWaveFloats;                              // 2 x kFPB error rows (kERow floats)
+    float* sE = sWave + 8 * kWaveFloats;                              // 2 x kFPB error rows (kNRow floats)
 
     const DevTables* tb = reinterpret_cast<const DevTables*>(p.tables);
     if (tid < 256) {
@@ -372,7 +380,12 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
     const int erb_role = p.erb_role == 2 ? 2 : 1;
     auto mic_erb_pass = [&](int c2) {
         const int64_t t2 = (int64_t)c2 * kFPB + 4 * q + gg;
-        float* er = sE + (c2 & 1) * kFPB * kERow + (4 * q + gg) * kERow;
+        float* er = sE + (c2 & 1) * kFPB * kNRow + (4 * q + gg) * kNRow;
+#if AEC_NLMS_MAGROW
+        // |E| row already in place (the nlms waves' stores, complete since tick c2 + 1's barriers)
+        erb_project<kMagPart>(er, sSched, sComb, L, lb, sw, t2 < T ? feats + t2 * 96 : nullptr);
+        return;
+#endif
         const float2* row = reinterpret_cast<const float2*>(er);
         float2 xa[8], xb[8], x128;
 #pragma unroll
@@ -407,11 +420,18 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
                 // buffer); frames past the stream end only perturb state nobody
                 // reads again (the unrolled loop stays branch-free)
                 const int64_t t0 = (int64_t)c1 * kFPB;
-                float* eb = sE + (c1 & 1) * kFPB * kERow;
+                float* eb = sE + (c1 & 1) * kFPB * kNRow;
 #pragma unroll
                 for (int i = 0; i < kFPB; ++i) {
                     const float2 e = st.step(dd[i], rr[i], mu, beta, delta);
+#if AEC_NLMS_MAGROW
+                    // |E| (mags_to_scr's expression: slot 0's real pair as (E, 0) each) at k ^ sw_i
+                    const int swi = 16 * (i & 1);
+                    eb[i * kNRow + (k ^ swi)] = mag(make_float2(e.x, k == 0 ? 0.f : e.y));
+                    if (k == 0) eb[i * kNRow + (256 ^ swi)] = mag(make_float2(e.y, 0.f));
+#else
                     reinterpret_cast<float2*>(eb + i * kERow)[k] = e;
+#endif
                     if (t0 + i < T) {
 #if AEC_SPEC_ST_NT
                         typedef float f2v __attribute__((ext_vector_type(2)));

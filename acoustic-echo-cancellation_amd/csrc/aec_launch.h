@@ -130,9 +130,13 @@ inline size_t analysis_smem_bytes(int sched_len) {
 }
 // K2n: tables + 8 wave regions (mic, ref waves; the nlms waves keep their
 // state in registers) + 2 x 16 error rows of 560 floats
+#ifndef AEC_NLMS_MAGROW
+#define AEC_NLMS_MAGROW 1
+#endif
 inline size_t nlms_smem_bytes(int sched_len, int /*taps*/) {
+    // error rows: |E| rows of 288 + 48 floats (AEC_NLMS_MAGROW), or E rows of 512 + 48
     return (size_t)sched_len * 16 * 16 + 32 * 8 +
-           (258 * 2 + 256 * 2 + 512 + (size_t)8 * 4 * kGroupFloats + (size_t)2 * kFPB * 560) * 4;
+           (258 * 2 + 256 * 2 + 512 + (size_t)8 * 4 * kGroupFloats + (size_t)2 * kFPB * (AEC_NLMS_MAGROW ? 336 : 560)) * 4;
 }
 inline size_t synthesis_smem_bytes() {
     return 260 * 16 + (258 * 2 + 256 * 2 + 512 + 256 + kFPB * 33 + 4 + (size_t)kFPB * kGroupFloats) * 4;
