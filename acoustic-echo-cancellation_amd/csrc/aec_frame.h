@@ -52,64 +52,6 @@ __device__ __forceinline__ void erb_project(float* scr, const float4* sSched, co
     wave_fence();
 }
 
-// The lane's schedule bins in registers (L = 32 entries: 16 VGPRs, two 16-bit byte offsets
-// (bin ^ sw) * 4 each), so that erb_project_reg issues the magnitude gathers of 8 entries
-// together with their weight reads: one LDS round trip per 8 entries instead of two (the
-// gather address no longer waits for the schedule read).  Loaded once per wave (sw fixed).
-constexpr int kErbRegL = 32;
-struct ErbBins {
-    uint32_t pk[kErbRegL / 2];
-};
-__device__ __forceinline__ void erb_bins_load(ErbBins& bn, const float4* sSched, int lb, int sw) {
-#pragma unroll
-    for (int e = 0; e < kErbRegL / 2; ++e) {
-        const uint32_t lo = (uint32_t)((__float_as_int(sSched[(2 * e) * 16 + lb].x) ^ sw) * 4);
-        const uint32_t hi = (uint32_t)((__float_as_int(sSched[(2 * e + 1) * 16 + lb].x) ^ sw) * 4);
-        bn.pk[e] = lo | (hi << 16);
-    }
-}
-// erb_project with L = kErbRegL and the bins from registers: the same entries, the same FMA
-// order, so the same bits
-template <int PART = 512>
-__device__ __forceinline__ void erb_project_reg(float* scr, const float4* sSched, const int2* sComb,
-                                                const ErbBins& bn, int lb, float* fo) {
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-    const char* base = reinterpret_cast<const char*>(scr);
-#pragma unroll
-    for (int g = 0; g < kErbRegL / 8; ++g) {
-        float mg[8];
-        float4 en[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int e = 8 * g + u;
-            const uint32_t off = (bn.pk[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
-            mg[u] = *reinterpret_cast<const float*>(base + off);
-            en[u] = sSched[e * 16 + lb];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            a0 = fmaf(en[u].y, mg[u], a0);
-            a1 = fmaf(en[u].z, mg[u], a1);
-            a2 = fmaf(en[u].w, mg[u], a2);
-        }
-        asm volatile("" ::: "memory");               // one group's loads in flight at a time
-    }
-    float* part = scr + PART;
-    part[3 * lb + 0] = a0;
-    part[3 * lb + 1] = a1;
-    part[3 * lb + 2] = a2;
-    wave_fence();
-    if (fo) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int band = lb + 16 * h;
-            const int2 cb = sComb[band];
-            fo[band] = part[cb.x] + (cb.y >= 0 ? part[cb.y] : 0.f);
-        }
-    }
-    wave_fence();
-}
-
 // Packed-FP32 complex helpers for the recursion: a complex value is a
 // float2 vector, so the products below map to v_pk_mul_f32 / v_pk_fma_f32
 // (two lanes of arithmetic per instruction slot).

@@ -142,14 +142,8 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
         nchs[s] = (Ts[s] + TF - 1) / TF;
         nchmax = max(nchmax, nchs[s]);
     }
-    // role layout: logical wave = physical wave, or (AEC_FUSED_MODE bit 14, NS = 2) the second
-    // recurrence on physical wave 4, which shares a SIMD with wave 0 (a workgroup's waves w and
-    // w + 4 go to one SIMD), the helpers on the other slots in order
-    const int lane = threadIdx.x & 63;
-    const int pwave = threadIdx.x >> 6;
-    const int wave = (NS == 2 && (y.fmode & 16384)) ? (pwave == 4 ? 1 : (pwave >= 1 && pwave <= 3 ? pwave + 1 : pwave))
-                                                     : pwave;
-    const int tid = wave * 64 + lane;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
     const float* W_ih = p.w;                  // [96][64]
     const float* W_hh = p.w + 96 * 64;        // [96][32]
     const float* b_ih = W_hh + 96 * 32;       // [96]
@@ -188,13 +182,7 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
     }
     if (wave < NS) {
         // ---------------- recurrence wave of stream `wave` (gru_kernel wave 0) ----------------
-        // priority 3 (AEC_FUSED_MODE bits 12-13 = v > 0: priority v - 1; timing experiments)
-        switch ((y.fmode >> 12) & 3) {
-            case 1: __builtin_amdgcn_s_setprio(0); break;
-            case 2: __builtin_amdgcn_s_setprio(1); break;
-            case 3: __builtin_amdgcn_s_setprio(2); break;
-            default: __builtin_amdgcn_s_setprio(3); break;
-        }
+        __builtin_amdgcn_s_setprio(3);
         const int s = wave;
         const int T = Ts[s], nch = nchs[s];
         const int j = lane & 31, kh = lane >> 5;

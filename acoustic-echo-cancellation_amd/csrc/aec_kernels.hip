@@ -292,9 +292,6 @@ constexpr int kERow = 512 + 48;        // floats per LDS error row (split path):
 #ifndef AEC_NLMS_MAGROW
 #define AEC_NLMS_MAGROW 1              // K2n: the nlms waves write |E| rows (0: E rows, mags on the ref waves)
 #endif
-#ifndef AEC_NLMS_ERBREG
-#define AEC_NLMS_ERBREG 1              // K2n: ERB schedule bins in registers on the transform waves
-#endif
 // K2n LDS row per frame of a chunk: with AEC_NLMS_MAGROW the nlms waves store |E[k]| at k ^ sw (the
 // swizzle of the group that projects the frame, sw = 16 (i & 1) for frame i), bins 0..256 -> 273
 // floats, then erb_project's 48 partials at kMagPart; otherwise the E row (256 float2) as before
@@ -381,16 +378,12 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
     // tick c2 + 1); this group's frame 4 q + gg.  Run by the ref waves
     // (erb_role 1) or by the nlms waves after their recursion (erb_role 2).
     const int erb_role = p.erb_role == 2 ? 2 : 1;
-    // the ERB schedule's bins in registers (L = 32; mode bit 4 or AEC_NLMS_ERBREG=0: read from LDS per entry)
-    const bool breg = AEC_NLMS_ERBREG && L == kErbRegL && role < 2 && !(p.mode & 16);
-    ErbBins bins;
     auto mic_erb_pass = [&](int c2) {
         const int64_t t2 = (int64_t)c2 * kFPB + 4 * q + gg;
         float* er = sE + (c2 & 1) * kFPB * kNRow + (4 * q + gg) * kNRow;
 #if AEC_NLMS_MAGROW
         // |E| row already in place (the nlms waves' stores, complete since tick c2 + 1's barriers)
-        if (breg) erb_project_reg<kMagPart>(er, sSched, sComb, bins, lb, t2 < T ? feats + t2 * 96 : nullptr);
-        else erb_project<kMagPart>(er, sSched, sComb, L, lb, sw, t2 < T ? feats + t2 * 96 : nullptr);
+        erb_project<kMagPart>(er, sSched, sComb, L, lb, sw, t2 < T ? feats + t2 * 96 : nullptr);
         return;
 #endif
         const float2* row = reinterpret_cast<const float2*>(er);
@@ -469,7 +462,6 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
     }
 
     // mic waves walk near(c), mic(c), near(c+1), ...; ref waves ref(c), ref(c+1), ...
-    if (breg) erb_bins_load(bins, sSched, lb, sw);
     float4 pf[kWavePf];
     if (role == 0) {
         if (have_near) wave_prefetch(pf, row_near, n_near, 4 * q, lane, al_near);
@@ -490,8 +482,7 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
                     if (!(p.mode & 2)) {
                         mags_to_scr(scr, lb, sw, xa, xb, x128);
                         wave_fence();
-                        if (breg) erb_project_reg(scr, sSched, sComb, bins, lb, t < T ? feats + t * 96 + 64 : nullptr);
-                        else erb_project(scr, sSched, sComb, L, lb, sw, t < T ? feats + t * 96 + 64 : nullptr);
+                        erb_project(scr, sSched, sComb, L, lb, sw, t < T ? feats + t * 96 + 64 : nullptr);
                     }
                 }
                 const bool more = c + 1 < nch;
@@ -507,8 +498,7 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
                                c + 1 < nch ? row_ref : nullptr, n_ref, wt + kFPB, al_ref, xa, xb, x128);
                 mags_to_scr(scr, lb, sw, xa, xb, x128);
                 wave_fence();
-                if (breg) erb_project_reg(scr, sSched, sComb, bins, lb, t < T ? feats + t * 96 + 32 : nullptr);
-                else erb_project(scr, sSched, sComb, L, lb, sw, t < T ? feats + t * 96 + 32 : nullptr);
+                erb_project(scr, sSched, sComb, L, lb, sw, t < T ? feats + t * 96 + 32 : nullptr);
                 row_to_scr(scr, lb, xa, xb, x128);
             }
         }

@@ -172,12 +172,9 @@ def test_fused_synthesis_bit_exact(golden_weights, golden_erb, monkeypatch):
     erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
     M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
     res = {}
-    # 'p': two streams per block with both recurrence waves on one SIMD (AEC_FUSED_MODE bit 14) at
-    # priority 1 (bits 12-13 = 2): the role placement and priorities change no arithmetic
-    for fused, ns in (('0', '2'), ('1', '1'), ('1', '2'), ('p', '2')):
-        monkeypatch.setenv('AEC_FUSED_SYNTH', '0' if fused == '0' else '1')   # read when the handle is created
+    for fused, ns in (('0', '2'), ('1', '1'), ('1', '2')):
+        monkeypatch.setenv('AEC_FUSED_SYNTH', fused)            # read when the handle is created
         monkeypatch.setenv('AEC_GRU_NS', ns)                    # streams per fused block, read per launch
-        monkeypatch.setenv('AEC_FUSED_MODE', str(16384 | (2 << 12)) if fused == 'p' else '0')
         net = _net(golden_weights, NLMS)
         net.set_debug(True)
         with torch.no_grad():
@@ -186,7 +183,7 @@ def test_fused_synthesis_bit_exact(golden_weights, golden_erb, monkeypatch):
         torch.cuda.synchronize()
         res[fused + ns] = (out.cpu().numpy(), loss.cpu().numpy(), est.cpu().numpy())
     o0, l0, e0 = res['02']
-    for key in ('11', '12', 'p2'):                               # one and two streams per block (B = 5: odd)
+    for key in ('11', '12'):                                     # one and two streams per block (B = 5: odd)
         o1, l1, e1 = res[key]
         assert np.array_equal(o0, o1), key
         for i, n in enumerate(lens):
@@ -198,9 +195,7 @@ def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatc
     """Few streams take the split NLMS path (frame-parallel transforms + rows,
     per-stream recursion, frame-parallel mic_erb; AEC_SMALLB) instead of the
     per-stream K2n block: the same per-frame arithmetic, so the waveform,
-    the features and the loss are bit-identical to the K2n path.  The K2n
-    path is run twice: ERB schedule bins held in registers (default) and
-    read from LDS per entry (AEC_NLMS_MODE bit 4), also bit-identical."""
+    the features and the loss are bit-identical to the K2n path."""
     from aec_amd import synth
     lens = [33333, 4097, 255, 16000, 256]
     L = max(lens)
@@ -212,9 +207,8 @@ def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatc
     erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
     M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
     res = {}
-    for small in ('0', '64', '0m'):
-        monkeypatch.setenv('AEC_SMALLB', small.rstrip('m'))     # read when the handle is created
-        monkeypatch.setenv('AEC_NLMS_MODE', '16' if small == '0m' else '0')
+    for small in ('0', '64'):
+        monkeypatch.setenv('AEC_SMALLB', small)                 # read when the handle is created
         net = _net(golden_weights, NLMS)
         net.set_debug(True)
         with torch.no_grad():
@@ -223,14 +217,12 @@ def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatc
         feats = {k: net.debug_intermediate(k, len(lens), T).cpu().numpy() for k in ('mic_erb', 'ref_erb', 'est_erb')}
         torch.cuda.synchronize()
         res[small] = (out.cpu().numpy(), loss.cpu().numpy(), feats)
-    o0, l0, f0 = res['0']
-    for key in ('64', '0m'):
-        o1, l1, f1 = res[key]
-        assert np.array_equal(o0, o1), key
-        assert np.array_equal(l0, l1, equal_nan=True), key   # the 256-sample row's loss is the reference's 0/0 NaN
-        for k in f0:
-            for i, n in enumerate(lens):
-                assert np.array_equal(f0[k][i, :n // 256 + 1], f1[k][i, :n // 256 + 1], equal_nan=True), (key, k, i)
+    (o0, l0, f0), (o1, l1, f1) = res['0'], res['64']
+    assert np.array_equal(o0, o1)
+    assert np.array_equal(l0, l1, equal_nan=True)       # the 256-sample row's loss is the reference's 0/0 NaN
+    for k in f0:
+        for i, n in enumerate(lens):
+            assert np.array_equal(f0[k][i, :n // 256 + 1], f1[k][i, :n // 256 + 1], equal_nan=True), (k, i)
 
 
 def test_max_batch_4096_streams_matches_single_calls(nlms_net, golden_erb):
