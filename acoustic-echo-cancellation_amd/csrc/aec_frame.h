@@ -22,9 +22,16 @@ __device__ __forceinline__ float mag(float2 x) {
 // partial sums, pieces of split bands combined through comb.  fo = the
 // frame's 32-float feature row, or null (frame beyond the stream: compute
 // nothing visible).  Leaves the wave fenced.
+__device__ __forceinline__ void erb_project_p(const float* scr, float* part, const float4* sSched, const int2* sComb,
+                                              int L, int lb, int sw, float* fo);
 template <int PART = 512>
 __device__ __forceinline__ void erb_project(float* scr, const float4* sSched, const int2* sComb, int L, int lb,
                                             int sw, float* fo) {
+    erb_project_p(scr, scr + PART, sSched, sComb, L, lb, sw, fo);
+}
+// the same with the 48 partials at `part` (anywhere in the group's LDS, e.g. away from the row)
+__device__ __forceinline__ void erb_project_p(const float* scr, float* part, const float4* sSched, const int2* sComb,
+                                              int L, int lb, int sw, float* fo) {
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
     for (int e = 0; e < L; e += 4) {
 #pragma unroll
@@ -36,7 +43,6 @@ __device__ __forceinline__ void erb_project(float* scr, const float4* sSched, co
             a2 = fmaf(en.w, mg, a2);
         }
     }
-    float* part = scr + PART;                      // 48 partials after the magnitudes
     part[3 * lb + 0] = a0;
     part[3 * lb + 1] = a1;
     part[3 * lb + 2] = a2;

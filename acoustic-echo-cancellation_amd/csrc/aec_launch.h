@@ -138,6 +138,11 @@ inline size_t nlms_smem_bytes(int sched_len, int /*taps*/) {
     return (size_t)sched_len * 16 * 16 + 32 * 8 +
            (258 * 2 + 256 * 2 + 512 + (size_t)8 * 4 * kGroupFloats + (size_t)2 * kFPB * (AEC_NLMS_MAGROW ? 336 : 560)) * 4;
 }
+// K2n, 16 waves: tables + 12 wave regions + 2 x 16 |E| rows of 276 floats
+inline size_t nlms16_smem_bytes(int sched_len) {
+    return (size_t)sched_len * 16 * 16 + 32 * 8 +
+           (258 * 2 + 256 * 2 + 512 + (size_t)12 * 4 * kGroupFloats + (size_t)2 * kFPB * 276) * 4;
+}
 inline size_t synthesis_smem_bytes() {
     return 260 * 16 + (258 * 2 + 256 * 2 + 512 + 256 + kFPB * 33 + 4 + (size_t)kFPB * kGroupFloats) * 4;
 }

@@ -195,7 +195,8 @@ def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatc
     """Few streams take the split NLMS path (frame-parallel transforms + rows,
     per-stream recursion, frame-parallel mic_erb; AEC_SMALLB) instead of the
     per-stream K2n block: the same per-frame arithmetic, so the waveform,
-    the features and the loss are bit-identical to the K2n path."""
+    the features and the loss are bit-identical to the K2n path; so is the
+    16-wave form of K2n (AEC_NLMS_K16=1)."""
     from aec_amd import synth
     lens = [33333, 4097, 255, 16000, 256]
     L = max(lens)
@@ -207,8 +208,9 @@ def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatc
     erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
     M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
     res = {}
-    for small in ('0', '64'):
-        monkeypatch.setenv('AEC_SMALLB', small)                 # read when the handle is created
+    for small in ('0', '64', '0k'):
+        monkeypatch.setenv('AEC_SMALLB', small.rstrip('k'))     # read when the handle is created
+        monkeypatch.setenv('AEC_NLMS_K16', '1' if small == '0k' else '0')   # read per launch
         net = _net(golden_weights, NLMS)
         net.set_debug(True)
         with torch.no_grad():
@@ -217,12 +219,14 @@ def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatc
         feats = {k: net.debug_intermediate(k, len(lens), T).cpu().numpy() for k in ('mic_erb', 'ref_erb', 'est_erb')}
         torch.cuda.synchronize()
         res[small] = (out.cpu().numpy(), loss.cpu().numpy(), feats)
-    (o0, l0, f0), (o1, l1, f1) = res['0'], res['64']
-    assert np.array_equal(o0, o1)
-    assert np.array_equal(l0, l1, equal_nan=True)       # the 256-sample row's loss is the reference's 0/0 NaN
-    for k in f0:
-        for i, n in enumerate(lens):
-            assert np.array_equal(f0[k][i, :n // 256 + 1], f1[k][i, :n // 256 + 1], equal_nan=True), (k, i)
+    o0, l0, f0 = res['0']
+    for key in ('64', '0k'):
+        o1, l1, f1 = res[key]
+        assert np.array_equal(o0, o1), key
+        assert np.array_equal(l0, l1, equal_nan=True), key   # the 256-sample row's loss is the reference's 0/0 NaN
+        for k in f0:
+            for i, n in enumerate(lens):
+                assert np.array_equal(f0[k][i, :n // 256 + 1], f1[k][i, :n // 256 + 1], equal_nan=True), (key, k, i)
 
 
 def test_max_batch_4096_streams_matches_single_calls(nlms_net, golden_erb):
