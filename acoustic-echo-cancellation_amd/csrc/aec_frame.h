@@ -22,16 +22,9 @@ __device__ __forceinline__ float mag(float2 x) {
 // partial sums, pieces of split bands combined through comb.  fo = the
 // frame's 32-float feature row, or null (frame beyond the stream: compute
 // nothing visible).  Leaves the wave fenced.
-__device__ __forceinline__ void erb_project_p(const float* scr, float* part, const float4* sSched, const int2* sComb,
-                                              int L, int lb, int sw, float* fo);
 template <int PART = 512>
 __device__ __forceinline__ void erb_project(float* scr, const float4* sSched, const int2* sComb, int L, int lb,
                                             int sw, float* fo) {
-    erb_project_p(scr, scr + PART, sSched, sComb, L, lb, sw, fo);
-}
-// the same with the 48 partials at `part` (anywhere in the group's LDS, e.g. away from the row)
-__device__ __forceinline__ void erb_project_p(const float* scr, float* part, const float4* sSched, const int2* sComb,
-                                              int L, int lb, int sw, float* fo) {
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
     for (int e = 0; e < L; e += 4) {
 #pragma unroll
@@ -43,6 +36,7 @@ __device__ __forceinline__ void erb_project_p(const float* scr, float* part, con
             a2 = fmaf(en.w, mg, a2);
         }
     }
+    float* part = scr + PART;                      // 48 partials after the magnitudes
     part[3 * lb + 0] = a0;
     part[3 * lb + 1] = a1;
     part[3 * lb + 2] = a2;
@@ -54,6 +48,46 @@ __device__ __forceinline__ void erb_project_p(const float* scr, float* part, con
             const int2 cb = sComb[band];
             fo[band] = part[cb.x] + (cb.y >= 0 ? part[cb.y] : 0.f);
         }
+    }
+    wave_fence();
+}
+
+// Two frames' ERB projections with the same lane schedule in one pass (rows sa, sb with the same
+// swizzle sw): each schedule entry is read once for both gathers, so a wave projecting two frames
+// per tick (K2n's ref waves: mic_erb of chunk c-2 and ref_erb of chunk c) halves its schedule reads
+// and dependent LDS round trips.  Per frame the same entries and FMA order as erb_project (the same
+// bits).  pa / pb: each frame's 48 partials; foa / fob: feature rows or null.
+__device__ __forceinline__ void erb_project2(const float* sa, float* pa, float* foa, const float* sb, float* pb,
+                                             float* fob, const float4* sSched, const int2* sComb, int L, int lb,
+                                             int sw) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f;
+    for (int e = 0; e < L; e += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float4 en = sSched[(e + u) * 16 + lb];
+            const int ix = __float_as_int(en.x) ^ sw;
+            const float ma = sa[ix], mb = sb[ix];
+            a0 = fmaf(en.y, ma, a0);
+            a1 = fmaf(en.z, ma, a1);
+            a2 = fmaf(en.w, ma, a2);
+            b0 = fmaf(en.y, mb, b0);
+            b1 = fmaf(en.z, mb, b1);
+            b2 = fmaf(en.w, mb, b2);
+        }
+    }
+    pa[3 * lb + 0] = a0;
+    pa[3 * lb + 1] = a1;
+    pa[3 * lb + 2] = a2;
+    pb[3 * lb + 0] = b0;
+    pb[3 * lb + 1] = b1;
+    pb[3 * lb + 2] = b2;
+    wave_fence();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int band = lb + 16 * h;
+        const int2 cb = sComb[band];
+        if (foa) foa[band] = pa[cb.x] + (cb.y >= 0 ? pa[cb.y] : 0.f);
+        if (fob) fob[band] = pb[cb.x] + (cb.y >= 0 ? pb[cb.y] : 0.f);
     }
     wave_fence();
 }

@@ -40,7 +40,7 @@
 
 namespace aec {
 #ifdef AEC_TICK_PROF
-constexpr int kNlmsWavesProf = 16;
+constexpr int kNlmsWavesProf = 12;
 #endif
 
 // --------------------------------------------------------------------------
@@ -492,159 +492,26 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
                 row_to_scr(scr, lb, xa, xb, x128);
             }
         } else {
-            if (erb_role == 1 && c >= 2 && !(p.mode & 4)) mic_erb_pass(c - 2);
+            const bool erb2 = erb_role == 1 && c >= 2 && !(p.mode & 4);     // mic_erb of chunk c-2 due
             if (c < nch && !(p.mode & 8)) {
                 nlms_transform(wr, scr, pf, p.cvals[b * 3 + 1], n_ref, wt, lane, gg, lb, sHann, sTwT, sTw512,
                                c + 1 < nch ? row_ref : nullptr, n_ref, wt + kFPB, al_ref, xa, xb, x128);
                 mags_to_scr(scr, lb, sw, xa, xb, x128);
                 wave_fence();
-                erb_project(scr, sSched, sComb, L, lb, sw, t < T ? feats + t * 96 + 32 : nullptr);
+                if (erb2 && AEC_NLMS_MAGROW && !(p.mode & 16)) {
+                    // ref_erb of chunk c and mic_erb of chunk c-2 (|E| rows) in one pass over the schedule
+                    const int64_t t2 = (int64_t)(c - 2) * kFPB + 4 * q + gg;
+                    float* er = sE + (c & 1) * kFPB * kNRow + (4 * q + gg) * kNRow;   // (c - 2) & 1
+                    erb_project2(er, er + kMagPart, t2 < T ? feats + t2 * 96 : nullptr, scr, scr + 512,
+                                 t < T ? feats + t * 96 + 32 : nullptr, sSched, sComb, L, lb, sw);
+                } else {
+                    if (erb2) mic_erb_pass(c - 2);
+                    erb_project(scr, sSched, sComb, L, lb, sw, t < T ? feats + t * 96 + 32 : nullptr);
+                }
                 row_to_scr(scr, lb, xa, xb, x128);
+            } else if (erb2) {
+                mic_erb_pass(c - 2);
             }
-        }
-        TICK_STAMP(1);
-        __syncthreads();                                              // rows of chunk c complete
-        TICK_STAMP(2);
-        __syncthreads();                                              // rows consumed
-        TICK_STAMP(3);
-    }
-}
-
-// --------------------------------------------------------------------------
-// K2n with 16 waves (4 per SIMD, <= 128 VGPRs): the same tick pipeline with four
-// roles, one wave of each per SIMD (wave w -> role w / 4, frames 4 (w % 4) .. +3):
-//   near waves, tick c: mic_erb of chunk c-2 from the |E| rows; near transform
-//        -> near_erb;
-//   mic  waves, tick c: mic transform -> row M (the group's LDS scratch);
-//   ref  waves, tick c: ref transform -> ref_erb -> row R;
-//   nlms waves, tick c: the recursion of chunk c-1 from registers -> |E| rows
-//        (LDS) and E (spec); between the tick's two barriers they copy the
-//        (M, R) rows of chunk c.
-// Against the 12-wave form: each transform wave runs one transform per tick
-// (the mic waves ran two), and every SIMD holds four waves to hide the LDS
-// and VALU dependency latency of the others.  The per-frame arithmetic is the
-// 12-wave kernel's (the same helpers in the same order): bit-identical output.
-// LDS: tables + 12 wave scratch regions + 2 x 16 |E| rows of kERow16 floats;
-// the mic_erb pass keeps its ERB partials in the near wave's own scratch.
-// --------------------------------------------------------------------------
-constexpr int kN16Waves = 16;
-constexpr int kERow16 = 276;           // |E| row: bins 0..256 at k ^ sw (<= 272), 16-B multiple
-
-template <int TAPS>
-__global__ __launch_bounds__(kN16Waves * 64, 1) void nlms_analysis16_kernel(NlmsArgs p) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int tid = threadIdx.x;
-    const int L = p.sched_len;
-
-    float4* sSched = reinterpret_cast<float4*>(smem);                 // L * 16
-    int2* sComb = reinterpret_cast<int2*>(sSched + L * 16);           // 32
-    float2* sTw512 = reinterpret_cast<float2*>(sComb + 32);           // 258
-    float2* sTwT = sTw512 + 258;                                      // 256
-    float* sHann = reinterpret_cast<float*>(sTwT + 256);              // 512
-    float* sWave = sHann + 512;                                       // 12 * kWaveFloats (near, mic, ref waves)
-    float* sE = sWave + 12 * kWaveFloats;                             // 2 x kFPB |E| rows (kERow16 floats)
-
-    const DevTables* tb = reinterpret_cast<const DevTables*>(p.tables);
-    if (tid < 256) {
-        sTwT[tid] = tb->twT[tid];
-        sTw512[tid] = tb->tw512[tid];
-        if (tid < 2) sTw512[256 + tid] = tb->tw512[256 + tid];
-        sHann[tid] = tb->hann[tid];
-        sHann[tid + 256] = tb->hann[tid + 256];
-        if (tid < 32) sComb[tid] = reinterpret_cast<const int2*>(p.sched + 4 * 16 * L)[tid];
-    }
-    {
-        const float4* sch = reinterpret_cast<const float4*>(p.sched);
-        for (int i = tid; i < L * 16; i += kN16Waves * 64) sSched[i] = sch[i];
-    }
-    const int wave = tid >> 6, lane = tid & 63;
-    const int role = wave >> 2, q = wave & 3;                        // 0 near, 1 mic, 2 ref, 3 nlms
-    const int gg = lane >> 4, lb = lane & 15, sw = 16 * (gg & 1);
-    float* wr = sWave + (role < 3 ? wave : 0) * kWaveFloats;
-    float* scr = wr + gg * kGroupFloats;
-    const int b = p.b0 + blockIdx.x;
-    const int n = (int)p.lens[b];
-    const int n_ref = p.slen[4 * b + 1], n_near = p.slen[4 * b + 2];
-    const int64_t T = n / kHop + 1;
-    const int nch = (int)((T + kFPB - 1) / kFPB);
-    const bool have_near = p.nsig == 3;
-    const int64_t ld = p.ld;
-    const float* row_mic = p.sig[0] + (int64_t)b * ld;
-    const float* row_ref = p.sig[1] + (int64_t)b * ld;
-    const float* row_near = have_near ? p.sig[2] + (int64_t)b * ld : nullptr;
-    const bool al_ld = (ld & 3) == 0;
-    const bool al_mic = al_ld && ((reinterpret_cast<uintptr_t>(p.sig[0]) & 15) == 0);
-    const bool al_ref = al_ld && ((reinterpret_cast<uintptr_t>(p.sig[1]) & 15) == 0);
-    const bool al_near = have_near && al_ld && ((reinterpret_cast<uintptr_t>(p.sig[2]) & 15) == 0);
-    float2* spec = p.spec + (int64_t)b * p.Tmax * kSpecRow;
-    float* feats = p.feats + (int64_t)b * p.Tmax * 96;
-    __syncthreads();
-
-    if (role == 3) {
-        const int k = lane + 64 * q;                                  // bin k; k = 0 also bin 256
-        NlmsBin<TAPS> st;
-        st.reset(k == 0);
-        float2 dd[kFPB], rr[kFPB];
-        for (int c = 0; c < nch + 2; ++c) {
-            TICK_STAMP(0);
-            const int c1 = c - 1;
-            if (c1 >= 0 && c1 < nch && !(p.mode & 1)) {
-                const int64_t t0 = (int64_t)c1 * kFPB;
-                float* eb = sE + (c1 & 1) * kFPB * kERow16;
-#pragma unroll
-                for (int i = 0; i < kFPB; ++i) {
-                    const float2 e = st.step(dd[i], rr[i], p.mu, p.beta, p.delta);
-                    const int swi = 16 * (i & 1);
-                    eb[i * kERow16 + (k ^ swi)] = mag(make_float2(e.x, k == 0 ? 0.f : e.y));
-                    if (k == 0) eb[i * kERow16 + (256 ^ swi)] = mag(make_float2(e.y, 0.f));
-                    if (t0 + i < T) spec[(t0 + i) * kSpecRow + k] = e;
-                }
-            }
-            TICK_STAMP(1);
-            __syncthreads();                                          // rows of chunk c complete
-            TICK_STAMP(2);
-            if (c < nch) {
-#pragma unroll
-                for (int i = 0; i < kFPB; ++i) {
-                    const float* base = sWave + (4 + (i >> 2)) * kWaveFloats + (i & 3) * kGroupFloats;
-                    dd[i] = reinterpret_cast<const float2*>(base)[k];
-                    rr[i] = reinterpret_cast<const float2*>(base + 4 * kWaveFloats)[k];
-                }
-            }
-            __syncthreads();                                          // rows consumed
-            TICK_STAMP(3);
-        }
-        return;
-    }
-
-    // near waves walk near(c), near(c+1), ...; mic waves mic(c), ...; ref waves ref(c), ...
-    const float* my_row = role == 0 ? row_near : (role == 1 ? row_mic : row_ref);
-    const int my_n = role == 0 ? n_near : (role == 1 ? n : n_ref);
-    const bool my_al = role == 0 ? al_near : (role == 1 ? al_mic : al_ref);
-    const float cval = p.cvals[b * 3 + (role == 0 ? 2 : (role == 1 ? 0 : 1))];
-    const bool transforms = role != 0 || have_near;
-    float4 pf[kWavePf];
-    if (transforms) wave_prefetch(pf, my_row, my_n, 4 * q, lane, my_al);
-    for (int c = 0; c < nch + 2; ++c) {
-        TICK_STAMP(0);
-        const int wt = c * kFPB + 4 * q;
-        const int64_t t = wt + gg;
-        if (role == 0 && c >= 2 && !(p.mode & 4)) {
-            // mic_erb of chunk c-2 (this group's frame 4 q + gg); partials in the own scratch
-            const int64_t t2 = (int64_t)(c - 2) * kFPB + 4 * q + gg;
-            const float* er = sE + (c & 1) * kFPB * kERow16 + (4 * q + gg) * kERow16;     // (c - 2) & 1
-            erb_project_p(er, scr + 512, sSched, sComb, L, lb, sw, t2 < T ? feats + t2 * 96 : nullptr);
-        }
-        if (transforms && c < nch && !(p.mode & 8)) {
-            float2 xa[8], xb[8], x128;
-            nlms_transform(wr, scr, pf, cval, my_n, wt, lane, gg, lb, sHann, sTwT, sTw512,
-                           c + 1 < nch ? my_row : nullptr, my_n, wt + kFPB, my_al, xa, xb, x128);
-            if (role != 1 && !(role == 0 && (p.mode & 2))) {
-                mags_to_scr(scr, lb, sw, xa, xb, x128);
-                wave_fence();
-                erb_project(scr, sSched, sComb, L, lb, sw, t < T ? feats + t * 96 + (role == 0 ? 64 : 32) : nullptr);
-            }
-            if (role != 0) row_to_scr(scr, lb, xa, xb, x128);
         }
         TICK_STAMP(1);
         __syncthreads();                                              // rows of chunk c complete
@@ -920,17 +787,7 @@ static hipError_t launch_nlms_t(const NlmsArgs& a, int nb, hipStream_t st) {
     // > 64 KiB of LDS: opt in once per instantiation
     static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(nlms_analysis_kernel<TAPS>),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    static const hipError_t attr16 = hipFuncSetAttribute(reinterpret_cast<const void*>(nlms_analysis16_kernel<TAPS>),
-                                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (attr != hipSuccess) return attr;
-    if (attr16 != hipSuccess) return attr16;
-    // the 16-wave form (AEC_NLMS_K16, read per launch; its LDS must fit: ERB schedules of <= 32 entries)
-    const char* k16 = std::getenv("AEC_NLMS_K16");
-    const size_t lds16 = nlms16_smem_bytes(a.sched_len);
-    if (k16 && std::atoi(k16) == 1 && lds16 <= 160 * 1024 && a.erb_role != 2 && AEC_NLMS_MAGROW) {
-        hipLaunchKernelGGL(nlms_analysis16_kernel<TAPS>, dim3(nb), dim3(kN16Waves * 64), lds16, st, a);
-        return hipGetLastError();
-    }
     hipLaunchKernelGGL(nlms_analysis_kernel<TAPS>, dim3(nb), dim3(kNlmsWaves * 64), nlms_smem_bytes(a.sched_len, TAPS),
                        st, a);
     return hipGetLastError();

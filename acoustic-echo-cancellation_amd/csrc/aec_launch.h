@@ -60,7 +60,8 @@ struct NlmsArgs {
     int prio;                // wave priorities (AEC_NLMS_PRIO, decimal digits mic|ref|nlms, 0..3 each)
     int erb_role;            // waves that run the mic_erb pass: 1 ref (AEC_NLMS_ERB=1), 2 nlms
     int mode;                // timing experiments only (AEC_NLMS_MODE): bit0 skip recursion,
-                             // bit1 skip near transform, bit2 skip mic ERB, bit3 skip mic/ref transforms
+                             // bit1 skip near transform, bit2 skip mic ERB, bit3 skip mic/ref transforms;
+                             // bit4 (valid results): the ref waves' two ERB projections in two passes
 };
 
 struct GruArgs {
@@ -137,11 +138,6 @@ inline size_t nlms_smem_bytes(int sched_len, int /*taps*/) {
     // error rows: |E| rows of 288 + 48 floats (AEC_NLMS_MAGROW), or E rows of 512 + 48
     return (size_t)sched_len * 16 * 16 + 32 * 8 +
            (258 * 2 + 256 * 2 + 512 + (size_t)8 * 4 * kGroupFloats + (size_t)2 * kFPB * (AEC_NLMS_MAGROW ? 336 : 560)) * 4;
-}
-// K2n, 16 waves: tables + 12 wave regions + 2 x 16 |E| rows of 276 floats
-inline size_t nlms16_smem_bytes(int sched_len) {
-    return (size_t)sched_len * 16 * 16 + 32 * 8 +
-           (258 * 2 + 256 * 2 + 512 + (size_t)12 * 4 * kGroupFloats + (size_t)2 * kFPB * 276) * 4;
 }
 inline size_t synthesis_smem_bytes() {
     return 260 * 16 + (258 * 2 + 256 * 2 + 512 + 256 + kFPB * 33 + 4 + (size_t)kFPB * kGroupFloats) * 4;

@@ -195,8 +195,9 @@ def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatc
     """Few streams take the split NLMS path (frame-parallel transforms + rows,
     per-stream recursion, frame-parallel mic_erb; AEC_SMALLB) instead of the
     per-stream K2n block: the same per-frame arithmetic, so the waveform,
-    the features and the loss are bit-identical to the K2n path; so is the
-    16-wave form of K2n (AEC_NLMS_K16=1)."""
+    the features and the loss are bit-identical to the K2n path; so is K2n
+    with the ref waves' two ERB projections in two passes (AEC_NLMS_MODE
+    bit 4) instead of the merged pass."""
     from aec_amd import synth
     lens = [33333, 4097, 255, 16000, 256]
     L = max(lens)
@@ -208,9 +209,9 @@ def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatc
     erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
     M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
     res = {}
-    for small in ('0', '64', '0k'):
-        monkeypatch.setenv('AEC_SMALLB', small.rstrip('k'))     # read when the handle is created
-        monkeypatch.setenv('AEC_NLMS_K16', '1' if small == '0k' else '0')   # read per launch
+    for small in ('0', '64', '0m'):
+        monkeypatch.setenv('AEC_SMALLB', small.rstrip('m'))     # read when the handle is created
+        monkeypatch.setenv('AEC_NLMS_MODE', '16' if small == '0m' else '0')
         net = _net(golden_weights, NLMS)
         net.set_debug(True)
         with torch.no_grad():
@@ -220,7 +221,7 @@ def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatc
         torch.cuda.synchronize()
         res[small] = (out.cpu().numpy(), loss.cpu().numpy(), feats)
     o0, l0, f0 = res['0']
-    for key in ('64', '0k'):
+    for key in ('64', '0m'):
         o1, l1, f1 = res[key]
         assert np.array_equal(o0, o1), key
         assert np.array_equal(l0, l1, equal_nan=True), key   # the 256-sample row's loss is the reference's 0/0 NaN

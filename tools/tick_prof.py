@@ -33,17 +33,16 @@ with torch.no_grad():
         net.forward_ragged(mic, ref, near, erb, [n] * B)
 torch.cuda.synchronize()
 lib = _lib.load()
-buf = np.zeros((2, 16, 48, 4), np.uint64)
+buf = np.zeros((2, 12, 48, 4), np.uint64)
 rc = lib.aec_debug_tick_prof(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes))
 assert rc == 0, rc
-k16 = os.environ.get('AEC_NLMS_K16') == '1'
-roles = ['near', 'mic', 'ref', 'nlms'] if k16 else ['mic', 'ref', 'nlms']
+roles = ['mic', 'ref', 'nlms']
 for blk in range(2):
     b = buf[blk].astype(np.int64)
     ticks = range(2, 40)
     tot = [b[0, c + 1, 0] - b[0, c, 0] for c in ticks]
     print(f'block {blk * 128}: tick period median {np.median(tot):.0f} cycles, total loop {b[0, 41, 3] - b[0, 0, 0]} cycles')
-    for r in range(len(roles)):
+    for r in range(3):
         for q in range(4):
             wv = 4 * r + q
             work = np.median([b[wv, c, 1] - b[wv, c, 0] for c in ticks])
