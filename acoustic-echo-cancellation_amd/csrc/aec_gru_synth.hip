@@ -180,6 +180,58 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
             default: break;
         }
     }
+    // OLA + WOLA of chunk k = c - 3 of every stream by 192 lanes (li = 0..191): the head waves by
+    // default, the gi waves with AEC_FUSED_MODE bit 15 (valid results; the same expressions)
+    const bool oal = ((y.ld_out & 3) == 0) && ((reinterpret_cast<uintptr_t>(y.out) & 15) == 0);
+    static_assert(kHeadLanes == kGiLanes, "OLA lane count");
+    auto ola = [&](int c, int li) {
+        // OLA + WOLA of chunk k = c - 3 of every stream (its TF frames in ring k & 1, slots
+        // s TF ..): hops TF k - 1 .. TF k + TF - 2; hop TF k - 1 uses the tail of frame TF k - 1
+        const int k = c - 3;
+        if (k >= 0 && k < nchmax && !(y.fmode & 2)) {
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                if (k >= nchs[s]) continue;
+                const float* ring = sOut + (k & 1) * (kSynWaves * 4 * kGroupFloats) + s * TF * kGroupFloats;
+                const float* tail_in = sTail + ((k & 1) * NS + s) * 256;
+                const int64_t j0 = (int64_t)k * TF - 1;
+                const int nh = (int)min((int64_t)TF, nhops[s] - j0);    // hops j0 .. j0 + nh - 1 below nhop
+                float* orow = y.out + (int64_t)bs[s] * y.ld_out;
+                if (oal) {
+                    for (int e = li; e < TF * (kHop / 4); e += kHeadLanes) {
+                        const int i = e >> 6, r = (e & 63) * 4;     // hop j0 + i = frame i-1 (2nd half) + frame i
+                        if (i >= nh || j0 + i < 0) continue;
+                        const float4 a = i == 0 ? *reinterpret_cast<const float4*>(tail_in + r)
+                                                : *reinterpret_cast<const float4*>(ring + (i - 1) * kGroupFloats + 256 + r);
+                        const float4 cv = *reinterpret_cast<const float4*>(ring + i * kGroupFloats + r);
+                        const float4 cf = *reinterpret_cast<const float4*>(sCoff + r);
+                        float4 o;
+                        o.x = (a.x + cv.x) * cf.x + 1e-9f;
+                        o.y = (a.y + cv.y) * cf.y + 1e-9f;
+                        o.z = (a.z + cv.z) * cf.z + 1e-9f;
+                        o.w = (a.w + cv.w) * cf.w + 1e-9f;
+#if AEC_OUT_NT
+                        typedef float f4v __attribute__((ext_vector_type(4)));
+                        __builtin_nontemporal_store(f4v{o.x, o.y, o.z, o.w},
+                                                    reinterpret_cast<f4v*>(orow + (j0 + i) * kHop + r));
+#else
+                        *reinterpret_cast<float4*>(orow + (j0 + i) * kHop + r) = o;
+#endif
+                    }
+                } else {
+                    for (int e = li; e < TF * kHop; e += kHeadLanes) {
+                        const int i = e >> 8, r = e & 255;
+                        if (i >= nh || j0 + i < 0) continue;
+                        const float a = i == 0 ? tail_in[r] : ring[(i - 1) * kGroupFloats + 256 + r];
+                        const float cv = ring[i * kGroupFloats + r];
+                        orow[(j0 + i) * kHop + r] = (a + cv) * sCoff[r] + 1e-9f;
+                    }
+                }
+                for (int r = li; r < 256; r += kHeadLanes)
+                    sTail[(((k + 1) & 1) * NS + s) * 256 + r] = ring[(TF - 1) * kGroupFloats + 256 + r];
+            }
+        }
+    };
     if (wave < NS) {
         // ---------------- recurrence wave of stream `wave` (gru_kernel wave 0) ----------------
         __builtin_amdgcn_s_setprio(3);
@@ -275,6 +327,7 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
                     sGi[((cg & 1) * kCH + q) * 96 + grow] = gru_gi(wih, sX + ((cg & 1) * kCH + q) * 64, gbias);
                 }
             }
+            if (y.fmode & 32768) ola(c, hl);
             GTICK(1);
             tick_barrier();
         }
@@ -291,7 +344,6 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
         float lacc[NS];
 #pragma unroll
         for (int s = 0; s < NS; ++s) lacc[s] = 0.f;
-        const bool oal = ((y.ld_out & 3) == 0) && ((reinterpret_cast<uintptr_t>(y.out) & 15) == 0);
         for (int c = -3; c <= nchmax + 2; ++c) {
             GTICK(0);
             const int ch = c - 1;
@@ -322,52 +374,7 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
                     sEst[((ch & 1) * kCH + q) * kEstS + hj_] = est;   // frames past the end: gain 0
                 }
             }
-            // OLA + WOLA of chunk k = c - 3 of every stream (its TF frames in ring k & 1, slots
-            // s TF ..): hops TF k - 1 .. TF k + TF - 2; hop TF k - 1 uses the tail of frame TF k - 1
-            const int k = c - 3;
-            if (k >= 0 && k < nchmax && !(y.fmode & 2)) {
-#pragma unroll
-                for (int s = 0; s < NS; ++s) {
-                    if (k >= nchs[s]) continue;
-                    const float* ring = sOut + (k & 1) * (kSynWaves * 4 * kGroupFloats) + s * TF * kGroupFloats;
-                    const float* tail_in = sTail + ((k & 1) * NS + s) * 256;
-                    const int64_t j0 = (int64_t)k * TF - 1;
-                    const int nh = (int)min((int64_t)TF, nhops[s] - j0);    // hops j0 .. j0 + nh - 1 below nhop
-                    float* orow = y.out + (int64_t)bs[s] * y.ld_out;
-                    if (oal) {
-                        for (int e = hh; e < TF * (kHop / 4); e += kHeadLanes) {
-                            const int i = e >> 6, r = (e & 63) * 4;     // hop j0 + i = frame i-1 (2nd half) + frame i
-                            if (i >= nh || j0 + i < 0) continue;
-                            const float4 a = i == 0 ? *reinterpret_cast<const float4*>(tail_in + r)
-                                                    : *reinterpret_cast<const float4*>(ring + (i - 1) * kGroupFloats + 256 + r);
-                            const float4 cv = *reinterpret_cast<const float4*>(ring + i * kGroupFloats + r);
-                            const float4 cf = *reinterpret_cast<const float4*>(sCoff + r);
-                            float4 o;
-                            o.x = (a.x + cv.x) * cf.x + 1e-9f;
-                            o.y = (a.y + cv.y) * cf.y + 1e-9f;
-                            o.z = (a.z + cv.z) * cf.z + 1e-9f;
-                            o.w = (a.w + cv.w) * cf.w + 1e-9f;
-#if AEC_OUT_NT
-                            typedef float f4v __attribute__((ext_vector_type(4)));
-                            __builtin_nontemporal_store(f4v{o.x, o.y, o.z, o.w},
-                                                        reinterpret_cast<f4v*>(orow + (j0 + i) * kHop + r));
-#else
-                            *reinterpret_cast<float4*>(orow + (j0 + i) * kHop + r) = o;
-#endif
-                        }
-                    } else {
-                        for (int e = hh; e < TF * kHop; e += kHeadLanes) {
-                            const int i = e >> 8, r = e & 255;
-                            if (i >= nh || j0 + i < 0) continue;
-                            const float a = i == 0 ? tail_in[r] : ring[(i - 1) * kGroupFloats + 256 + r];
-                            const float cv = ring[i * kGroupFloats + r];
-                            orow[(j0 + i) * kHop + r] = (a + cv) * sCoff[r] + 1e-9f;
-                        }
-                    }
-                    for (int r = hh; r < 256; r += kHeadLanes)
-                        sTail[(((k + 1) & 1) * NS + s) * 256 + r] = ring[(TF - 1) * kGroupFloats + 256 + r];
-                }
-            }
+            if (!(y.fmode & 32768)) ola(c, hh);
             GTICK(1);
             tick_barrier();
         }

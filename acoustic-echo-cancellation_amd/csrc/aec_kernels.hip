@@ -426,9 +426,13 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
                     const float2 e = st.step(dd[i], rr[i], mu, beta, delta);
 #if AEC_NLMS_MAGROW
                     // |E| (mags_to_scr's expression: slot 0's real pair as (E, 0) each) at k ^ sw_i
+                    // bin 256 (lane k = 0's second real bin): every lane computes and stores it, the
+                    // others into the row's partials area (rewritten by the mic_erb pass before it is
+                    // read; lanes of a 32-lane half on distinct banks), so the wave holding slot 0
+                    // runs no divergent branch
                     const int swi = 16 * (i & 1);
                     eb[i * kNRow + (k ^ swi)] = mag(make_float2(e.x, k == 0 ? 0.f : e.y));
-                    if (k == 0) eb[i * kNRow + (256 ^ swi)] = mag(make_float2(e.y, 0.f));
+                    eb[i * kNRow + (k == 0 ? (256 ^ swi) : kMagPart + (k & 31))] = mag(make_float2(e.y, 0.f));
 #else
                     reinterpret_cast<float2*>(eb + i * kERow)[k] = e;
 #endif
