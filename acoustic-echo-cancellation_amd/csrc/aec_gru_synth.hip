@@ -13,9 +13,9 @@
 // recurrence wave each, on different SIMDs; 8 frames of each per tick):
 //
 //   waves 0..NS-1  recurrence of stream s, chunk c          (gru_kernel's code)
-//   3 gi waves     stage feats of chunk c+2, load chunk c+3, gi = W_ih x + b of chunk c+1;
+//   3 gi waves     stage feats of chunk c+2, load chunk c+3, gi = W_ih x + b of chunk c+1
+//   3 head waves   head / mask / est_erb / loss of chunk c-1 -> est (HBM + LDS ring);
 //                  OLA + WOLA of chunk c-3 from the frame ring -> out
-//   3 head waves   head / mask / est_erb / loss of chunk c-1 -> est (HBM + LDS ring)
 //   4 synth waves  synthesis (gains, irFFT, window) of chunk c-2 into the LDS
 //                  frame ring;  E rows of chunk c-1 into registers
 //
@@ -180,72 +180,6 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
             default: break;
         }
     }
-    // OLA + WOLA of chunk k = c - 3 of every stream by the 192 lanes of the gi waves (li = 0..191),
-    // after their input projections (the head waves, which ran it before, were the tick's long pole
-    // next to the synthesis waves: profiles/r05f_gru_tick_ola.txt)
-    const bool oal = ((y.ld_out & 3) == 0) && ((reinterpret_cast<uintptr_t>(y.out) & 15) == 0);
-    static_assert(kHeadLanes == kGiLanes && kHeadLanes == 3 * 64, "OLA lane count (3 hops per lane pass)");
-    auto ola = [&](int c, int li) {
-        // OLA + WOLA of chunk k = c - 3 of every stream (its TF frames in ring k & 1, slots
-        // s TF ..): hops TF k - 1 .. TF k + TF - 2; hop TF k - 1 uses the tail of frame TF k - 1
-        const int k = c - 3;
-        if (k >= 0 && k < nchmax && !(y.fmode & 2)) {
-#pragma unroll
-            for (int s = 0; s < NS; ++s) {
-                if (k >= nchs[s]) continue;
-                const float* ring = sOut + (k & 1) * (kSynWaves * 4 * kGroupFloats) + s * TF * kGroupFloats;
-                const float* tail_in = sTail + ((k & 1) * NS + s) * 256;
-                const int64_t j0 = (int64_t)k * TF - 1;
-                const int nh = (int)min((int64_t)TF, nhops[s] - j0);    // hops j0 .. j0 + nh - 1 below nhop
-                float* orow = y.out + (int64_t)bs[s] * y.ld_out;
-                if (oal) {
-                    // lane li: float4 r = 4 (li & 63) of hops i0, i0 + 3, i0 + 6 (i0 = li / 64; 192 lanes,
-                    // 64 float4 per hop): every load first (one LDS round trip), then the stores
-                    constexpr int kU = (TF * (kHop / 4) + kHeadLanes - 1) / kHeadLanes;
-                    const int r = (li & 63) * 4, i0 = li >> 6;
-                    float4 A[kU], C[kU];
-                    bool ok[kU];
-                    const float4 cf = *reinterpret_cast<const float4*>(sCoff + r);
-#pragma unroll
-                    for (int u = 0; u < kU; ++u) {
-                        const int i = i0 + 3 * u;                   // hop j0 + i = frame i-1 (2nd half) + frame i
-                        ok[u] = i < TF && i < nh && j0 + i >= 0;
-                        const int ic = ok[u] ? i : 1;
-                        A[u] = ic == 0 ? *reinterpret_cast<const float4*>(tail_in + r)
-                                       : *reinterpret_cast<const float4*>(ring + (ic - 1) * kGroupFloats + 256 + r);
-                        C[u] = *reinterpret_cast<const float4*>(ring + ic * kGroupFloats + r);
-                    }
-#pragma unroll
-                    for (int u = 0; u < kU; ++u) {
-                        if (!ok[u]) continue;
-                        const int i = i0 + 3 * u;
-                        float4 o;
-                        o.x = (A[u].x + C[u].x) * cf.x + 1e-9f;
-                        o.y = (A[u].y + C[u].y) * cf.y + 1e-9f;
-                        o.z = (A[u].z + C[u].z) * cf.z + 1e-9f;
-                        o.w = (A[u].w + C[u].w) * cf.w + 1e-9f;
-#if AEC_OUT_NT
-                        typedef float f4v __attribute__((ext_vector_type(4)));
-                        __builtin_nontemporal_store(f4v{o.x, o.y, o.z, o.w},
-                                                    reinterpret_cast<f4v*>(orow + (j0 + i) * kHop + r));
-#else
-                        *reinterpret_cast<float4*>(orow + (j0 + i) * kHop + r) = o;
-#endif
-                    }
-                } else {
-                    for (int e = li; e < TF * kHop; e += kHeadLanes) {
-                        const int i = e >> 8, r = e & 255;
-                        if (i >= nh || j0 + i < 0) continue;
-                        const float a = i == 0 ? tail_in[r] : ring[(i - 1) * kGroupFloats + 256 + r];
-                        const float cv = ring[i * kGroupFloats + r];
-                        orow[(j0 + i) * kHop + r] = (a + cv) * sCoff[r] + 1e-9f;
-                    }
-                }
-                for (int r = li; r < 256; r += kHeadLanes)
-                    sTail[(((k + 1) & 1) * NS + s) * 256 + r] = ring[(TF - 1) * kGroupFloats + 256 + r];
-            }
-        }
-    };
     if (wave < NS) {
         // ---------------- recurrence wave of stream `wave` (gru_kernel wave 0) ----------------
         __builtin_amdgcn_s_setprio(3);
@@ -341,7 +275,6 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
                     sGi[((cg & 1) * kCH + q) * 96 + grow] = gru_gi(wih, sX + ((cg & 1) * kCH + q) * 64, gbias);
                 }
             }
-            ola(c, hl);
             GTICK(1);
             tick_barrier();
         }
@@ -358,6 +291,7 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
         float lacc[NS];
 #pragma unroll
         for (int s = 0; s < NS; ++s) lacc[s] = 0.f;
+        const bool oal = ((y.ld_out & 3) == 0) && ((reinterpret_cast<uintptr_t>(y.out) & 15) == 0);
         for (int c = -3; c <= nchmax + 2; ++c) {
             GTICK(0);
             const int ch = c - 1;
@@ -386,6 +320,52 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
                         }
                     }
                     sEst[((ch & 1) * kCH + q) * kEstS + hj_] = est;   // frames past the end: gain 0
+                }
+            }
+            // OLA + WOLA of chunk k = c - 3 of every stream (its TF frames in ring k & 1, slots
+            // s TF ..): hops TF k - 1 .. TF k + TF - 2; hop TF k - 1 uses the tail of frame TF k - 1
+            const int k = c - 3;
+            if (k >= 0 && k < nchmax && !(y.fmode & 2)) {
+#pragma unroll
+                for (int s = 0; s < NS; ++s) {
+                    if (k >= nchs[s]) continue;
+                    const float* ring = sOut + (k & 1) * (kSynWaves * 4 * kGroupFloats) + s * TF * kGroupFloats;
+                    const float* tail_in = sTail + ((k & 1) * NS + s) * 256;
+                    const int64_t j0 = (int64_t)k * TF - 1;
+                    const int nh = (int)min((int64_t)TF, nhops[s] - j0);    // hops j0 .. j0 + nh - 1 below nhop
+                    float* orow = y.out + (int64_t)bs[s] * y.ld_out;
+                    if (oal) {
+                        for (int e = hh; e < TF * (kHop / 4); e += kHeadLanes) {
+                            const int i = e >> 6, r = (e & 63) * 4;     // hop j0 + i = frame i-1 (2nd half) + frame i
+                            if (i >= nh || j0 + i < 0) continue;
+                            const float4 a = i == 0 ? *reinterpret_cast<const float4*>(tail_in + r)
+                                                    : *reinterpret_cast<const float4*>(ring + (i - 1) * kGroupFloats + 256 + r);
+                            const float4 cv = *reinterpret_cast<const float4*>(ring + i * kGroupFloats + r);
+                            const float4 cf = *reinterpret_cast<const float4*>(sCoff + r);
+                            float4 o;
+                            o.x = (a.x + cv.x) * cf.x + 1e-9f;
+                            o.y = (a.y + cv.y) * cf.y + 1e-9f;
+                            o.z = (a.z + cv.z) * cf.z + 1e-9f;
+                            o.w = (a.w + cv.w) * cf.w + 1e-9f;
+#if AEC_OUT_NT
+                            typedef float f4v __attribute__((ext_vector_type(4)));
+                            __builtin_nontemporal_store(f4v{o.x, o.y, o.z, o.w},
+                                                        reinterpret_cast<f4v*>(orow + (j0 + i) * kHop + r));
+#else
+                            *reinterpret_cast<float4*>(orow + (j0 + i) * kHop + r) = o;
+#endif
+                        }
+                    } else {
+                        for (int e = hh; e < TF * kHop; e += kHeadLanes) {
+                            const int i = e >> 8, r = e & 255;
+                            if (i >= nh || j0 + i < 0) continue;
+                            const float a = i == 0 ? tail_in[r] : ring[(i - 1) * kGroupFloats + 256 + r];
+                            const float cv = ring[i * kGroupFloats + r];
+                            orow[(j0 + i) * kHop + r] = (a + cv) * sCoff[r] + 1e-9f;
+                        }
+                    }
+                    for (int r = hh; r < 256; r += kHeadLanes)
+                        sTail[(((k + 1) & 1) * NS + s) * 256 + r] = ring[(TF - 1) * kGroupFloats + 256 + r];
                 }
             }
             GTICK(1);

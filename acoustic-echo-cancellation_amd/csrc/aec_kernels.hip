@@ -298,78 +298,6 @@ constexpr int kERow = 512 + 48;        // floats per LDS error row (split path):
 constexpr int kMagPart = 288;
 constexpr int kNRow = AEC_NLMS_MAGROW ? kMagPart + 48 : kERow;
 
-#ifndef AEC_NLMS_DIRECT
-#define AEC_NLMS_DIRECT 0     // K2n: frame samples loaded straight into the FFT input layout (no LDS staging)
-#endif
-#if AEC_NLMS_DIRECT
-// Direct frame loads: group gg's lane lb loads its frame's samples in the FFT input layout from
-// global memory, pv[a] = (x[s + 32 a + 2 lb], x[s + 32 a + 2 lb + 1]), s = 256 (t - 1), through
-// the row's buffer descriptor (outside [0, n) the range check returns 0); the hop staging through
-// LDS (wave_commit's stores and load_frame's sample reads) is gone.  Adjacent frames overlap by
-// half, so each sample is fetched twice, the second time from L1 / L2.
-typedef float2 FramePf[16];
-__device__ __forceinline__ void frame_prefetch(FramePf& pv, const float* __restrict__ row, int n, int t, int lb,
-                                               bool al8) {
-    const uint64_t ra = reinterpret_cast<uint64_t>(row);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)ra);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(ra >> 32));
-    const int nb = __builtin_amdgcn_readfirstlane(n * 4);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, nb, 0x00020000);
-    const int base = ((t - 1) * kHop + 2 * lb) * 4;
-    if (__builtin_expect(al8, 1)) {
-#pragma unroll
-        for (int a = 0; a < 16; ++a) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, base + 128 * a, 0, AEC_LOAD_CPOL);
-            pv[a] = make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
-        }
-    } else {
-#pragma unroll
-        for (int a = 0; a < 16; ++a)
-            pv[a] = make_float2(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, base + 128 * a, 0, AEC_LOAD_CPOL)),
-                                __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, base + 128 * a + 4, 0, AEC_LOAD_CPOL)));
-    }
-}
-// wave_commit's normalisation and mask, then load_frame's window: the same expressions.  wt: the
-// wave's first frame; a wave whose 4 frames lie inside [0, n) skips the mask (wave-uniform branch)
-__device__ __forceinline__ void frame_commit(float2 (&v)[16], const FramePf& pv, float c, int n, int wt, int gg,
-                                             int lb, const float* hann) {
-    const float2* h2 = reinterpret_cast<const float2*>(hann);
-    const int s0 = (wt + gg - 1) * kHop + 2 * lb;
-    if (wt >= 1 && (wt + kWaveFrames) * kHop <= n) {
-#pragma unroll
-        for (int a = 0; a < 16; ++a) {
-            const float2 w = h2[16 * a + lb];
-            v[a] = make_float2((pv[a].x - c) * w.x, (pv[a].y - c) * w.y);
-        }
-        return;
-    }
-#pragma unroll
-    for (int a = 0; a < 16; ++a) {
-        const int i = s0 + 32 * a;
-        const float x0 = (i + 0 >= 0 && i + 0 < n) ? pv[a].x - c : 0.f;
-        const float x1 = (i + 1 >= 0 && i + 1 < n) ? pv[a].y - c : 0.f;
-        const float2 w = h2[16 * a + lb];
-        v[a] = make_float2(x0 * w.x, x1 * w.y);
-    }
-}
-#endif
-
-// One transform pass of a wave: commit the prefetched samples of (signal,
-// 4 frames at wt), prefetch the next task, window + rFFT -> xa / xb / x128.
-#if AEC_NLMS_DIRECT
-__device__ __forceinline__ void nlms_transform(float* wr, float* scr, FramePf& pf, float cval, int n, int wt,
-                                               int lane, int gg, int lb, const float* sHann, const float2* sTwT,
-                                               const float2* sTw512, const float* next_row, int next_n, int next_wt,
-                                               bool next_al, float2 (&xa)[8], float2 (&xb)[8], float2& x128) {
-    asm volatile("" ::: "memory");
-    float2 v[16];
-    frame_commit(v, pf, cval, n, wt, gg, lb, sHann);
-    if (next_row) frame_prefetch(pf, next_row, next_n, next_wt + gg, lb, next_al);
-    fft256<false>(v, lb, scr, sTwT);
-    rfft_unpack(v, lb, sTw512, xa, xb, x128);
-}
-#else
 __device__ __forceinline__ void nlms_transform(float* wr, float* scr, float4 (&pf)[kWavePf], float cval, int n, int wt,
                                                int lane, int gg, int lb, const float* sHann, const float2* sTwT,
                                                const float2* sTw512, const float* next_row, int next_n, int next_wt,
@@ -384,7 +312,6 @@ __device__ __forceinline__ void nlms_transform(float* wr, float* scr, float4 (&p
     fft256<false>(v, lb, scr, sTwT);
     rfft_unpack(v, lb, sTw512, xa, xb, x128);
 }
-#endif
 
 template <int TAPS>
 __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsArgs p) {
@@ -438,25 +365,18 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
     const float* row_mic = p.sig[0] + (int64_t)b * ld;
     const float* row_ref = p.sig[1] + (int64_t)b * ld;
     const float* row_near = have_near ? p.sig[2] + (int64_t)b * ld : nullptr;
-#if AEC_NLMS_DIRECT
-    // float2 loads: every row 8-B aligned
-    const bool al_ld = (ld & 1) == 0;
-    const bool al_mic = al_ld && ((reinterpret_cast<uintptr_t>(p.sig[0]) & 7) == 0);
-    const bool al_ref = al_ld && ((reinterpret_cast<uintptr_t>(p.sig[1]) & 7) == 0);
-    const bool al_near = have_near && al_ld && ((reinterpret_cast<uintptr_t>(p.sig[2]) & 7) == 0);
-#else
     const bool al_ld = (ld & 3) == 0;
     const bool al_mic = al_ld && ((reinterpret_cast<uintptr_t>(p.sig[0]) & 15) == 0);
     const bool al_ref = al_ld && ((reinterpret_cast<uintptr_t>(p.sig[1]) & 15) == 0);
     const bool al_near = have_near && al_ld && ((reinterpret_cast<uintptr_t>(p.sig[2]) & 15) == 0);
-#endif
     float2* spec = p.spec + (int64_t)b * p.Tmax * kSpecRow;
     float* feats = p.feats + (int64_t)b * p.Tmax * 96;
     const float mu = p.mu, beta = p.beta, delta = p.delta;
     // mic_erb of chunk c2 from its error rows (complete since the barriers of
     // tick c2 + 1); this group's frame 4 q + gg.  Run by the ref waves
     // (erb_role 1) or by the nlms waves after their recursion (erb_role 2).
-    const int erb_role = p.erb_role == 2 ? 2 : 1;
+    // 1: ref waves (merged with the ref ERB), 2: nlms waves, 3: mic waves (merged with the near ERB)
+    const int erb_role = (p.erb_role == 2 || p.erb_role == 3) ? p.erb_role : 1;
     auto mic_erb_pass = [&](int c2) {
         const int64_t t2 = (int64_t)c2 * kFPB + 4 * q + gg;
         float* er = sE + (c2 & 1) * kFPB * kNRow + (4 * q + gg) * kNRow;
@@ -545,15 +465,6 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
     }
 
     // mic waves walk near(c), mic(c), near(c+1), ...; ref waves ref(c), ref(c+1), ...
-#if AEC_NLMS_DIRECT
-    FramePf pf;
-    if (role == 0) {
-        if (have_near) frame_prefetch(pf, row_near, n_near, 4 * q + gg, lb, al_near);
-        else frame_prefetch(pf, row_mic, n, 4 * q + gg, lb, al_mic);
-    } else {
-        frame_prefetch(pf, row_ref, n_ref, 4 * q + gg, lb, al_ref);
-    }
-#else
     float4 pf[kWavePf];
     if (role == 0) {
         if (have_near) wave_prefetch(pf, row_near, n_near, 4 * q, lane, al_near);
@@ -561,13 +472,14 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
     } else {
         wave_prefetch(pf, row_ref, n_ref, 4 * q, lane, al_ref);
     }
-#endif
     for (int c = 0; c < nch + 2; ++c) {
         TICK_STAMP(0);
         const int wt = c * kFPB + 4 * q;
         const int64_t t = wt + gg;
         float2 xa[8], xb[8], x128;
         if (role == 0) {
+            const bool erb2 = erb_role == 3 && c >= 2 && !(p.mode & 4);     // mic_erb of chunk c-2 due here
+            bool erb2_done = false;
             if (c < nch && !(p.mode & 8)) {
                 if (have_near) {
                     nlms_transform(wr, scr, pf, p.cvals[b * 3 + 2], n_near, wt, lane, gg, lb, sHann, sTwT, sTw512,
@@ -575,7 +487,16 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
                     if (!(p.mode & 2)) {
                         mags_to_scr(scr, lb, sw, xa, xb, x128);
                         wave_fence();
-                        erb_project(scr, sSched, sComb, L, lb, sw, t < T ? feats + t * 96 + 64 : nullptr);
+                        if (erb2 && AEC_NLMS_MAGROW && !(p.mode & 16)) {
+                            // near_erb of chunk c and mic_erb of chunk c-2 in one pass over the schedule
+                            const int64_t t2 = (int64_t)(c - 2) * kFPB + 4 * q + gg;
+                            float* er = sE + (c & 1) * kFPB * kNRow + (4 * q + gg) * kNRow;   // (c - 2) & 1
+                            erb_project2(er, er + kMagPart, t2 < T ? feats + t2 * 96 : nullptr, scr, scr + 512,
+                                         t < T ? feats + t * 96 + 64 : nullptr, sSched, sComb, L, lb, sw);
+                            erb2_done = true;
+                        } else {
+                            erb_project(scr, sSched, sComb, L, lb, sw, t < T ? feats + t * 96 + 64 : nullptr);
+                        }
                     }
                 }
                 const bool more = c + 1 < nch;
@@ -584,6 +505,7 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
                                have_near ? al_near : al_mic, xa, xb, x128);
                 row_to_scr(scr, lb, xa, xb, x128);
             }
+            if (erb2 && !erb2_done) mic_erb_pass(c - 2);
         } else {
             const bool erb2 = erb_role == 1 && c >= 2 && !(p.mode & 4);     // mic_erb of chunk c-2 due
             if (c < nch && !(p.mode & 8)) {
