@@ -180,6 +180,10 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
             default: break;
         }
     }
+    // the overlap-add of chunk c-3 on the recurrence waves (each its own stream, after the tick's
+    // steps; AEC_FUSED_MODE bit 15) instead of the head waves: the same expressions
+    const bool ola_rec = NS == 2 && (y.fmode & 32768) != 0 && y.ld_out % 4 == 0 &&
+                         (reinterpret_cast<uintptr_t>(y.out) & 15) == 0;
     if (wave < NS) {
         // ---------------- recurrence wave of stream `wave` (gru_kernel wave 0) ----------------
         __builtin_amdgcn_s_setprio(3);
@@ -217,6 +221,42 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
                     }
                     gr = ngr; gz = ngz; gn = ngn;
                 }
+            }
+            const int k = c - 3;
+            if (NS == 2 && ola_rec && k >= 0 && k < nch && !(y.fmode & 2)) {
+                // lane: float4 column r = 4 lane of the chunk's TF hops; frame halves from the ring
+                // (all loads first), hop j0 + i = frame i-1 (2nd half) + frame i (1st half)
+                const float* ring = sOut + (k & 1) * (kSynWaves * 4 * kGroupFloats) + s * TF * kGroupFloats;
+                const float* tail_in = sTail + ((k & 1) * NS + s) * 256;
+                const int64_t j0 = (int64_t)k * TF - 1;
+                const int nh = (int)min((int64_t)TF, nhops[s] - j0);
+                const int r = 4 * lane;
+                float4 fh[NS == 2 ? TF : 1], sh[NS == 2 ? TF : 1];
+                const float4 tl = *reinterpret_cast<const float4*>(tail_in + r);
+                const float4 cf = *reinterpret_cast<const float4*>(sCoff + r);
+#pragma unroll
+                for (int i = 0; i < TF; ++i) {
+                    fh[i] = *reinterpret_cast<const float4*>(ring + i * kGroupFloats + r);
+                    sh[i] = *reinterpret_cast<const float4*>(ring + i * kGroupFloats + 256 + r);
+                }
+                float* orow = y.out + (int64_t)bs[s] * y.ld_out;
+#pragma unroll
+                for (int i = 0; i < TF; ++i) {
+                    if (i >= nh || j0 + i < 0) continue;
+                    const float4 a = i == 0 ? tl : sh[i - 1];
+                    float4 o;
+                    o.x = (a.x + fh[i].x) * cf.x + 1e-9f;
+                    o.y = (a.y + fh[i].y) * cf.y + 1e-9f;
+                    o.z = (a.z + fh[i].z) * cf.z + 1e-9f;
+                    o.w = (a.w + fh[i].w) * cf.w + 1e-9f;
+#if AEC_OUT_NT
+                    typedef float f4v __attribute__((ext_vector_type(4)));
+                    __builtin_nontemporal_store(f4v{o.x, o.y, o.z, o.w}, reinterpret_cast<f4v*>(orow + (j0 + i) * kHop + r));
+#else
+                    *reinterpret_cast<float4*>(orow + (j0 + i) * kHop + r) = o;
+#endif
+                }
+                *reinterpret_cast<float4*>(sTail + (((k + 1) & 1) * NS + s) * 256 + r) = sh[TF - 1];
             }
             GTICK(1);
             tick_barrier();
@@ -325,7 +365,7 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
             // OLA + WOLA of chunk k = c - 3 of every stream (its TF frames in ring k & 1, slots
             // s TF ..): hops TF k - 1 .. TF k + TF - 2; hop TF k - 1 uses the tail of frame TF k - 1
             const int k = c - 3;
-            if (k >= 0 && k < nchmax && !(y.fmode & 2)) {
+            if (k >= 0 && k < nchmax && !(y.fmode & 2) && !ola_rec) {
 #pragma unroll
                 for (int s = 0; s < NS; ++s) {
                     if (k >= nchs[s]) continue;

@@ -375,8 +375,8 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
     // mic_erb of chunk c2 from its error rows (complete since the barriers of
     // tick c2 + 1); this group's frame 4 q + gg.  Run by the ref waves
     // (erb_role 1) or by the nlms waves after their recursion (erb_role 2).
-    // 1: ref waves (merged with the ref ERB), 2: nlms waves, 3: mic waves (merged with the near ERB)
-    const int erb_role = (p.erb_role == 2 || p.erb_role == 3) ? p.erb_role : 1;
+    // 1: ref waves (merged with the ref ERB), 2: nlms waves
+    const int erb_role = p.erb_role == 2 ? 2 : 1;
     auto mic_erb_pass = [&](int c2) {
         const int64_t t2 = (int64_t)c2 * kFPB + 4 * q + gg;
         float* er = sE + (c2 & 1) * kFPB * kNRow + (4 * q + gg) * kNRow;
@@ -478,8 +478,6 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
         const int64_t t = wt + gg;
         float2 xa[8], xb[8], x128;
         if (role == 0) {
-            const bool erb2 = erb_role == 3 && c >= 2 && !(p.mode & 4);     // mic_erb of chunk c-2 due here
-            bool erb2_done = false;
             if (c < nch && !(p.mode & 8)) {
                 if (have_near) {
                     nlms_transform(wr, scr, pf, p.cvals[b * 3 + 2], n_near, wt, lane, gg, lb, sHann, sTwT, sTw512,
@@ -487,16 +485,7 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
                     if (!(p.mode & 2)) {
                         mags_to_scr(scr, lb, sw, xa, xb, x128);
                         wave_fence();
-                        if (erb2 && AEC_NLMS_MAGROW && !(p.mode & 16)) {
-                            // near_erb of chunk c and mic_erb of chunk c-2 in one pass over the schedule
-                            const int64_t t2 = (int64_t)(c - 2) * kFPB + 4 * q + gg;
-                            float* er = sE + (c & 1) * kFPB * kNRow + (4 * q + gg) * kNRow;   // (c - 2) & 1
-                            erb_project2(er, er + kMagPart, t2 < T ? feats + t2 * 96 : nullptr, scr, scr + 512,
-                                         t < T ? feats + t * 96 + 64 : nullptr, sSched, sComb, L, lb, sw);
-                            erb2_done = true;
-                        } else {
-                            erb_project(scr, sSched, sComb, L, lb, sw, t < T ? feats + t * 96 + 64 : nullptr);
-                        }
+                        erb_project(scr, sSched, sComb, L, lb, sw, t < T ? feats + t * 96 + 64 : nullptr);
                     }
                 }
                 const bool more = c + 1 < nch;
@@ -505,7 +494,6 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
                                have_near ? al_near : al_mic, xa, xb, x128);
                 row_to_scr(scr, lb, xa, xb, x128);
             }
-            if (erb2 && !erb2_done) mic_erb_pass(c - 2);
         } else {
             const bool erb2 = erb_role == 1 && c >= 2 && !(p.mode & 4);     // mic_erb of chunk c-2 due
             if (c < nch && !(p.mode & 8)) {

@@ -172,9 +172,11 @@ def test_fused_synthesis_bit_exact(golden_weights, golden_erb, monkeypatch):
     erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
     M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
     res = {}
-    for fused, ns in (('0', '2'), ('1', '1'), ('1', '2')):
-        monkeypatch.setenv('AEC_FUSED_SYNTH', fused)            # read when the handle is created
+    # 'o': the overlap-add on the recurrence waves (AEC_FUSED_MODE bit 15, two streams per block)
+    for fused, ns in (('0', '2'), ('1', '1'), ('1', '2'), ('o', '2')):
+        monkeypatch.setenv('AEC_FUSED_SYNTH', '0' if fused == '0' else '1')   # read when the handle is created
         monkeypatch.setenv('AEC_GRU_NS', ns)                    # streams per fused block, read per launch
+        monkeypatch.setenv('AEC_FUSED_MODE', '32768' if fused == 'o' else '0')
         net = _net(golden_weights, NLMS)
         net.set_debug(True)
         with torch.no_grad():
@@ -183,7 +185,7 @@ def test_fused_synthesis_bit_exact(golden_weights, golden_erb, monkeypatch):
         torch.cuda.synchronize()
         res[fused + ns] = (out.cpu().numpy(), loss.cpu().numpy(), est.cpu().numpy())
     o0, l0, e0 = res['02']
-    for key in ('11', '12'):                                     # one and two streams per block (B = 5: odd)
+    for key in ('11', '12', 'o2'):                               # one and two streams per block (B = 5: odd)
         o1, l1, e1 = res[key]
         assert np.array_equal(o0, o1), key
         for i, n in enumerate(lens):
@@ -197,8 +199,7 @@ def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatc
     per-stream K2n block: the same per-frame arithmetic, so the waveform,
     the features and the loss are bit-identical to the K2n path; so is K2n
     with the ref waves' two ERB projections in two passes (AEC_NLMS_MODE
-    bit 4) instead of the merged pass, and with the mic_erb pass merged into
-    the mic waves' near ERB instead (AEC_NLMS_ERB=3)."""
+    bit 4) instead of the merged pass."""
     from aec_amd import synth
     lens = [33333, 4097, 255, 16000, 256]
     L = max(lens)
@@ -210,10 +211,9 @@ def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatc
     erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
     M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
     res = {}
-    for small in ('0', '64', '0m', '0e'):
-        monkeypatch.setenv('AEC_SMALLB', small.rstrip('me'))    # read when the handle is created
+    for small in ('0', '64', '0m'):
+        monkeypatch.setenv('AEC_SMALLB', small.rstrip('m'))     # read when the handle is created
         monkeypatch.setenv('AEC_NLMS_MODE', '16' if small == '0m' else '0')
-        monkeypatch.setenv('AEC_NLMS_ERB', '3' if small == '0e' else '1')
         net = _net(golden_weights, NLMS)
         net.set_debug(True)
         with torch.no_grad():
@@ -223,7 +223,7 @@ def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatc
         torch.cuda.synchronize()
         res[small] = (out.cpu().numpy(), loss.cpu().numpy(), feats)
     o0, l0, f0 = res['0']
-    for key in ('64', '0m', '0e'):
+    for key in ('64', '0m'):
         o1, l1, f1 = res[key]
         assert np.array_equal(o0, o1), key
         assert np.array_equal(l0, l1, equal_nan=True), key   # the 256-sample row's loss is the reference's 0/0 NaN
