@@ -125,6 +125,119 @@ __global__ __launch_bounds__(NT) void moments_kernel(const float* __restrict__ m
     }
 }
 
+// K1 through LDS-DMA (AEC_MOM_CFG=3): the same per-thread float4 sequence (thread tid sums float4
+// lo/4 + tid + 256 m for m = 0, 1, ...) and the same block reduction, so bit-identical partials,
+// but the loads land in a per-wave LDS ring (buffer_load ... lds, 4 KB in flight per wave) instead of
+// registers.  The point is its footprint: ~20 VGPRs and 16 KB of LDS per block, which fits beside a
+// K2n block (153 VGPRs x 3 waves per SIMD, 131 KB of LDS) on the same CU, so with batches in
+// flight the next batch's moments pass can stream under this batch's analysis instead of holding
+// whole CUs (the register-loaded kernel needs 36 VGPRs, 4 more than a K2n CU has left).
+constexpr int kMomSlots = 4;
+__device__ __forceinline__ void mom_wait_vm(int n) {
+    // s_waitcnt vmcnt(n) (n < 16), other counters left alone
+    switch (n) {
+        case 0: __builtin_amdgcn_s_waitcnt(0x0F70); break;
+        case 1: __builtin_amdgcn_s_waitcnt(0x0F71); break;
+        case 2: __builtin_amdgcn_s_waitcnt(0x0F72); break;
+        default: __builtin_amdgcn_s_waitcnt(0x0F73); break;
+    }
+}
+__global__ __launch_bounds__(256) void moments_lds_kernel(const float* __restrict__ mic, const float* __restrict__ ref,
+                                                          const float* __restrict__ near, int64_t ld,
+                                                          const int32_t* __restrict__ slen, double2* __restrict__ mom,
+                                                          int b0) {
+    // one array per ring slot: a read of slot j waits only for the DMAs into slot j
+    __shared__ __attribute__((aligned(16))) float4 sR0[256];
+    __shared__ __attribute__((aligned(16))) float4 sR1[256];
+    __shared__ __attribute__((aligned(16))) float4 sR2[256];
+    __shared__ __attribute__((aligned(16))) float4 sR3[256];
+    const int ch = blockIdx.x, s = blockIdx.y, b = b0 + blockIdx.z;
+    const float* base = (s == 0 ? mic : (s == 1 ? ref : near));
+    const float* x = base + (int64_t)b * ld;
+    const int64_t n = slen[4 * b + s];
+    const int64_t per = ((n + kMomChunks - 1) / kMomChunks + 1023) & ~(int64_t)1023;
+    const int64_t lo = ch * per, hi = min(n, lo + per);
+    double s1 = 0.0, s2 = 0.0;
+    const int tid = threadIdx.x, wave = tid >> 6;
+    auto acc4 = [&](const float4 v) {
+        const double a = v.x, bb = v.y, c = v.z, d = v.w;
+        s1 += (a + bb) + (c + d);
+        s2 += (a * a + bb * bb) + (c * c + d * d);
+    };
+    if (lo < hi) {
+        int64_t i = lo + tid;
+        if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+            const int64_t end4 = hi / 4, b4 = lo / 4;
+            const int M = (int)((end4 - b4 + 255) / 256);      // DMA rounds (the last may be partial)
+            const uint64_t xa = reinterpret_cast<uint64_t>(x + 4 * b4);
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<void*>(xa), (short)0, (int)((end4 - b4) * 16), 0x00020000);
+            // slot J is a distinct __shared__ array, named at compile time (static_for), so the
+            // compiler's wait before an LDS read covers only the DMAs into that slot
+            auto slot = [&](auto Jc) -> float4* {
+                constexpr int J = decltype(Jc)::value;
+                if constexpr (J == 0) return sR0;
+                else if constexpr (J == 1) return sR1;
+                else if constexpr (J == 2) return sR2;
+                else return sR3;
+            };
+            auto issue = [&](int m, float4* sl) {              // the wave's 64 float4 of round m -> slot
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (__attribute__((address_space(3))) void*)(sl + 64 * wave), 16,
+                    (uint32_t)((256 * m + tid) * 16), 0, 0, 2);  // nt: each sample is read once here
+            };
+            static_for<0, kMomSlots>([&](auto Jc) {
+                constexpr int J = decltype(Jc)::value;
+                if (J < M) issue(J, slot(Jc));
+            });
+            for (int m0 = 0; m0 < M; m0 += kMomSlots) {
+                static_for<0, kMomSlots>([&](auto Jc) {
+                    constexpr int J = decltype(Jc)::value;
+                    const int m = m0 + J;
+                    if (m < M) {
+                        mom_wait_vm(min(kMomSlots - 1, M - 1 - m));     // round m landed
+                        // the read in asm: the compiler's own DMA tracking would wait for every
+                        // DMA in flight (vmcnt(0)) before any LDS read; the wait above is exact
+                        const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)(
+                            slot(Jc) + tid);
+                        float4 v;
+                        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(la) : "memory");
+                        if (b4 + tid + 256 * (int64_t)m < end4) acc4(v);
+                        if (m + kMomSlots < M) issue(m + kMomSlots, slot(Jc));
+                    }
+                });
+            }
+            i = end4 * 4 + tid;
+        }
+        for (; i < hi; i += 256) {
+            const double a = x[i];
+            s1 += a;
+            s2 += a * a;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s1 += __shfl_xor(s1, o);
+        s2 += __shfl_xor(s2, o);
+    }
+    __shared__ double r1[4], r2[4];
+    if ((tid & 63) == 0) {
+        r1[tid >> 6] = s1;
+        r2[tid >> 6] = s2;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double t1[4], t2[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) { t1[w] = r1[w]; t2[w] = r2[w]; }
+#pragma unroll
+        for (int st = 1; st < 4; st <<= 1)
+#pragma unroll
+            for (int w = 0; w + st < 4; w += 2 * st) { t1[w] += t1[w + st]; t2[w] += t2[w + st]; }
+        mom[((int64_t)b * 3 + s) * kMomChunks + ch] = make_double2(t1[0], t2[0]);
+    }
+}
+
 // c for every (stream, signal): cvals[b*3 + s]
 __global__ __launch_bounds__(256) void norm_finalize_kernel(const double2* __restrict__ mom,
                                                             const int32_t* __restrict__ slen,
@@ -753,6 +866,10 @@ hipError_t launch_moments(const float* mic, const float* ref, const float* near,
     const dim3 g(kMomChunks, nsig, nb);
     if (cfg == 1)
         hipLaunchKernelGGL((moments_kernel<4, 256, false>), g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0);
+    else if (cfg == 2)
+        hipLaunchKernelGGL((moments_kernel<2, 256, true>), g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0);
+    else if (cfg == 3)
+        hipLaunchKernelGGL(moments_lds_kernel, g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0);
     else
         hipLaunchKernelGGL((moments_kernel<4, 256, true>), g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0);
     return hipGetLastError();
