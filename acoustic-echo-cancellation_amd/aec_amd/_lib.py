@@ -23,6 +23,7 @@ _STATUS = {0: 'AEC_OK', 1: 'AEC_ERR_INVALID_ARG', 2: 'AEC_ERR_OOM', 3: 'AEC_ERR_
 
 # every symbol include/aec_hip.h declares
 EXPORTS = ('aec_weights_count', 'aec_create', 'aec_set_weights', 'aec_set_erb', 'aec_process', 'aec_process_siglens',
+           'aec_prepare', 'aec_prepare_siglens',
            'aec_stream_open', 'aec_stream_reset', 'aec_stream_step',
            'aec_set_debug', 'aec_debug_copy', 'aec_profile_enable', 'aec_profile_read',
            'aec_erb_tables_check', 'aec_num_frames', 'aec_out_len', 'aec_last_error', 'aec_destroy',
@@ -81,6 +82,10 @@ def load():
     lib.aec_process.restype = ctypes.c_int
     lib.aec_process_siglens.argtypes = [P, P, P, P, P, ctypes.c_int32, ctypes.c_int64, P, ctypes.c_int64, P, P]
     lib.aec_process_siglens.restype = ctypes.c_int
+    lib.aec_prepare.argtypes = [P, P, P, P, P, ctypes.c_int32, ctypes.c_int64, P]
+    lib.aec_prepare.restype = ctypes.c_int
+    lib.aec_prepare_siglens.argtypes = [P, P, P, P, P, ctypes.c_int32, ctypes.c_int64, P]
+    lib.aec_prepare_siglens.restype = ctypes.c_int
     lib.aec_stream_open.argtypes = [P, ctypes.c_int32]
     lib.aec_stream_open.restype = ctypes.c_int
     lib.aec_stream_reset.argtypes = [P, ctypes.c_int32, P]
@@ -214,6 +219,14 @@ class Handle:
         st = fn(self.h, mic_ptr, ref_ptr, near_ptr, lens.ctypes.data, int(B), int(ld),
                 out_ptr, int(ld_out), loss_ptr, stream)
         check(st, self.h, 'aec_process_siglens' if lens.ndim == 2 else 'aec_process')
+
+    def prepare(self, mic_ptr, ref_ptr, near_ptr, lengths, B, ld, stream):
+        """Look-ahead normaliser pass of the batch a later process() takes (aec_prepare[_siglens])."""
+        import numpy as np
+        lens = np.ascontiguousarray(lengths, dtype=np.int64)
+        fn = self.lib.aec_prepare_siglens if lens.ndim == 2 else self.lib.aec_prepare
+        st = fn(self.h, mic_ptr, ref_ptr, near_ptr, lens.ctypes.data, int(B), int(ld), stream)
+        check(st, self.h, 'aec_prepare_siglens' if lens.ndim == 2 else 'aec_prepare')
 
     def stream_open(self, B):
         check(self.lib.aec_stream_open(self.h, int(B)), self.h, 'aec_stream_open')

@@ -287,6 +287,30 @@ class Little_net(nn.Module):
                           stream)
         return out, loss
 
+    def prepare_ragged(self, mic, ref, near, lengths):
+        """Queue the normaliser pass (ERB.py:254-256) of the batch the next
+        ``forward_ragged`` on this net will take, on the current stream
+        (``aec_prepare_siglens``): a serving loop runs it on a side stream while
+        the previous batch is still in flight.  The tensors must be the very
+        ones (contiguous float32, same data) passed to that ``forward_ragged``;
+        otherwise it drops the look-ahead and runs the pass itself.  Outputs are
+        bit-identical either way."""
+        dev = mic.device
+        if dev.type != 'cuda':
+            raise RuntimeError(f'Little_net (gfx950) needs its inputs on a HIP device, got {dev}')
+        for t in [mic, ref] + ([near] if near is not None else []):
+            if t.shape != mic.shape or t.device != dev or not t.is_contiguous() or t.dtype != torch.float32:
+                raise ValueError('prepare_ragged needs contiguous float32 mic / ref / near of one shape and device')
+        B, L = mic.shape
+        lengths = np.asarray(lengths, dtype=np.int64)
+        if lengths.shape not in ((B,), (B, 3)) or (lengths < 1).any() or (lengths > L).any():
+            raise ValueError('lengths must be [B] or [B, 3] with 1 <= length <= N')
+        h, _ = self._handle(dev)
+        if B > 0:
+            with torch.cuda.device(dev):
+                h.prepare(mic.data_ptr(), ref.data_ptr(), near.data_ptr() if near is not None else None,
+                          lengths, B, L, torch.cuda.current_stream(dev).cuda_stream)
+
     # --- streaming (include/aec_hip.h aec_stream_*) ------------------------------
     def stream_open(self, B, erb, device=None):
         """Open B concurrent streams (state zeroed) on ``device``: afterwards

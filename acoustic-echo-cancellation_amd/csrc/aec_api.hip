@@ -196,6 +196,24 @@ struct aec_handle {
     int64_t* d_len = nullptr;    // [B] mic length: sets the frame count and output length
     int32_t* d_slen = nullptr;   // [B][4] per-signal lengths (mic, ref, near, -): normaliser + zero padding
     int64_t nitems = 0, nsitems = 0;
+    // look-ahead normaliser passes (aec_prepare_siglens), consumed in order by the process calls
+    struct PreSlot {
+        double2* mom = nullptr;       // [cap][3][kMomChunks]
+        float* cvals = nullptr;       // [cap][3]
+        int32_t* slen = nullptr;      // device [cap][4]
+        int32_t* host = nullptr;      // pinned [cap][4] (upload staging)
+        int64_t cap = 0;
+        hipEvent_t done = nullptr;    // recorded after norm_finalize on the prepare stream
+        hipEvent_t freed = nullptr;   // recorded after the consuming call's kernels
+        bool used = false;            // done / freed recorded at least once
+        bool freed_rec = false;
+        const float* sig[3] = {nullptr, nullptr, nullptr};
+        int64_t ld = 0;
+        int nsig = 0;
+        std::vector<int64_t> l3;
+    };
+    PreSlot pre[2];
+    int pre_head = 0, pre_count = 0;
     struct ListSlot {
         char* host = nullptr;    // pinned
         size_t cap = 0;
@@ -600,9 +618,34 @@ aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref
     s = prepare_lists(h, lengths3, B, nsig_in, st);
     if (s != AEC_OK) return s;
     const int nsig = near ? 3 : 2;
+    // a matching look-ahead pass (aec_prepare_siglens): wait for it instead of running it
+    aec_handle::PreSlot* ps = nullptr;
+    if (h->pre_count > 0) {
+        aec_handle::PreSlot& c = h->pre[h->pre_head];
+        if (c.sig[0] == mic && c.sig[1] == ref && c.sig[2] == near && c.ld == ld && c.nsig == nsig &&
+            c.l3.size() == (size_t)B * 3 && std::memcmp(c.l3.data(), lengths3, (size_t)B * 3 * sizeof(int64_t)) == 0) {
+            ps = &c;
+            h->pre_head = (h->pre_head + 1) & 1;
+            --h->pre_count;
+        } else {
+            h->pre_count = 0;   // stale: drop every pending look-ahead (their slots stay fenced by done)
+        }
+    }
+    // the consumed slot is free again once this call's kernels have read its cvals (every exit)
+    struct PreRelease {
+        aec_handle::PreSlot* ps;
+        hipStream_t st;
+        ~PreRelease() {
+            if (ps && hipEventRecord(ps->freed, st) == hipSuccess) ps->freed_rec = true;
+        }
+    } pre_rel{ps, st};
+    const float* cvals = ps ? ps->cvals : h->d_cvals;
+    if (ps) HIP_TRY(h, hipStreamWaitEvent(st, ps->done, 0));
     mark(h, st);
-    HIP_TRY(h, launch_moments(mic, ref, near, ld, h->d_slen, h->d_mom, 0, B, nsig, st));
-    HIP_TRY(h, launch_norm_finalize(h->d_mom, h->d_slen, h->d_cvals, 0, B, nsig, st));
+    if (!ps) {
+        HIP_TRY(h, launch_moments(mic, ref, near, ld, h->d_slen, h->d_mom, 0, B, nsig, st));
+        HIP_TRY(h, launch_norm_finalize(h->d_mom, h->d_slen, h->d_cvals, 0, B, nsig, st));
+    }
     if (h->cfg.nlms_taps > 0 && B <= h->small_b && h->nlms_mode == 0) {
         // few streams: transforms frame-parallel (K2 + rows), recursion per stream, mic_erb frame-parallel
         const size_t need = (size_t)B * Tmax * 512 + (size_t)B * 256;      // + one dummy row per stream
@@ -617,7 +660,7 @@ aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref
         AnalysisArgs a{};
         a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
         a.ld = ld; a.items = h->d_items; a.nitems = h->nitems;
-        a.num_cus = h->num_cus; a.cvals = h->d_cvals; a.slen = h->d_slen;
+        a.num_cus = h->num_cus; a.cvals = cvals; a.slen = h->d_slen;
         a.tables = reinterpret_cast<const float*>(h->d_tab);
         a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
         a.feats = h->d_feats; a.Tmax = Tmax; a.rows = h->d_rows;
@@ -631,7 +674,7 @@ aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref
     } else if (h->cfg.nlms_taps > 0) {
         NlmsArgs a{};
         a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
-        a.ld = ld; a.lens = h->d_len; a.slen = h->d_slen; a.b0 = 0; a.cvals = h->d_cvals;
+        a.ld = ld; a.lens = h->d_len; a.slen = h->d_slen; a.b0 = 0; a.cvals = cvals;
         a.tables = reinterpret_cast<const float*>(h->d_tab);
         a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
         a.feats = h->d_feats; a.Tmax = Tmax; a.spec = h->d_spec;
@@ -645,7 +688,7 @@ aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref
         AnalysisArgs a{};
         a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
         a.ld = ld; a.items = h->d_items; a.nitems = h->nitems;
-        a.num_cus = h->num_cus; a.cvals = h->d_cvals; a.slen = h->d_slen;
+        a.num_cus = h->num_cus; a.cvals = cvals; a.slen = h->d_slen;
         a.tables = reinterpret_cast<const float*>(h->d_tab);
         a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
         a.feats = h->d_feats; a.Tmax = Tmax;
@@ -664,7 +707,7 @@ aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref
 
     SynthArgs y{};
     y.mic = mic; y.ld = ld; y.items = h->d_sitems; y.nitems = h->nsitems; y.num_cus = h->num_cus;
-    y.cvals = h->d_cvals;
+    y.cvals = cvals;
     y.tables = reinterpret_cast<const float*>(h->d_tab);
     y.bintab = h->d_bintab; y.est = h->d_est; y.Tmax = Tmax;
     y.out = out; y.ld_out = ld_out;
@@ -684,6 +727,70 @@ aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref
     h->last_B = B;
     h->last_T = Tmax;
     return cg.end();
+}
+
+aec_status aec_prepare_siglens(aec_handle* h, const float* mic, const float* ref, const float* near,
+                               const int64_t* lengths3, int32_t B, int64_t ld, void* stream) {
+    if (!h) return AEC_ERR_INVALID_ARG;
+    if (B <= 0 || !lengths3 || !mic || !ref) return fail(h, AEC_ERR_INVALID_ARG, "bad batch / lengths / signals");
+    if (h->pre_count >= 2) return fail(h, AEC_ERR_INVALID_ARG, "two look-ahead batches already pending");
+    const int nsig = near ? 3 : 2;
+    for (int b = 0; b < B; ++b) {
+        const int64_t n = lengths3[3 * b];
+        for (int sg = 0; sg < nsig; ++sg) {
+            const int64_t ns = lengths3[3 * b + sg];
+            if (ns < 1 || ns > ld) return fail(h, AEC_ERR_INVALID_ARG, "length out of [1, ld]");
+            if (ns > INT32_MAX - 4096) return fail(h, AEC_ERR_UNSUPPORTED, "stream longer than 2^31 - 4096 samples");
+            if (ns / 256 != n / 256)
+                return fail(h, AEC_ERR_INVALID_ARG, "ref / near frame count differs from mic's (N//256 + 1)");
+        }
+    }
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    AEC_ON_DEVICE(h);
+    aec_handle::PreSlot& ps = h->pre[(h->pre_head + h->pre_count) & 1];
+    if (ps.used) HIP_TRY(h, hipEventSynchronize(ps.done));      // its staging copy has been read
+    if (B > ps.cap) {
+        if (ps.freed_rec) HIP_TRY(h, hipEventSynchronize(ps.freed));
+        (void)hipFree(ps.mom); (void)hipFree(ps.cvals); (void)hipFree(ps.slen);
+        if (ps.host) (void)hipHostFree(ps.host);
+        ps.mom = nullptr; ps.cvals = nullptr; ps.slen = nullptr; ps.host = nullptr; ps.cap = 0;
+        const int64_t cap = B + B / 4;
+        HIP_TRY(h, hipMalloc(&ps.mom, (size_t)cap * 3 * kMomChunks * sizeof(double2)));
+        HIP_TRY(h, hipMalloc(&ps.cvals, (size_t)cap * 3 * sizeof(float)));
+        HIP_TRY(h, hipMalloc(&ps.slen, (size_t)cap * 4 * sizeof(int32_t)));
+        HIP_TRY(h, hipHostMalloc(reinterpret_cast<void**>(&ps.host), (size_t)cap * 4 * sizeof(int32_t)));
+        ps.cap = cap;
+    }
+    if (!ps.done) HIP_TRY(h, hipEventCreateWithFlags(&ps.done, hipEventDisableTiming));
+    if (!ps.freed) HIP_TRY(h, hipEventCreateWithFlags(&ps.freed, hipEventDisableTiming));
+    // the call that consumed this slot last has read its cvals; a dropped pass into it has finished
+    if (ps.freed_rec) HIP_TRY(h, hipStreamWaitEvent(st, ps.freed, 0));
+    if (ps.used) HIP_TRY(h, hipStreamWaitEvent(st, ps.done, 0));
+    for (int b = 0; b < B; ++b) {   // prepare_lists' per-signal lengths
+        for (int sg = 0; sg < 3; ++sg)
+            ps.host[4 * b + sg] = (int32_t)(sg < nsig ? lengths3[3 * b + sg] : lengths3[3 * b]);
+        ps.host[4 * b + 3] = 0;
+    }
+    HIP_TRY(h, hipMemcpyAsync(ps.slen, ps.host, (size_t)B * 4 * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(h, launch_moments(mic, ref, near, ld, ps.slen, ps.mom, 0, B, nsig, st));
+    HIP_TRY(h, launch_norm_finalize(ps.mom, ps.slen, ps.cvals, 0, B, nsig, st));
+    HIP_TRY(h, hipEventRecord(ps.done, st));
+    ps.used = true;
+    ps.sig[0] = mic; ps.sig[1] = ref; ps.sig[2] = near;
+    ps.ld = ld;
+    ps.nsig = nsig;
+    ps.l3.assign(lengths3, lengths3 + (size_t)B * 3);
+    ++h->pre_count;
+    return AEC_OK;
+}
+
+aec_status aec_prepare(aec_handle* h, const float* mic, const float* ref, const float* near,
+                       const int64_t* lengths, int32_t B, int64_t ld, void* stream) {
+    if (!h) return AEC_ERR_INVALID_ARG;
+    if (B <= 0 || !lengths) return fail(h, AEC_ERR_INVALID_ARG, "bad batch / lengths");
+    std::vector<int64_t> l3((size_t)B * 3);
+    for (int b = 0; b < B; ++b) l3[3 * b] = l3[3 * b + 1] = l3[3 * b + 2] = lengths[b];
+    return aec_prepare_siglens(h, mic, ref, near, l3.data(), B, ld, stream);
 }
 
 aec_status aec_debug_copy(aec_handle* h, int32_t what, float* dst, size_t n, void* stream) {
@@ -1003,6 +1110,14 @@ void aec_destroy(aec_handle* h) {
         if (sl.host) (void)hipHostFree(sl.host);
     }
     (void)hipFree(h->d_w); (void)hipFree(h->d_tab); (void)hipFree(h->d_sched); (void)hipFree(h->d_bintab);
+    for (auto& ps : h->pre) {
+        if (ps.used) (void)hipEventSynchronize(ps.done);
+        if (ps.freed_rec) (void)hipEventSynchronize(ps.freed);
+        (void)hipFree(ps.mom); (void)hipFree(ps.cvals); (void)hipFree(ps.slen);
+        if (ps.host) (void)hipHostFree(ps.host);
+        if (ps.done) (void)hipEventDestroy(ps.done);
+        if (ps.freed) (void)hipEventDestroy(ps.freed);
+    }
     (void)hipFree(h->d_mom); (void)hipFree(h->d_cvals); (void)hipFree(h->d_lists);
     (void)hipFree(h->d_feats); (void)hipFree(h->d_est); (void)hipFree(h->d_dbg); (void)hipFree(h->d_spec);
     (void)hipFree(h->d_state); (void)hipFree(h->d_rows);

@@ -254,6 +254,9 @@ __device__ __forceinline__ void fft256_packed(float2 (&v)[16], int lb, float* sc
 #ifndef AEC_FFT_PK
 #define AEC_FFT_PK 1
 #endif
+#ifndef AEC_FFT_PK_INV
+#define AEC_FFT_PK_INV 0   // the inverse on the packed core too (A/B builds)
+#endif
 template <bool INV>
 __device__ __forceinline__ void fft256(float2 (&v)[16], int lb, float* scr, const float2* twT) {
     // forward transforms packed, inverse scalar: the packed inverse made the
@@ -261,7 +264,7 @@ __device__ __forceinline__ void fft256(float2 (&v)[16], int lb, float* scr, cons
     // SIMDs with the synthesis waves), and every synthesis path must run the
     // same inverse arithmetic (the fused / separate / streaming kernels are
     // tested bit-identical)
-    if constexpr (AEC_FFT_PK && !INV) fft256_packed<INV>(v, lb, scr, twT);
+    if constexpr (AEC_FFT_PK && (!INV || AEC_FFT_PK_INV)) fft256_packed<INV>(v, lb, scr, twT);
     else fft256_scalar<INV>(v, lb, scr, twT);
 }
 

@@ -265,7 +265,10 @@ __device__ __forceinline__ void synth_pack(const float2 (&xa)[8], const float2 (
     });
 }
 
-// irFFT-256 of the packed frame, window and 1/512 -> scr[0..511] (natural order)
+// irFFT-256 of the packed frame, window and 1/512 -> scr[0..511] (natural order).
+// PRE: sHann holds hann / 512 (exact: a power-of-two scale of normal values), so the
+// product is the same float with one multiply instead of two.
+template <bool PRE = false>
 __device__ __forceinline__ void synth_fft(float2 (&v)[16], const float2* sTwT, const float* sHann, float* scr, int lb) {
     fft256<true>(v, lb, scr, sTwT);
     // v[kP(m2)] = 512 * (x[2m] + i x[2m+1]), m = lb + 16 m2 ; window + 1/512
@@ -275,7 +278,8 @@ __device__ __forceinline__ void synth_fft(float2 (&v)[16], const float2* sTwT, c
     for (int m2 = 0; m2 < 16; ++m2) {
         const float2 z = v[kP(m2)];
         const float2 w = h2[lb + 16 * m2];
-        s2[lb + 16 * m2] = make_float2(z.x * (w.x * (1.f / 512.f)), z.y * (w.y * (1.f / 512.f)));
+        if constexpr (PRE) s2[lb + 16 * m2] = make_float2(z.x * w.x, z.y * w.y);
+        else s2[lb + 16 * m2] = make_float2(z.x * (w.x * (1.f / 512.f)), z.y * (w.y * (1.f / 512.f)));
     }
 }
 

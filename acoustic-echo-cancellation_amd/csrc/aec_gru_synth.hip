@@ -26,6 +26,9 @@
 #ifndef AEC_OUT_NT
 #define AEC_OUT_NT 1   // waveform stores nt: written once, never re-read on the device (fused kernel -1 %)
 #endif
+#ifndef AEC_SYN_HANN_PRE
+#define AEC_SYN_HANN_PRE 0   // synthesis window table pre-scaled by 1/512 (bit-identical; A/B)
+#endif
 #ifndef AEC_SPEC_LD_NT
 #define AEC_SPEC_LD_NT 0   // E-spectrum row loads nt (A/B builds only)
 #endif
@@ -164,7 +167,7 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
             sCoff[i] = tb->inv_coff[i];
         }
         for (int i = tid; i < 2 * NS * 256; i += kThreads) sTail[i] = 0.f;
-        for (int i = tid; i < 512; i += kThreads) sHann[i] = tb->hann[i];
+        for (int i = tid; i < 512; i += kThreads) sHann[i] = AEC_SYN_HANN_PRE ? tb->hann[i] * (1.f / 512.f) : tb->hann[i];
     }
 
     {
@@ -469,7 +472,7 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
                 float2 v[16];
                 synth_pack(xa, xb, x128, sEst + ((cs & 1) * kCH + fl) * kEstS, sBin, sTw512, lb, v);
                 if (next) load_rows(c - 1);
-                synth_fft(v, sTwT, sHann, scr, lb);
+                synth_fft<AEC_SYN_HANN_PRE>(v, sTwT, sHann, scr, lb);
             } else if (next) {
                 load_rows(c - 1);
             }

@@ -108,6 +108,25 @@ aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref
                                const int64_t* lengths3, int32_t B, int64_t ld,
                                float* out, int64_t ld_out, float* loss, void* stream);
 
+/* Optional look-ahead (serving): queue the per-stream normaliser pass of a batch
+ * (c = mean/std of each signal over its length, ERB.py:254-256 — a full read of
+ * every signal before the first frame can be normalised) on `stream`, ahead of
+ * the aec_process / aec_process_siglens call that will take the batch.  That
+ * call (on any stream) waits for it on the device instead of running the pass
+ * itself; it matches on the signal pointers, ld, B and the lengths.  At most two
+ * batches may be pending per handle (AEC_ERR_INVALID_ARG beyond); a process call
+ * whose batch does not match the oldest pending one drops every pending one and
+ * runs the pass itself.  The signals must stay unchanged until that call.
+ * Outputs are bit-identical with and without the look-ahead (the same kernels).
+ * No reference counterpart: the reference computes the normaliser inside
+ * Little_net.forward (ERB.py:254-256).
+ *   lengths3 : host [B][3] int64, as aec_process_siglens (lengths may be NULL-free
+ *              [B] via aec_prepare with one length per stream) */
+aec_status aec_prepare_siglens(aec_handle* h, const float* mic, const float* ref, const float* near,
+                               const int64_t* lengths3, int32_t B, int64_t ld, void* stream);
+aec_status aec_prepare(aec_handle* h, const float* mic, const float* ref, const float* near,
+                       const int64_t* lengths, int32_t B, int64_t ld, void* stream);
+
 /* Streaming (serving): the reference's per-frame loop (Little_net.forward,
  * ERB.py:252-334) advanced by one 256-sample hop per stream per call, as ONE
  * fused kernel launch (frame -> rFFT -> [FD-NLMS] -> ERB -> GRU step -> head

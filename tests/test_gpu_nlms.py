@@ -232,6 +232,51 @@ def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatc
                 assert np.array_equal(f0[k][i, :n // 256 + 1], f1[k][i, :n // 256 + 1], equal_nan=True), (key, k, i)
 
 
+def test_normaliser_lookahead_bit_exact(nlms_net, golden_erb):
+    """aec_prepare_siglens (Little_net.prepare_ragged): the normaliser pass of a
+    batch queued on a side stream ahead of its forward_ragged call.  The
+    waveform and loss are bit-identical to the call without look-ahead, for the
+    batch K2n path (B = 70) and the split path (B = 5), with per-signal
+    lengths; a look-ahead for other lengths is dropped (the call runs the pass
+    itself, still exact); at most two look-aheads may be pending."""
+    from aec_amd import synth
+    dev = 'cuda:0'
+    erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
+    side = torch.cuda.Stream()
+    for lens in ([33333, 4097, 255, 16000, 256], [16000, 4097, 33333, 12000, 700, 256, 5000] * 10):
+        L = max(lens)
+        mic, ref, near = (np.zeros((len(lens), L), np.float32) for _ in range(3))
+        for i, n in enumerate(lens):
+            m, r, nn_ = synth.scene(n, 900 + i)
+            mic[i, :n], ref[i, :n], near[i, :n] = m, r, nn_
+        M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
+        l3 = np.array([[n, n - n % 256 + (n % 256) // 2, n] for n in lens], np.int64)   # ref shorter, same frames
+        with torch.no_grad():
+            o0, s0 = nlms_net.forward_ragged(M, R, N, erb_t, l3)
+            o0, s0 = o0.cpu().numpy(), s0.cpu().numpy()
+            for rep in range(2):                      # the second round reuses the handle's slots
+                with torch.cuda.stream(side):
+                    nlms_net.prepare_ragged(M, R, N, l3)
+                torch.cuda.current_stream().wait_stream(side) if rep else None
+                o1, s1 = nlms_net.forward_ragged(M, R, N, erb_t, l3)
+                assert np.array_equal(o0, o1.cpu().numpy()), (len(lens), rep)
+                assert np.array_equal(s0, s1.cpu().numpy(), equal_nan=True), (len(lens), rep)
+            with torch.cuda.stream(side):             # stale: other lengths
+                nlms_net.prepare_ragged(M, R, N, [L] * len(lens))
+            o2, s2 = nlms_net.forward_ragged(M, R, N, erb_t, l3)
+            assert np.array_equal(o0, o2.cpu().numpy())
+            with torch.cuda.stream(side):
+                nlms_net.prepare_ragged(M, R, N, l3)
+                nlms_net.prepare_ragged(M, R, N, l3)
+                with pytest.raises(RuntimeError):
+                    nlms_net.prepare_ragged(M, R, N, l3)
+            o3, _ = nlms_net.forward_ragged(M, R, N, erb_t, l3)   # takes the first; the second is dropped next
+            assert np.array_equal(o0, o3.cpu().numpy())
+            o4, _ = nlms_net.forward_ragged(M, R, N, erb_t, l3)   # takes the second
+            assert np.array_equal(o0, o4.cpu().numpy())
+        torch.cuda.synchronize()
+
+
 def test_max_batch_4096_streams_matches_single_calls(nlms_net, golden_erb):
     """BASELINE C4/C5's 4,096-stream sweep point at 10 s: > 4 GiB spectrum and
     input buffers (64-bit row / spectrum offsets), ragged lengths.  Sampled
