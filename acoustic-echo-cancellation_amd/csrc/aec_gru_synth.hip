@@ -26,6 +26,9 @@
 #ifndef AEC_OUT_NT
 #define AEC_OUT_NT 1   // waveform stores nt: written once, never re-read on the device (fused kernel -1 %)
 #endif
+#ifndef AEC_OLA_REC
+#define AEC_OLA_REC 1   // NS = 2: overlap-add on the recurrence waves (0: on the head waves, A/B builds)
+#endif
 #ifndef AEC_SYN_HANN_PRE
 #define AEC_SYN_HANN_PRE 0   // synthesis window table pre-scaled by 1/512 (bit-identical; A/B)
 #endif
@@ -183,10 +186,11 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
             default: break;
         }
     }
-    // the overlap-add of chunk c-3 on the recurrence waves (each its own stream, after the tick's
-    // steps; AEC_FUSED_MODE bit 15) instead of the head waves: the same expressions
-    const bool ola_rec = NS == 2 && (y.fmode & 32768) != 0 && y.ld_out % 4 == 0 &&
-                         (reinterpret_cast<uintptr_t>(y.out) & 15) == 0;
+    // NS = 2: the overlap-add of chunk c-3 runs on the recurrence waves (each its own stream, after
+    // the tick's steps; the host takes NS = 1 for an output that is not 16-B aligned) instead of the
+    // head waves: the same expressions.  Without the head's overlap-add code the kernel fits 160
+    // VGPRs, so a 32-VGPR moments wave (the look-ahead pass of another batch) fits beside it.
+    constexpr bool ola_rec = NS == 2 && AEC_OLA_REC;
     if (wave < NS) {
         // ---------------- recurrence wave of stream `wave` (gru_kernel wave 0) ----------------
         __builtin_amdgcn_s_setprio(3);
@@ -226,7 +230,7 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
                 }
             }
             const int k = c - 3;
-            if (NS == 2 && ola_rec && k >= 0 && k < nch && !(y.fmode & 2)) {
+            if (ola_rec && k >= 0 && k < nch && !(y.fmode & 2)) {
                 // lane: float4 column r = 4 lane of the chunk's TF hops; frame halves from the ring
                 // (all loads first), hop j0 + i = frame i-1 (2nd half) + frame i (1st half)
                 const float* ring = sOut + (k & 1) * (kSynWaves * 4 * kGroupFloats) + s * TF * kGroupFloats;
@@ -368,7 +372,7 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
             // OLA + WOLA of chunk k = c - 3 of every stream (its TF frames in ring k & 1, slots
             // s TF ..): hops TF k - 1 .. TF k + TF - 2; hop TF k - 1 uses the tail of frame TF k - 1
             const int k = c - 3;
-            if (k >= 0 && k < nchmax && !(y.fmode & 2) && !ola_rec) {
+            if (!ola_rec && k >= 0 && k < nchmax && !(y.fmode & 2)) {
 #pragma unroll
                 for (int s = 0; s < NS; ++s) {
                     if (k >= nchs[s]) continue;
@@ -499,7 +503,9 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
 hipError_t launch_gru_synth(const GruArgs& g, const SynthArgs& y, int B, hipStream_t st) {
     if (B <= 0) return hipSuccess;
     const char* env = getenv("AEC_GRU_NS");
-    const int ns = env && atoi(env) == 1 ? 1 : 2;
+    // NS = 2 writes the waveform with 16-B stores (overlap-add on the recurrence waves)
+    const bool al16 = y.ld_out % 4 == 0 && (reinterpret_cast<uintptr_t>(y.out) & 15) == 0;
+    const int ns = (env && atoi(env) == 1) || (AEC_OLA_REC && !al16) ? 1 : 2;
 #define AEC_GRU_SYNTH(NS_)                                                                                     \
     do {                                                                                                       \
         static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gru_synth_kernel<NS_>), \

@@ -128,30 +128,48 @@ __global__ __launch_bounds__(NT) void moments_kernel(const float* __restrict__ m
 // K1 through LDS-DMA (AEC_MOM_CFG=3): the same per-thread float4 sequence (thread tid sums float4
 // lo/4 + tid + 256 m for m = 0, 1, ...) and the same block reduction, so bit-identical partials,
 // but the loads land in a per-wave LDS ring (buffer_load ... lds, 4 KB in flight per wave) instead of
-// registers.  The point is its footprint: ~20 VGPRs and 16 KB of LDS per block, which fits beside a
-// K2n block (153 VGPRs x 3 waves per SIMD, 131 KB of LDS) on the same CU, so with batches in
-// flight the next batch's moments pass can stream under this batch's analysis instead of holding
-// whole CUs (the register-loaded kernel needs 36 VGPRs, 4 more than a K2n CU has left).
-constexpr int kMomSlots = 4;
+// registers.  The point is its footprint: 30 VGPRs and 16 KiB of LDS per block, which fits beside a
+// K2n block (153 -> 160 VGPRs x 3 waves per SIMD, 131 KiB of LDS) or a gru_synth block (160 x 3,
+// 132 KiB) on the same CU, so with batches in flight the next batch's moments pass (aec_prepare)
+// streams under the compute kernels instead of holding whole CUs (the register-loaded kernel
+// needs 36 VGPRs, 4 more than such a CU has left).
+#ifndef AEC_MOM_SLOTS
+#define AEC_MOM_SLOTS 4
+#endif
+constexpr int kMomSlots = AEC_MOM_SLOTS;   // ring of 4 KiB rounds (4: 16 KiB, 30 VGPRs; 5: 20 KiB, 32 VGPRs)
 __device__ __forceinline__ void mom_wait_vm(int n) {
     // s_waitcnt vmcnt(n) (n < 16), other counters left alone
     switch (n) {
         case 0: __builtin_amdgcn_s_waitcnt(0x0F70); break;
         case 1: __builtin_amdgcn_s_waitcnt(0x0F71); break;
         case 2: __builtin_amdgcn_s_waitcnt(0x0F72); break;
-        default: __builtin_amdgcn_s_waitcnt(0x0F73); break;
+        case 3: __builtin_amdgcn_s_waitcnt(0x0F73); break;
+        case 4: __builtin_amdgcn_s_waitcnt(0x0F74); break;
+        default: __builtin_amdgcn_s_waitcnt(0x0F75); break;
     }
 }
+// the one-item form compiles to <= 32 VGPRs and <= 20 KiB of LDS: one block fits beside a K2n (160 VGPRs x 3
+// waves per SIMD, 131 KiB) or a gru_synth block (160 x 3, 132 KiB)
+template <bool PERSIST>
 __global__ __launch_bounds__(256) void moments_lds_kernel(const float* __restrict__ mic, const float* __restrict__ ref,
                                                           const float* __restrict__ near, int64_t ld,
                                                           const int32_t* __restrict__ slen, double2* __restrict__ mom,
-                                                          int b0) {
+                                                          int b0, int nsig, int nwork) {
     // one array per ring slot: a read of slot j waits only for the DMAs into slot j
     __shared__ __attribute__((aligned(16))) float4 sR0[256];
     __shared__ __attribute__((aligned(16))) float4 sR1[256];
     __shared__ __attribute__((aligned(16))) float4 sR2[256];
     __shared__ __attribute__((aligned(16))) float4 sR3[256];
-    const int ch = blockIdx.x, s = blockIdx.y, b = b0 + blockIdx.z;
+    __shared__ __attribute__((aligned(16))) float4 sR4[256];
+    __shared__ __attribute__((aligned(16))) float4 sR5[256];
+    __shared__ double r1[4], r2[4];
+    // work item w = (chunk, signal, stream) in moments_kernel's grid order; a grid smaller than
+    // nwork walks the items (persistent form: a few blocks that share CUs with other kernels)
+    // (PERSIST = false: one item per block, the 3-D grid (chunk, signal, stream) of moments_kernel)
+    for (int w = PERSIST ? (int)blockIdx.x : 0; w < (PERSIST ? nwork : 1); w += PERSIST ? gridDim.x : 1) {
+    const int ch = PERSIST ? w % kMomChunks : (int)blockIdx.x;
+    const int s = PERSIST ? (w / kMomChunks) % nsig : (int)blockIdx.y;
+    const int b = b0 + (PERSIST ? w / (kMomChunks * nsig) : (int)blockIdx.z);
     const float* base = (s == 0 ? mic : (s == 1 ? ref : near));
     const float* x = base + (int64_t)b * ld;
     const int64_t n = slen[4 * b + s];
@@ -179,7 +197,9 @@ __global__ __launch_bounds__(256) void moments_lds_kernel(const float* __restric
                 if constexpr (J == 0) return sR0;
                 else if constexpr (J == 1) return sR1;
                 else if constexpr (J == 2) return sR2;
-                else return sR3;
+                else if constexpr (J == 3) return sR3;
+                else if constexpr (J == 4) return sR4;
+                else return sR5;
             };
             auto issue = [&](int m, float4* sl) {              // the wave's 64 float4 of round m -> slot
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -220,7 +240,6 @@ __global__ __launch_bounds__(256) void moments_lds_kernel(const float* __restric
         s1 += __shfl_xor(s1, o);
         s2 += __shfl_xor(s2, o);
     }
-    __shared__ double r1[4], r2[4];
     if ((tid & 63) == 0) {
         r1[tid >> 6] = s1;
         r2[tid >> 6] = s2;
@@ -229,12 +248,14 @@ __global__ __launch_bounds__(256) void moments_lds_kernel(const float* __restric
     if (tid == 0) {
         double t1[4], t2[4];
 #pragma unroll
-        for (int w = 0; w < 4; ++w) { t1[w] = r1[w]; t2[w] = r2[w]; }
+        for (int q = 0; q < 4; ++q) { t1[q] = r1[q]; t2[q] = r2[q]; }
 #pragma unroll
         for (int st = 1; st < 4; st <<= 1)
 #pragma unroll
-            for (int w = 0; w + st < 4; w += 2 * st) { t1[w] += t1[w + st]; t2[w] += t2[w + st]; }
+            for (int q = 0; q + st < 4; q += 2 * st) { t1[q] += t1[q + st]; t2[q] += t2[q + st]; }
         mom[((int64_t)b * 3 + s) * kMomChunks + ch] = make_double2(t1[0], t2[0]);
+    }
+    __syncthreads();                                    // r1 / r2 read before the next item rewrites them
     }
 }
 
@@ -857,22 +878,36 @@ hipError_t launch_mic_erb(const float2* spec, float* feats, const int64_t* lens,
 hipError_t launch_moments(const float* mic, const float* ref, const float* near, int64_t ld,
                           const int32_t* slen, double2* mom, int b0, int nb, int nsig, hipStream_t st) {
     if (nb <= 0) return hipSuccess;
-    // 4 float4 in flight per thread, nontemporal loads (each sample is read once
-    // here; the analysis pass re-reads it from HBM anyway).  256 x 10 s x 3
-    // signals: 0.104 ms (4.7 TB/s) with default-policy loads, 0.080 ms
-    // (6.1 TB/s) with nt; 8 float4 / 512-thread / 1024-thread blocks measured
-    // 0.085-0.091 ms.  AEC_MOM_CFG=1 selects the default-policy loads (A/B).
-    static const int cfg = [] { const char* e = std::getenv("AEC_MOM_CFG"); return e ? std::atoi(e) : 0; }();
+    // Default (AEC_MOM_CFG unset or 3): moments_lds_kernel, one 256-thread block per (chunk, signal,
+    // stream), 4 KiB rounds through a 4-round LDS ring: 30 VGPRs and 16 KiB, so a block fits beside a
+    // K2n or gru_synth block and the look-ahead pass (aec_prepare) of the next batch streams under
+    // the compute kernels of the batches in flight (C2 0.581-0.592 against 0.597-0.600 ms,
+    // profiles/r05r_persist8_lookahead_ab.log).  Standalone 0.080 ms for 256 x 10 s x 3 signals.
+    // Timing variants (bit-identical partials): 0 moments_kernel, 4 float4 per thread in registers,
+    // nt loads (0.078 ms standalone; 36 VGPRs: fits beside neither compute kernel); 1 the same with
+    // default-policy loads (0.104 ms); 2 two float4 per thread; 4 moments_lds persistent,
+    // AEC_MOM_GRID blocks walking the items (40 VGPRs; slower, profiles/r05_notes.md r05n).
+    static const int cfg = [] { const char* e = std::getenv("AEC_MOM_CFG"); return e ? std::atoi(e) : 3; }();
     const dim3 g(kMomChunks, nsig, nb);
-    if (cfg == 9) return hipSuccess;   // TIMING ONLY: no moments pass (results invalid)
-    if (cfg == 1)
+    // 9, TIMING ONLY: after the first 16 launches no moments pass (every workspace then keeps the
+    // partials of its last pass: valid only while each handle's inputs repeat, as in bench.py
+    // --lookahead 0)
+    static int launches = 0;
+    if (cfg == 9 && ++launches > 16) return hipSuccess;
+    const int nwork = kMomChunks * nsig * nb;
+    if (cfg == 0)
+        hipLaunchKernelGGL((moments_kernel<4, 256, true>), g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0);
+    else if (cfg == 1)
         hipLaunchKernelGGL((moments_kernel<4, 256, false>), g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0);
     else if (cfg == 2)
         hipLaunchKernelGGL((moments_kernel<2, 256, true>), g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0);
-    else if (cfg == 3)
-        hipLaunchKernelGGL(moments_lds_kernel, g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0);
-    else
-        hipLaunchKernelGGL((moments_kernel<4, 256, true>), g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0);
+    else if (cfg == 4) {
+        static const int pgrid = [] { const char* e = std::getenv("AEC_MOM_GRID"); return e ? std::atoi(e) : 256; }();
+        hipLaunchKernelGGL(moments_lds_kernel<true>, dim3(std::max(1, std::min(pgrid, nwork))), dim3(256), 0, st, mic,
+                           ref, near, ld, slen, mom, b0, nsig, nwork);
+    } else {
+        hipLaunchKernelGGL(moments_lds_kernel<false>, g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0, nsig, nwork);
+    }
     return hipGetLastError();
 }
 

@@ -1027,6 +1027,9 @@ static aec_status run_persist(aec_crn_handle* h, int l, int32_t B, int64_t Tmax,
     const char* ss = getenv("AEC_CRN_PERSIST_STALL");
     const int stall = ss && atoi(ss) != 0 ? (1 << 30) : 0;
     static const int pra = [] { const char* v = getenv("CRN_PERSIST_RA"); return v ? atoi(v) : 1; }();
+    // waves per block: 4 (lstm_persist2_kernel) or 8 (lstm_persist3_kernel); AEC_CRN_PERSIST_WAVES, read per call
+    const char* pwe = getenv("AEC_CRN_PERSIST_WAVES");
+    const int pw = pwe && atoi(pwe) == 8 ? 8 : 4;
     // one block per CU: 64 streams (two teams of 32 blocks) per 64 CUs, at most 256 streams per launch
     const int32_t chunk = 64 * std::min(4, h->num_cus / 64);
     for (int32_t b0 = 0; b0 < B; b0 += chunk) {
@@ -1046,7 +1049,7 @@ static aec_status run_persist(aec_crn_handle* h, int l, int32_t B, int64_t Tmax,
         a.stall = stall;
         // arrival counters only: the error word keeps any timeout of this call's earlier launches
         CRN_TRY(h, hipMemsetAsync(h->psync, 0, crn::kPersistCounters * sizeof(int), st));
-        CRN_TRY(h, crn::launch_lstm_persist(a, st));
+        CRN_TRY(h, pw == 8 ? crn::launch_lstm_persist3(a, st) : crn::launch_lstm_persist(a, st));
     }
     CRN_TRY(h, hipEventRecord(ev, st));
     return AEC_OK;

@@ -94,7 +94,8 @@ def parse():
     ap.add_argument('--no-sweep', action='store_true',
                     help='skip the batch sweep (B = 1 ... 4096 streams, 3 calls each, after the timed region)')
     ap.add_argument('--lookahead', type=int, default=1,
-                    help='C2: queue the next batch\'s normaliser pass on a side stream (aec_prepare) during each step')
+                    help='C2: step k queues the normaliser pass of batch k + LOOKAHEAD on a side stream (aec_prepare); '
+                         '0 = off')
     ap.add_argument('--inflight', type=int, default=2,
                     help='batches in flight (HIP streams, one handle each; 1 = strictly sequential)')
     ap.add_argument('--no-c3', action='store_true', help='skip the BASELINE config 3 (DCCRN bf16) figure')
@@ -292,7 +293,7 @@ def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu, nlms=N
     kstep = [0]
 
     def step():
-        k = kstep[0] % inflight
+        k = kstep[0]
         kstep[0] += 1
         with torch.cuda.stream(streams[k]):
             return nets[k].forward_ragged(mic, far, lens, want_spec=False)
@@ -766,10 +767,10 @@ def main():
         nets.append(extra.to(dev))
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
     kstep = [0]
-    # look-ahead (aec_prepare): step k queues the normaliser pass of step k+1's batch on a side
+    # look-ahead (aec_prepare): step k queues the normaliser pass of batch k + LOOKAHEAD on a side
     # stream before its own kernels, so that HBM-bound pass runs under the compute of the batches
-    # in flight instead of in front of step k+1's analysis.  Every step still runs one pass (the
-    # timed region's first batch takes the pass queued by the last warm-up step).
+    # in flight instead of in front of that batch's analysis.  Every step still runs one pass (the
+    # timed region's first batches take the passes queued by the last warm-up steps).
     side = torch.cuda.Stream(dev) if args.lookahead else None
 
     def step():
@@ -777,9 +778,9 @@ def main():
         kstep[0] += 1
         if side is not None:
             with torch.cuda.stream(side):
-                nets[kstep[0] % inflight].prepare_ragged(mic, ref, near, lens)
-        with torch.cuda.stream(streams[k]):
-            return nets[k].forward_ragged(mic, ref, near, erb, lens)
+                nets[(k + args.lookahead) % inflight].prepare_ragged(mic, ref, near, lens)
+        with torch.cuda.stream(streams[k % inflight]):
+            return nets[k % inflight].forward_ragged(mic, ref, near, erb, lens)
 
     with torch.no_grad():
         for _ in range(2):
@@ -799,7 +800,7 @@ def main():
         h0.profile_enable(False)
         # warm-up steps in the timed loop's own form (the last one queues the first timed batch's
         # look-ahead pass)
-        for _ in range(max(args.warmup, inflight)):
+        for _ in range(max(args.warmup, inflight, args.lookahead)):
             step()
         torch.cuda.synchronize(dev)
         # the timed region: K steps, `inflight` batches in flight
@@ -968,7 +969,7 @@ def main():
             'config': {'workload': WORKLOAD[args.pipeline],
                        'streams_per_gpu': B, 'samples_per_stream': n, 'frames_per_stream': T,
                        'frame': '256-sample hop', 'pipeline': args.pipeline, 'batches_in_flight': inflight,
-                       'normaliser_lookahead': bool(args.lookahead and args.pipeline != 'crn'),
+                       'normaliser_lookahead_batches': args.lookahead if args.pipeline != 'crn' else 0,
                        'parallelism': f'streams sharded, {world} rank(s)'},
             'value_per_gpu': round(value / world, 1),
             'aggregate_frames_per_s': round(value, 1),

@@ -299,6 +299,35 @@ def test_persistent_recurrence_matches_step_kernel(monkeypatch):
     assert np.array_equal(outs['1'][1], outs['1'][0][:3])   # batch composition stays bit-exact
 
 
+def test_persistent_recurrence_8_waves_bit_exact(monkeypatch):
+    """lstm_persist3_kernel (crn_persist3.hip: 8 waves per block, two per
+    SIMD, each wave 8 units x 4 gates x one K half of W_hh; the four gates of a
+    cell meet through a DPP exchange) against lstm_persist2_kernel (4 waves,
+    16 units each) on the same 300-stream bf16 batch (launches of 256 + 44
+    streams): the same MFMA K steps, the same K-half order and the same cell
+    expressions, so the outputs are bit-identical; a second, 3-stream call
+    checks batch composition."""
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+    from aec_amd import synth
+    B, n = 300, 8000
+    mic, far, _ = synth.batch(B, n, seed0=900)
+    M, F = (torch.from_numpy(a).to('cuda:0') for a in (mic, far))
+    monkeypatch.delenv('AEC_CRN_PERSIST', raising=False)
+    outs = {}
+    for waves in ('4', '8'):
+        monkeypatch.setenv('AEC_CRN_PERSIST_WAVES', waves)     # read per call
+        net, m, conf = build('v2E_16000', 'bf16')
+        with torch.no_grad():
+            o, _, _ = net.forward_ragged(M, F, [n] * B, want_spec=False)
+            o2, _, _ = net.forward_ragged(M[:3], F[:3], [n] * 3, want_spec=False)
+        torch.cuda.synchronize()
+        outs[waves] = (o.cpu().numpy(), o2.cpu().numpy())
+    assert np.isfinite(outs['8'][0]).all()
+    assert np.array_equal(outs['8'][0], outs['4'][0])
+    assert np.array_equal(outs['8'][1], outs['8'][0][:3])
+
+
 def test_persistent_timeout_fails_that_call(monkeypatch):
     """A persistent-grid timeout is reported by the call that hit it: with the
     poll targets made unreachable (AEC_CRN_PERSIST_STALL, read per call: a

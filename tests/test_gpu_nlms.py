@@ -172,11 +172,10 @@ def test_fused_synthesis_bit_exact(golden_weights, golden_erb, monkeypatch):
     erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
     M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
     res = {}
-    # 'o': the overlap-add on the recurrence waves (AEC_FUSED_MODE bit 15, two streams per block)
-    for fused, ns in (('0', '2'), ('1', '1'), ('1', '2'), ('o', '2')):
-        monkeypatch.setenv('AEC_FUSED_SYNTH', '0' if fused == '0' else '1')   # read when the handle is created
+    # NS = 1: overlap-add on the head waves; NS = 2: on the recurrence waves (aec_gru_synth.hip)
+    for fused, ns in (('0', '2'), ('1', '1'), ('1', '2')):
+        monkeypatch.setenv('AEC_FUSED_SYNTH', fused)             # read when the handle is created
         monkeypatch.setenv('AEC_GRU_NS', ns)                    # streams per fused block, read per launch
-        monkeypatch.setenv('AEC_FUSED_MODE', '32768' if fused == 'o' else '0')
         net = _net(golden_weights, NLMS)
         net.set_debug(True)
         with torch.no_grad():
@@ -185,7 +184,7 @@ def test_fused_synthesis_bit_exact(golden_weights, golden_erb, monkeypatch):
         torch.cuda.synchronize()
         res[fused + ns] = (out.cpu().numpy(), loss.cpu().numpy(), est.cpu().numpy())
     o0, l0, e0 = res['02']
-    for key in ('11', '12', 'o2'):                               # one and two streams per block (B = 5: odd)
+    for key in ('11', '12'):                                     # one and two streams per block (B = 5: odd)
         o1, l1, e1 = res[key]
         assert np.array_equal(o0, o1), key
         for i, n in enumerate(lens):

@@ -17,7 +17,7 @@ elif [ "$REV" != tree ]; then
 fi
 OUT=$R/acoustic-echo-cancellation_amd/aec_amd/ab
 mkdir -p "$OUT" "$W/obj"
-SRCS="aec_api.hip aec_kernels.hip aec_gru.hip aec_gru_synth.hip aec_stream.hip crn_api.hip crn_kernels.hip crn_persist.hip crn_stream.hip aec_train.hip"
+SRCS="aec_api.hip aec_kernels.hip aec_gru.hip aec_gru_synth.hip aec_stream.hip crn_api.hip crn_kernels.hip crn_persist.hip crn_persist3.hip crn_stream.hip aec_train.hip"
 for s in $SRCS; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result -fno-slp-vectorize "$@" \
       -I"$SRC" -c "$SRC/$s" -o "$W/obj/${s%.hip}.o" &

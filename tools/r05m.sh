@@ -12,3 +12,5 @@ for i in 1 2; do for la in 0 1; do for mc in 0 3; do
   echo "lookahead $la mom $mc #$i: $(tail -1 $O/r05m_la${la}_m${mc}_$i.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["kernel_ms_per_step"])')"
 done; done; done
 bash $R/tools/r05l.sh
+bash $R/tools/env_ab.sh AEC_NLMS_PRIO "0 10 20 120" 2 > $O/r05m_prio.log 2>&1 || { echo "prio ab failed"; tail $O/r05m_prio.log; exit 1; }
+cat $O/r05m_prio.log
