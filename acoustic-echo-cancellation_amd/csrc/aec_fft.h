@@ -255,15 +255,16 @@ __device__ __forceinline__ void fft256_packed(float2 (&v)[16], int lb, float* sc
 #define AEC_FFT_PK 1
 #endif
 #ifndef AEC_FFT_PK_INV
-#define AEC_FFT_PK_INV 0   // the inverse on the packed core too (A/B builds)
+#define AEC_FFT_PK_INV 1   // the inverse on the packed core too (0: scalar inverse, A/B builds)
 #endif
 template <bool INV>
 __device__ __forceinline__ void fft256(float2 (&v)[16], int lb, float* scr, const float2* twT) {
-    // forward transforms packed, inverse scalar: the packed inverse made the
-    // fused GRU + synthesis kernel 4 % slower (its recurrence wave shares the
-    // SIMDs with the synthesis waves), and every synthesis path must run the
-    // same inverse arithmetic (the fused / separate / streaming kernels are
-    // tested bit-identical)
+    // both directions on the packed core: in round 2 the packed inverse made the fused GRU +
+    // synthesis kernel 4 % slower (one recurrence wave per block shared the SIMDs with the
+    // synthesis waves); with two streams per block and the overlap-add on the recurrence waves
+    // it shortens the synthesis waves' tick share (9.2-9.7 k -> 8.9-9.4 k cycles) and the kernel
+    // by 1-2 % (profiles/r05_notes.md, r05m / r05t).  Every synthesis path runs this same inverse
+    // (the fused / separate / streaming kernels are tested bit-identical)
     if constexpr (AEC_FFT_PK && (!INV || AEC_FFT_PK_INV)) fft256_packed<INV>(v, lb, scr, twT);
     else fft256_scalar<INV>(v, lb, scr, twT);
 }

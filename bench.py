@@ -96,8 +96,11 @@ def parse():
     ap.add_argument('--lookahead', type=int, default=1,
                     help='C2: step k queues the normaliser pass of batch k + LOOKAHEAD on a side stream (aec_prepare); '
                          '0 = off')
-    ap.add_argument('--inflight', type=int, default=2,
-                    help='batches in flight (HIP streams, one handle each; 1 = strictly sequential)')
+    ap.add_argument('--inflight', type=int, default=3,
+                    help='C2 batches in flight (HIP streams, one handle each; 1 = strictly sequential; 3 measured '
+                         '1-2 %% faster than 2, profiles/r05_notes.md r05t)')
+    ap.add_argument('--crn-inflight', type=int, default=2,
+                    help='CRN (C3 / C4 / --pipeline crn) batches in flight')
     ap.add_argument('--no-c3', action='store_true', help='skip the BASELINE config 3 (DCCRN bf16) figure')
     ap.add_argument('--c3-steps', type=int, default=10, help='timed steps of the config 3 figure')
     ap.add_argument('--no-train', action='store_true', help='skip the training-step figure')
@@ -283,7 +286,7 @@ def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu, nlms=N
     mic, far, _ = (torch.from_numpy(a).to(dev) for a in synth.batch(B, n, seed0=1000 * rank))
     lens = [n] * B
 
-    inflight = max(1, args.inflight)
+    inflight = max(1, args.crn_inflight)
     nets = [net]
     for _ in range(inflight - 1):
         extra = mod.DCCRN(conf, dtype=dtype, nlms=nlms).eval()
@@ -293,7 +296,7 @@ def run_crn(args, dev, rank, world, dtype, steps, warmup, B, n, with_cpu, nlms=N
     kstep = [0]
 
     def step():
-        k = kstep[0]
+        k = kstep[0] % inflight
         kstep[0] += 1
         with torch.cuda.stream(streams[k]):
             return nets[k].forward_ragged(mic, far, lens, want_spec=False)
@@ -779,8 +782,8 @@ def main():
         if side is not None:
             with torch.cuda.stream(side):
                 nets[(k + args.lookahead) % inflight].prepare_ragged(mic, ref, near, lens)
-        with torch.cuda.stream(streams[k % inflight]):
-            return nets[k % inflight].forward_ragged(mic, ref, near, erb, lens)
+        with torch.cuda.stream(streams[k]):
+            return nets[k].forward_ragged(mic, ref, near, erb, lens)
 
     with torch.no_grad():
         for _ in range(2):

@@ -7,7 +7,7 @@ ALT=$1; shift
 mkdir -p $R/gpurun_out
 for v in base alt base alt; do
   if [ $v = alt ]; then export AEC_HIP_LIB=$ALT; else unset AEC_HIP_LIB; fi
-  timeout -k 10 200 python $R/bench.py --pipeline crn --steps 5 --warmup 2 --no-cpu --no-rtf --no-sweep --inflight 1 "$@" > $R/gpurun_out/crn_lib_ab_$v.log 2>&1 || { tail -5 $R/gpurun_out/crn_lib_ab_$v.log; exit 1; }
+  timeout -k 10 200 python $R/bench.py --pipeline crn --steps 5 --warmup 2 --no-cpu --no-rtf --no-sweep --crn-inflight 1 "$@" > $R/gpurun_out/crn_lib_ab_$v.log 2>&1 || { tail -5 $R/gpurun_out/crn_lib_ab_$v.log; exit 1; }
   python - "$v" "$R/gpurun_out/crn_lib_ab_$v.log" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])

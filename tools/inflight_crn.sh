@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 for k in 1 2; do
-  timeout -k 10 300 python bench.py --pipeline crn --steps 10 --warmup 2 --no-cpu --no-rtf --inflight $k > gpurun_out/inflc_$k.json 2> gpurun_out/inflc_$k.err || exit 1
+  timeout -k 10 300 python bench.py --pipeline crn --steps 10 --warmup 2 --no-cpu --no-rtf --crn-inflight $k > gpurun_out/inflc_$k.json 2> gpurun_out/inflc_$k.err || exit 1
   python - "$k" <<'PY'
 import json, sys
 d = json.loads(open(f'gpurun_out/inflc_{sys.argv[1]}.json').read().strip().splitlines()[-1])
