@@ -11,10 +11,15 @@ import sys
 
 summ = json.load(open(sys.argv[1]))
 tag = sys.argv[2]
-front = [v['launches'] for k, v in summ.items() if 'stream_front' in k or 'stream_enc' in k]
-hops = max(front)
+# the 256-stream hops: the front kernel at the largest grid (c5_prof.py also runs a 1-stream
+# latency probe, whose hops are more numerous); that configuration's kernels launch once or twice
+# per hop
+grid = lambda k: int(k.rsplit('grid', 1)[1]) if 'grid' in k else 0
+fk = max((k for k in summ if 'stream_front' in k or 'stream_enc' in k), key=grid)
+hops = summ[fk]['launches']
 per_hop = {k: v for k, v in summ.items()
-           if v['launches'] >= hops and not k.startswith(('__amd_rocclr', 'at::native'))}
+           if v['launches'] in (hops, 2 * hops) and grid(k) >= grid(fk) // 2
+           and not k.startswith(('__amd_rocclr', 'at::native'))}
 total = sum(v['hbm_bytes_per_launch'] * v['launches'] for v in per_hop.values()) / hops
 out = dict(pipeline='c5_stream', dtype='fp8', B=256, hops_counted=hops,
            source=f'rocprofv3 --pmc passes (tools/c5_pmc.sh {tag}) over tools/c5_prof.py',

@@ -6,6 +6,10 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 AB=$R/acoustic-echo-cancellation_amd/aec_amd/ab
 mkdir -p $O
+for i in 1 2; do for k in 20 100; do
+  timeout -k 10 150 python $R/bench.py --no-cpu --no-c3 --no-rtf --no-sweep --no-train --steps $k > $O/r05z_steps_${k}_$i.log 2>&1 || { echo "bench steps $k failed"; exit 1; }
+  echo "steps $k #$i: $(tail -1 $O/r05z_steps_${k}_$i.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"])')"
+done; done
 bash $R/tools/profile.sh r05z_full --inflight 1 > $O/r05z_profile.log 2>&1 || { echo "profile failed"; tail $O/r05z_profile.log; exit 1; }
 echo "profile done"
 bash $R/tools/sq_pmc.sh r05z_sq > $O/r05z_sq.log 2>&1 || { echo "sq failed"; tail $O/r05z_sq.log; exit 1; }

@@ -20,3 +20,5 @@ bash $R/tools/crn_pmc.sh r05z_crnpmc > $O/r05z_crnpmc.log 2>&1 || { echo "crn pm
 echo "crn pmc done"
 CRN_GEMM_XCD=8 bash $R/tools/crn_pmc.sh r05z_crnpmc_xcd8 > $O/r05z_crnpmc_xcd8.log 2>&1 || { echo "crn pmc xcd failed"; tail -5 $O/r05z_crnpmc_xcd8.log; exit 1; }
 echo "crn pmc xcd8 done"
+timeout -k 10 500 python $R/bench.py > $O/r05z_bench100.log 2>&1 || { echo "bench failed"; tail -20 $O/r05z_bench100.log; exit 1; }
+tail -1 $O/r05z_bench100.log | head -c 400; echo
