@@ -75,7 +75,9 @@ VALUE_SEMANTICS = ('value = aggregate frames/s of all ranks (frames of every ran
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--steps', type=int, default=100,
+                    help='timed steps (C2: 100 x ~0.54 ms; the fill and drain of three batches in flight are ~1.5 ms, '
+                         '~15 %% of a 20-step region, profiles/r05z_steps_ab.log)')
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--streams', type=int, default=256)
     ap.add_argument('--seconds', type=float, default=10.0)

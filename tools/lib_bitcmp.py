@@ -42,5 +42,7 @@ for k in ('mic_erb', 'ref_erb', 'est_erb'):
     f = net.debug_intermediate(k, len(lens), T).cpu().numpy()
     for i, n in enumerate(lens):
         h.update(f[i, :n // 256 + 1].tobytes())
+if os.environ.get('LIB_BITCMP_DUMP'):   # the arrays themselves, to locate a difference
+    np.savez(os.environ['LIB_BITCMP_DUMP'], out=out.cpu().numpy(), loss=loss.cpu().numpy())
 print('sha1', h.hexdigest(), 'out/loss/mic_erb/ref_erb/est_erb of', len(lens), 'ragged streams,',
       os.path.basename(os.environ.get('AEC_HIP_LIB', 'libaec_hip.so')))
