@@ -10,7 +10,11 @@ import sys
 def hops(d):
     rows = list(csv.DictReader(open(os.path.join(d, 'trace', 'run_kernel_trace.csv'))))
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
-    idx = [i for i, r in enumerate(rows) if 'stream_front' in r['Kernel_Name'] or 'stream_enc' in r['Kernel_Name']]
+    # the hops at the largest stream count (tools/c5_prof.py also steps a 1-stream latency probe)
+    front = [r for r in rows if 'stream_front' in r['Kernel_Name'] or 'stream_enc' in r['Kernel_Name']]
+    gmax = max(int(r['Grid_Size_X']) * int(r['Grid_Size_Y']) for r in front)
+    idx = [i for i, r in enumerate(rows) if ('stream_front' in r['Kernel_Name'] or 'stream_enc' in r['Kernel_Name'])
+           and int(r['Grid_Size_X']) * int(r['Grid_Size_Y']) == gmax]
     out = []
     for a, b in zip(idx[5:-1], idx[6:]):
         seq = rows[a:b]
