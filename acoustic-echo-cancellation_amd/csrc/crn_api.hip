@@ -2002,9 +2002,13 @@ aec_status aec_crn_stream_step(aec_crn_handle* h, const float* mic, const float*
     if (dg.err != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
     const int par = (int)(ss.k & 1);
     const StreamIo io{mic, far, ld_in, out, ld_out};
+    // direct launches by default: the hop's 7 kernels run back to back either way, but ~8 us pass
+    // between two replays of a graph, more than the direct launches' gaps (256 streams 0.1085 vs
+    // 0.1135 ms per hop, one stream 0.105 vs 0.113 ms synchronous; profiles/r05_notes.md r05x/r05y).
+    // AEC_CRN_GRAPH=1 captures the hop once per ring parity and replays it.
     static const int use_graph = [] {
         const char* v = getenv("AEC_CRN_GRAPH");
-        return v ? atoi(v) : 1;
+        return v ? atoi(v) : 0;
     }();
     bool launched = false;
     if (use_graph) {

@@ -413,7 +413,7 @@ def c5_flop_split(conf):
 
 
 def c5_roofline(conf, B, ms_per_hop, pmc):
-    """The whole hop (one hipGraph launch of the step's kernels) against the
+    """The whole hop (the step's 7 kernel launches) against the
     MFMA roofline: time at peak = the MX-fp8 FLOPs at the dense fp8 peak + the
     bf16 FLOPs at the dense bf16 peak; frac = that time / the measured hop."""
     sp = c5_flop_split(conf)
@@ -426,7 +426,7 @@ def c5_roofline(conf, B, ms_per_hop, pmc):
         traffic = pmc.get('hbm_bytes_per_hop')
     return dict(bound='mfma', achieved=round(ach, 1), peak=round(blended, 1), unit='TFLOP/s',
                 frac=round(t_peak / t, 4), traffic=traffic,
-                kernel='the per-hop step (one hipGraph launch: front, NLMS, encoder GEMMs, 2 MX LSTM layer '
+                kernel='the per-hop step (7 launches: front, NLMS, encoder GEMMs, 2 MX LSTM layer '
                        'steps, decoder GEMMs, back)',
                 alg_flops_per_frame=sp['total'], fp8_flops_per_frame=sp['fp8'], bf16_flops_per_frame=sp['bf16'],
                 frames_per_launch=B,
@@ -503,7 +503,7 @@ def c5_erle(net, dev, conf, nlms, streams=2, n=160000):
 
 def run_c5_stream(dev, B=256, hops=200, dtype='fp8', world=1, with_cpu=False, sweep=(1024, 4096),
                   cpu_seconds=10.0, with_erle=False):
-    """BASELINE config 5: the hipGraph-captured per-hop step of the DCCRN
+    """BASELINE config 5: the per-hop step of the DCCRN (7 launches; AEC_CRN_GRAPH=1 replays them as a hipGraph)
     (MX-fp8 LSTM input projections, recurrence and wide conv layers) fed by the FD-NLMS,
     B concurrent streams per GPU, one 256-sample hop per stream per step
     (aec_crn_stream_step).  With world > 1 every rank steps its own B streams
@@ -579,7 +579,7 @@ def run_c5_stream(dev, B=256, hops=200, dtype='fp8', world=1, with_cpu=False, sw
     if os.path.exists(pp):
         pmc = json.load(open(pp))
     res = dict(workload=f'C5 (BASELINE configs[4]): {world} GPU(s) x {B} concurrent streams, one 256-sample hop per '
-                        f'stream per step through the hipGraph-captured STFT -> FD-NLMS (4 taps) -> DCCRN v2 '
+                        f'stream per step through the per-hop STFT -> FD-NLMS (4 taps) -> DCCRN v2 '
                         f'(net_conf, {dtype}' + (': bf16 + MX-fp8 LSTM input projections, LSTM recurrence (W_ih, W_hh, '
                         'x, h) and encoder 4-5 / decoder 4-6 convs'
                         if dtype == 'fp8' else '') + ') -> iSTFT step; input = one random hop pair per stream, '

@@ -128,9 +128,9 @@ aec_status aec_crn_stft(aec_crn_handle* h, const float* x, const int64_t* length
 /* Streaming (serving): one 256-sample hop per stream per call, the per-frame
  * loop of the same network (the DCCRN has no utterance-global statistic, so a
  * streamed utterance equals the batch result: frame t needs hops t-1 and t,
- * ConvSTFT framing dccrn.py:45-52).  The launches of one frame are captured
- * once in a hipGraph per ring parity and replayed (AEC_CRN_GRAPH=0: direct
- * launches): 7 for the fp8 step at net_conf (fused front = STFT, FD-NLMS and
+ * ConvSTFT framing dccrn.py:45-52).  The launches of one frame go out
+ * directly (AEC_CRN_GRAPH=1: captured once in a hipGraph per ring parity and
+ * replayed; the replays measured slower): 7 for the fp8 step at net_conf (fused front = STFT, FD-NLMS and
  * encoder levels 0-4; one MX conv level; two LSTM layer steps; two MX conv
  * levels; fused back = decoder levels 4-1, mask, iSTFT).  The fp8 step folds
  * encoder / decoder level 4 into the fused kernels only while B <= the
