@@ -283,6 +283,15 @@ __device__ __forceinline__ void synth_fft(float2 (&v)[16], const float2* sTwT, c
     }
 }
 
+// irFFT-256 of the packed frame without the window: scr[0..511] = 512 x (time samples), natural
+// order; the overlap-add applies hann / 512 (aec_gru_synth.hip, AEC_OLA_WIN)
+__device__ __forceinline__ void synth_fft_raw(float2 (&v)[16], const float2* sTwT, float* scr, int lb) {
+    fft256<true>(v, lb, scr, sTwT);
+    float2* s2 = reinterpret_cast<float2*>(scr);
+#pragma unroll
+    for (int m2 = 0; m2 < 16; ++m2) s2[lb + 16 * m2] = v[kP(m2)];
+}
+
 // Synthesis of one frame by its 16-lane group: per-bin ERB gain
 // g[k] = sum_j est_erb[j] erb[k][j] over the <= 2 bands covering bin k
 // (ERB.py:306-307) applied to the spectrum (:309-310), inverse real pack,

@@ -17,7 +17,8 @@
 //   3 head waves   head / mask / est_erb / loss of chunk c-1 -> est (HBM + LDS ring);
 //                  OLA + WOLA of chunk c-3 from the frame ring -> out
 //   4 synth waves  synthesis (gains, irFFT, window) of chunk c-2 into the LDS
-//                  frame ring;  E rows of chunk c-1 into registers
+//                  frame ring (NS = 2: the window is applied in the overlap-add);
+//                  E rows of chunk c-1 into registers
 //
 // one block barrier per tick of 16 frame slots.  The arithmetic of every
 // output sample is the unfused path's (synth_frame, the same OLA expression),
@@ -28,6 +29,11 @@
 #endif
 #ifndef AEC_OLA_REC
 #define AEC_OLA_REC 1   // NS = 2: overlap-add on the recurrence waves (0: on the head waves, A/B builds)
+#endif
+#ifndef AEC_OLA_WIN
+// NS = 2: the synthesis window applied in the recurrence waves' overlap-add instead of the synthesis
+// waves (bit-identical; gru_synth 0.360-0.366 against 0.387 ms, profiles/r05_notes.md r05z2)
+#define AEC_OLA_WIN 1
 #endif
 #ifndef AEC_SYN_HANN_PRE
 #define AEC_SYN_HANN_PRE 0   // synthesis window table pre-scaled by 1/512 (bit-identical; A/B)
@@ -241,6 +247,22 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
                 float4 fh[NS == 2 ? TF : 1], sh[NS == 2 ? TF : 1];
                 const float4 tl = *reinterpret_cast<const float4*>(tail_in + r);
                 const float4 cf = *reinterpret_cast<const float4*>(sCoff + r);
+                // AEC_OLA_WIN: the ring holds the raw irFFT output; window x 1/512 here (hann / 512
+                // is exact).  The products go through inline asm: HIP contracts across statements
+                // (-ffp-contract=fast), and a product fused into the following add would round
+                // differently from synth_fft's stored product
+                float4 w1 = make_float4(1.f, 1.f, 1.f, 1.f), w2 = w1;
+                if constexpr (AEC_OLA_WIN) {
+                    const float4 h1 = *reinterpret_cast<const float4*>(sHann + r);
+                    const float4 h2 = *reinterpret_cast<const float4*>(sHann + 256 + r);
+                    w1 = make_float4(h1.x * (1.f / 512.f), h1.y * (1.f / 512.f), h1.z * (1.f / 512.f), h1.w * (1.f / 512.f));
+                    w2 = make_float4(h2.x * (1.f / 512.f), h2.y * (1.f / 512.f), h2.z * (1.f / 512.f), h2.w * (1.f / 512.f));
+                }
+                auto mulr = [](float x, float y) {
+                    float r;
+                    asm("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+                    return r;
+                };
 #pragma unroll
                 for (int i = 0; i < TF; ++i) {
                     fh[i] = *reinterpret_cast<const float4*>(ring + i * kGroupFloats + r);
@@ -250,12 +272,16 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
 #pragma unroll
                 for (int i = 0; i < TF; ++i) {
                     if (i >= nh || j0 + i < 0) continue;
-                    const float4 a = i == 0 ? tl : sh[i - 1];
+                    float4 a = i == 0 ? tl : sh[i - 1], b = fh[i];
+                    if constexpr (AEC_OLA_WIN) {
+                        a = make_float4(mulr(a.x, w2.x), mulr(a.y, w2.y), mulr(a.z, w2.z), mulr(a.w, w2.w));
+                        b = make_float4(mulr(b.x, w1.x), mulr(b.y, w1.y), mulr(b.z, w1.z), mulr(b.w, w1.w));
+                    }
                     float4 o;
-                    o.x = (a.x + fh[i].x) * cf.x + 1e-9f;
-                    o.y = (a.y + fh[i].y) * cf.y + 1e-9f;
-                    o.z = (a.z + fh[i].z) * cf.z + 1e-9f;
-                    o.w = (a.w + fh[i].w) * cf.w + 1e-9f;
+                    o.x = (a.x + b.x) * cf.x + 1e-9f;
+                    o.y = (a.y + b.y) * cf.y + 1e-9f;
+                    o.z = (a.z + b.z) * cf.z + 1e-9f;
+                    o.w = (a.w + b.w) * cf.w + 1e-9f;
 #if AEC_OUT_NT
                     typedef float f4v __attribute__((ext_vector_type(4)));
                     __builtin_nontemporal_store(f4v{o.x, o.y, o.z, o.w}, reinterpret_cast<f4v*>(orow + (j0 + i) * kHop + r));
@@ -476,7 +502,8 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
                 float2 v[16];
                 synth_pack(xa, xb, x128, sEst + ((cs & 1) * kCH + fl) * kEstS, sBin, sTw512, lb, v);
                 if (next) load_rows(c - 1);
-                synth_fft<AEC_SYN_HANN_PRE>(v, sTwT, sHann, scr, lb);
+                if constexpr (ola_rec && AEC_OLA_WIN) synth_fft_raw(v, sTwT, scr, lb);
+                else synth_fft<AEC_SYN_HANN_PRE>(v, sTwT, sHann, scr, lb);
             } else if (next) {
                 load_rows(c - 1);
             }
