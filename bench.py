@@ -69,6 +69,7 @@ def path_flops(pipeline):
 # max-over-ranks time), from which the driver computes the scaling efficiency itself;
 # BASELINE's metric is per GPU, which is `value_per_gpu` (= value / n_gpus).
 MIN_WARM_STEPS = 40   # C2 warm-up floor (untimed), see run(): the clock ramp of the first ~20 ms of load
+WARM_MS = 30.0        # time-based untimed warm-up floor for the short C5 / training timed regions
 VALUE_SEMANTICS = ('value = aggregate frames/s of all ranks (frames of every rank / max-over-ranks time); '
                    'value_per_gpu = value / n_gpus (the metric\'s per-GPU figure)')
 
@@ -528,9 +529,15 @@ def run_c5_stream(dev, B=256, hops=200, dtype='fp8', world=1, with_cpu=False, sw
         far = 0.1 * torch.randn(bb, 256, device=dev, generator=g)
         out = torch.empty(bb, 256, device=dev)
         with torch.no_grad():
-            for _ in range(10):
-                net.stream_step(mic, far, out)
-            torch.cuda.synchronize(dev)
+            # untimed warm-up of at least WARM_MS of back-to-back hops: the chip's clocks ramp over
+            # the first ~20 ms of continuous load, longer than 200 hops at B=1
+            tw = time.perf_counter()
+            nw = 0
+            while nw < 10 or (time.perf_counter() - tw) * 1e3 < WARM_MS:
+                for _ in range(10):
+                    net.stream_step(mic, far, out)
+                nw += 10
+                torch.cuda.synchronize(dev)
             if barrier and world > 1:
                 dist.barrier()
             t0 = time.perf_counter()
@@ -662,8 +669,13 @@ def run_train(dev, B=16, n=160000, steps=10, warmup=2, with_cpu=False):
             ev[3].record()
         return loss
 
-    for _ in range(warmup):
+    tw = time.perf_counter()
+    nw = 0
+    while nw < warmup or (time.perf_counter() - tw) * 1e3 < WARM_MS:   # clock-ramp floor, as time_hops
         one()
+        nw += 1
+        if nw % 8 == 0:
+            torch.cuda.synchronize(dev)
     torch.cuda.synchronize(dev)
     for _ in range(3):                        # stage split: a separate, event-bracketed pass
         one(True)
