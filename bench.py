@@ -100,6 +100,9 @@ def parse():
     ap.add_argument('--lookahead', type=int, default=1,
                     help='C2: step k queues the normaliser pass of batch k + LOOKAHEAD on a side stream (aec_prepare); '
                          '0 = off')
+    ap.add_argument('--lookahead-cus', type=int, default=0,
+                    help='C2: the look-ahead side stream runs on this many CUs only (hipExtStreamCreateWithCUMask; '
+                         'every (256 / N)-th CU), so the HBM-bound pass holds few CUs; 0 = all CUs')
     ap.add_argument('--inflight', type=int, default=3,
                     help='C2 batches in flight (HIP streams, one handle each; 1 = strictly sequential; 3 measured '
                          '1-2 %% faster than 2, profiles/r05_notes.md r05t)')
@@ -110,6 +113,25 @@ def parse():
     ap.add_argument('--no-train', action='store_true', help='skip the training-step figure')
     ap.add_argument('--train-steps', type=int, default=10, help='timed steps of the training-step figure')
     return ap.parse_args()
+
+
+def cu_masked_stream(dev, ncu):
+    """A HIP stream whose kernels run on `ncu` CUs only (every (n_cu / ncu)-th), wrapped for torch."""
+    import ctypes
+    import torch
+    total = torch.cuda.get_device_properties(dev).multi_processor_count
+    step = max(1, total // ncu)
+    words = [0] * ((total + 31) // 32)
+    for c in range(0, total, step)[:ncu]:
+        words[c // 32] |= 1 << (c % 32)
+    hip = ctypes.CDLL('libamdhip64.so')
+    st = ctypes.c_void_p()
+    arr = (ctypes.c_uint32 * len(words))(*words)
+    with torch.cuda.device(dev):
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(len(words)), arr)
+    if rc != 0:
+        raise RuntimeError(f'hipExtStreamCreateWithCUMask failed: {rc}')
+    return torch.cuda.ExternalStream(st.value, device=dev)
 
 
 def roofline(pipeline, kernel, ms_per_launch, frames_per_launch, pmc):
@@ -789,7 +811,9 @@ def main():
     # stream before its own kernels, so that HBM-bound pass runs under the compute of the batches
     # in flight instead of in front of that batch's analysis.  Every step still runs one pass (the
     # timed region's first batches take the passes queued by the last warm-up steps).
-    side = torch.cuda.Stream(dev) if args.lookahead else None
+    side = None
+    if args.lookahead:
+        side = cu_masked_stream(dev, args.lookahead_cus) if args.lookahead_cus > 0 else torch.cuda.Stream(dev)
 
     def step():
         k = kstep[0] % inflight
@@ -992,6 +1016,7 @@ def main():
                        'streams_per_gpu': B, 'samples_per_stream': n, 'frames_per_stream': T,
                        'frame': '256-sample hop', 'pipeline': args.pipeline, 'batches_in_flight': inflight,
                        'normaliser_lookahead_batches': args.lookahead if args.pipeline != 'crn' else 0,
+                       'normaliser_lookahead_cus': args.lookahead_cus if args.pipeline != 'crn' else 0,
                        'parallelism': f'streams sharded, {world} rank(s)'},
             'value_per_gpu': round(value / world, 1),
             'aggregate_frames_per_s': round(value, 1),
