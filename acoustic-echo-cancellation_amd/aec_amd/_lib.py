@@ -23,19 +23,19 @@ _STATUS = {0: 'AEC_OK', 1: 'AEC_ERR_INVALID_ARG', 2: 'AEC_ERR_OOM', 3: 'AEC_ERR_
 
 # every symbol include/aec_hip.h declares
 EXPORTS = ('aec_weights_count', 'aec_create', 'aec_set_weights', 'aec_set_erb', 'aec_process', 'aec_process_siglens',
-           'aec_prepare', 'aec_prepare_siglens',
+           'aec_prepare', 'aec_prepare_siglens', 'aec_process_prepared',
            'aec_stream_open', 'aec_stream_reset', 'aec_stream_step',
            'aec_set_debug', 'aec_debug_copy', 'aec_profile_enable', 'aec_profile_read',
            'aec_erb_tables_check', 'aec_num_frames', 'aec_out_len', 'aec_last_error', 'aec_destroy',
            'aec_set_weights_device', 'aec_train_forward', 'aec_train_backward', 'aec_train_generation',
-           'aec_adam_step', 'aec_adam_step_multi')
+           'aec_adam_step', 'aec_adam_step_multi', 'aec_build_info')
 
 
 # every symbol include/aec_crn.h declares
 CRN_EXPORTS = ('aec_crn_param_count', 'aec_crn_create', 'aec_crn_set_params', 'aec_crn_process', 'aec_crn_stft',
                'aec_crn_error_spec',
                'aec_crn_stream_open', 'aec_crn_stream_reset', 'aec_crn_stream_step',
-               'aec_crn_profile_enable', 'aec_crn_profile_read', 'aec_crn_last_error', 'aec_crn_destroy')
+               'aec_crn_stream_set_graph', 'aec_crn_stream_stats', 'aec_crn_profile_enable', 'aec_crn_profile_read', 'aec_crn_last_error', 'aec_crn_destroy')
 
 
 class CrnConfig(ctypes.Structure):
@@ -82,10 +82,14 @@ def load():
     lib.aec_process.restype = ctypes.c_int
     lib.aec_process_siglens.argtypes = [P, P, P, P, P, ctypes.c_int32, ctypes.c_int64, P, ctypes.c_int64, P, P]
     lib.aec_process_siglens.restype = ctypes.c_int
-    lib.aec_prepare.argtypes = [P, P, P, P, P, ctypes.c_int32, ctypes.c_int64, P]
+    lib.aec_prepare.argtypes = [P, P, P, P, P, ctypes.c_int32, ctypes.c_int64, P, ctypes.POINTER(ctypes.c_uint64)]
     lib.aec_prepare.restype = ctypes.c_int
-    lib.aec_prepare_siglens.argtypes = [P, P, P, P, P, ctypes.c_int32, ctypes.c_int64, P]
+    lib.aec_prepare_siglens.argtypes = [P, P, P, P, P, ctypes.c_int32, ctypes.c_int64, P,
+                                        ctypes.POINTER(ctypes.c_uint64)]
     lib.aec_prepare_siglens.restype = ctypes.c_int
+    lib.aec_process_prepared.argtypes = [P, ctypes.c_uint64, P, P, P, P, ctypes.c_int32, ctypes.c_int64, P,
+                                         ctypes.c_int64, P, P]
+    lib.aec_process_prepared.restype = ctypes.c_int
     lib.aec_stream_open.argtypes = [P, ctypes.c_int32]
     lib.aec_stream_open.restype = ctypes.c_int
     lib.aec_stream_reset.argtypes = [P, ctypes.c_int32, P]
@@ -107,6 +111,8 @@ def load():
     lib.aec_num_frames.restype = ctypes.c_int64
     lib.aec_out_len.argtypes = [ctypes.c_int64]
     lib.aec_out_len.restype = ctypes.c_int64
+    lib.aec_build_info.argtypes = []
+    lib.aec_build_info.restype = ctypes.c_char_p
     lib.aec_last_error.argtypes = [P]
     lib.aec_last_error.restype = ctypes.c_char_p
     lib.aec_destroy.argtypes = [P]
@@ -144,6 +150,11 @@ def load():
     lib.aec_crn_stream_reset.restype = ctypes.c_int
     lib.aec_crn_stream_step.argtypes = [P, P, P, ctypes.c_int64, P, ctypes.c_int64, P]
     lib.aec_crn_stream_step.restype = ctypes.c_int
+    lib.aec_crn_stream_set_graph.argtypes = [P, ctypes.c_int32]
+    lib.aec_crn_stream_set_graph.restype = ctypes.c_int
+    lib.aec_crn_stream_stats.argtypes = [P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64),
+                                         ctypes.POINTER(ctypes.c_int64)]
+    lib.aec_crn_stream_stats.restype = ctypes.c_int
     lib.aec_crn_profile_enable.argtypes = [P, ctypes.c_int32]
     lib.aec_crn_profile_enable.restype = ctypes.c_int
     lib.aec_crn_profile_read.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
@@ -154,6 +165,15 @@ def load():
     lib.aec_crn_destroy.restype = None
     _lib = lib
     return lib
+
+
+def build_info():
+    """aec_build_info(): dict(arch, ab_knobs (bool), mode_knobs (list of names))."""
+    txt = load().aec_build_info().decode()
+    head, _, knobs = txt.partition(' mode_knobs=')
+    d = dict(kv.split('=', 1) for kv in head.split())
+    return dict(arch=d.get('arch'), ab_knobs=d.get('ab_knobs') == 'on',
+                mode_knobs=[k.split('(')[0] for k in knobs.split()], text=txt)
 
 
 def check(status, handle=None, what='', crn=False):
@@ -210,23 +230,34 @@ class Handle:
     def set_debug(self, on: bool):
         check(self.lib.aec_set_debug(self.h, int(bool(on))), self.h, 'aec_set_debug')
 
-    def process(self, mic_ptr, ref_ptr, near_ptr, lengths, B, ld, out_ptr, ld_out, loss_ptr, stream):
+    def process(self, mic_ptr, ref_ptr, near_ptr, lengths, B, ld, out_ptr, ld_out, loss_ptr, stream, token=0):
         """lengths: [B] (one length per stream) or [B, 3] (mic, ref, near lengths:
-        aec_process_siglens)."""
+        aec_process_siglens); token: a look-ahead of prepare() to consume
+        (aec_process_prepared), 0 = none."""
         import numpy as np
         lens = np.ascontiguousarray(lengths, dtype=np.int64)
+        if token:
+            if lens.ndim == 1:
+                lens = np.repeat(lens[:, None], 3, axis=1)
+            st = self.lib.aec_process_prepared(self.h, int(token), mic_ptr, ref_ptr, near_ptr, lens.ctypes.data, int(B),
+                                               int(ld), out_ptr, int(ld_out), loss_ptr, stream)
+            check(st, self.h, 'aec_process_prepared')
+            return
         fn = self.lib.aec_process_siglens if lens.ndim == 2 else self.lib.aec_process
         st = fn(self.h, mic_ptr, ref_ptr, near_ptr, lens.ctypes.data, int(B), int(ld),
                 out_ptr, int(ld_out), loss_ptr, stream)
         check(st, self.h, 'aec_process_siglens' if lens.ndim == 2 else 'aec_process')
 
     def prepare(self, mic_ptr, ref_ptr, near_ptr, lengths, B, ld, stream):
-        """Look-ahead normaliser pass of the batch a later process() takes (aec_prepare[_siglens])."""
+        """Look-ahead normaliser pass of the batch a later process(token=...) takes
+        (aec_prepare[_siglens]); returns its token."""
         import numpy as np
         lens = np.ascontiguousarray(lengths, dtype=np.int64)
         fn = self.lib.aec_prepare_siglens if lens.ndim == 2 else self.lib.aec_prepare
-        st = fn(self.h, mic_ptr, ref_ptr, near_ptr, lens.ctypes.data, int(B), int(ld), stream)
+        tok = ctypes.c_uint64(0)
+        st = fn(self.h, mic_ptr, ref_ptr, near_ptr, lens.ctypes.data, int(B), int(ld), stream, ctypes.byref(tok))
         check(st, self.h, 'aec_prepare_siglens' if lens.ndim == 2 else 'aec_prepare')
+        return int(tok.value)
 
     def stream_open(self, B):
         check(self.lib.aec_stream_open(self.h, int(B)), self.h, 'aec_stream_open')
@@ -358,6 +389,16 @@ class CrnHandle:
     def stream_step(self, mic_ptr, far_ptr, ld_in, out_ptr, ld_out, stream):
         check(self.lib.aec_crn_stream_step(self.h, mic_ptr, far_ptr, int(ld_in), out_ptr, int(ld_out), stream),
               self.h, 'aec_crn_stream_step', True)
+
+    def stream_set_graph(self, mode):
+        check(self.lib.aec_crn_stream_set_graph(self.h, int(mode)), self.h, 'aec_crn_stream_set_graph', True)
+
+    def stream_stats(self):
+        """-> dict(graph_mode, graph_replays, direct_hops) of the open streams"""
+        m, g, d = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int64()
+        check(self.lib.aec_crn_stream_stats(self.h, ctypes.byref(m), ctypes.byref(g), ctypes.byref(d)), self.h,
+              'aec_crn_stream_stats', True)
+        return dict(graph_mode=int(m.value), graph_replays=int(g.value), direct_hops=int(d.value))
 
     def profile_enable(self, on: bool):
         check(self.lib.aec_crn_profile_enable(self.h, int(bool(on))), self.h, 'aec_crn_profile_enable', True)

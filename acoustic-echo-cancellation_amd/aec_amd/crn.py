@@ -206,17 +206,25 @@ class _DCCRNBase(nn.Module):
         return torch.cat([spec[..., 0], spec[..., 1]], dim=2).transpose(1, 2)
 
     # ---- streaming (include/aec_crn.h aec_crn_stream_*) ------------------------
-    def stream_open(self, B, device='cuda'):
+    def stream_open(self, B, device='cuda', graph=None):
         """Open B concurrent streams (state zeroed).  Then feed one 256-sample
         hop per stream per ``stream_step``; the output of step k is hop k-1 of
         the batch forward's out_wav (the first step's output is the trimmed
         warm-up region).  Feed N//256 + 1 hops per utterance, the last one
-        zero-padded."""
+        zero-padded.  ``graph``: True replays each hop's launches from a
+        hipGraph, False launches them directly, None keeps the library's
+        choice (AEC_CRN_GRAPH, default direct); see ``stream_stats``."""
         self._check(torch.zeros(1, device=device))
         dev = torch.device(device)
         h = self._handle(dev)
         h.stream_open(B)
+        if graph is not None:
+            h.stream_set_graph(1 if graph else 0)
         self._stream = (h, dev, int(B))
+
+    def stream_stats(self):
+        """dict(graph_mode, graph_replays, direct_hops) since ``stream_open``."""
+        return self._stream[0].stream_stats()
 
     def stream_reset(self, b=-1):
         h, dev, _ = self._stream

@@ -236,14 +236,18 @@ class Little_net(nn.Module):
         mic, ref, near = (t.detach().contiguous().float() for t in (mic, ref, near))
         return _TrainStep.apply(self, mic, ref, near, erb, *params)
 
-    def forward_ragged(self, mic, ref, near, erb, lengths):
+    def forward_ragged(self, mic, ref, near, erb, lengths, lookahead=None):
         """Batched call with per-row true lengths (rows zero-padded to a common
         width).  ``lengths`` is [B] (one length per row) or [B, 3] (mic, ref,
         near lengths of each row: every signal normalised over and padded
         beyond its own length, as test.py:139 feeds the reference; the three
         must share the frame count N//256 + 1).  Returns out
         [B, 256*(max(mic lengths)//256)] (row b valid up to 256*(n_mic//256),
-        zero beyond) and per-row losses [B] (None when ``near`` is None)."""
+        zero beyond) and per-row losses [B] (None when ``near`` is None).
+        ``lookahead``: the token ``prepare_ragged`` returned for exactly these
+        tensors and lengths; its queued normaliser pass is used instead of
+        running one (a token that is not pending, or was prepared for other
+        tensors / lengths, raises)."""
         if torch.is_grad_enabled() and (mic.requires_grad or any(p.requires_grad for p in self._params())
                                         and self.training):
             raise NotImplementedError('forward_ragged is the inference path (batch=1 semantics per row): call it '
@@ -284,21 +288,26 @@ class Little_net(nn.Module):
             with torch.cuda.device(dev):
                 h.process(mic.data_ptr(), ref.data_ptr(), near.data_ptr() if near is not None else None,
                           lengths, B, L, out.data_ptr() if lout > 0 else None, max(lout, 1), loss.data_ptr() if loss is not None else None,
-                          stream)
+                          stream, token=lookahead or 0)
         return out, loss
 
-    def prepare_ragged(self, mic, ref, near, lengths):
-        """Queue the normaliser pass (ERB.py:254-256) of the batch the next
-        ``forward_ragged`` on this net will take, on the current stream
-        (``aec_prepare_siglens``): a serving loop runs it on a side stream while
-        the previous batch is still in flight.  The tensors must be the very
-        ones (contiguous float32, same data) passed to that ``forward_ragged``;
-        otherwise it drops the look-ahead and runs the pass itself.  Outputs are
-        bit-identical either way."""
+    def prepare_ragged(self, mic, ref, near, lengths, producer=None):
+        """Queue the normaliser pass (ERB.py:254-256) of a batch a later
+        ``forward_ragged(..., lookahead=token)`` on this net takes, on the
+        current stream (``aec_prepare_siglens``): a serving loop runs it on a
+        side stream while the previous batch is still in flight.  Returns the
+        token.  The tensors must be the very ones (contiguous float32, same
+        data) passed to that ``forward_ragged``; a plain ``forward_ragged``
+        never takes a look-ahead.  ``producer``: the stream that wrote the
+        tensors (the pass waits for it; None = the caller has ordered them).
+        The tensors are recorded on the current stream, so the caching
+        allocator does not hand their memory out while the pass reads it.
+        Outputs are bit-identical with and without the look-ahead."""
         dev = mic.device
         if dev.type != 'cuda':
             raise RuntimeError(f'Little_net (gfx950) needs its inputs on a HIP device, got {dev}')
-        for t in [mic, ref] + ([near] if near is not None else []):
+        tens = [mic, ref] + ([near] if near is not None else [])
+        for t in tens:
             if t.shape != mic.shape or t.device != dev or not t.is_contiguous() or t.dtype != torch.float32:
                 raise ValueError('prepare_ragged needs contiguous float32 mic / ref / near of one shape and device')
         B, L = mic.shape
@@ -306,10 +315,16 @@ class Little_net(nn.Module):
         if lengths.shape not in ((B,), (B, 3)) or (lengths < 1).any() or (lengths > L).any():
             raise ValueError('lengths must be [B] or [B, 3] with 1 <= length <= N')
         h, _ = self._handle(dev)
-        if B > 0:
-            with torch.cuda.device(dev):
-                h.prepare(mic.data_ptr(), ref.data_ptr(), near.data_ptr() if near is not None else None,
-                          lengths, B, L, torch.cuda.current_stream(dev).cuda_stream)
+        if B == 0:
+            return 0
+        cur = torch.cuda.current_stream(dev)
+        if producer is not None:
+            cur.wait_stream(producer)
+        for t in tens:
+            t.record_stream(cur)
+        with torch.cuda.device(dev):
+            return h.prepare(mic.data_ptr(), ref.data_ptr(), near.data_ptr() if near is not None else None,
+                             lengths, B, L, cur.cuda_stream)
 
     # --- streaming (include/aec_hip.h aec_stream_*) ------------------------------
     def stream_open(self, B, erb, device=None):

@@ -211,9 +211,11 @@ struct aec_handle {
         int64_t ld = 0;
         int nsig = 0;
         std::vector<int64_t> l3;
+        uint64_t token = 0;
     };
     PreSlot pre[2];
     int pre_head = 0, pre_count = 0;
+    uint64_t next_token = 1;
     struct ListSlot {
         char* host = nullptr;    // pinned
         size_t cap = 0;
@@ -237,12 +239,12 @@ struct aec_handle {
     std::vector<int64_t> last_lens;                 // [B][3] of the last call (work lists rebuilt on change)
     std::vector<WorkItem> h_items, h_sitems;        // host copies of the last work lists
     int debug = 0;
-    int gru_mode = 0;            // AEC_GRU_MODE (timing experiments; results invalid unless 0)
-    int nlms_mode = 0;           // AEC_NLMS_MODE (timing experiments; results invalid unless 0)
-    int nlms_prio = 0;           // AEC_NLMS_PRIO: wave priorities mic|ref|nlms digits (0: all equal, fastest measured)
-    int nlms_erb = 1;            // AEC_NLMS_ERB: role running the mic_erb pass (1 ref, 2 nlms)
+    int gru_mode = 0;            // AEC_GRU_MODE (A/B builds: timing experiments; results invalid unless 0)
+    int nlms_mode = 0;           // AEC_NLMS_MODE: bit 4 two-pass ref ERB (tested); bits 0-3 A/B builds only (skip work)
+    int nlms_prio = 0;           // AEC_NLMS_PRIO (A/B builds): wave priorities mic|ref|nlms digits (0 fastest measured)
+    int nlms_erb = 1;            // AEC_NLMS_ERB (A/B builds): role running the mic_erb pass (1 ref, 2 nlms)
     int fused = 1;               // AEC_FUSED_SYNTH: GRU + synthesis in one kernel (NLMS path)
-    int fused_mode = 0;          // AEC_FUSED_MODE (timing experiments; results invalid unless 0)
+    int fused_mode = 0;          // AEC_FUSED_MODE (A/B builds: timing experiments; results invalid unless 0)
     int small_b = 64;            // AEC_SMALLB: NLMS batches up to this many streams take the split path
                                  // (per 10 s step: B = 1 0.477 -> 0.336 ms, B = 16 0.486 -> 0.354,
                                  // B = 64 0.504 -> 0.485; B = 128 slower)
@@ -340,6 +342,12 @@ int64_t aec_out_len(int64_t n) { return 256 * (n / 256); }
 
 const char* aec_last_error(const aec_handle* h) { return h ? h->err.c_str() : "null handle"; }
 
+const char* aec_build_info(void) {
+    static const std::string info = std::string("arch=gfx950 ab_knobs=") + (AEC_AB_BUILD ? "on" : "off") +
+                                    " mode_knobs=" + aec::kModeKnobs;
+    return info.c_str();
+}
+
 
 aec_status aec_set_weights(aec_handle* h, const float* w, size_t n) {
     if (!h) return AEC_ERR_INVALID_ARG;
@@ -384,14 +392,18 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
     if (!h) return AEC_ERR_OOM;
     h->cfg = *cfg;
     h->device = device;
-    if (const char* m = std::getenv("AEC_GRU_MODE")) h->gru_mode = std::atoi(m);
-    if (const char* m = std::getenv("AEC_NLMS_MODE")) h->nlms_mode = std::atoi(m);
-    if (const char* m = std::getenv("AEC_NLMS_PRIO")) h->nlms_prio = std::atoi(m);
-    if (const char* m = std::getenv("AEC_NLMS_ERB")) h->nlms_erb = std::atoi(m);
-    if (const char* m = std::getenv("AEC_FUSED_SYNTH")) h->fused = std::atoi(m);
-    if (const char* m = std::getenv("AEC_FUSED_MODE")) h->fused_mode = std::atoi(m);
-    if (const char* m = std::getenv("AEC_SMALLB")) h->small_b = std::atoi(m);
-    if (const char* m = std::getenv("AEC_BPTT_SERIAL")) h->bptt_serial = std::atoi(m);
+    // tested modes (aec_knobs.h): the two-pass ERB projection of K2n's ref waves (AEC_NLMS_MODE bit 4),
+    // the unfused GRU + synthesis, the small-batch split path, the serial BPTT recursion
+    h->nlms_mode = AEC_MODE_KNOB("AEC_NLMS_MODE", 0) & 16;
+    h->fused = AEC_MODE_KNOB("AEC_FUSED_SYNTH", h->fused);
+    h->small_b = AEC_MODE_KNOB("AEC_SMALLB", h->small_b);
+    h->bptt_serial = AEC_MODE_KNOB("AEC_BPTT_SERIAL", h->bptt_serial);
+    // A/B builds only: work-skipping timing bits and role priorities
+    h->gru_mode = AEC_AB_KNOB("AEC_GRU_MODE", 0);
+    h->nlms_mode |= AEC_AB_KNOB("AEC_NLMS_MODE", 0) & ~16;
+    h->nlms_prio = AEC_AB_KNOB("AEC_NLMS_PRIO", 0);
+    h->nlms_erb = AEC_AB_KNOB("AEC_NLMS_ERB", h->nlms_erb);
+    h->fused_mode = AEC_AB_KNOB("AEC_FUSED_MODE", 0);
     {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
@@ -575,7 +587,25 @@ aec_status aec_process(aec_handle* h, const float* mic, const float* ref, const 
     return aec_process_siglens(h, mic, ref, near, l3.data(), B, ld, out, ld_out, loss, stream);
 }
 
+static aec_status process_impl(aec_handle* h, uint64_t token, const float* mic, const float* ref, const float* near,
+                               const int64_t* lengths3, int32_t B, int64_t ld, float* out, int64_t ld_out,
+                               float* loss, void* stream);
+
 aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref, const float* near,
+                               const int64_t* lengths3, int32_t B, int64_t ld, float* out, int64_t ld_out,
+                               float* loss, void* stream) {
+    return process_impl(h, 0, mic, ref, near, lengths3, B, ld, out, ld_out, loss, stream);
+}
+
+aec_status aec_process_prepared(aec_handle* h, uint64_t token, const float* mic, const float* ref, const float* near,
+                                const int64_t* lengths3, int32_t B, int64_t ld, float* out, int64_t ld_out,
+                                float* loss, void* stream) {
+    if (!h) return AEC_ERR_INVALID_ARG;
+    if (token == 0) return fail(h, AEC_ERR_INVALID_ARG, "look-ahead token 0");
+    return process_impl(h, token, mic, ref, near, lengths3, B, ld, out, ld_out, loss, stream);
+}
+
+static aec_status process_impl(aec_handle* h, uint64_t token, const float* mic, const float* ref, const float* near,
                                const int64_t* lengths3, int32_t B, int64_t ld, float* out, int64_t ld_out,
                                float* loss, void* stream) {
     if (!h) return AEC_ERR_INVALID_ARG;
@@ -607,6 +637,25 @@ aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref
     const bool nlms_batch = h->cfg.nlms_taps > 0 && !(B <= h->small_b && h->nlms_mode == 0);
     if (nlms_batch && nlms_smem_bytes(h->sched_len, h->cfg.nlms_taps) > 160 * 1024)   // before any launch
         return fail(h, AEC_ERR_UNSUPPORTED, "erb schedule too long for the NLMS kernel's LDS budget");
+    const int nsig = near ? 3 : 2;
+    // aec_process_prepared: the look-ahead pass named by `token` (aec_prepare_siglens), checked
+    // before anything is launched; the pending ones queued before it are dropped (their slots stay
+    // fenced by their done / freed events)
+    aec_handle::PreSlot* ps = nullptr;
+    if (token) {
+        int k = 0;
+        while (k < h->pre_count && h->pre[(h->pre_head + k) & 1].token != token) ++k;
+        if (k == h->pre_count) return fail(h, AEC_ERR_INVALID_ARG, "look-ahead token not pending");
+        aec_handle::PreSlot& c = h->pre[(h->pre_head + k) & 1];
+        if (!(c.sig[0] == mic && c.sig[1] == ref && c.sig[2] == near && c.ld == ld && c.nsig == nsig &&
+              c.l3.size() == (size_t)B * 3 &&
+              std::memcmp(c.l3.data(), lengths3, (size_t)B * 3 * sizeof(int64_t)) == 0))
+            return fail(h, AEC_ERR_INVALID_ARG, "look-ahead prepared for other signals / ld / B / lengths");
+        ps = &c;
+        h->pre_head = (h->pre_head + k + 1) & 1;
+        h->pre_count -= k + 1;
+        c.token = 0;
+    }
     // this call overwrites the features a pending aec_train_backward would read
     h->train_B = 0;
     ++h->train_gen;
@@ -617,20 +666,6 @@ aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref
     if (s != AEC_OK) return s;
     s = prepare_lists(h, lengths3, B, nsig_in, st);
     if (s != AEC_OK) return s;
-    const int nsig = near ? 3 : 2;
-    // a matching look-ahead pass (aec_prepare_siglens): wait for it instead of running it
-    aec_handle::PreSlot* ps = nullptr;
-    if (h->pre_count > 0) {
-        aec_handle::PreSlot& c = h->pre[h->pre_head];
-        if (c.sig[0] == mic && c.sig[1] == ref && c.sig[2] == near && c.ld == ld && c.nsig == nsig &&
-            c.l3.size() == (size_t)B * 3 && std::memcmp(c.l3.data(), lengths3, (size_t)B * 3 * sizeof(int64_t)) == 0) {
-            ps = &c;
-            h->pre_head = (h->pre_head + 1) & 1;
-            --h->pre_count;
-        } else {
-            h->pre_count = 0;   // stale: drop every pending look-ahead (their slots stay fenced by done)
-        }
-    }
     // the consumed slot is free again once this call's kernels have read its cvals (every exit)
     struct PreRelease {
         aec_handle::PreSlot* ps;
@@ -730,8 +765,9 @@ aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref
 }
 
 aec_status aec_prepare_siglens(aec_handle* h, const float* mic, const float* ref, const float* near,
-                               const int64_t* lengths3, int32_t B, int64_t ld, void* stream) {
+                               const int64_t* lengths3, int32_t B, int64_t ld, void* stream, uint64_t* token) {
     if (!h) return AEC_ERR_INVALID_ARG;
+    if (token) *token = 0;
     if (B <= 0 || !lengths3 || !mic || !ref) return fail(h, AEC_ERR_INVALID_ARG, "bad batch / lengths / signals");
     if (h->pre_count >= 2) return fail(h, AEC_ERR_INVALID_ARG, "two look-ahead batches already pending");
     const int nsig = near ? 3 : 2;
@@ -780,17 +816,19 @@ aec_status aec_prepare_siglens(aec_handle* h, const float* mic, const float* ref
     ps.ld = ld;
     ps.nsig = nsig;
     ps.l3.assign(lengths3, lengths3 + (size_t)B * 3);
+    ps.token = h->next_token++;
+    if (token) *token = ps.token;
     ++h->pre_count;
     return AEC_OK;
 }
 
 aec_status aec_prepare(aec_handle* h, const float* mic, const float* ref, const float* near,
-                       const int64_t* lengths, int32_t B, int64_t ld, void* stream) {
+                       const int64_t* lengths, int32_t B, int64_t ld, void* stream, uint64_t* token) {
     if (!h) return AEC_ERR_INVALID_ARG;
     if (B <= 0 || !lengths) return fail(h, AEC_ERR_INVALID_ARG, "bad batch / lengths");
     std::vector<int64_t> l3((size_t)B * 3);
     for (int b = 0; b < B; ++b) l3[3 * b] = l3[3 * b + 1] = l3[3 * b + 2] = lengths[b];
-    return aec_prepare_siglens(h, mic, ref, near, l3.data(), B, ld, stream);
+    return aec_prepare_siglens(h, mic, ref, near, l3.data(), B, ld, stream, token);
 }
 
 aec_status aec_debug_copy(aec_handle* h, int32_t what, float* dst, size_t n, void* stream) {

@@ -529,10 +529,9 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
 // streams per block: AEC_GRU_NS (1 or 2, default 2), read per launch
 hipError_t launch_gru_synth(const GruArgs& g, const SynthArgs& y, int B, hipStream_t st) {
     if (B <= 0) return hipSuccess;
-    const char* env = getenv("AEC_GRU_NS");
     // NS = 2 writes the waveform with 16-B stores (overlap-add on the recurrence waves)
     const bool al16 = y.ld_out % 4 == 0 && (reinterpret_cast<uintptr_t>(y.out) & 15) == 0;
-    const int ns = (env && atoi(env) == 1) || (AEC_OLA_REC && !al16) ? 1 : 2;
+    const int ns = AEC_MODE_KNOB("AEC_GRU_NS", 2) == 1 || (AEC_OLA_REC && !al16) ? 1 : 2;
 #define AEC_GRU_SYNTH(NS_)                                                                                     \
     do {                                                                                                       \
         static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gru_synth_kernel<NS_>), \

@@ -878,36 +878,42 @@ hipError_t launch_mic_erb(const float2* spec, float* feats, const int64_t* lens,
 hipError_t launch_moments(const float* mic, const float* ref, const float* near, int64_t ld,
                           const int32_t* slen, double2* mom, int b0, int nb, int nsig, hipStream_t st) {
     if (nb <= 0) return hipSuccess;
-    // Default (AEC_MOM_CFG unset or 3): moments_lds_kernel, one 256-thread block per (chunk, signal,
-    // stream), 4 KiB rounds through a 4-round LDS ring: 30 VGPRs and 16 KiB, so a block fits beside a
-    // K2n or gru_synth block and the look-ahead pass (aec_prepare) of the next batch streams under
-    // the compute kernels of the batches in flight (C2 0.581-0.592 against 0.597-0.600 ms,
-    // profiles/r05r_persist8_lookahead_ab.log).  Standalone 0.080 ms for 256 x 10 s x 3 signals.
-    // Timing variants (bit-identical partials): 0 moments_kernel, 4 float4 per thread in registers,
-    // nt loads (0.078 ms standalone; 36 VGPRs: fits beside neither compute kernel); 1 the same with
-    // default-policy loads (0.104 ms); 2 two float4 per thread; 4 moments_lds persistent,
-    // AEC_MOM_GRID blocks walking the items (40 VGPRs; slower, profiles/r05_notes.md r05n).
-    static const int cfg = [] { const char* e = std::getenv("AEC_MOM_CFG"); return e ? std::atoi(e) : 3; }();
+    // moments_lds_kernel, one 256-thread block per (chunk, signal, stream), 4 KiB rounds through a
+    // 4-round LDS ring: 30 VGPRs and 16 KiB, so a block fits beside a K2n or gru_synth block and the
+    // look-ahead pass (aec_prepare) of the next batch streams under the compute kernels of the
+    // batches in flight (C2 0.581-0.592 against 0.597-0.600 ms, profiles/r05r_persist8_lookahead_ab.log).
+    // Standalone 0.080 ms for 256 x 10 s x 3 signals.
     const dim3 g(kMomChunks, nsig, nb);
-    // 9, TIMING ONLY: after the first 16 launches no moments pass (every workspace then keeps the
-    // partials of its last pass: valid only while each handle's inputs repeat, as in bench.py
-    // --lookahead 0)
+    const int nwork = kMomChunks * nsig * nb;
+#if AEC_AB_BUILD
+    // A/B builds (AEC_MOM_CFG; bit-identical partials): 0 moments_kernel, 4 float4 per thread in
+    // registers, nt loads (0.078 ms standalone; 36 VGPRs: fits beside neither compute kernel); 1 the
+    // same with default-policy loads (0.104 ms); 2 two float4 per thread; 4 moments_lds persistent,
+    // AEC_MOM_GRID blocks walking the items (40 VGPRs; slower, profiles/r05_notes.md r05n); 9 TIMING
+    // ONLY: no pass after the first 16 launches (partials of each workspace's last pass)
+    static const int cfg = AEC_AB_KNOB("AEC_MOM_CFG", 3);
     static int launches = 0;
     if (cfg == 9 && ++launches > 16) return hipSuccess;
-    const int nwork = kMomChunks * nsig * nb;
-    if (cfg == 0)
+    if (cfg == 0) {
         hipLaunchKernelGGL((moments_kernel<4, 256, true>), g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0);
-    else if (cfg == 1)
+        return hipGetLastError();
+    }
+    if (cfg == 1) {
         hipLaunchKernelGGL((moments_kernel<4, 256, false>), g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0);
-    else if (cfg == 2)
+        return hipGetLastError();
+    }
+    if (cfg == 2) {
         hipLaunchKernelGGL((moments_kernel<2, 256, true>), g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0);
-    else if (cfg == 4) {
-        static const int pgrid = [] { const char* e = std::getenv("AEC_MOM_GRID"); return e ? std::atoi(e) : 256; }();
+        return hipGetLastError();
+    }
+    if (cfg == 4) {
+        static const int pgrid = AEC_AB_KNOB("AEC_MOM_GRID", 256);
         hipLaunchKernelGGL(moments_lds_kernel<true>, dim3(std::max(1, std::min(pgrid, nwork))), dim3(256), 0, st, mic,
                            ref, near, ld, slen, mom, b0, nsig, nwork);
-    } else {
-        hipLaunchKernelGGL(moments_lds_kernel<false>, g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0, nsig, nwork);
+        return hipGetLastError();
     }
+#endif
+    hipLaunchKernelGGL(moments_lds_kernel<false>, g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0, nsig, nwork);
     return hipGetLastError();
 }
 

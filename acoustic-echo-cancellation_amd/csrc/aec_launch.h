@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "aec_fft.h"
+#include "aec_knobs.h"
 
 namespace aec {
 

@@ -692,7 +692,7 @@ struct Bufs {
 // K slices of an MX conv GEMM in the per-hop step (its grid alone covers a fraction of the
 // CUs): >= 3 stages of 128 k per slice.  Chosen per layer, never from the row count.
 static int conv_ksplit(int kpad) {
-    static const int mx = [] { const char* v = getenv("AEC_CRN_SPLITK"); return v ? atoi(v) : 4; }();
+    static const int mx = AEC_AB_KNOB("AEC_CRN_SPLITK", 4);
     const int nst = kpad / 128;
     int ks = 1;
     while (ks * 2 <= mx && nst >= 6 * ks) ks *= 2;
@@ -763,8 +763,7 @@ static int run_enc_batch_try(aec_crn_handle* h, const Bufs& bf, int64_t F, hipSt
 template <typename T>
 static int run_enc_batch(aec_crn_handle* h, const Bufs& bf, int64_t F, hipStream_t st, aec_status* s) {
     *s = AEC_OK;
-    const char* v = getenv("AEC_CRN_BATCH_ENC");
-    const int mode = v ? atoi(v) : 1;
+    const int mode = AEC_MODE_KNOB("AEC_CRN_BATCH_ENC", 1);
     if (mode == 0) return 0;
     const int n = run_enc_batch_try<T>(h, bf, F, st, s);
     if (n == 0 && *s == AEC_OK && mode == 2) {
@@ -1021,15 +1020,10 @@ static aec_status run_persist(aec_crn_handle* h, int l, int32_t B, int64_t Tmax,
         h->persist_pending = true;
     }
     // polls before a wave gives up; AEC_CRN_SPIN_LIMIT (read per call) forces a timeout in the tests
-    const char* sl = getenv("AEC_CRN_SPIN_LIMIT");
-    const int spin = sl ? std::max(1, atoi(sl)) : crn::kPersistSpinLimit;
-    // AEC_CRN_PERSIST_STALL=1 (read per call, tests only): the poll targets are never reached
-    const char* ss = getenv("AEC_CRN_PERSIST_STALL");
-    const int stall = ss && atoi(ss) != 0 ? (1 << 30) : 0;
-    static const int pra = [] { const char* v = getenv("CRN_PERSIST_RA"); return v ? atoi(v) : 1; }();
-    // waves per block: 4 (lstm_persist2_kernel) or 8 (lstm_persist3_kernel); AEC_CRN_PERSIST_WAVES, read per call
-    const char* pwe = getenv("AEC_CRN_PERSIST_WAVES");
-    const int pw = pwe && atoi(pwe) == 8 ? 8 : 4;
+    const int spin = std::max(1, AEC_MODE_KNOB("AEC_CRN_SPIN_LIMIT", crn::kPersistSpinLimit));
+    // AEC_CRN_PERSIST_STALL=1 (read per call, the timeout test's hook): the poll targets are never reached
+    const int stall = AEC_MODE_KNOB("AEC_CRN_PERSIST_STALL", 0) != 0 ? (1 << 30) : 0;
+    static const int pra = AEC_AB_KNOB("CRN_PERSIST_RA", 1);
     // one block per CU: 64 streams (two teams of 32 blocks) per 64 CUs, at most 256 streams per launch
     const int32_t chunk = 64 * std::min(4, h->num_cus / 64);
     for (int32_t b0 = 0; b0 < B; b0 += chunk) {
@@ -1049,7 +1043,7 @@ static aec_status run_persist(aec_crn_handle* h, int l, int32_t B, int64_t Tmax,
         a.stall = stall;
         // arrival counters only: the error word keeps any timeout of this call's earlier launches
         CRN_TRY(h, hipMemsetAsync(h->psync, 0, crn::kPersistCounters * sizeof(int), st));
-        CRN_TRY(h, pw == 8 ? crn::launch_lstm_persist3(a, st) : crn::launch_lstm_persist(a, st));
+        CRN_TRY(h, crn::launch_lstm_persist(a, st));
     }
     CRN_TRY(h, hipEventRecord(ev, st));
     return AEC_OK;
@@ -1089,8 +1083,7 @@ static aec_status persist_wait(aec_crn_handle* h) {
 template <typename T>
 static bool run_dec_batch(aec_crn_handle* h, const Bufs& bf, int64_t F, hipStream_t st, aec_status* s) {
     *s = AEC_OK;
-    const char* v = getenv("AEC_CRN_BATCH_DEC");
-    const int mode = v ? atoi(v) : 1;
+    const int mode = AEC_MODE_KNOB("AEC_CRN_BATCH_DEC", 1);
     if (mode == 0) return false;
     bool ok = sizeof(T) == 2 && h->es == 2 && h->L >= 4;
     crn::DecBatchArgs da{};
@@ -1181,9 +1174,8 @@ static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int
     mark(h, st);
     // bf16: the mask level runs inside the back kernel (no f32 mask round trip) unless the
     // caller wants the mask itself (AEC_CRN_BACK_MASK=0: the row GEMM, A/B and bit-equality)
-    const char* bm_env = getenv("AEC_CRN_BACK_MASK");
     const Packed& pm = h->decf[h->L - 1];
-    const bool mask_in_back = sizeof(T) == 2 && !(bm_env && atoi(bm_env) == 0) && pm.w && !mask_out &&
+    const bool mask_in_back = sizeof(T) == 2 && AEC_MODE_KNOB("AEC_CRN_BACK_MASK", 1) != 0 && pm.w && !mask_out &&
                               (out || spec) && pm.N == 4 && pm.kpad <= 128 && pm.kpad % 32 == 0 && pm.act != 1;
     {
         // decoder levels cl = L .. 4 as row GEMMs, cl = 3, 2 fused when they fit, then the mask
@@ -1226,6 +1218,10 @@ static aec_status run(aec_crn_handle* h, const float* mic, const float* far, int
 struct StreamState {
     int32_t B = 0;
     int64_t k = 0;                       // hops consumed since open / reset-all
+    // per-hop launch mode of this handle's streams: 0 direct launches, 1 hipGraph replay
+    // (AEC_CRN_GRAPH read at stream_open, aec_crn_stream_set_graph afterwards); hops run each way
+    int graph_mode = 0;
+    int64_t graph_replays = 0, direct_hops = 0;
     std::vector<void*> allocs;
     void* x0 = nullptr;
     std::vector<void*> cat;
@@ -1476,8 +1472,7 @@ static bool stream_dec_ok(const aec_crn_handle* h) {
     // levels 0-2), bit 1 fused back (decoder cl = 3..1 + mask + irFFT), bit 2 encoder level 3 in the
     // front, bit 3 decoder cl = 4 (MX) in the back, bit 4 encoder level 4 (MX) in the front; the MX
     // folds (bits 3, 4) are further limited to streams <= CUs at stream_open
-    const char* v = getenv("AEC_CRN_STREAM_FUSE");
-    if (v && !(atoi(v) & 2)) return false;
+    if (!(AEC_MODE_KNOB("AEC_CRN_STREAM_FUSE", 31) & 2)) return false;
     const int* ch = h->cfg.conv_channels;
     const int caps[3] = {crn::kStreamDecChunks0, crn::kStreamDecChunks1, crn::kStreamDecChunks2};
     for (int l = 0; l < 3; ++l) {
@@ -1497,8 +1492,7 @@ static bool stream_dec_ok(const aec_crn_handle* h) {
 // fused-parity MX GEMM at net_conf's shape (16 input bins x 256 channels -> 2 x 64 columns, K = 768)
 // reading cat[4]'s shadow, split into 1 or 2 K slices
 static bool stream_dec_mx_ok(const aec_crn_handle* h) {
-    const char* v = getenv("AEC_CRN_STREAM_FUSE");
-    if (v && !(atoi(v) & 8)) return false;
+    if (!(AEC_MODE_KNOB("AEC_CRN_STREAM_FUSE", 31) & 8)) return false;
     if (h->L < 5 || !h->ss) return false;
     const int* ch = h->cfg.conv_channels;
     const Packed& pk = h->decf[h->L - 4];
@@ -1511,8 +1505,7 @@ static bool stream_dec_mx_ok(const aec_crn_handle* h) {
 // MX GEMM at net_conf's shape (8 output bins x 256 channels, K = 5 taps x 128, one K slice) on level
 // 3's shadow, its output with a shadow for level 5
 static bool stream_enc_mx_ok(const aec_crn_handle* h) {
-    const char* v = getenv("AEC_CRN_STREAM_FUSE");
-    if (v && !(atoi(v) & 16)) return false;
+    if (!(AEC_MODE_KNOB("AEC_CRN_STREAM_FUSE", 31) & 16)) return false;
     if (h->L < 6 || !h->ss) return false;
     const int* ch = h->cfg.conv_channels;
     const Packed& pk = h->enc[4];
@@ -1526,8 +1519,8 @@ static bool stream_enc_mx_ok(const aec_crn_handle* h) {
 // of 16 bins x 16 channels, K <= 160, no MX shadow on the output
 static int stream_enc_levels(const aec_crn_handle* h) {
     if (h->es != 2) return 0;
-    const char* v = getenv("AEC_CRN_STREAM_FUSE");
-    if (v && !(atoi(v) & 1)) return 0;
+    const int fuse = AEC_MODE_KNOB("AEC_CRN_STREAM_FUSE", 31);
+    if (!(fuse & 1)) return 0;
     const int* ch = h->cfg.conv_channels;
     int n = 0;
     // levels 0-2 together, at net_conf's shapes (crn_stream_enc_kernel's compile-time chunk counts)
@@ -1542,7 +1535,7 @@ static int stream_enc_levels(const aec_crn_handle* h) {
     }
     if (n < 3) return 0;
     // level 3 (16 x 128 from the 32 x 64 map; its MX shadow written in the kernel): AEC_CRN_STREAM_FUSE bit 2
-    if (n == 3 && h->L > 4 && (!v || (atoi(v) & 4))) {
+    if (n == 3 && h->L > 4 && (fuse & 4)) {
         const Packed& pk = h->enc[3];
         const int nc = (pk.K + 31) / 32;
         if (!pk.wq && pk.act == 1 && pk.N == 128 && ch[3] == 64 && ch[4] == 128 && nc == crn::kStreamEncChunks3 &&
@@ -1579,7 +1572,7 @@ static aec_status stream_launches(aec_crn_handle* h, int par, const StreamIo& io
         ss.front_node[par] = last_node(st);
         ss.enc_args[par] = ea;
         // AEC_CRN_ENC_MX_RERUN=1 (debugging only): the level-4 GEMM runs after the fused front anyway
-        static const bool rerun = [] { const char* v = getenv("AEC_CRN_ENC_MX_RERUN"); return v && atoi(v); }();
+        static const bool rerun = AEC_AB_KNOB("AEC_CRN_ENC_MX_RERUN", 0) != 0;
         first = ss.enc_nlev + (ss.enc_mx && !rerun ? 1 : 0);
     } else {
         crn::StreamFrontArgs fa{prev_mic, io.mic, prev_far, io.far, h->d_tab, ss.x0, B};
@@ -1717,8 +1710,8 @@ aec_status aec_crn_create(const aec_crn_config* cfg, const float* params, size_t
     aec::DevTables tab;
     aec::build_dev_tables(tab);
     if (hipMemcpy(h->d_tab, &tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess) return bail(AEC_ERR_HIP);
-    if (const char* v = getenv("AEC_CRN_PERSIST")) h->persist = atoi(v) != 0;
-    if (const char* v = getenv("AEC_CRN_MX8_SHADOW")) h->mx8_shadow = atoi(v) != 0;
+    h->persist = AEC_MODE_KNOB("AEC_CRN_PERSIST", h->persist) != 0;
+    h->mx8_shadow = AEC_MODE_KNOB("AEC_CRN_MX8_SHADOW", h->mx8_shadow) != 0;
     if (hipDeviceGetAttribute(&h->num_cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) h->num_cus = 0;
     if (h->es == 2 && crn::persist_supported(h->H, h->CELLS, h->S, h->num_cus)) {
         // team arrival counters + error word, and a pinned copy of the error word
@@ -1731,7 +1724,7 @@ aec_status aec_crn_create(const aec_crn_config* cfg, const float* params, size_t
     h->enc.assign(h->L, Packed{});
     h->dec.assign(2 * h->L, Packed{});
     h->decf.assign(h->L, Packed{});
-    if (const char* m = std::getenv("CRN_DEC_FUSE")) h->dec_fuse_max = std::atoi(m);
+    h->dec_fuse_max = AEC_AB_KNOB("CRN_DEC_FUSE", h->dec_fuse_max);
     h->lih.assign(h->nrnn, Packed{});
     h->lcat.assign(h->nrnn, Packed{});
     h->lhh.assign(h->nrnn, Packed{});
@@ -1902,8 +1895,7 @@ aec_status aec_crn_stream_open(aec_crn_handle* h, int32_t B) {
     }
     // dtype 2, NavieComplexLSTM: the recurrence runs as lstm_step_mx8_kernel (AEC_CRN_STEP_MX=0: the bf16
     // step + combine, A/B only)
-    const char* step_mx_env = getenv("AEC_CRN_STEP_MX");
-    const int step_mx = step_mx_env ? atoi(step_mx_env) : 1;
+    const int step_mx = AEC_MODE_KNOB("AEC_CRN_STEP_MX", 1);
     ss.mx_step = step_mx != 0 && h->mx8 && C * S == 4 && h->nrnn > 0 && h->lcat[0].wq != nullptr;
     if (ss.mx_step && h->nrnn > 2) {
         CRN_TRY(h, alloc(&ss.xnb, (size_t)B * S * H * es));
@@ -1959,6 +1951,40 @@ aec_status aec_crn_stream_open(aec_crn_handle* h, int32_t B) {
     CRN_TRY(h, hipStreamCreateWithFlags(&ss.cap, hipStreamNonBlocking));
     CRN_TRY(h, hipDeviceSynchronize());
     ss.k = 0;
+    ss.graph_mode = AEC_MODE_KNOB("AEC_CRN_GRAPH", 0) != 0;
+    return AEC_OK;
+}
+
+static void stream_drop_graphs(StreamState& ss) {
+    for (int p = 0; p < 2; ++p) {
+        if (ss.graph[p]) (void)hipGraphExecDestroy(ss.graph[p]);
+        if (ss.gsrc[p]) (void)hipGraphDestroy(ss.gsrc[p]);
+        ss.graph[p] = nullptr;
+        ss.gsrc[p] = nullptr;
+        ss.front_node[p] = ss.back_node[p] = nullptr;
+    }
+}
+
+aec_status aec_crn_stream_set_graph(aec_crn_handle* h, int32_t mode) {
+    if (!h || !h->ss || mode < 0 || mode > 1) return AEC_ERR_INVALID_ARG;
+    aec::DeviceGuard dg(h->device);
+    if (dg.err != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
+    StreamState& ss = *h->ss;
+    if (ss.graph_mode != mode) {
+        // the instantiated graphs may still be running: they are destroyed after the device drains
+        CRN_TRY(h, hipDeviceSynchronize());
+        stream_drop_graphs(ss);
+        ss.graph_mode = mode;
+    }
+    return AEC_OK;
+}
+
+aec_status aec_crn_stream_stats(const aec_crn_handle* h, int32_t* graph_mode, int64_t* graph_replays,
+                                int64_t* direct_hops) {
+    if (!h || !h->ss) return AEC_ERR_INVALID_ARG;
+    if (graph_mode) *graph_mode = h->ss->graph_mode;
+    if (graph_replays) *graph_replays = h->ss->graph_replays;
+    if (direct_hops) *direct_hops = h->ss->direct_hops;
     return AEC_OK;
 }
 
@@ -2002,46 +2028,43 @@ aec_status aec_crn_stream_step(aec_crn_handle* h, const float* mic, const float*
     if (dg.err != hipSuccess) return crn_fail(h, AEC_ERR_HIP, "hipSetDevice failed");
     const int par = (int)(ss.k & 1);
     const StreamIo io{mic, far, ld_in, out, ld_out};
-    // direct launches by default: the hop's 7 kernels run back to back either way, but ~8 us pass
-    // between two replays of a graph, more than the direct launches' gaps (256 streams 0.1085 vs
-    // 0.1135 ms per hop, one stream 0.105 vs 0.113 ms synchronous; profiles/r05_notes.md r05x/r05y).
-    // AEC_CRN_GRAPH=1 captures the hop once per ring parity and replays it.
-    static const int use_graph = [] {
-        const char* v = getenv("AEC_CRN_GRAPH");
-        return v ? atoi(v) : 0;
-    }();
-    bool launched = false;
-    if (use_graph) {
+    // two per-hop modes, chosen per handle (aec_crn_stream_set_graph; AEC_CRN_GRAPH at stream_open):
+    // direct launches (default) or the hop's launches captured once per ring parity in a hipGraph
+    // and replayed.  The 7 kernels of a hop run back to back either way; ~8 us pass between two
+    // graph replays, more than the direct launches' gaps (profiles/r05_notes.md r05x/r05y).  A
+    // graph that cannot be captured or instantiated fails the call: no silent fallback.
+    if (ss.graph_mode) {
         if (!ss.graph[par]) {
-            // capture the ~26 launches of one frame once per ring parity; replay every hop
             hipGraph_t g = nullptr;
-            if (hipStreamBeginCapture(ss.cap, hipStreamCaptureModeThreadLocal) == hipSuccess) {
-                const aec_status s = h->es == 4 ? stream_launches<float>(h, par, io, ss.cap)
-                                                : stream_launches<bf16_t>(h, par, io, ss.cap);
-                const hipError_t e = hipStreamEndCapture(ss.cap, &g);
-                if (s == AEC_OK && e == hipSuccess && g && ss.front_node[par] && ss.back_node[par]) {
-                    if (hipGraphInstantiate(&ss.graph[par], g, nullptr, nullptr, 0) == hipSuccess) {
-                        ss.gsrc[par] = g;              // the node handles belong to it
-                        g = nullptr;
-                    } else {
-                        ss.graph[par] = nullptr;
-                    }
-                }
+            hipError_t e = hipStreamBeginCapture(ss.cap, hipStreamCaptureModeThreadLocal);
+            if (e != hipSuccess) return crn_fail(h, AEC_ERR_HIP, std::string("hipStreamBeginCapture: ") + hipGetErrorString(e));
+            const aec_status s = h->es == 4 ? stream_launches<float>(h, par, io, ss.cap)
+                                            : stream_launches<bf16_t>(h, par, io, ss.cap);
+            e = hipStreamEndCapture(ss.cap, &g);
+            (void)hipGetLastError();
+            std::string why;
+            if (s != AEC_OK) why = "a launch failed under capture: " + h->err;
+            else if (e != hipSuccess || !g) why = std::string("hipStreamEndCapture: ") + hipGetErrorString(e);
+            else if (!ss.front_node[par] || !ss.back_node[par]) why = "the front / back kernel nodes were not captured";
+            else if ((e = hipGraphInstantiate(&ss.graph[par], g, nullptr, nullptr, 0)) != hipSuccess)
+                why = std::string("hipGraphInstantiate: ") + hipGetErrorString(e);
+            if (!why.empty()) {
                 if (g) (void)hipGraphDestroy(g);
-                (void)hipGetLastError();
+                ss.graph[par] = nullptr;
+                ss.front_node[par] = ss.back_node[par] = nullptr;
+                return crn_fail(h, AEC_ERR_HIP, "graph mode: " + why);
             }
+            ss.gsrc[par] = g;                          // the node handles belong to it
         } else {
             const aec_status s = stream_set_io(h, par, io);
             if (s != AEC_OK) return s;
         }
-        if (ss.graph[par]) {
-            CRN_TRY(h, hipGraphLaunch(ss.graph[par], st));
-            launched = true;
-        }
-    }
-    if (!launched) {
+        CRN_TRY(h, hipGraphLaunch(ss.graph[par], st));
+        ss.graph_replays++;
+    } else {
         const aec_status s = h->es == 4 ? stream_launches<float>(h, par, io, st) : stream_launches<bf16_t>(h, par, io, st);
         if (s != AEC_OK) return s;
+        ss.direct_hops++;
     }
     ss.k++;
     return AEC_OK;

@@ -1064,14 +1064,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_rows_dma_kernel(RowSrc a, c
                                         smem + wave * (PF * 16 * FN * 16 * (int)sizeof(OutT)));
 }
 
-static int env_int(const char* name, int dflt) {
-    const char* v = getenv(name);
-    return v ? atoi(v) : dflt;
-}
-
 // tile order of the row / MX GEMMs (RowEpi::xcd_gm): CRN_GEMM_XCD
 static int gemm_xcd_gm() {
-    static const int g = env_int("CRN_GEMM_XCD", 0);
+    static const int g = AEC_AB_KNOB("CRN_GEMM_XCD", 0);
     return g;
 }
 
@@ -1104,15 +1099,15 @@ hipError_t launch_gemm_rows(const RowSrc& a, const T* bt, int64_t ldb, int nstag
     } while (0)
 #define CRN_GEMM_DMA_RB(WM, WN, FM, FN, NBUF, RB) CRN_GEMM_DMA_RBP(WM, WN, FM, FN, NBUF, RB, 0)
 #define CRN_GEMM_DMA(WM, WN, FM, FN, NBUF) CRN_GEMM_DMA_RB(WM, WN, FM, FN, NBUF, 128)
-    static const int dma = env_int("CRN_GEMM_DMA", 2);    // 0 = register-staged core, else NBUF
-    static const int big = env_int("CRN_GEMM_BIG", 0);    // 256x128 tiles (8 waves) for large M (measured slower)
-    static const int sq = env_int("CRN_GEMM_SQ", 1);      // 256x256 tiles (8 waves) when N % 256 == 0
-    static const int rb64 = env_int("CRN_GEMM_RB64", 0);  // 128x128 tiles with 64-B K slices, 4 buffers
-    static const int gmode = env_int("CRN_GEMM_MODE", 0);  // timing experiments only (results invalid unless 0)
+    static const int dma = AEC_AB_KNOB("CRN_GEMM_DMA", 2);    // 0 = register-staged core, else NBUF
+    static const int big = AEC_AB_KNOB("CRN_GEMM_BIG", 0);    // 256x128 tiles (8 waves) for large M (measured slower)
+    static const int sq = AEC_AB_KNOB("CRN_GEMM_SQ", 1);      // 256x256 tiles (8 waves) when N % 256 == 0
+    static const int rb64 = AEC_AB_KNOB("CRN_GEMM_RB64", 0);  // 128x128 tiles with 64-B K slices, 4 buffers
+    static const int gmode = AEC_AB_KNOB("CRN_GEMM_MODE", 0);  // timing experiments only (results invalid unless 0)
     // CRN_GEMM_PIPE: 0 = gemm_core_dma everywhere; 1 = pipelined core on the
     // 256x256 tiles; 2 = + transposed accumulators / packed epilogue there;
     // 3 = pipelined core + packed epilogue on the 128x128 / 128x64 DMA tiles too
-    static const int pipe = env_int("CRN_GEMM_PIPE", 3);
+    static const int pipe = AEC_AB_KNOB("CRN_GEMM_PIPE", 3);
     RowEpi ee = e;
     ee.mode = gmode;
     ee.xcd_gm = gemm_xcd_gm();
@@ -1666,7 +1661,7 @@ template <typename T>
 hipError_t launch_lstm_step(const StepArgs& a, int cells, int seqs, hipStream_t st) {
     // CRN_STEP_MODE (timing experiments only, results invalid unless 0): bit0 skip the
     // cell update, bit1 skip the recurrent GEMM, bit2 skip the Gx / c DMA
-    static const int step_mode = env_int("CRN_STEP_MODE", 0);
+    static const int step_mode = AEC_AB_KNOB("CRN_STEP_MODE", 0);
     if (a.H % 32 || (a.H * (int)sizeof(T)) % kStageBytes) return hipErrorInvalidValue;
 #define CRN_STEP(C, S_, SB_, NB_, RB_, NW_)                                                                            \
     do {                                                                                                          \
@@ -1686,7 +1681,7 @@ hipError_t launch_lstm_step(const StepArgs& a, int cells, int seqs, hipStream_t 
     // 3 = 16 streams, 2 buffers (3 blocks per CU, v2 only); 4 = 32 streams, 4 buffers of 64-B K
     // slices (2 blocks per CU, 3 slices in flight per block: slower, 37.8 vs 32.8 ms of LSTM per
     // 256 x 10 s batch — the step GEMM is not bound by the slices in flight)
-    static const int cfg = env_int("CRN_STEP_CFG", 1);
+    static const int cfg = AEC_AB_KNOB("CRN_STEP_CFG", 1);
     constexpr int NB0 = sizeof(T) == 2 ? 3 : 2;
     if ((a.H * (int)sizeof(T)) % 64) return hipErrorInvalidValue;
     if (cells == 2 && seqs == 2) {
@@ -1828,7 +1823,7 @@ hipError_t launch_lstm_combine(const T* y, T* dst, int64_t nframes, int H, int c
     const int64_t n = nframes * H;
     if (n <= 0) return hipSuccess;
     if (q8 && (H % 64 || (1 << dshift) % 32 || cells * seqs != 4)) return hipErrorInvalidValue;
-    const int vec = env_int("CRN_COMBINE_VEC", 1);             // read per call (tests compare both forms)
+    const int vec = AEC_MODE_KNOB("CRN_COMBINE_VEC", 1);             // read per call (tests compare both forms)
     if constexpr (sizeof(T) == 2) {
         if (vec && cells == 2 && seqs == 2 && H % 512 == 0 && dshift >= 5 && ldf % 8 == 0 && ldd % 8 == 0 &&
             ((reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0) {
@@ -2214,11 +2209,10 @@ hipError_t launch_lstm_step_mx8(const StepMxArgs& a, hipStream_t st) {
         const int nsb = (a.B + SB_ - 1) / SB_;                                                                    \
         hipLaunchKernelGGL(kern, dim3(a.H / 32, 2 * nsb), dim3(256), lds, st, a2);                                \
     } while (0)
-    static const int smode = env_int("CRN_MX_STEP_MODE", 0);
+    static const int smode = AEC_AB_KNOB("CRN_MX_STEP_MODE", 0);
     StepMxArgs a2 = a;
     a2.mode = smode;
-    const char* sreg_env = getenv("AEC_CRN_MX_SREG");  // read per launch (captured once per stream open)
-    const int sreg = sreg_env ? atoi(sreg_env) : 1;
+    const int sreg = AEC_MODE_KNOB("AEC_CRN_MX_SREG", 1);  // read per launch (captured once per stream open)
     if (a.H == 1024 && sreg)
         CRN_MXSTEP(kMxSB, 3, true);
     else

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "aec_knobs.h"
 #include "aec_tables.h"
 #include "crn_gemm.h"
 
@@ -362,8 +363,6 @@ bool persist_supported(int H, int cells, int seqs, int num_cus);
 // the team's rows in two halves whose phases alternate, so each half's cell
 // update and hand-off run under the other half's MFMAs
 hipError_t launch_lstm_persist(const PersistArgs& a, hipStream_t st);
-// the same recurrence with 8 waves per block (two per SIMD, crn_persist3.hip; AEC_CRN_PERSIST_WAVES=8)
-hipError_t launch_lstm_persist3(const PersistArgs& a, hipStream_t st);
 
 // tile width the host must pad the weight rows (N) to for a GEMM of N columns
 inline int gemm_bn(int N) { return N <= 16 ? 16 : N <= 32 ? 32 : N <= 64 ? 64 : 128; }

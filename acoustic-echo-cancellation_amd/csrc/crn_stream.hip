@@ -761,7 +761,7 @@ static hipError_t launch_enc_batch_fr(const EncBatchArgs& a, hipStream_t st) {
 hipError_t launch_enc_batch(const EncBatchArgs& a, hipStream_t st) {
     if (a.F <= 0) return hipSuccess;
     if (!enc_batch_ok(a)) return hipErrorInvalidValue;
-    static const int fr = [] { const char* v = getenv("AEC_CRN_ENC_FR"); return v ? atoi(v) : 4; }();   // A/B only
+    static const int fr = AEC_AB_KNOB("AEC_CRN_ENC_FR", 4);
     switch (fr) {
         case 2: return launch_enc_batch_fr<2>(a, st);
         case 8: return launch_enc_batch_fr<8>(a, st);

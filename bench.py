@@ -115,6 +115,35 @@ def parse():
     return ap.parse_args()
 
 
+# knobs that only an A/B build reads (csrc/aec_knobs.h AEC_AB_KNOB): timing experiments and
+# work-skipping switches.  The product library ignores them; a bench line is refused when one is
+# set, so that no driver line can be read as having run a timing-only mode.
+AB_ONLY_KNOBS = ('AEC_MOM_CFG', 'AEC_MOM_GRID', 'AEC_GRU_MODE', 'AEC_NLMS_PRIO', 'AEC_NLMS_ERB', 'AEC_FUSED_MODE',
+                 'AEC_CRN_ENC_FR', 'AEC_CRN_SPLITK', 'CRN_PERSIST_RA', 'AEC_CRN_ENC_MX_RERUN', 'CRN_DEC_FUSE',
+                 'CRN_GEMM_XCD', 'CRN_GEMM_DMA', 'CRN_GEMM_BIG', 'CRN_GEMM_SQ', 'CRN_GEMM_RB64', 'CRN_GEMM_MODE',
+                 'CRN_GEMM_PIPE', 'CRN_STEP_MODE', 'CRN_STEP_CFG', 'CRN_MX_STEP_MODE', 'AEC_CRN_PERSIST_WAVES')
+# test hooks (fault injection) of the product library: never in a bench run
+TEST_ONLY_KNOBS = ('AEC_CRN_PERSIST_STALL', 'AEC_CRN_SPIN_LIMIT')
+
+
+def knob_provenance():
+    """Every AEC_* / CRN_* environment variable set, and the library's build
+    description (aec_build_info); raises when a timing-only / test-only knob
+    is set or the loaded library is an A/B build."""
+    from aec_amd import _lib
+    env = {k: v for k, v in sorted(os.environ.items()) if k.startswith(('AEC_', 'CRN_'))}
+    bad = [k for k in env if k in AB_ONLY_KNOBS or k in TEST_ONLY_KNOBS]
+    if bad:
+        raise SystemExit(f'bench.py: timing-only / test-only knobs set {bad}: refusing to produce a bench line')
+    info = _lib.build_info()
+    if info['ab_knobs']:
+        raise SystemExit(f'bench.py: {_lib.LIB_PATH} is an A/B build ({info["text"]}): refusing')
+    unknown = [k for k in env if k not in info['mode_knobs'] and k not in ('AEC_HIP_LIB', 'AEC_BENCH_BACKEND')]
+    return dict(env=env, library=os.path.relpath(_lib.LIB_PATH, REPO), build_info=info['text'],
+                defaults=not any(k in info['mode_knobs'] for k in env) and 'AEC_HIP_LIB' not in env,
+                unknown_names=unknown)
+
+
 def cu_masked_stream(dev, ncu):
     """A HIP stream whose kernels run on `ncu` CUs only (every (n_cu / ncu)-th), wrapped for torch."""
     import ctypes
@@ -527,15 +556,16 @@ def c5_erle(net, dev, conf, nlms, streams=2, n=160000):
 
 def run_c5_stream(dev, B=256, hops=200, dtype='fp8', world=1, with_cpu=False, sweep=(1024, 4096),
                   cpu_seconds=10.0, with_erle=False):
-    """BASELINE config 5: the per-hop step of the DCCRN (7 launches; AEC_CRN_GRAPH=1 replays them as a hipGraph)
+    """BASELINE config 5: the per-hop step of the DCCRN (7 launches; timed launched directly and
+    replayed from its hipGraphs)
     (MX-fp8 LSTM input projections, recurrence and wide conv layers) fed by the FD-NLMS,
     B concurrent streams per GPU, one 256-sample hop per stream per step
     (aec_crn_stream_step).  With world > 1 every rank steps its own B streams
     (no data-path collective); the timed region is bracketed by barriers and
     the time is the max over ranks.  Input: one random hop pair per stream,
     resident in the same device buffers every step (the graph's input nodes
-    keep their pointers; parity of the step on real audio is
-    tests/test_gpu_bench_shapes.py)."""
+    keep their pointers; parity of the step on real audio, and graph replay ==
+    direct launches bit for bit, is tests/test_gpu_bench_shapes.py)."""
     import torch
     import torch.distributed as dist
     import aec_amd
@@ -544,8 +574,8 @@ def run_c5_stream(dev, B=256, hops=200, dtype='fp8', world=1, with_cpu=False, sw
     conf = dict(aec_amd.net_conf)
     net = aec_amd.dccrn2.DCCRN(conf, dtype=dtype, nlms=aec_amd.nlms_conf).eval().to(dev)
 
-    def time_hops(bb, nhops, barrier):
-        net.stream_open(bb, device=dev)
+    def time_hops(bb, nhops, barrier, graph=False):
+        net.stream_open(bb, device=dev, graph=graph)
         g = torch.Generator(device=dev).manual_seed(5)
         mic = 0.1 * torch.randn(bb, 256, device=dev, generator=g)
         far = 0.1 * torch.randn(bb, 256, device=dev, generator=g)
@@ -572,6 +602,13 @@ def run_c5_stream(dev, B=256, hops=200, dtype='fp8', world=1, with_cpu=False, sw
         return shard.max_over_ranks(el) / nhops if barrier else el / nhops
 
     dt = time_hops(B, hops, True)
+    # BASELINE configs[4] names the hipGraph-captured per-hop step: the same hops replayed from the
+    # per-parity graphs (bit-identical, tests/test_gpu_bench_shapes.py), timed the same way; the
+    # library's counters prove every timed hop was a replay
+    dt_graph = time_hops(B, hops, True, graph=True)
+    gstats = net.stream_stats()
+    if gstats['graph_mode'] != 1 or gstats['direct_hops'] != 0 or gstats['graph_replays'] < hops:
+        raise RuntimeError(f'C5 graph mode did not replay every hop: {gstats}')
     streams_sweep = None
     lat_b1 = None
     if world == 1:
@@ -615,6 +652,10 @@ def run_c5_stream(dev, B=256, hops=200, dtype='fp8', world=1, with_cpu=False, sw
                         if dtype == 'fp8' else '') + ') -> iSTFT step; input = one random hop pair per stream, '
                         'resident in the same device buffers every step',
                dtype=dtype, n_gpus=world, streams=B * world, hops=hops, ms_per_hop=round(dt * 1e3, 4),
+               launch_mode='direct launches (the library default; ms_per_hop)',
+               graph_ms_per_hop=round(dt_graph * 1e3, 4),
+               graph_frames_per_s_per_gpu=round(B / dt_graph, 1),
+               graph_stats=dict(gstats, note='aec_crn_stream_stats after the graph-mode timing (warm-up + timed hops)'),
                frames_per_s=round(world * B / dt, 1), frames_per_s_per_gpu=round(B / dt, 1),
                rtf=round(dt / 0.016, 5), roofline=c5_roofline(conf, B, dt * 1e3, pmc),
                latency_ms_per_hop_b1=lat_b1['ms_per_hop_synchronous_median'] if lat_b1 else None,
@@ -739,6 +780,7 @@ def main_crn(args):
     B = args.streams
     n = int(round(args.seconds * 16000))
     import aec_amd
+    prov = knob_provenance()
     nl = aec_amd.nlms_conf if args.crn_nlms else None
     r = run_crn(args, dev, rank, world, args.crn_dtype, args.steps, args.warmup, B, n, not args.no_cpu, nl)
     if rank == 0:
@@ -759,6 +801,7 @@ def main_crn(args):
         }
         line.update({k: r[k] for k in ('rtf_batch1', 'stage_ms_per_step', 'roofline', 'pipeline_roofline',
                                        'erle', 'cpu_baseline')})
+        line['knobs'] = prov
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -778,6 +821,7 @@ def main():
     dev = torch.device('cuda', local)
     import aec_amd
     from aec_amd import shard, synth
+    prov = knob_provenance()
 
     B = args.streams
     n = int(round(args.seconds * 16000))
@@ -815,14 +859,18 @@ def main():
     if args.lookahead:
         side = cu_masked_stream(dev, args.lookahead_cus) if args.lookahead_cus > 0 else torch.cuda.Stream(dev)
 
+    tokens = {}                                  # step index -> look-ahead token of its batch
+
     def step():
-        k = kstep[0] % inflight
+        n_ = kstep[0]
+        k = n_ % inflight
         kstep[0] += 1
         if side is not None:
             with torch.cuda.stream(side):
-                nets[(k + args.lookahead) % inflight].prepare_ragged(mic, ref, near, lens)
+                tokens[n_ + args.lookahead] = nets[(k + args.lookahead) % inflight].prepare_ragged(mic, ref, near,
+                                                                                                  lens)
         with torch.cuda.stream(streams[k]):
-            return nets[k].forward_ragged(mic, ref, near, erb, lens)
+            return nets[k].forward_ragged(mic, ref, near, erb, lens, lookahead=tokens.pop(n_, None))
 
     with torch.no_grad():
         for _ in range(2):
@@ -956,8 +1004,8 @@ def main():
     c4 = None
     if world == 1 and not args.no_c3:
         # C4's per-GPU leg: FD-NLMS + DCCRN post-filter (bf16) on one GPU's shard of utterances
-        c4 = run_crn(args, dev, rank, world, 'bf16', args.c3_steps, 2, 256, 160000, False, aec_amd.nlms_conf,
-                     with_erle=not args.no_cpu)
+        c4 = run_crn(args, dev, rank, world, 'bf16', args.c3_steps, 2, 256, 160000, not args.no_cpu,
+                     aec_amd.nlms_conf, with_erle=not args.no_cpu)
         c4 = dict(workload='C4 (BASELINE configs[3]) per-GPU leg: end-to-end STFT -> FD-NLMS (4 taps) -> DCCRN v2 '
                            'post-filter (dccrn2.py, configs.net_conf, bf16 MFMA) -> iSTFT on one GPU\'s shard of 256 '
                            'concurrent 10 s 16 kHz utterances (the 8-GPU job runs this per rank, no data-path '
@@ -965,7 +1013,7 @@ def main():
                   dtype='bf16', steps=args.c3_steps, batches_in_flight=c4['batches_in_flight'],
                   frames_per_s=c4['value'], ms_per_step=c4['ms_per_step'],
                   stage_ms_per_step=c4['stage_ms_per_step'], roofline=c4['roofline'],
-                  pipeline_roofline=c4['pipeline_roofline'], erle=c4['erle'])
+                  pipeline_roofline=c4['pipeline_roofline'], erle=c4['erle'], cpu_baseline=c4['cpu_baseline'])
     c5s = None
     if not args.no_c3:
         # C5 is quoted on 8 GPUs: the per-hop step runs on every rank (streams sharded, weak scaling)
@@ -1010,7 +1058,10 @@ def main():
         line = {
             'metric': '16kHz frames/sec/GPU (batched AEC) + RTF@batch=1; ERLE delta vs reference',
             'value': round(value, 1), 'unit': 'frames/s', 'n_gpus': world, 'steps': args.steps,
-            'warmup': args.warmup, 'warmup_steps_run': warm_steps, 'ms_per_step': round(ms_step, 4), 'higher_is_better': True,
+            'warmup': args.warmup, 'warmup_requested': args.warmup, 'warmup_steps_run': warm_steps,
+            'warmup_note': f'warmup = the --warmup argument (driver contract); {warm_steps} untimed steps ran '
+                           f'(floor {MIN_WARM_STEPS}: the clock ramp)',
+            'ms_per_step': round(ms_step, 4), 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
             'config': {'workload': WORKLOAD[args.pipeline],
                        'streams_per_gpu': B, 'samples_per_stream': n, 'frames_per_stream': T,
@@ -1041,6 +1092,7 @@ def main():
             'c4_nlms_crn_bf16_per_gpu': c4,
             'c5_stream_fp8': c5s,
             'train_step': tr,
+            'knobs': prov,
         }
         if sweep:
             line['batch_sweep_frames_per_s'] = sweep

@@ -128,9 +128,13 @@ aec_status aec_crn_stft(aec_crn_handle* h, const float* x, const int64_t* length
 /* Streaming (serving): one 256-sample hop per stream per call, the per-frame
  * loop of the same network (the DCCRN has no utterance-global statistic, so a
  * streamed utterance equals the batch result: frame t needs hops t-1 and t,
- * ConvSTFT framing dccrn.py:45-52).  The launches of one frame go out
- * directly (AEC_CRN_GRAPH=1: captured once in a hipGraph per ring parity and
- * replayed; the replays measured slower): 7 for the fp8 step at net_conf (fused front = STFT, FD-NLMS and
+ * ConvSTFT framing dccrn.py:45-52).  Per handle, the launches of one frame
+ * go out directly (mode 0, the default) or are captured once per ring parity
+ * in a hipGraph and replayed (mode 1: aec_crn_stream_set_graph, or
+ * AEC_CRN_GRAPH=1 in the environment when aec_crn_stream_open runs); both
+ * modes give bit-identical outputs, and a graph that cannot be captured or
+ * instantiated fails the step with AEC_ERR_HIP (no silent fallback).
+ * 7 launches for the fp8 step at net_conf (fused front = STFT, FD-NLMS and
  * encoder levels 0-4; one MX conv level; two LSTM layer steps; two MX conv
  * levels; fused back = decoder levels 4-1, mask, iSTFT).  The fp8 step folds
  * encoder / decoder level 4 into the fused kernels only while B <= the
@@ -150,6 +154,15 @@ aec_status aec_crn_stream_open(aec_crn_handle* h, int32_t B);
 aec_status aec_crn_stream_reset(aec_crn_handle* h, int32_t b, void* stream);
 aec_status aec_crn_stream_step(aec_crn_handle* h, const float* mic, const float* far, int64_t ld_in, float* out,
                                int64_t ld_out, void* stream);
+/* Per-hop launch mode of the open streams: 0 = direct launches, 1 = hipGraph
+ * replay (the per-frame step of BASELINE config 5, dccrn2.py:118-218 per hop).
+ * Switching synchronises the device and drops the captured graphs; the stream
+ * state is kept. */
+aec_status aec_crn_stream_set_graph(aec_crn_handle* h, int32_t mode);
+/* The mode in effect and how many hops ran as graph replays / direct launches
+ * since aec_crn_stream_open (any pointer may be NULL). */
+aec_status aec_crn_stream_stats(const aec_crn_handle* h, int32_t* graph_mode, int64_t* graph_replays,
+                                int64_t* direct_hops);
 
 /* Kernel timing (HIP events on `stream`): ms[0..4] = front, encoder,
  * lstm (input projection + steps + combine), decoder, back; summed over the

@@ -111,21 +111,30 @@ aec_status aec_process_siglens(aec_handle* h, const float* mic, const float* ref
 /* Optional look-ahead (serving): queue the per-stream normaliser pass of a batch
  * (c = mean/std of each signal over its length, ERB.py:254-256 — a full read of
  * every signal before the first frame can be normalised) on `stream`, ahead of
- * the aec_process / aec_process_siglens call that will take the batch.  That
- * call (on any stream) waits for it on the device instead of running the pass
- * itself; it matches on the signal pointers, ld, B and the lengths.  At most two
- * batches may be pending per handle (AEC_ERR_INVALID_ARG beyond); a process call
- * whose batch does not match the oldest pending one drops every pending one and
- * runs the pass itself.  The signals must stay unchanged until that call.
- * Outputs are bit-identical with and without the look-ahead (the same kernels).
- * No reference counterpart: the reference computes the normaliser inside
- * Little_net.forward (ERB.py:254-256).
- *   lengths3 : host [B][3] int64, as aec_process_siglens (lengths may be NULL-free
- *              [B] via aec_prepare with one length per stream) */
+ * the aec_process_prepared call that will take the batch.  *token (non-NULL)
+ * receives the look-ahead's identity; only aec_process_prepared with that token
+ * consumes it (on any stream: it waits for the pass on the device instead of
+ * running it).  aec_process / aec_process_siglens never consume a look-ahead, so
+ * a buffer refilled at the same address is never normalised with stale
+ * constants by accident.  At most two look-aheads may be pending per handle
+ * (AEC_ERR_INVALID_ARG beyond).  The caller guarantees that the signals are
+ * unchanged between the two calls (the pass reads them when it runs on
+ * `stream`).  Outputs are bit-identical with and without the look-ahead (the
+ * same kernels).  No reference counterpart: the reference computes the
+ * normaliser inside Little_net.forward (ERB.py:254-256).
+ *   lengths3 : host [B][3] int64, as aec_process_siglens (aec_prepare: one
+ *              length per stream, [B]) */
 aec_status aec_prepare_siglens(aec_handle* h, const float* mic, const float* ref, const float* near,
-                               const int64_t* lengths3, int32_t B, int64_t ld, void* stream);
+                               const int64_t* lengths3, int32_t B, int64_t ld, void* stream, uint64_t* token);
 aec_status aec_prepare(aec_handle* h, const float* mic, const float* ref, const float* near,
-                       const int64_t* lengths, int32_t B, int64_t ld, void* stream);
+                       const int64_t* lengths, int32_t B, int64_t ld, void* stream, uint64_t* token);
+/* aec_process_siglens taking the look-ahead `token` names: the pending
+ * look-aheads queued before it are dropped, and the call fails
+ * (AEC_ERR_INVALID_ARG, nothing launched) when the token is not pending or was
+ * prepared for other signal pointers, ld, B or lengths. */
+aec_status aec_process_prepared(aec_handle* h, uint64_t token, const float* mic, const float* ref, const float* near,
+                                const int64_t* lengths3, int32_t B, int64_t ld, float* out, int64_t ld_out,
+                                float* loss, void* stream);
 
 /* Streaming (serving): the reference's per-frame loop (Little_net.forward,
  * ERB.py:252-334) advanced by one 256-sample hop per stream per call, as ONE
@@ -221,6 +230,12 @@ int64_t aec_num_frames(int64_t n_samples);   /* n//256 + 1 */
 int64_t aec_out_len(int64_t n_samples);      /* 256*(n//256) */
 
 const char* aec_last_error(const aec_handle* h);
+
+/* Build description of this library (no reference counterpart: bench and test
+ * provenance).  "arch=gfx950 ab_knobs=off mode_knobs=<names>": ab_knobs=on marks
+ * an A/B build (-DAEC_AB_KNOBS) that reads timing-only / work-skipping knobs;
+ * mode_knobs lists the environment variables that select tested modes. */
+const char* aec_build_info(void);
 void aec_destroy(aec_handle* h);
 
 #ifdef __cplusplus

@@ -9,10 +9,13 @@ and the MX layer step's config coverage (include/aec_crn.h).
   pinned to the float64 oracle by tests/test_crn_oracle.py, which the
   reference goldens pin): out_wav relative RMS <= BF16_WAV_TOL and ERLE within
   ERLE_DB dB.
-* C5's per-GPU unit (`c5_stream_fp8`): the hipGraph per-hop NLMS -> DCCRN fp8
-  step at 256 streams (8 MX stream blocks, 512 blocks per layer step) over
-  201 hops: every stream within STREAM_VS_BATCH_TOL of the fp8 batch forward of the
-  same signal, three within FP8_WAV_TOL of the reference op mix.
+* C5's per-GPU unit (`c5_stream_fp8`): the per-hop NLMS -> DCCRN fp8 step
+  at 256 streams (8 MX stream blocks, 512 blocks per layer step) over 201
+  hops, launched directly (the default): every stream within
+  STREAM_VS_BATCH_TOL of the fp8 batch forward of the same signal, three
+  within FP8_WAV_TOL of the reference op mix; and the same step replayed from
+  its hipGraphs (BASELINE configs[4]'s named mode), bit-equal to the direct
+  launches, with the library's hop counters proving the replays ran.
 * The MX layer step (lstm_step_mx8_kernel) with rnn_layers = 3 (a middle layer
   reads one xn set and writes the other) against the bf16 step + combine
   (AEC_CRN_STEP_MX=0), and a config whose layout the MX step cannot take
@@ -126,12 +129,47 @@ def test_c5_fp8_stream_256_streams():
     margin('C5 fp8 256 streams: |ERLE delta| dB vs reference op mix', max(abs(d) for d in d_erle), ERLE_DB)
 
 
-def _stream_run(net, M, F, B, nh):
-    net.stream_open(B)
+def _stream_run(net, M, F, B, nh, graph=None):
+    net.stream_open(B, graph=graph)
     with torch.no_grad():
         outs = [net.stream_step(M[:, 256 * k:256 * (k + 1)], F[:, 256 * k:256 * (k + 1)]).clone() for k in range(nh)]
     torch.cuda.synchronize()
     return torch.cat(outs[1:], dim=1).cpu().numpy()
+
+
+def test_c5_fp8_stream_graph_replay_bit_exact():
+    """BASELINE configs[4]'s hipGraph-captured per-frame step: the same 256
+    streams x 201 hops with every hop replayed from the captured graphs
+    (aec_crn_stream_set_graph(h, 1)) equal the direct launches bit for bit,
+    and the library reports that every hop really ran as a graph replay (a
+    failed capture would fail the step, not fall back)."""
+    net, conf, w = build('fp8')
+    B, nh = 256, 201
+    n = 256 * (nh - 1)
+    g = torch.Generator(device='cuda:0').manual_seed(77)
+    M = torch.zeros(B, 256 * nh, device='cuda:0')
+    F = torch.zeros_like(M)
+    F[:, :n] = 0.1 * torch.randn(B, n, device='cuda:0', generator=g)
+    M[:, :n] = 0.5 * F[:, :n] + 0.02 * torch.randn(B, n, device='cuda:0', generator=g)
+    direct = _stream_run(net, M, F, B, nh, graph=False)
+    st = net.stream_stats()
+    assert st == dict(graph_mode=0, graph_replays=0, direct_hops=nh)
+    graph = _stream_run(net, M, F, B, nh, graph=True)
+    st = net.stream_stats()
+    assert st == dict(graph_mode=1, graph_replays=nh, direct_hops=0)
+    assert np.isfinite(graph).all() and np.abs(graph).max() > 0
+    assert np.array_equal(graph, direct)
+    # switching mode mid-stream keeps the state: hops alternate between the modes
+    net.stream_open(B, graph=False)
+    outs = []
+    with torch.no_grad():
+        for k in range(nh):
+            net._stream[0].stream_set_graph(k % 2)
+            outs.append(net.stream_step(M[:, 256 * k:256 * (k + 1)], F[:, 256 * k:256 * (k + 1)]).clone())
+    torch.cuda.synchronize()
+    st = net.stream_stats()
+    assert st['graph_replays'] == nh // 2 and st['direct_hops'] == nh - nh // 2
+    assert np.array_equal(torch.cat(outs[1:], dim=1).cpu().numpy(), direct)
 
 
 def _stream_inputs(B, n, seed0):

@@ -172,10 +172,13 @@ def test_f32_long_utterance_against_oracle():
     assert rel(spec[0].cpu().numpy(), r['out_spec']) <= F32_TOL
 
 
+@pytest.mark.parametrize('graph', [False, True], ids=['direct', 'graph'])
 @pytest.mark.parametrize('dtype', ['f32', 'bf16', 'fp8'])
-def test_streaming_equals_batch(dtype):
-    """aec_crn_stream_step (hipGraph-replayed per-frame loop) reproduces the
-    batch forward hop by hop, with per-stream reset mid-run.  The GEMMs, LSTM
+def test_streaming_equals_batch(dtype, graph):
+    """aec_crn_stream_step (the per-frame loop; its launches direct or
+    replayed from the per-parity hipGraphs, whose input / output nodes are
+    re-pointed at each call's buffers) reproduces the batch forward hop by
+    hop, with per-stream reset mid-run.  The GEMMs, LSTM
     step and combine are the same kernels; the streaming front / back kernels
     restate the batch transforms, and the compiler contracts a few of their
     multiply-adds differently, so f32 agrees to ~1e-6 relative (observed max
@@ -197,12 +200,14 @@ def test_streaming_equals_batch(dtype):
     far = torch.zeros_like(mic)
     mic[:, :L] = pad(0)
     far[:, :L] = pad(1)
-    net.stream_open(B)
+    net.stream_open(B, graph=graph)
     outs = []
     with torch.no_grad():
         for k in range(nh):
             outs.append(net.stream_step(mic[:, 256 * k:256 * (k + 1)], far[:, 256 * k:256 * (k + 1)]).clone())
     torch.cuda.synchronize()
+    assert net.stream_stats() == dict(graph_mode=int(graph), graph_replays=nh if graph else 0,
+                                      direct_hops=0 if graph else nh)
     got = torch.cat(outs[1:], dim=1)                    # step k emits hop k-1
     tol = {'f32': 1e-5, 'bf16': 1e-2, 'fp8': 2e-2}[dtype]
     for b, n in enumerate(lens):
@@ -299,35 +304,6 @@ def test_persistent_recurrence_matches_step_kernel(monkeypatch):
     assert np.array_equal(outs['1'][1], outs['1'][0][:3])   # batch composition stays bit-exact
 
 
-def test_persistent_recurrence_8_waves_bit_exact(monkeypatch):
-    """lstm_persist3_kernel (crn_persist3.hip: 8 waves per block, two per
-    SIMD, each wave 8 units x 4 gates x one K half of W_hh; the four gates of a
-    cell meet through a DPP exchange) against lstm_persist2_kernel (4 waves,
-    16 units each) on the same 300-stream bf16 batch (launches of 256 + 44
-    streams): the same MFMA K steps, the same K-half order and the same cell
-    expressions, so the outputs are bit-identical; a second, 3-stream call
-    checks batch composition."""
-    if not torch.cuda.is_available():
-        pytest.skip('no HIP device')
-    from aec_amd import synth
-    B, n = 300, 8000
-    mic, far, _ = synth.batch(B, n, seed0=900)
-    M, F = (torch.from_numpy(a).to('cuda:0') for a in (mic, far))
-    monkeypatch.delenv('AEC_CRN_PERSIST', raising=False)
-    outs = {}
-    for waves in ('4', '8'):
-        monkeypatch.setenv('AEC_CRN_PERSIST_WAVES', waves)     # read per call
-        net, m, conf = build('v2E_16000', 'bf16')
-        with torch.no_grad():
-            o, _, _ = net.forward_ragged(M, F, [n] * B, want_spec=False)
-            o2, _, _ = net.forward_ragged(M[:3], F[:3], [n] * 3, want_spec=False)
-        torch.cuda.synchronize()
-        outs[waves] = (o.cpu().numpy(), o2.cpu().numpy())
-    assert np.isfinite(outs['8'][0]).all()
-    assert np.array_equal(outs['8'][0], outs['4'][0])
-    assert np.array_equal(outs['8'][1], outs['8'][0][:3])
-
-
 def test_persistent_timeout_fails_that_call(monkeypatch):
     """A persistent-grid timeout is reported by the call that hit it: with the
     poll targets made unreachable (AEC_CRN_PERSIST_STALL, read per call: a
@@ -404,7 +380,7 @@ def test_fp8_shadow_operands_bit_exact(monkeypatch):
     LSTM combine), with no quantisation pass; AEC_CRN_MX8_SHADOW=0 quantises
     the implicit rows first.  Same rule (E8M0 per 32 k from the bf16 values)
     on the same values, so the batch forward (ragged rows: M tails, conv
-    padding taps) and the hipGraph per-hop step are bit-identical."""
+    padding taps) and the per-hop step are bit-identical."""
     from aec_amd import synth
     lens = [16000, 9000, 12345, 256, 4000]
     L = max(lens)

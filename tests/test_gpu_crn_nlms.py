@@ -16,7 +16,7 @@ written here):
 * bf16 network fed E: out_wav <= 1e-2 (the CRN's bf16 bar);
 * fp8 per-hop step (64 streams): every stream within 2e-2 of the fp8 batch
   forward, three within the CRN's fp8 bar (2e-2) of the oracle;
-* streaming (hipGraph-replayed per-hop step, NLMS state carried per stream)
+* streaming (per-hop step, NLMS state carried per stream)
   vs batch: <= 1e-5 f32 (the CRN streaming bar; the NLMS arithmetic itself is
   the same NlmsBin code on the same fp32 operands);
 * batch composition (ragged rows in one call vs one call per row): bit-exact.
@@ -137,8 +137,7 @@ def test_nlms_ragged_batch_equals_single_calls(dtype):
 
 @pytest.mark.parametrize('taps', [1, 4, 8])
 def test_nlms_stream_step_equals_batch_and_oracle(taps):
-    """The per-hop NLMS -> CRN step (aec_crn_stream_step, one hipGraph per ring
-    parity) reproduces the batch forward and the oracle, with a per-stream
+    """The per-hop NLMS -> CRN step (aec_crn_stream_step, direct launches) reproduces the batch forward and the oracle, with a per-stream
     reset (the NLMS state of that stream restarts) mid-run."""
     nl = dict(NLMS, taps=taps)
     net, m, conf, w = build('v2E_2125', 'f32', nlms=nl)
@@ -191,7 +190,7 @@ FP8_WAV_TOL = 2e-2
 
 
 def test_fp8_nlms_stream_step_close_to_oracle():
-    """BASELINE config 5's unit: the hipGraph-captured per-hop step with the
+    """BASELINE config 5's unit: the per-hop step (direct launches) with the
     FD-NLMS in front and MX-fp8 GEMMs (dtype 'fp8'), 64 concurrent streams
     (the 64 x 64-tile MX GEMM at M = 64 x 128 bins), against the fp8 batch
     forward of the same network for every stream (<= 2e-2: the step kernels

@@ -232,12 +232,16 @@ def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatc
 
 
 def test_normaliser_lookahead_bit_exact(nlms_net, golden_erb):
-    """aec_prepare_siglens (Little_net.prepare_ragged): the normaliser pass of a
-    batch queued on a side stream ahead of its forward_ragged call.  The
-    waveform and loss are bit-identical to the call without look-ahead, for the
-    batch K2n path (B = 70) and the split path (B = 5), with per-signal
-    lengths; a look-ahead for other lengths is dropped (the call runs the pass
-    itself, still exact); at most two look-aheads may be pending."""
+    """aec_prepare_siglens / aec_process_prepared (Little_net.prepare_ragged ->
+    forward_ragged(lookahead=token)): the normaliser pass of a batch queued on a
+    side stream ahead of its forward call.  The waveform and loss are
+    bit-identical to the call without look-ahead, for the batch K2n path
+    (B = 70) and the split path (B = 5), with per-signal lengths.  A token
+    prepared for other lengths is refused (nothing runs); a token that is not
+    pending is refused; a later token drops the older pending one; at most two
+    look-aheads may be pending; and a plain forward never consumes a pending
+    look-ahead, so a buffer refilled at the same address with the same lengths
+    is normalised with its own statistics (no stale constants)."""
     from aec_amd import synth
     dev = 'cuda:0'
     erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
@@ -250,29 +254,46 @@ def test_normaliser_lookahead_bit_exact(nlms_net, golden_erb):
             mic[i, :n], ref[i, :n], near[i, :n] = m, r, nn_
         M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
         l3 = np.array([[n, n - n % 256 + (n % 256) // 2, n] for n in lens], np.int64)   # ref shorter, same frames
+        cur = torch.cuda.current_stream()
         with torch.no_grad():
             o0, s0 = nlms_net.forward_ragged(M, R, N, erb_t, l3)
             o0, s0 = o0.cpu().numpy(), s0.cpu().numpy()
             for rep in range(2):                      # the second round reuses the handle's slots
                 with torch.cuda.stream(side):
-                    nlms_net.prepare_ragged(M, R, N, l3)
-                torch.cuda.current_stream().wait_stream(side) if rep else None
-                o1, s1 = nlms_net.forward_ragged(M, R, N, erb_t, l3)
+                    tok = nlms_net.prepare_ragged(M, R, N, l3, producer=cur)
+                assert tok > 0
+                o1, s1 = nlms_net.forward_ragged(M, R, N, erb_t, l3, lookahead=tok)
                 assert np.array_equal(o0, o1.cpu().numpy()), (len(lens), rep)
                 assert np.array_equal(s0, s1.cpu().numpy(), equal_nan=True), (len(lens), rep)
-            with torch.cuda.stream(side):             # stale: other lengths
-                nlms_net.prepare_ragged(M, R, N, [L] * len(lens))
-            o2, s2 = nlms_net.forward_ragged(M, R, N, erb_t, l3)
-            assert np.array_equal(o0, o2.cpu().numpy())
+                with pytest.raises(RuntimeError, match='not pending'):      # consumed
+                    nlms_net.forward_ragged(M, R, N, erb_t, l3, lookahead=tok)
+            with torch.cuda.stream(side):             # other lengths: refused, then dropped by a later token
+                bad = nlms_net.prepare_ragged(M, R, N, [L] * len(lens), producer=cur)
+            with pytest.raises(RuntimeError, match='other signals'):
+                nlms_net.forward_ragged(M, R, N, erb_t, l3, lookahead=bad)
             with torch.cuda.stream(side):
-                nlms_net.prepare_ragged(M, R, N, l3)
-                nlms_net.prepare_ragged(M, R, N, l3)
-                with pytest.raises(RuntimeError):
+                t1 = nlms_net.prepare_ragged(M, R, N, l3, producer=cur)
+                with pytest.raises(RuntimeError):     # two pending (bad, t1)
                     nlms_net.prepare_ragged(M, R, N, l3)
-            o3, _ = nlms_net.forward_ragged(M, R, N, erb_t, l3)   # takes the first; the second is dropped next
+            o2, _ = nlms_net.forward_ragged(M, R, N, erb_t, l3, lookahead=t1)   # drops `bad`
+            assert np.array_equal(o0, o2.cpu().numpy())
+            with pytest.raises(RuntimeError, match='not pending'):
+                nlms_net.forward_ragged(M, R, N, erb_t, l3, lookahead=bad)
+            # a pending look-ahead, then the buffers refilled in place (same pointers, same lengths):
+            # the plain forward runs its own pass on the new contents
+            with torch.cuda.stream(side):
+                stale = nlms_net.prepare_ragged(M, R, N, l3, producer=cur)
+            side.synchronize()
+            M2, R2, N2 = M.clone(), R.clone(), N.clone()
+            M.mul_(3.0).add_(0.01)
+            R.mul_(0.5)
+            ofresh, _ = nlms_net.forward_ragged(M.clone(), R.clone(), N.clone(), erb_t, l3)
+            oplain, _ = nlms_net.forward_ragged(M, R, N, erb_t, l3)
+            assert np.array_equal(ofresh.cpu().numpy(), oplain.cpu().numpy())
+            assert not np.array_equal(oplain.cpu().numpy(), o0)
+            M.copy_(M2), R.copy_(R2), N.copy_(N2)
+            o3, _ = nlms_net.forward_ragged(M, R, N, erb_t, l3, lookahead=stale)   # still pending, contents restored
             assert np.array_equal(o0, o3.cpu().numpy())
-            o4, _ = nlms_net.forward_ragged(M, R, N, erb_t, l3)   # takes the second
-            assert np.array_equal(o0, o4.cpu().numpy())
         torch.cuda.synchronize()
 
 

@@ -75,6 +75,28 @@ def test_clib_exports_every_declared_symbol():
     assert lib.aec_weights_count(16) == 0
 
 
+AB_KNOBS = ('AEC_MOM_CFG', 'AEC_MOM_GRID', 'AEC_GRU_MODE', 'AEC_NLMS_PRIO', 'AEC_NLMS_ERB', 'AEC_FUSED_MODE',
+            'AEC_CRN_ENC_FR', 'AEC_CRN_SPLITK', 'CRN_PERSIST_RA', 'AEC_CRN_ENC_MX_RERUN', 'CRN_DEC_FUSE',
+            'CRN_GEMM_XCD', 'CRN_GEMM_DMA', 'CRN_GEMM_BIG', 'CRN_GEMM_SQ', 'CRN_GEMM_RB64', 'CRN_GEMM_MODE',
+            'CRN_GEMM_PIPE', 'CRN_STEP_MODE', 'CRN_STEP_CFG', 'CRN_MX_STEP_MODE', 'AEC_CRN_PERSIST_WAVES')
+
+
+def test_product_library_reads_only_mode_knobs():
+    """The product libaec_hip.so is not an A/B build: none of the timing-only /
+    work-skipping knob names (csrc/aec_knobs.h AEC_AB_KNOB) is in the binary,
+    and every AEC_* / CRN_* environment name it holds is a listed mode knob."""
+    from aec_amd import _lib
+    info = _lib.build_info()
+    assert info['arch'] == 'gfx950' and info['ab_knobs'] is False, info
+    blob = open(_lib.LIB_PATH, 'rb').read()
+    for k in AB_KNOBS:
+        assert k.encode() + b'\0' not in blob, k
+    names = set(m.decode() for m in re.findall(rb'\0((?:AEC|CRN)_[A-Z0-9_]+)\0', blob))
+    names -= {'AEC_OK'}
+    assert names <= set(info['mode_knobs']), names - set(info['mode_knobs'])
+    assert 'AEC_CRN_GRAPH' in info['mode_knobs']
+
+
 def test_product_path_does_not_import_oracle():
     pkg = os.path.join(REPO, 'acoustic-echo-cancellation_amd')
     for root, _, files in os.walk(pkg):

@@ -1,3 +1,5 @@
+// ARCHIVED (round 6): not built into libaec_hip.so. The 8-wave persistent LSTM recurrence was
+// bit-identical to crn_persist.hip and measured 15 % slower; kept for the record.
 // crn_persist3.hip — persistent LSTM recurrence of the DCCRN, 8 waves per
 // block (gfx950).  The geometry, hand-off protocol and numerics are
 // lstm_persist2_kernel's (crn_persist.hip; reference NavieComplexLSTM,

@@ -46,6 +46,7 @@ kstep = [0]
 
 
 done_ev = {}
+tokens = {}
 
 
 def step(ev=None):
@@ -57,9 +58,9 @@ def step(ev=None):
         if gate is not None and a.paced:
             side.wait_event(gate)
         with torch.cuda.stream(side):
-            nets[(k + a.lookahead) % a.inflight].prepare_ragged(mic, ref, near, lens)
+            tokens[n + a.lookahead] = nets[(k + a.lookahead) % a.inflight].prepare_ragged(mic, ref, near, lens)
     with torch.cuda.stream(streams[k]):
-        nets[k].forward_ragged(mic, ref, near, erb, lens)
+        nets[k].forward_ragged(mic, ref, near, erb, lens, lookahead=tokens.pop(n, None))
         if ev is not None:
             ev.record(streams[k])
         e = torch.cuda.Event()
