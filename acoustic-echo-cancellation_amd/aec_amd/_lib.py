@@ -11,7 +11,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # AEC_HIP_LIB: alternative build of the same library (A/B timing experiments)
-LIB_PATH = os.environ.get('AEC_HIP_LIB') or os.path.join(_HERE, 'libaec_hip.so')
+_DEFAULT_LIB = os.path.join(_HERE, 'libaec_hip.so')
+LIB_PATH = os.environ.get('AEC_HIP_LIB') or _DEFAULT_LIB
 
 # aec_status codes (include/aec_hip.h)
 AEC_OK = 0
@@ -87,9 +88,12 @@ def load():
     lib.aec_prepare_siglens.argtypes = [P, P, P, P, P, ctypes.c_int32, ctypes.c_int64, P,
                                         ctypes.POINTER(ctypes.c_uint64)]
     lib.aec_prepare_siglens.restype = ctypes.c_int
-    lib.aec_process_prepared.argtypes = [P, ctypes.c_uint64, P, P, P, P, ctypes.c_int32, ctypes.c_int64, P,
-                                         ctypes.c_int64, P, P]
-    lib.aec_process_prepared.restype = ctypes.c_int
+    if LIB_PATH != _DEFAULT_LIB and not hasattr(lib, 'aec_process_prepared'):
+        pass                                   # an older A/B build (AEC_HIP_LIB) without the symbol
+    else:
+        lib.aec_process_prepared.argtypes = [P, ctypes.c_uint64, P, P, P, P, ctypes.c_int32, ctypes.c_int64, P,
+                                             ctypes.c_int64, P, P]
+        lib.aec_process_prepared.restype = ctypes.c_int
     lib.aec_stream_open.argtypes = [P, ctypes.c_int32]
     lib.aec_stream_open.restype = ctypes.c_int
     lib.aec_stream_reset.argtypes = [P, ctypes.c_int32, P]
@@ -111,8 +115,9 @@ def load():
     lib.aec_num_frames.restype = ctypes.c_int64
     lib.aec_out_len.argtypes = [ctypes.c_int64]
     lib.aec_out_len.restype = ctypes.c_int64
-    lib.aec_build_info.argtypes = []
-    lib.aec_build_info.restype = ctypes.c_char_p
+    if LIB_PATH == _DEFAULT_LIB or hasattr(lib, 'aec_build_info'):
+        lib.aec_build_info.argtypes = []
+        lib.aec_build_info.restype = ctypes.c_char_p
     lib.aec_last_error.argtypes = [P]
     lib.aec_last_error.restype = ctypes.c_char_p
     lib.aec_destroy.argtypes = [P]
@@ -169,7 +174,10 @@ def load():
 
 def build_info():
     """aec_build_info(): dict(arch, ab_knobs (bool), mode_knobs (list of names))."""
-    txt = load().aec_build_info().decode()
+    lib = load()
+    if not hasattr(lib, 'aec_build_info'):     # an older A/B build (AEC_HIP_LIB)
+        return dict(arch=None, ab_knobs=True, mode_knobs=[], text='(no aec_build_info: older build)')
+    txt = lib.aec_build_info().decode()
     head, _, knobs = txt.partition(' mode_knobs=')
     d = dict(kv.split('=', 1) for kv in head.split())
     return dict(arch=d.get('arch'), ab_knobs=d.get('ab_knobs') == 'on',

@@ -3,7 +3,7 @@
 // Reference path: Little_net.forward (Stage2_lhm/scripts/network/ERB.py:252-334).
 // Pipeline per batch of B streams (each stream has batch=1 semantics):
 //
-//   K1 moments_kernel   partial sums for x <- x - mean(x)/std(x) (ERB.py:254-256)
+//   K1 moments_lds_kernel  partial sums for x <- x - mean(x)/std(x) (ERB.py:254-256)
 //   K2 analysis_kernel  frame + Hann + rFFT-512 (attention_ccrn.py:45-52) -> |X| (ERB.py:277-279)
 //                       -> ERB band energies (ERB.py:282-284) for mic / ref / near
 //   K2n nlms_analysis_kernel  K2 with the FD-NLMS canceller (one block per stream);
@@ -48,87 +48,10 @@ constexpr int kNlmsWavesProf = 12;
 // scalar c = mean/std (unbiased) is finished by every consumer from the
 // kMomChunks partials in a fixed order (deterministic, no atomics).
 // --------------------------------------------------------------------------
-template <int U, int NT, bool NTL>
-__global__ __launch_bounds__(NT) void moments_kernel(const float* __restrict__ mic,
-                                                      const float* __restrict__ ref,
-                                                      const float* __restrict__ near, int64_t ld,
-                                                      const int32_t* __restrict__ slen,
-                                                      double2* __restrict__ mom, int b0) {
-    const int ch = blockIdx.x, s = blockIdx.y, b = b0 + blockIdx.z;
-    const float* base = (s == 0 ? mic : (s == 1 ? ref : near));
-    const float* x = base + (int64_t)b * ld;
-    const int64_t n = slen[4 * b + s];
-    // chunk start = a multiple of 1024 samples (float4-aligned); a vector pass
-    // reads U float4 per thread (1024 U samples), then single float4s, then the
-    // scalar tail
-    const int64_t per = ((n + kMomChunks - 1) / kMomChunks + 1023) & ~(int64_t)1023;
-    const int64_t lo = ch * per, hi = min(n, lo + per);
-    double s1 = 0.0, s2 = 0.0;
-    const int tid = threadIdx.x;
-    auto acc4 = [&](const float4 v) {
-        const double a = v.x, bb = v.y, c = v.z, d = v.w;
-        s1 += (a + bb) + (c + d);
-        s2 += (a * a + bb * bb) + (c * c + d * d);
-    };
-    if (lo < hi) {
-        int64_t i = lo + tid;                                  // scalar start (unaligned rows)
-        if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
-            const float4* x4 = reinterpret_cast<const float4*>(x);
-            const int64_t end4 = hi / 4;
-            int64_t i4 = lo / 4 + tid;
-            for (; i4 + NT * (U - 1) < end4; i4 += NT * U) {
-                float4 v[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    if constexpr (NTL) {
-                        typedef float f4v __attribute__((ext_vector_type(4)));
-                        const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(x4 + i4 + NT * u));
-                        v[u] = make_float4(t.x, t.y, t.z, t.w);
-                    } else {
-                        v[u] = x4[i4 + NT * u];
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) acc4(v[u]);
-            }
-            for (; i4 < end4; i4 += NT) acc4(x4[i4]);
-            i = end4 * 4 + tid;
-        }
-        for (; i < hi; i += NT) {
-            const double a = x[i];
-            s1 += a;
-            s2 += a * a;
-        }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        s1 += __shfl_xor(s1, o);
-        s2 += __shfl_xor(s2, o);
-    }
-    constexpr int W = NT / 64;
-    __shared__ double r1[W], r2[W];
-    if ((tid & 63) == 0) {
-        r1[tid >> 6] = s1;
-        r2[tid >> 6] = s2;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        // pairwise over the block's waves in a fixed order
-        double t1[W], t2[W];
-#pragma unroll
-        for (int w = 0; w < W; ++w) { t1[w] = r1[w]; t2[w] = r2[w]; }
-#pragma unroll
-        for (int st = 1; st < W; st <<= 1)        // (r0 + r1) + (r2 + r3) at W = 4
-#pragma unroll
-            for (int w = 0; w + st < W; w += 2 * st) { t1[w] += t1[w + st]; t2[w] += t2[w + st]; }
-        mom[((int64_t)b * 3 + s) * kMomChunks + ch] = make_double2(t1[0], t2[0]);
-    }
-}
-
-// K1 through LDS-DMA (AEC_MOM_CFG=3): the same per-thread float4 sequence (thread tid sums float4
-// lo/4 + tid + 256 m for m = 0, 1, ...) and the same block reduction, so bit-identical partials,
-// but the loads land in a per-wave LDS ring (buffer_load ... lds, 4 KB in flight per wave) instead of
-// registers.  The point is its footprint: 30 VGPRs and 16 KiB of LDS per block, which fits beside a
+// K1 through LDS-DMA: thread tid sums float4 lo/4 + tid + 256 m for m = 0, 1, ... (then a fixed
+// wave + block reduction); the loads land in a per-wave LDS ring (buffer_load ... lds, 4 KB in flight
+// per wave) instead of registers (round 5's register-loaded moments_kernel gave bit-identical
+// partials; it was retired in round 6 with the other timing variants).  The point is its footprint: 30 VGPRs and 16 KiB of LDS per block, which fits beside a
 // K2n block (153 -> 160 VGPRs x 3 waves per SIMD, 131 KiB of LDS) or a gru_synth block (160 x 3,
 // 132 KiB) on the same CU, so with batches in flight the next batch's moments pass (aec_prepare)
 // streams under the compute kernels instead of holding whole CUs (the register-loaded kernel
@@ -150,11 +73,10 @@ __device__ __forceinline__ void mom_wait_vm(int n) {
 }
 // the one-item form compiles to <= 32 VGPRs and <= 20 KiB of LDS: one block fits beside a K2n (160 VGPRs x 3
 // waves per SIMD, 131 KiB) or a gru_synth block (160 x 3, 132 KiB)
-template <bool PERSIST>
 __global__ __launch_bounds__(256) void moments_lds_kernel(const float* __restrict__ mic, const float* __restrict__ ref,
                                                           const float* __restrict__ near, int64_t ld,
                                                           const int32_t* __restrict__ slen, double2* __restrict__ mom,
-                                                          int b0, int nsig, int nwork) {
+                                                          int b0) {
     // one array per ring slot: a read of slot j waits only for the DMAs into slot j
     __shared__ __attribute__((aligned(16))) float4 sR0[256];
     __shared__ __attribute__((aligned(16))) float4 sR1[256];
@@ -163,13 +85,8 @@ __global__ __launch_bounds__(256) void moments_lds_kernel(const float* __restric
     __shared__ __attribute__((aligned(16))) float4 sR4[256];
     __shared__ __attribute__((aligned(16))) float4 sR5[256];
     __shared__ double r1[4], r2[4];
-    // work item w = (chunk, signal, stream) in moments_kernel's grid order; a grid smaller than
-    // nwork walks the items (persistent form: a few blocks that share CUs with other kernels)
-    // (PERSIST = false: one item per block, the 3-D grid (chunk, signal, stream) of moments_kernel)
-    for (int w = PERSIST ? (int)blockIdx.x : 0; w < (PERSIST ? nwork : 1); w += PERSIST ? gridDim.x : 1) {
-    const int ch = PERSIST ? w % kMomChunks : (int)blockIdx.x;
-    const int s = PERSIST ? (w / kMomChunks) % nsig : (int)blockIdx.y;
-    const int b = b0 + (PERSIST ? w / (kMomChunks * nsig) : (int)blockIdx.z);
+    // one item per block: the 3-D grid (chunk, signal, stream)
+    const int ch = (int)blockIdx.x, s = (int)blockIdx.y, b = b0 + (int)blockIdx.z;
     const float* base = (s == 0 ? mic : (s == 1 ? ref : near));
     const float* x = base + (int64_t)b * ld;
     const int64_t n = slen[4 * b + s];
@@ -254,8 +171,6 @@ __global__ __launch_bounds__(256) void moments_lds_kernel(const float* __restric
 #pragma unroll
             for (int q = 0; q + st < 4; q += 2 * st) { t1[q] += t1[q + st]; t2[q] += t2[q + st]; }
         mom[((int64_t)b * 3 + s) * kMomChunks + ch] = make_double2(t1[0], t2[0]);
-    }
-    __syncthreads();                                    // r1 / r2 read before the next item rewrites them
     }
 }
 
@@ -883,37 +798,10 @@ hipError_t launch_moments(const float* mic, const float* ref, const float* near,
     // look-ahead pass (aec_prepare) of the next batch streams under the compute kernels of the
     // batches in flight (C2 0.581-0.592 against 0.597-0.600 ms, profiles/r05r_persist8_lookahead_ab.log).
     // Standalone 0.080 ms for 256 x 10 s x 3 signals.
-    const dim3 g(kMomChunks, nsig, nb);
-    const int nwork = kMomChunks * nsig * nb;
-#if AEC_AB_BUILD
-    // A/B builds (AEC_MOM_CFG; bit-identical partials): 0 moments_kernel, 4 float4 per thread in
-    // registers, nt loads (0.078 ms standalone; 36 VGPRs: fits beside neither compute kernel); 1 the
-    // same with default-policy loads (0.104 ms); 2 two float4 per thread; 4 moments_lds persistent,
-    // AEC_MOM_GRID blocks walking the items (40 VGPRs; slower, profiles/r05_notes.md r05n); 9 TIMING
-    // ONLY: no pass after the first 16 launches (partials of each workspace's last pass)
-    static const int cfg = AEC_AB_KNOB("AEC_MOM_CFG", 3);
-    static int launches = 0;
-    if (cfg == 9 && ++launches > 16) return hipSuccess;
-    if (cfg == 0) {
-        hipLaunchKernelGGL((moments_kernel<4, 256, true>), g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0);
-        return hipGetLastError();
-    }
-    if (cfg == 1) {
-        hipLaunchKernelGGL((moments_kernel<4, 256, false>), g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0);
-        return hipGetLastError();
-    }
-    if (cfg == 2) {
-        hipLaunchKernelGGL((moments_kernel<2, 256, true>), g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0);
-        return hipGetLastError();
-    }
-    if (cfg == 4) {
-        static const int pgrid = AEC_AB_KNOB("AEC_MOM_GRID", 256);
-        hipLaunchKernelGGL(moments_lds_kernel<true>, dim3(std::max(1, std::min(pgrid, nwork))), dim3(256), 0, st, mic,
-                           ref, near, ld, slen, mom, b0, nsig, nwork);
-        return hipGetLastError();
-    }
-#endif
-    hipLaunchKernelGGL(moments_lds_kernel<false>, g, dim3(256), 0, st, mic, ref, near, ld, slen, mom, b0, nsig, nwork);
+    // (Round 6: a canonical one-wave-per-chunk form with f32 pre-summed float4s measured 0.4 % slower
+    // in the step, profiles/r06c_moments_canonical_ab.log, tools/archive/r06c_canonical_moments.patch.)
+    hipLaunchKernelGGL(moments_lds_kernel, dim3(kMomChunks, nsig, nb), dim3(256), 0, st, mic, ref, near, ld, slen, mom,
+                       b0);
     return hipGetLastError();
 }
 

@@ -132,16 +132,18 @@ def knob_provenance():
     is set or the loaded library is an A/B build."""
     from aec_amd import _lib
     env = {k: v for k, v in sorted(os.environ.items()) if k.startswith(('AEC_', 'CRN_'))}
+    # AEC_BENCH_AB=1: an A/B timing run (tools/*_ab.sh) of a variant build; its line says so
+    ab_run = env.get('AEC_BENCH_AB') == '1'
     bad = [k for k in env if k in AB_ONLY_KNOBS or k in TEST_ONLY_KNOBS]
-    if bad:
+    if bad and not ab_run:
         raise SystemExit(f'bench.py: timing-only / test-only knobs set {bad}: refusing to produce a bench line')
     info = _lib.build_info()
-    if info['ab_knobs']:
+    if info['ab_knobs'] and not ab_run:
         raise SystemExit(f'bench.py: {_lib.LIB_PATH} is an A/B build ({info["text"]}): refusing')
-    unknown = [k for k in env if k not in info['mode_knobs'] and k not in ('AEC_HIP_LIB', 'AEC_BENCH_BACKEND')]
+    unknown = [k for k in env if k not in info['mode_knobs'] and k not in ('AEC_HIP_LIB', 'AEC_BENCH_BACKEND',
+                                                                          'AEC_BENCH_AB')]
     return dict(env=env, library=os.path.relpath(_lib.LIB_PATH, REPO), build_info=info['text'],
-                defaults=not any(k in info['mode_knobs'] for k in env) and 'AEC_HIP_LIB' not in env,
-                unknown_names=unknown)
+                defaults=not env, ab_timing_run=ab_run, unknown_names=unknown)
 
 
 def cu_masked_stream(dev, ncu):
