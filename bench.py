@@ -202,6 +202,39 @@ def roofline(pipeline, kernel, ms_per_launch, frames_per_launch, pmc):
                 frac=round(tfl / FP32_PEAK_TFLOPS, 4), **common)
 
 
+SQ_KERNEL = {'analysis': 'nlms_analysis_kernel', 'gru_synthesis': 'gru_synth_kernel', 'moments': 'moments_lds_kernel'}
+
+
+def sq_limiter(kernel, path=None):
+    """What limits a C2 kernel, from the committed SQ counter pass of the same build
+    (profiles/sq_latest_full.json; counters in quad-cycles).  A wave64 VALU
+    instruction holds one wave for a quad-cycle and the SIMD-32 issues two per
+    quad-cycle from different waves (MI355X_MICROARCH.md, cycle constants), so
+    the SIMD's VALU pipe use = waves per SIMD x VALU-active per wave / 2.
+    limiter: 'valu-issue' at >= 0.8 of that pipe, else 'latency' with the
+    stall split (dependency / issue stalls vs s_waitcnt + barrier waits)."""
+    path = path or os.path.join(REPO, 'profiles', 'sq_latest_full.json')
+    name = SQ_KERNEL.get(kernel)
+    if not name or not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    row = next((v for k, v in d.get('kernels', d).items() if name in k and isinstance(v, dict) and 'derived' in v),
+               None)
+    if row is None:
+        return None
+    dv, av = row['derived'], row['avg']
+    waves_per_simd = d.get('waves_per_simd', {}).get(kernel, 3)
+    pipe = waves_per_simd * dv['SQ_ACTIVE_INST_VALU/wave_cycles'] / 2
+    out = dict(source=os.path.relpath(path, REPO), waves_per_simd=waves_per_simd,
+               valu_active_per_wave=dv['SQ_ACTIVE_INST_VALU/wave_cycles'], valu_pipe_use=round(pipe, 3),
+               issue_stall_per_wave=dv['SQ_WAIT_INST_ANY/wave_cycles'], waitcnt_barrier_per_wave=dv['SQ_WAIT_ANY/wave_cycles'],
+               valu_instr_per_wave=dv['SQ_INSTS_VALU/wave'])
+    out['limiter'] = 'valu-issue' if pipe >= 0.8 else (
+        'latency: dependency / issue stalls %.0f %%, s_waitcnt + barrier waits %.0f %% of wave cycles'
+        % (100 * dv['SQ_WAIT_INST_ANY/wave_cycles'], 100 * dv['SQ_WAIT_ANY/wave_cycles']))
+    return out
+
+
 def cpu_baseline(seconds, B=256, n=160000):
     """The reference op mix on host cores (oracle/torch_port.py), bounded
     sample: B = 256 x 10 s streams, then a few batch-1 calls."""
@@ -964,6 +997,9 @@ def main():
     if os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path))
     roof = roofline(args.pipeline, dom, per_launch_ms[dom], int(round(B * T / calls_per_step)), pmc)
+    if args.pipeline == 'full':
+        roof['sq'] = sq_limiter(dom)
+        roof['limiter'] = roof['sq']['limiter'] if roof['sq'] else None
     # every kernel of the step against its own roofline (the fused GRU + synthesis kernel runs two
     # streams per block on half the CUs, so the longest launch is not the one holding the most CU
     # time): the same figures as `roofline`, per kernel
@@ -973,6 +1009,9 @@ def main():
             r = roofline(args.pipeline, k, per_launch_ms[k], int(round(B * T / calls_per_step)), pmc)
             kernel_rooflines[k] = {x: r[x] for x in ('bound', 'frac', 'hbm_frac', 'fp32_frac', 'ms_per_launch',
                                                      'traffic', 'traffic_alg_bytes_per_launch')}
+            # `bound` is the roofline the kernel's algorithmic work is priced against; `sq` says what
+            # the counters show limits it (C2's kernels: latency, not HBM or VALU throughput)
+            kernel_rooflines[k]['sq'] = sq_limiter(k) if args.pipeline == 'full' else None
     pipe_t = ms_step * 1e-3
     pipe_gbs = PIPE['bytes'] * B * T / pipe_t / 1e9
     pipe_tfl = path_flops(args.pipeline) * B * T / pipe_t / 1e12
