@@ -4,6 +4,7 @@ exports every symbol include/aec_hip.h declares."""
 import ctypes
 import os
 import re
+import sys
 
 import numpy as np
 import torch
@@ -137,3 +138,27 @@ def test_erb_device_tables_match_dense(golden_erb):
     import pytest
     with pytest.raises(RuntimeError, match='UNSUPPORTED'):
         _lib.erb_tables_check(bad, mags, est)
+
+
+def test_bench_refuses_timing_only_knobs(monkeypatch):
+    """bench.py records every AEC_* / CRN_* variable and the library's build
+    description, and refuses to produce a line when a timing-only (A/B build)
+    or test-only knob is set (a driver line must show it ran the
+    defaults)."""
+    import importlib
+    import pytest
+    sys.path.insert(0, REPO)
+    bench = importlib.import_module('bench')
+    for k in list(os.environ):
+        if k.startswith(('AEC_', 'CRN_')):
+            monkeypatch.delenv(k)
+    prov = bench.knob_provenance()
+    assert prov['env'] == {} and prov['defaults'] is True and 'ab_knobs=off' in prov['build_info']
+    monkeypatch.setenv('AEC_CRN_GRAPH', '1')                    # a tested mode: recorded, not refused
+    prov = bench.knob_provenance()
+    assert prov['env'] == {'AEC_CRN_GRAPH': '1'} and prov['defaults'] is False and prov['unknown_names'] == []
+    for k in ('AEC_MOM_CFG', 'AEC_CRN_PERSIST_STALL'):
+        monkeypatch.setenv(k, '9')
+        with pytest.raises(SystemExit):
+            bench.knob_provenance()
+        monkeypatch.delenv(k)
