@@ -154,8 +154,16 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
         nchs[s] = (Ts[s] + TF - 1) / TF;
         nchmax = max(nchmax, nchs[s]);
     }
+#if AEC_AB_BUILD
+    // A/B builds: y.wmap relabels hardware wave i (SIMD i % 4) as role wave (wmap >> 4 i) & 15, to
+    // measure other role-to-SIMD placements (AEC_GRU_WMAP); every index below uses the role ids
+    const int lane = threadIdx.x & 63;
+    const int wave = y.wmap ? (int)((y.wmap >> (4 * (threadIdx.x >> 6))) & 15) : (int)(threadIdx.x >> 6);
+    const int tid = wave * 64 + lane;
+#else
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
+#endif
     const float* W_ih = p.w;                  // [96][64]
     const float* W_hh = p.w + 96 * 64;        // [96][32]
     const float* b_ih = W_hh + 96 * 32;       // [96]
@@ -532,6 +540,21 @@ hipError_t launch_gru_synth(const GruArgs& g, const SynthArgs& y, int B, hipStre
     // NS = 2 writes the waveform with 16-B stores (overlap-add on the recurrence waves)
     const bool al16 = y.ld_out % 4 == 0 && (reinterpret_cast<uintptr_t>(y.out) & 15) == 0;
     const int ns = AEC_MODE_KNOB("AEC_GRU_NS", 2) == 1 || (AEC_OLA_REC && !al16) ? 1 : 2;
+    SynthArgs ya = y;
+    ya.wmap = 0;
+#if AEC_AB_BUILD
+    // role placements for NS = 2 (role waves: 0-1 recurrence, 2-4 gi, 5-7 head, 8-11 synthesis;
+    // hardware wave i runs on SIMD i % 4), entry k = role of hardware wave k
+    static const unsigned long long kWmaps[] = {
+        0,                      // identity: SIMD0 rec0 gi2 syn0 | rec1 head0 syn1 | gi0 head1 syn2 | gi1 head2 syn3
+        0x46327591BA80ull,      // 1: rec0 rec1 gi0 | syn0 syn1 gi1 | syn2 head0 head1 | syn3 head2 gi2
+        0xBA9874326510ull,      // 2: rec0 gi0 syn0 | rec1 gi1 syn1 | head0 gi2 syn2 | head1 head2 syn3
+        0x4765B321A980ull,      // 3: rec0 rec1 head0 | syn0 gi0 head1 | syn1 gi1 head2 | syn2 syn3 gi2
+        0x76584321BA90ull,      // 4: rec0 rec1 syn0 | syn1 gi0 head0 | syn2 gi1 head1 | syn3 gi2 head2
+    };
+    const int wm = AEC_AB_KNOB("AEC_GRU_WMAP", 0);
+    if (ns == 2 && wm > 0 && wm < (int)(sizeof(kWmaps) / sizeof(kWmaps[0]))) ya.wmap = kWmaps[wm];
+#endif
 #define AEC_GRU_SYNTH(NS_)                                                                                     \
     do {                                                                                                       \
         static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gru_synth_kernel<NS_>), \
@@ -539,7 +562,7 @@ hipError_t launch_gru_synth(const GruArgs& g, const SynthArgs& y, int B, hipStre
                                                            (int)gru_synth_smem_bytes());                       \
         if (attr != hipSuccess) return attr;                                                                   \
         hipLaunchKernelGGL(gru_synth_kernel<NS_>, dim3((B + NS_ - 1) / NS_), dim3(64 * (NS_ + kHelperWaves)),   \
-                           gru_synth_smem_bytes(), st, g, y, B);                                               \
+                           gru_synth_smem_bytes(), st, g, ya, B);                                              \
     } while (0)
     if (ns == 1)
         AEC_GRU_SYNTH(1);

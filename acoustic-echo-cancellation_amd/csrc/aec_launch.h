@@ -95,6 +95,7 @@ struct SynthArgs {
     const float2* spec;      // NLMS error spectrum [B][Tmax][256], or null: re-derive the mic spectrum
     int fmode;               // fused kernel timing experiments only (AEC_FUSED_MODE; results invalid
                              // unless 0): bit0 skip the synthesis, bit1 skip the OLA, bit2 skip the E loads
+    unsigned long long wmap; // A/B builds only: role wave of hardware wave i = (wmap >> 4 i) & 15 (0: identity)
 };
 
 // Fused streaming step (aec_stream.hip): one 256-sample hop of B streams.
