@@ -250,6 +250,14 @@ struct aec_handle {
                                  // B = 64 0.504 -> 0.485; B = 128 slower)
     float2* d_rows = nullptr;    // split path: packed mic / ref rows [B][T][2][256]
     size_t rows_cap = 0;         // float2 elements
+    // split path, pipelined (AEC_SMALLB_PIPE, default on): the recursion and mic_erb run in producer
+    // blocks of the GRU + synthesis launch (aec_gru_synth.hip, launch_gru_synth_pipe)
+    int small_pipe = 1;
+    unsigned long long* d_progress = nullptr;       // [progress_cap] per-stream published chunks
+    int progress_cap = 0;
+    unsigned long long pipe_epoch = 0;
+    int* h_pipe_err = nullptr;   // host-mapped: a consumer wave of an earlier launch stopped waiting
+    int* d_pipe_err = nullptr;
     int64_t last_B = 0, last_T = 0;
     // kernel timing (aec_profile_*)
     int profile = 0;
@@ -397,6 +405,7 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
     h->nlms_mode = AEC_MODE_KNOB("AEC_NLMS_MODE", 0) & 16;
     h->fused = AEC_MODE_KNOB("AEC_FUSED_SYNTH", h->fused);
     h->small_b = AEC_MODE_KNOB("AEC_SMALLB", h->small_b);
+    h->small_pipe = AEC_MODE_KNOB("AEC_SMALLB_PIPE", h->small_pipe);
     h->bptt_serial = AEC_MODE_KNOB("AEC_BPTT_SERIAL", h->bptt_serial);
     // A/B builds only: work-skipping timing bits and role priorities
     h->gru_mode = AEC_AB_KNOB("AEC_GRU_MODE", 0);
@@ -656,6 +665,12 @@ static aec_status process_impl(aec_handle* h, uint64_t token, const float* mic, 
         h->pre_count -= k + 1;
         c.token = 0;
     }
+    // a consumer of an earlier pipelined launch gave up waiting for its producer: that call's
+    // output is invalid; reported once, here
+    if (h->h_pipe_err && *reinterpret_cast<volatile int*>(h->h_pipe_err)) {
+        *h->h_pipe_err = 0;
+        return fail(h, AEC_ERR_HIP, "an earlier small-batch pipelined call timed out waiting for its producer blocks");
+    }
     // this call overwrites the features a pending aec_train_backward would read
     h->train_B = 0;
     ++h->train_gen;
@@ -675,6 +690,28 @@ static aec_status process_impl(aec_handle* h, uint64_t token, const float* mic, 
         }
     } pre_rel{ps, st};
     const float* cvals = ps ? ps->cvals : h->d_cvals;
+    // the pipelined split path: one GRU + synthesis launch of 2 B blocks (producers first) runs the
+    // recursion and mic_erb too; it needs one block per CU for each and the one tap count it is
+    // built for, and runs the GRU one stream per block (the AEC_GRU_NS rule for small batches)
+    const bool pipe = h->small_pipe && h->cfg.nlms_taps == kPipeTaps && B <= h->small_b && h->nlms_mode == 0 &&
+                      h->fused && h->gru_mode == 0 && 2 * (int64_t)B <= (int64_t)h->num_cus &&
+                      AEC_MODE_KNOB("AEC_GRU_NS", 0) != 2;
+    if (pipe) {
+        if (B > h->progress_cap) {
+            if (h->have_last) HIP_TRY(h, hipEventSynchronize(h->ev_last));
+            if (h->d_progress) HIP_TRY(h, hipFree(h->d_progress));
+            h->d_progress = nullptr;
+            h->progress_cap = 0;
+            HIP_TRY(h, hipMalloc(&h->d_progress, (size_t)B * sizeof(unsigned long long)));
+            HIP_TRY(h, hipMemset(h->d_progress, 0, (size_t)B * sizeof(unsigned long long)));
+            h->progress_cap = B;
+        }
+        if (!h->h_pipe_err) {
+            HIP_TRY(h, hipHostMalloc(reinterpret_cast<void**>(&h->h_pipe_err), sizeof(int), hipHostMallocMapped));
+            *h->h_pipe_err = 0;
+            HIP_TRY(h, hipHostGetDevicePointer(reinterpret_cast<void**>(&h->d_pipe_err), h->h_pipe_err, 0));
+        }
+    }
     if (ps) HIP_TRY(h, hipStreamWaitEvent(st, ps->done, 0));
     mark(h, st);
     if (!ps) {
@@ -701,11 +738,13 @@ static aec_status process_impl(aec_handle* h, uint64_t token, const float* mic, 
         a.feats = h->d_feats; a.Tmax = Tmax; a.rows = h->d_rows;
         mark(h, st);
         HIP_TRY(h, launch_analysis(a, st));
-        HIP_TRY(h, launch_nlms_recursion(h->d_rows, h->d_spec, h->d_len, Tmax, h->cfg.nlms_taps, h->cfg.nlms_mu,
-                                         h->cfg.nlms_beta, h->cfg.nlms_delta, 0, B, h->d_rows + (size_t)B * Tmax * 512,
-                                         st));
-        HIP_TRY(h, launch_mic_erb(h->d_spec, h->d_feats, h->d_len, Tmax, h->d_sched, h->sched_len, h->d_items,
-                                  h->nitems, st));
+        if (!pipe) {
+            HIP_TRY(h, launch_nlms_recursion(h->d_rows, h->d_spec, h->d_len, Tmax, h->cfg.nlms_taps, h->cfg.nlms_mu,
+                                             h->cfg.nlms_beta, h->cfg.nlms_delta, 0, B,
+                                             h->d_rows + (size_t)B * Tmax * 512, st));
+            HIP_TRY(h, launch_mic_erb(h->d_spec, h->d_feats, h->d_len, Tmax, h->d_sched, h->sched_len, h->d_items,
+                                      h->nitems, st));
+        }
     } else if (h->cfg.nlms_taps > 0) {
         NlmsArgs a{};
         a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
@@ -748,7 +787,17 @@ static aec_status process_impl(aec_handle* h, uint64_t token, const float* mic, 
     y.out = out; y.ld_out = ld_out;
     y.spec = h->cfg.nlms_taps > 0 ? h->d_spec : nullptr;
     y.fmode = h->fused_mode;
-    if (y.spec && h->fused && h->gru_mode == 0) {
+    if (pipe) {
+        PipeArgs q{};
+        q.rows = h->d_rows; q.spec = h->d_spec; q.feats = h->d_feats;
+        q.sched = h->d_sched; q.sched_len = h->sched_len;
+        q.mu = h->cfg.nlms_mu; q.beta = h->cfg.nlms_beta; q.delta = h->cfg.nlms_delta;
+        q.progress = h->d_progress; q.epoch = ++h->pipe_epoch; q.err = h->d_pipe_err;
+        q.spin_limit = 1 << 20;       // ~1-2 s of polls: far beyond any producer's lead
+        HIP_TRY(h, launch_gru_synth_pipe(g, y, q, B, st));
+        mark(h, st);
+        mark(h, st);
+    } else if (y.spec && h->fused && h->gru_mode == 0) {
         // one kernel: the synthesis runs two chunks behind the recurrence
         HIP_TRY(h, launch_gru_synth(g, y, B, st));
         mark(h, st);
@@ -1158,7 +1207,8 @@ void aec_destroy(aec_handle* h) {
     }
     (void)hipFree(h->d_mom); (void)hipFree(h->d_cvals); (void)hipFree(h->d_lists);
     (void)hipFree(h->d_feats); (void)hipFree(h->d_est); (void)hipFree(h->d_dbg); (void)hipFree(h->d_spec);
-    (void)hipFree(h->d_state); (void)hipFree(h->d_rows);
+    (void)hipFree(h->d_state); (void)hipFree(h->d_rows); (void)hipFree(h->d_progress);
+    if (h->h_pipe_err) (void)hipHostFree(h->h_pipe_err);
     (void)hipFree(h->d_th); (void)hipFree(h->d_tloss); (void)hipFree(h->d_rec); (void)hipFree(h->d_dg);
     (void)hipFree(h->d_part); (void)hipFree(h->d_scan);
     delete h;

@@ -111,13 +111,138 @@ __device__ __forceinline__ void tick_barrier() {
     asm volatile("" ::: "memory");
 }
 
+// Device-coherent (sc1) 4- and 8-byte accesses for the data the small-batch pipeline hands from a
+// producer block to a consumer block of the same launch (other CUs, other XCDs): relaxed agent-scope
+// atomics, which the compiler emits as sc1 loads / stores past the non-coherent caches.
+__device__ __forceinline__ float ld_coherent(const float* a) {
+    return __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(const_cast<float*>(a)), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ float2 ld_coherent2(const float2* a) {
+    const unsigned long long v = __hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<float2*>(a)),
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_float2(__uint_as_float((unsigned)v), __uint_as_float((unsigned)(v >> 32)));
+}
+__device__ __forceinline__ void st_coherent(float* a, float v) {
+    __hip_atomic_store(reinterpret_cast<unsigned*>(a), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_coherent2(float2* a, float2 v) {
+    const unsigned long long u = (unsigned long long)__float_as_uint(v.x) | ((unsigned long long)__float_as_uint(v.y) << 32);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(a), u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Producer block of the small-batch pipeline (gru_synth_kernel<1, true>, blocks 0 .. nb-1): stream
+// b's FD-NLMS recursion and mic_erb, one 16-frame chunk per tick, ahead of the consumer block
+// (nb + b) that runs the GRU and the synthesis of the same stream.  The arithmetic is the split
+// path's own: nlms_recursion_kernel's NlmsBin steps (waves 0-3, one lane per bin slot, rows
+// prefetched 8 frames ahead) into an LDS ring, then mic_erb_kernel's pass over those rows (waves
+// 4-7, 4 frames each, one chunk behind), so E, the features and the waveform are bit-identical to
+// the three-launch split path (tests/test_gpu_nlms.py::test_small_batch_pipeline_bit_exact).  The E
+// rows and mic_erb leave through sc1 stores; every storing wave drains (vmcnt(0)) before the tick
+// barrier, after which one lane publishes (epoch << 32) | chunks done.
+template <int TAPS>
+__device__ __forceinline__ void pipe_producer(const GruArgs& p, const PipeArgs& q, int b, float* smem) {
+    constexpr int kERowF = 512 + 48;                   // magnitudes (swizzled) + 48 ERB partials
+    constexpr int oPSched = 0;                         // float4[48][16]
+    constexpr int oPComb = oPSched + 48 * 16 * 4;      // int2[32]
+    constexpr int oPE = oPComb + 64;                   // float2[2][16][256] E ring
+    constexpr int oPScr = oPE + 2 * kCH * 256 * 2;     // [16][kERowF]
+    static_assert(oPScr + kCH * kERowF <= kFusedFloats, "producer LDS");
+    float4* sSched = reinterpret_cast<float4*>(smem + oPSched);
+    int2* sComb = reinterpret_cast<int2*>(smem + oPComb);
+    float2* sE = reinterpret_cast<float2*>(smem + oPE);
+    float* sScr = smem + oPScr;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int L = q.sched_len;
+    for (int i = tid; i < L * 16; i += blockDim.x) sSched[i] = reinterpret_cast<const float4*>(q.sched)[i];
+    if (tid < 32) sComb[tid] = reinterpret_cast<const int2*>(q.sched + 4 * 16 * L)[tid];
+    __syncthreads();
+    const int64_t T = p.lens[b] / kHop + 1;
+    const int nch = (int)((T + kCH - 1) / kCH);
+    const unsigned long long ep = q.epoch << 32;
+    if (wave < 4) {
+        const int k = tid;
+        const float2* r0 = q.rows + (int64_t)b * p.Tmax * 512;
+        NlmsBin<TAPS> st;
+        st.reset(k == 0);
+        float2 dd[8], rr[8];
+        auto fetch = [&](int64_t t, int i) {               // rows past the end: any valid row (results unused)
+            const int64_t tc = t < T ? t : T - 1;
+            dd[i] = r0[tc * 512 + k];
+            rr[i] = r0[tc * 512 + 256 + k];
+        };
+#pragma unroll
+        for (int i = 0; i < 8; ++i) fetch(i, i);
+        for (int c = 0; c <= nch; ++c) {
+            if (c < nch) {
+                float2* er = sE + (c & 1) * (kCH * 256) + k;
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const float2 e = st.step(dd[i], rr[i], q.mu, q.beta, q.delta);
+                        er[(8 * hh + i) * 256] = e;
+                        fetch((int64_t)c * kCH + 8 * hh + i + 8, i);
+                    }
+            }
+            tick_barrier();
+            if (tid == 0 && c >= 1)
+                __hip_atomic_store(q.progress + b, ep | (unsigned long long)c, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } else if (wave < 8) {
+        const int w4 = wave - 4;
+        const int gg = lane >> 4, lb = lane & 15, sw = 16 * (gg & 1);
+        const int fs = 4 * w4 + gg;                        // the group's frame slot of the chunk
+        float* er = sScr + fs * kERowF;
+        float2 xa[8], xb[8], x128;
+        for (int c = 0; c <= nch; ++c) {
+            if (c >= 1) {
+                const int cp = c - 1;
+                const float2* rowc = sE + (cp & 1) * (kCH * 256);
+                const int64_t t = (int64_t)cp * kCH + fs;
+                row_to_pairs(rowc + fs * 256, lb, true, xa, xb, x128);
+                mags_to_scr(er, lb, sw, xa, xb, x128);
+                wave_fence();
+                erb_project(er, sSched, sComb, L, lb, sw, nullptr);
+                if (t < T) {                               // erb_project's feature-row expression
+                    const float* part = er + 512;
+                    float* fo = q.feats + ((int64_t)b * p.Tmax + t) * 96;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int band = lb + 16 * h;
+                        const int2 cb = sComb[band];
+                        st_coherent(fo + band, part[cb.x] + (cb.y >= 0 ? part[cb.y] : 0.f));
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {             // the wave's 4 E rows -> spec
+                    const int idx = lane + 64 * j, fr = 4 * w4 + (idx >> 8), slot = idx & 255;
+                    const int64_t tt = (int64_t)cp * kCH + fr;
+                    if (tt < T) st_coherent2(q.spec + ((int64_t)b * p.Tmax + tt) * 256 + slot, rowc[fr * 256 + slot]);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            tick_barrier();
+        }
+    } else {
+        for (int c = 0; c <= nch; ++c) tick_barrier();
+    }
+}
+
 // NS streams per block (one recurrence wave each, waves 0 .. NS-1), TF = 16 / NS frames of
 // every stream per tick, so the helper roles see 16 frame slots per tick whatever NS is.
 // With NS = 2 the block holds two independent recurrence chains on two SIMDs (the chain of
 // one stream leaves its CU mostly idle) and half the blocks occupy half the CUs for about
 // the same time: the CUs the other half frees run the next batch's analysis kernel.
-template <int NS>
-__global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(GruArgs p, SynthArgs y, int nb) {
+// PIPE (NS = 1): blocks 0 .. nb-1 are the streams' producers (pipe_producer), block nb + i consumes
+// stream i: its gi waves wait for a chunk's mic_erb and its synthesis waves for its E rows (polls
+// of the producer's counter, sc1 loads of the rows).  Producers come first in the grid, so every
+// consumer's producer was dispatched before it (no wait on a block that cannot start).
+template <int NS, bool PIPE = false>
+__global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(GruArgs p, SynthArgs y, int nb,
+                                                                                 PipeArgs q) {
+    static_assert(!PIPE || NS == 1, "the pipeline runs one stream per consumer block");
     constexpr int TF = kCH / NS;
     constexpr int kThreads = 64 * (NS + kHelperWaves);
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -137,6 +262,13 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
     float* sCoff = smem + oCoff;
     float* sTail = smem + oTail;
     float* sOut = smem + oOut;
+    if constexpr (PIPE) {
+        if ((int)blockIdx.x < nb) {
+            pipe_producer<kPipeTaps>(p, q, p.b0 + (int)blockIdx.x, smem);
+            return;
+        }
+    }
+    const int blk = PIPE ? (int)blockIdx.x - nb : (int)blockIdx.x;
 
     // the block's streams (an odd last block: stream 1 absent, its addresses those of stream 0)
     int bs[NS], Ts[NS], nchs[NS];
@@ -145,9 +277,9 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
     int nchmax = 0;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-        const int i = NS * blockIdx.x + s;
+        const int i = NS * blk + s;
         vs[s] = i < nb;
-        bs[s] = p.b0 + (vs[s] ? i : NS * blockIdx.x);
+        bs[s] = p.b0 + (vs[s] ? i : NS * blk);
         const int64_t n = p.lens[bs[s]];
         Ts[s] = vs[s] ? (int)(n / kHop + 1) : 0;
         nhops[s] = vs[s] ? n / kHop : 0;                  // output hops (T - 1)
@@ -172,6 +304,29 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
     const float* b1 = W1 + 32 * 64;           // [32]
     const float* W2 = b1 + 32;                // [32][32]
     const float* b2 = W2 + 32 * 32;           // [32]
+    // PIPE: wait until the producer has published chunks [0, need) of the block's stream (lane 0
+    // polls; bounded: past q.spin_limit polls the wave sets the error word and stops waiting)
+    bool stalled = false;
+    auto wait_chunks = [&](int need) {
+        if constexpr (PIPE) {
+            if (stalled) return;
+            const unsigned long long target = (q.epoch << 32) | (unsigned long long)need;
+            int bad = 0;
+            if (lane == 0) {
+                int n = 0;
+                while (__hip_atomic_load(q.progress + bs[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++n > q.spin_limit) {
+                        __hip_atomic_store(q.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        bad = 1;
+                        break;
+                    }
+                }
+            }
+            stalled = __builtin_amdgcn_readfirstlane(bad) != 0;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");    // no load above the poll
+        }
+    };
 
     // synthesis tables (read after the first tick barrier)
     {
@@ -324,7 +479,8 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
                     if (s == z) Tq = Ts[z], bq = bs[z];
                 const bool ok = e < kCH * 32 && t < Tq;
                 const float* f = p.feats + ((int64_t)bq * p.Tmax + t) * 96 + (e & 31);
-                pm[u] = ok ? f[0] : 0.f;
+                if constexpr (PIPE) pm[u] = ok ? ld_coherent(f) : 0.f;       // mic_erb from the producer
+                else pm[u] = ok ? f[0] : 0.f;
                 pr[u] = ok ? f[32] : 0.f;
                 pn[u] = ok && p.has_near ? f[64] : 0.f;
             }
@@ -347,7 +503,10 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
                     }
                 }
             }
-            if (c + 3 < nchmax) load_chunk(c + 3);
+            if (c + 3 < nchmax) {
+                wait_chunks(c + 4);
+                load_chunk(c + 3);
+            }
             const int cg = c + 1;
             if (cg >= 0 && cg < nchmax && !(y.fmode & 2048)) {
 #pragma unroll 2
@@ -485,18 +644,24 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
             for (int m = 0; m < 8; ++m) {
                 const int kk = lb + 16 * m;
 #if AEC_SPEC_LD_NT
+                if constexpr (PIPE) {
+                    const float2 a = ld_coherent2(row + kk), c2 = ld_coherent2(row + ((256 - kk) & 255));
+                    xa[m] = kk == 0 ? make_float2(a.x, 0.f) : a;
+                    xb[m] = kk == 0 ? make_float2(a.y, 0.f) : c2;
+                    continue;
+                }
                 typedef float f2v __attribute__((ext_vector_type(2)));
                 const f2v av = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(row + kk));
                 const f2v cv = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(row + ((256 - kk) & 255)));
                 const float2 a = make_float2(av.x, av.y), c2 = make_float2(cv.x, cv.y);
 #else
-                const float2 a = row[kk];
-                const float2 c2 = row[(256 - kk) & 255];
+                const float2 a = PIPE ? ld_coherent2(row + kk) : row[kk];
+                const float2 c2 = PIPE ? ld_coherent2(row + ((256 - kk) & 255)) : row[(256 - kk) & 255];
 #endif
                 xa[m] = kk == 0 ? make_float2(a.x, 0.f) : a;
                 xb[m] = kk == 0 ? make_float2(a.y, 0.f) : c2;
             }
-            x128 = row[128];
+            x128 = PIPE ? ld_coherent2(row + 128) : row[128];
         };
         for (int c = -3; c <= nchmax + 2; ++c) {
             GTICK(0);
@@ -509,10 +674,14 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
                 float* scr = sOut + (cs & 1) * (kSynWaves * 4 * kGroupFloats) + fl * kGroupFloats;
                 float2 v[16];
                 synth_pack(xa, xb, x128, sEst + ((cs & 1) * kCH + fl) * kEstS, sBin, sTw512, lb, v);
-                if (next) load_rows(c - 1);
+                if (next) {
+                    wait_chunks(c);
+                    load_rows(c - 1);
+                }
                 if constexpr (ola_rec && AEC_OLA_WIN) synth_fft_raw(v, sTwT, scr, lb);
                 else synth_fft<AEC_SYN_HANN_PRE>(v, sTwT, sHann, scr, lb);
             } else if (next) {
+                wait_chunks(c);
                 load_rows(c - 1);
             }
             GTICK(1);
@@ -534,12 +703,21 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
     }
 }
 
-// streams per block: AEC_GRU_NS (1 or 2, default 2), read per launch
+// Streams per block.  NS = 1 finishes a batch sooner (a stream's recurrence takes 16 frames per
+// tick, against 8 with NS = 2: 0.26 against 0.39 ms for 256 streams alone); NS = 2 takes half the
+// CUs for about as long, and with batches in flight those CUs run the next batch's analysis (the
+// C2 step 1.3 % faster).  So NS = 1 while the batch fills at most half the CUs (the
+// latency-bound calls: batch 1 0.454 -> 0.364 ms, 64 streams 0.588 -> 0.479 ms,
+// profiles/r06h_b1.log), NS = 2 above.  AEC_GRU_NS = 1 / 2 forces one (a mode knob, read per
+// launch; the two are bit-identical in the waveform and est_erb, the loss is summed in another
+// order, <= 1e-6 relative).
 hipError_t launch_gru_synth(const GruArgs& g, const SynthArgs& y, int B, hipStream_t st) {
     if (B <= 0) return hipSuccess;
     // NS = 2 writes the waveform with 16-B stores (overlap-add on the recurrence waves)
     const bool al16 = y.ld_out % 4 == 0 && (reinterpret_cast<uintptr_t>(y.out) & 15) == 0;
-    const int ns = AEC_MODE_KNOB("AEC_GRU_NS", 2) == 1 || (AEC_OLA_REC && !al16) ? 1 : 2;
+    const int force = AEC_MODE_KNOB("AEC_GRU_NS", 0);
+    const bool one = force == 1 || (force != 2 && 2 * (int64_t)B <= (int64_t)std::max(y.num_cus, 2));
+    const int ns = one || (AEC_OLA_REC && !al16) ? 1 : 2;
     SynthArgs ya = y;
     ya.wmap = 0;
 #if AEC_AB_BUILD
@@ -562,13 +740,31 @@ hipError_t launch_gru_synth(const GruArgs& g, const SynthArgs& y, int B, hipStre
                                                            (int)gru_synth_smem_bytes());                       \
         if (attr != hipSuccess) return attr;                                                                   \
         hipLaunchKernelGGL(gru_synth_kernel<NS_>, dim3((B + NS_ - 1) / NS_), dim3(64 * (NS_ + kHelperWaves)),   \
-                           gru_synth_smem_bytes(), st, g, ya, B);                                              \
+                           gru_synth_smem_bytes(), st, g, ya, B, PipeArgs{});                                  \
     } while (0)
     if (ns == 1)
         AEC_GRU_SYNTH(1);
     else
         AEC_GRU_SYNTH(2);
 #undef AEC_GRU_SYNTH
+    return hipGetLastError();
+}
+
+// The small-batch pipeline (B <= the split path's limit, 2 B blocks <= one per CU: the host checks):
+// B producer blocks, then B consumer blocks (NS = 1).
+hipError_t launch_gru_synth_pipe(const GruArgs& g, const SynthArgs& y, const PipeArgs& q, int B, hipStream_t st) {
+    if (B <= 0) return hipSuccess;
+    if (!q.rows || !q.spec || !q.feats || !q.sched || q.sched_len > 48 || !q.progress || !q.err || !y.spec ||
+        q.spin_limit <= 0)
+        return hipErrorInvalidValue;
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gru_synth_kernel<1, true>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)gru_synth_smem_bytes());
+    if (attr != hipSuccess) return attr;
+    SynthArgs ya = y;
+    ya.wmap = 0;
+    hipLaunchKernelGGL((gru_synth_kernel<1, true>), dim3(2 * B), dim3(64 * (1 + kHelperWaves)), gru_synth_smem_bytes(),
+                       st, g, ya, B, q);
     return hipGetLastError();
 }
 

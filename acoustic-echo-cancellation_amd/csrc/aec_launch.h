@@ -164,6 +164,22 @@ hipError_t launch_synthesis(const SynthArgs& a, hipStream_t st);
 hipError_t launch_stream_step(const StreamStepArgs& a, int B, int taps, hipStream_t st);
 // K3+K4 fused (aec_gru_synth.hip): GRU + head + synthesis of the NLMS error spectrum
 hipError_t launch_gru_synth(const GruArgs& g, const SynthArgs& y, int B, hipStream_t st);
+// Small-batch pipeline: the split path's NLMS recursion and mic_erb run in producer blocks of the
+// GRU + synthesis launch (gru_synth_kernel<1, true>), chunk by chunk ahead of the recurrence
+struct PipeArgs {
+    const float2* rows;               // K2's packed mic / ref rows [B][Tmax][2][256]
+    float2* spec;                     // E rows [B][Tmax][256] (out)
+    float* feats;                     // mic_erb = feats[b][t][0:32] (out)
+    const float* sched;               // ERB schedule (aec_tables.h)
+    int sched_len;
+    float mu, beta, delta;
+    unsigned long long* progress;     // [B]: (epoch << 32) | chunks of the stream published
+    unsigned long long epoch;         // this launch's epoch (per handle, increasing)
+    int* err;                         // host-mapped word: a consumer wave gave up waiting
+    int spin_limit;                   // polls (s_sleep 1 each) before giving up
+};
+constexpr int kPipeTaps = 4;          // the one tap count the pipeline is instantiated for
+hipError_t launch_gru_synth_pipe(const GruArgs& g, const SynthArgs& y, const PipeArgs& q, int B, hipStream_t st);
 size_t gru_synth_smem_bytes();
 
 // Training step (aec_train.hip): the backward of Little_net's loss through the

@@ -231,6 +231,64 @@ def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatc
                 assert np.array_equal(f0[k][i, :n // 256 + 1], f1[k][i, :n // 256 + 1], equal_nan=True), (key, k, i)
 
 
+@pytest.mark.parametrize('B,n', [(5, 0), (1, 160000), (64, 160000)])
+def test_small_batch_pipeline_bit_exact(golden_weights, golden_erb, monkeypatch, B, n):
+    """The pipelined split path (AEC_SMALLB_PIPE, default on): the NLMS
+    recursion and mic_erb run in producer blocks of the GRU + synthesis launch,
+    one 16-frame chunk ahead of the consumer block of the same stream (spin
+    waits on a per-stream counter, sc1 hand-off).  Waveform, mic_erb / ref_erb /
+    est_erb and loss are bit-identical to the three-launch split path
+    (AEC_SMALLB_PIPE=0) and the waveform to the per-stream K2n block
+    (AEC_SMALLB=0): ragged lengths (n = 0: 33333, 4097, 255, 16000, 256), one
+    10 s stream (the batch-1 latency case) and 64 of them (128 blocks spread
+    over every XCD).  Repeated calls reuse the counters (a new epoch per call)."""
+    from aec_amd import synth
+    if n == 0:
+        lens = [33333, 4097, 255, 16000, 256]
+        rows = [synth.scene(m, 900 + i) for i, m in enumerate(lens)]
+        L = max(lens)
+        mic, ref, near = (np.zeros((B, L), np.float32) for _ in range(3))
+        for i, (m, r, nn_) in enumerate(rows):
+            mic[i, :lens[i]], ref[i, :lens[i]], near[i, :lens[i]] = m, r, nn_
+    else:
+        lens = [n] * B
+        L = n
+        mic, ref, near = synth.batch(B, n, seed0=950)
+    dev = 'cuda:0'
+    erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
+    M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
+    T = L // 256 + 1
+    res = {}
+    for key, env in (('pipe', {'AEC_SMALLB_PIPE': '1'}), ('split', {'AEC_SMALLB_PIPE': '0'}),
+                     ('k2n', {'AEC_SMALLB': '0'})):
+        for k in ('AEC_SMALLB_PIPE', 'AEC_SMALLB'):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)                               # read when the handle is created
+        net = _net(golden_weights, NLMS)
+        net.set_debug(True)
+        with torch.no_grad():
+            outs = [net.forward_ragged(M, R, N, erb_t, lens) for _ in range(2 if key == 'pipe' else 1)]
+        feats = {k: net.debug_intermediate(k, B, T).cpu().numpy() for k in ('mic_erb', 'ref_erb', 'est_erb')}
+        torch.cuda.synchronize()
+        res[key] = [(o.cpu().numpy(), l.cpu().numpy()) for o, l in outs], feats
+    (o0, l0), (o0b, l0b) = res['pipe'][0]
+    assert np.array_equal(o0, o0b) and np.array_equal(l0, l0b, equal_nan=True)   # second epoch
+    f0 = res['pipe'][1]
+    (o1, l1), = res['split'][0]
+    assert np.array_equal(o0, o1)
+    assert np.array_equal(l0, l1, equal_nan=True)
+    for k in f0:
+        for i, m in enumerate(lens):
+            assert np.array_equal(f0[k][i, :m // 256 + 1], res['split'][1][k][i, :m // 256 + 1], equal_nan=True), (k, i)
+    (o2, _), = res['k2n'][0]
+    assert np.array_equal(o0, o2)
+    if n:
+        o, l = O.aec_forward(mic[0], ref[0], near[0], golden_erb.astype(np.float32), golden_weights, nlms_cfg=NLMS)
+        assert _rms(o0[0], o) <= WAVE_RMS_TOL
+        assert _loss_ok(float(l0[0]), l)
+
+
 def test_normaliser_lookahead_bit_exact(nlms_net, golden_erb):
     """aec_prepare_siglens / aec_process_prepared (Little_net.prepare_ragged ->
     forward_ragged(lookahead=token)): the normaliser pass of a batch queued on a
