@@ -245,9 +245,10 @@ struct aec_handle {
     int nlms_erb = 1;            // AEC_NLMS_ERB (A/B builds): role running the mic_erb pass (1 ref, 2 nlms)
     int fused = 1;               // AEC_FUSED_SYNTH: GRU + synthesis in one kernel (NLMS path)
     int fused_mode = 0;          // AEC_FUSED_MODE (A/B builds: timing experiments; results invalid unless 0)
-    int small_b = 64;            // AEC_SMALLB: NLMS batches up to this many streams take the split path
-                                 // (per 10 s step: B = 1 0.477 -> 0.336 ms, B = 16 0.486 -> 0.354,
-                                 // B = 64 0.504 -> 0.485; B = 128 slower)
+    int small_b = -1;            // AEC_SMALLB: NLMS batches up to this many streams take the split path;
+                                 // default half the CUs (the pipelined split path's limit).  Against the
+                                 // per-stream K2n block, one 10 s call: B = 1 0.258 vs 0.557 ms, 65 0.343
+                                 // vs 0.491, 96 0.413 vs 0.505, 128 0.490 vs 0.527 (r06h, r06m)
     float2* d_rows = nullptr;    // split path: packed mic / ref rows [B][T][2][256]
     size_t rows_cap = 0;         // float2 elements
     // split path, pipelined (AEC_SMALLB_PIPE, default on): the recursion and mic_erb run in producer
@@ -418,6 +419,7 @@ aec_status aec_create(const aec_config* cfg, const float* weights, size_t n_weig
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
             h->num_cus = cus;
     }
+    if (h->small_b < 0) h->small_b = h->num_cus / 2;
     auto bail = [&](aec_status s) { aec_destroy(h); return s; };
     DeviceGuard dg(device);
     if (dg.err != hipSuccess) return bail(AEC_ERR_HIP);
