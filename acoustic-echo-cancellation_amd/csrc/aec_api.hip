@@ -716,11 +716,15 @@ static aec_status process_impl(aec_handle* h, uint64_t token, const float* mic, 
     }
     if (ps) HIP_TRY(h, hipStreamWaitEvent(st, ps->done, 0));
     mark(h, st);
+    // the NLMS split path's K2 takes the normaliser scalars straight from the moment partials (the
+    // same expression as norm_finalize_kernel): one launch fewer on the latency-bound small batches
+    const bool split = h->cfg.nlms_taps > 0 && B <= h->small_b && h->nlms_mode == 0;
+    const bool fold_norm = split && !ps;
     if (!ps) {
         HIP_TRY(h, launch_moments(mic, ref, near, ld, h->d_slen, h->d_mom, 0, B, nsig, st));
-        HIP_TRY(h, launch_norm_finalize(h->d_mom, h->d_slen, h->d_cvals, 0, B, nsig, st));
+        if (!fold_norm) HIP_TRY(h, launch_norm_finalize(h->d_mom, h->d_slen, h->d_cvals, 0, B, nsig, st));
     }
-    if (h->cfg.nlms_taps > 0 && B <= h->small_b && h->nlms_mode == 0) {
+    if (split) {
         // few streams: transforms frame-parallel (K2 + rows), recursion per stream, mic_erb frame-parallel
         const size_t need = (size_t)B * Tmax * 512 + (size_t)B * 256;      // + one dummy row per stream
         if (need > h->rows_cap) {
@@ -734,7 +738,7 @@ static aec_status process_impl(aec_handle* h, uint64_t token, const float* mic, 
         AnalysisArgs a{};
         a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
         a.ld = ld; a.items = h->d_items; a.nitems = h->nitems;
-        a.num_cus = h->num_cus; a.cvals = cvals; a.slen = h->d_slen;
+        a.num_cus = h->num_cus; a.cvals = fold_norm ? nullptr : cvals; a.mom = h->d_mom; a.slen = h->d_slen;
         a.tables = reinterpret_cast<const float*>(h->d_tab);
         a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
         a.feats = h->d_feats; a.Tmax = Tmax; a.rows = h->d_rows;

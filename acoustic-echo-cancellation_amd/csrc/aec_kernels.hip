@@ -250,7 +250,8 @@ __global__ __launch_bounds__(256, 3) void analysis_kernel(AnalysisArgs p) {
             asm volatile("" ::: "memory");
             // signal s's own length: its normaliser and zero padding (mic = it.n)
             const int ns = s == 0 ? (int)it.n : p.slen[4 * it.b + s];
-            wave_commit(wr, pf, p.cvals[it.b * 3 + s], ns, it.wt, lane);
+            const float cv = p.cvals ? p.cvals[it.b * 3 + s] : norm_scalar(p.mom, it.b, s, p.slen[4 * it.b + s]);
+            wave_commit(wr, pf, cv, ns, it.wt, lane);
             if (s + 1 < p.nsig)
                 wave_prefetch(pf, p.sig[s + 1] + (int64_t)it.b * p.ld, p.slen[4 * it.b + s + 1], it.wt, lane,
                               (al >> (s + 1)) & 1);

@@ -29,7 +29,9 @@ struct AnalysisArgs {
     const WorkItem* items;   // host-built list (valid items only)
     int64_t nitems;
     int num_cus;
-    const float* cvals;      // [B][3] normaliser scalars
+    const float* cvals;      // [B][3] normaliser scalars, or null: computed from mom (the NLMS split path
+                             // without a look-ahead; norm_finalize_kernel's expression, the same bits)
+    const double2* mom;      // [B][3][kMomChunks] moment partials (read when cvals is null)
     const int32_t* slen;     // [B][4] per-signal lengths (mic, ref, near, -); mic = the item's n
     const float* tables;     // DevTables
     const float* sched;      // ERB schedule: float4[L][16] then int2[32] (aec_tables.h)
