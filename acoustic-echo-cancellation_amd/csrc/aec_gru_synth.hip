@@ -96,13 +96,13 @@ static_assert(kHeadWaves * kMaxNS <= 8, "loss slots");
 size_t gru_synth_smem_bytes() { return (size_t)kFusedFloats * 4; }
 
 #ifdef AEC_TICK_PROF
-// timing experiments only (tools/gru_tick_prof.py): s_memtime stamps of blocks 0 and 64 per wave and
+// timing experiments only (tools/gru_tick_prof.py): s_memtime stamps of (consumer) blocks 0 and 64 per wave and
 // tick: loop top, work done (before the tick barrier)
 __device__ unsigned long long g_gtick[2][12][96][2];
 #define GTICK(slot)                                                                                    \
     do {                                                                                               \
-        if ((blockIdx.x == 0 || blockIdx.x == 64) && lane == 0 && c + 3 < 96)                          \
-            g_gtick[blockIdx.x ? 1 : 0][wave][c + 3][slot] = __builtin_amdgcn_s_memtime();             \
+        if ((blk == 0 || blk == 64) && lane == 0 && c + 3 < 96)                                        \
+            g_gtick[blk ? 1 : 0][wave][c + 3][slot] = __builtin_amdgcn_s_memtime();                     \
     } while (0)
 #else
 #define GTICK(slot) do {} while (0)
@@ -119,6 +119,11 @@ __device__ __forceinline__ void tick_barrier() {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 }
+
+// role of hardware wave k = nibble k (0: identity).  NS = 1: SIMD0 rec gi0 gi1 | gi2 head0 syn0 |
+// head1 syn1 syn2 | head2 syn3 (role waves: 0 recurrence, 1-3 gi, 4-6 head, 7-10 synthesis)
+template <int NS>
+constexpr unsigned long long kRoleMap = NS == 1 ? 0x972A8416530ull : 0ull;
 
 // Device-coherent (sc1) 4- and 8-byte accesses for the data the small-batch pipeline hands from a
 // producer block to a consumer block of the same launch (other CUs, other XCDs): relaxed agent-scope
@@ -295,16 +300,19 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
         nchs[s] = (Ts[s] + TF - 1) / TF;
         nchmax = max(nchmax, nchs[s]);
     }
+    // Role placement: hardware wave i (SIMD i % 4) runs role wave (wmap >> 4 i) & 15; every index
+    // below uses the role ids.  NS = 2 keeps the identity; NS = 1 (11 waves, SIMD 3 holds two) puts
+    // the two lightest roles (gi waves) beside the recurrence wave, whose priority slows whatever
+    // shares its SIMD: tick 11.0 k -> 9.6 k cycles, batch 1 0.257 -> 0.233 ms (r06o_wmap1_ab.log).
+    // A/B builds: y.wmap (AEC_GRU_WMAP) overrides it.
 #if AEC_AB_BUILD
-    // A/B builds: y.wmap relabels hardware wave i (SIMD i % 4) as role wave (wmap >> 4 i) & 15, to
-    // measure other role-to-SIMD placements (AEC_GRU_WMAP); every index below uses the role ids
-    const int lane = threadIdx.x & 63;
-    const int wave = y.wmap ? (int)((y.wmap >> (4 * (threadIdx.x >> 6))) & 15) : (int)(threadIdx.x >> 6);
-    const int tid = wave * 64 + lane;
+    const unsigned long long wmap = y.wmap ? y.wmap : kRoleMap<NS>;
 #else
-    const int tid = threadIdx.x;
-    const int wave = tid >> 6, lane = tid & 63;
+    constexpr unsigned long long wmap = kRoleMap<NS>;
 #endif
+    const int lane = threadIdx.x & 63;
+    const int wave = wmap ? (int)((wmap >> (4 * (threadIdx.x >> 6))) & 15) : (int)(threadIdx.x >> 6);
+    const int tid = wave * 64 + lane;
     const float* W_ih = p.w;                  // [96][64]
     const float* W_hh = p.w + 96 * 64;        // [96][32]
     const float* b_ih = W_hh + 96 * 32;       // [96]
@@ -718,6 +726,21 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
     }
 }
 
+#if AEC_AB_BUILD
+// role placements for NS = 1 (role waves: 0 recurrence, 1-3 gi, 4-6 head, 7-10 synthesis; hardware
+// wave i on SIMD i % 4, so SIMD 3 holds two waves), entry k = role of hardware wave k
+static unsigned long long wmap_ns1(int wm) {
+    static const unsigned long long kWmaps1[] = {
+        0xA9876543210ull,       // 0 identity: SIMD0 rec head0 syn1 | gi0 head1 syn2 | gi1 head2 syn3 | gi2 syn0
+        0x972A8416530ull,       // 1 (the product's kRoleMap<1>): rec gi0 gi1 | gi2 head0 syn0 | head1 syn1 syn2 | head2 syn3
+        0x874A6519320ull,       // 2: rec gi0 head0 | gi1 head1 syn0 | gi2 head2 syn1 | syn2 syn3
+        0x987A5416320ull,       // 3: rec gi0 syn0 | gi1 head0 syn1 | gi2 head1 syn2 | head2 syn3
+        0xA8269715430ull,       // 4: rec gi0 gi1 | gi2 syn0 syn1 | head0 syn2 syn3 | head1 head2
+    };
+    return wm >= 0 && wm < (int)(sizeof(kWmaps1) / sizeof(kWmaps1[0])) ? kWmaps1[wm] : 0;
+}
+#endif
+
 // Streams per block.  NS = 1 finishes a batch sooner (a stream's recurrence takes 16 frames per
 // tick, against 8 with NS = 2: 0.26 against 0.39 ms for 256 streams alone); NS = 2 takes half the
 // CUs for about as long, and with batches in flight those CUs run the next batch's analysis (the
@@ -747,6 +770,7 @@ hipError_t launch_gru_synth(const GruArgs& g, const SynthArgs& y, int B, hipStre
     };
     const int wm = AEC_AB_KNOB("AEC_GRU_WMAP", 0);
     if (ns == 2 && wm > 0 && wm < (int)(sizeof(kWmaps) / sizeof(kWmaps[0]))) ya.wmap = kWmaps[wm];
+    if (ns == 1) ya.wmap = wmap_ns1(AEC_AB_KNOB("AEC_GRU_WMAP", 1));
 #endif
 #define AEC_GRU_SYNTH(NS_)                                                                                     \
     do {                                                                                                       \
@@ -778,6 +802,9 @@ hipError_t launch_gru_synth_pipe(const GruArgs& g, const SynthArgs& y, const Pip
     if (attr != hipSuccess) return attr;
     SynthArgs ya = y;
     ya.wmap = 0;
+#if AEC_AB_BUILD
+    ya.wmap = wmap_ns1(AEC_AB_KNOB("AEC_GRU_WMAP", 1));
+#endif
     hipLaunchKernelGGL((gru_synth_kernel<1, true>), dim3(2 * B), dim3(64 * (1 + kHelperWaves)), gru_synth_smem_bytes(),
                        st, g, ya, B, q);
     return hipGetLastError();

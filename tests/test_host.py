@@ -76,7 +76,7 @@ def test_clib_exports_every_declared_symbol():
     assert lib.aec_weights_count(16) == 0
 
 
-AB_KNOBS = ('AEC_MOM_CFG', 'AEC_MOM_GRID', 'AEC_GRU_MODE', 'AEC_NLMS_PRIO', 'AEC_NLMS_ERB', 'AEC_FUSED_MODE',
+AB_KNOBS = ('AEC_MOM_CFG', 'AEC_MOM_GRID', 'AEC_GRU_MODE', 'AEC_GRU_WMAP', 'AEC_NLMS_PRIO', 'AEC_NLMS_ERB', 'AEC_FUSED_MODE',
             'AEC_CRN_ENC_FR', 'AEC_CRN_SPLITK', 'CRN_PERSIST_RA', 'AEC_CRN_ENC_MX_RERUN', 'CRN_DEC_FUSE',
             'CRN_GEMM_XCD', 'CRN_GEMM_DMA', 'CRN_GEMM_BIG', 'CRN_GEMM_SQ', 'CRN_GEMM_RB64', 'CRN_GEMM_MODE',
             'CRN_GEMM_PIPE', 'CRN_STEP_MODE', 'CRN_STEP_CFG', 'CRN_MX_STEP_MODE', 'AEC_CRN_PERSIST_WAVES')
