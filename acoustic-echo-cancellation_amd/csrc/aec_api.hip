@@ -800,6 +800,13 @@ static aec_status process_impl(aec_handle* h, uint64_t token, const float* mic, 
         q.mu = h->cfg.nlms_mu; q.beta = h->cfg.nlms_beta; q.delta = h->cfg.nlms_delta;
         q.progress = h->d_progress; q.epoch = ++h->pipe_epoch; q.err = h->d_pipe_err;
         q.spin_limit = 1 << 20;       // ~1-2 s of polls: far beyond any producer's lead
+        // test hook: producers publish nothing and consumers give up after N polls (the timeout path:
+        // this call's output is invalid, the handle's next call fails)
+        const int stall = AEC_MODE_KNOB("AEC_SMALLB_PIPE_STALL", 0);
+        if (stall > 0) {
+            q.stall = 1;
+            q.spin_limit = stall;
+        }
         HIP_TRY(h, launch_gru_synth_pipe(g, y, q, B, st));
         mark(h, st);
         mark(h, st);

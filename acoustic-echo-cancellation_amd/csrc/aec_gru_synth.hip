@@ -200,7 +200,7 @@ __device__ __forceinline__ void pipe_producer(const GruArgs& p, const PipeArgs& 
                     }
             }
             tick_barrier();
-            if (tid == 0 && c >= 1)
+            if (tid == 0 && c >= 1 && !q.stall)
                 __hip_atomic_store(q.progress + b, ep | (unsigned long long)c, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         }

@@ -22,7 +22,7 @@ inline int knob_env(const char* name, int dflt) {
 // every AEC_MODE_KNOB of the library (keep in sync: tests/test_host.py checks the binary's strings)
 inline const char* const kModeKnobs =
     "AEC_NLMS_MODE(bit 4 only) AEC_FUSED_SYNTH AEC_GRU_NS AEC_SMALLB AEC_SMALLB_PIPE AEC_BPTT_SERIAL AEC_CRN_PERSIST "
-    "AEC_CRN_SPIN_LIMIT AEC_CRN_PERSIST_STALL AEC_CRN_MX8_SHADOW AEC_CRN_STEP_MX AEC_CRN_MX_SREG "
+    "AEC_CRN_SPIN_LIMIT AEC_CRN_PERSIST_STALL AEC_SMALLB_PIPE_STALL AEC_CRN_MX8_SHADOW AEC_CRN_STEP_MX AEC_CRN_MX_SREG "
     "AEC_CRN_STREAM_FUSE CRN_COMBINE_VEC AEC_CRN_BACK_MASK AEC_CRN_BATCH_ENC AEC_CRN_BATCH_DEC AEC_CRN_GRAPH";
 
 }  // namespace aec

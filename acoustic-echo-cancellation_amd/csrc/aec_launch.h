@@ -179,6 +179,7 @@ struct PipeArgs {
     unsigned long long epoch;         // this launch's epoch (per handle, increasing)
     int* err;                         // host-mapped word: a consumer wave gave up waiting
     int spin_limit;                   // polls (s_sleep 1 each) before giving up
+    int stall;                        // test hook (AEC_SMALLB_PIPE_STALL): producers never publish
 };
 constexpr int kPipeTaps = 4;          // the one tap count the pipeline is instantiated for
 hipError_t launch_gru_synth_pipe(const GruArgs& g, const SynthArgs& y, const PipeArgs& q, int B, hipStream_t st);

@@ -123,7 +123,7 @@ AB_ONLY_KNOBS = ('AEC_MOM_CFG', 'AEC_MOM_GRID', 'AEC_GRU_MODE', 'AEC_GRU_WMAP', 
                  'CRN_GEMM_XCD', 'CRN_GEMM_DMA', 'CRN_GEMM_BIG', 'CRN_GEMM_SQ', 'CRN_GEMM_RB64', 'CRN_GEMM_MODE',
                  'CRN_GEMM_PIPE', 'CRN_STEP_MODE', 'CRN_STEP_CFG', 'CRN_MX_STEP_MODE', 'AEC_CRN_PERSIST_WAVES')
 # test hooks (fault injection) of the product library: never in a bench run
-TEST_ONLY_KNOBS = ('AEC_CRN_PERSIST_STALL', 'AEC_CRN_SPIN_LIMIT')
+TEST_ONLY_KNOBS = ('AEC_CRN_PERSIST_STALL', 'AEC_CRN_SPIN_LIMIT', 'AEC_SMALLB_PIPE_STALL')
 
 
 def knob_provenance():

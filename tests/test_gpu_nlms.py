@@ -289,6 +289,33 @@ def test_small_batch_pipeline_bit_exact(golden_weights, golden_erb, monkeypatch,
         assert _loss_ok(float(l0[0]), l)
 
 
+def test_small_batch_pipeline_timeout_reported(golden_weights, golden_erb, monkeypatch):
+    """The pipeline's spin waits are bounded: with the producers made silent
+    (AEC_SMALLB_PIPE_STALL=N, read per call: nothing is published and every
+    consumer wave gives up after N polls) the launch still drains, the
+    handle's next call fails loudly (the timed-out call's output is invalid),
+    and the call after that is bit-identical to a fresh handle."""
+    from aec_amd import synth
+    B, n = 3, 20000
+    mic, ref, near = synth.batch(B, n, seed0=970)
+    dev = 'cuda:0'
+    erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
+    M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
+    net = _net(golden_weights, NLMS)
+    with torch.no_grad():
+        monkeypatch.setenv('AEC_SMALLB_PIPE_STALL', '64')
+        net.forward_ragged(M, R, N, erb_t, [n] * B)
+        torch.cuda.synchronize()
+        monkeypatch.delenv('AEC_SMALLB_PIPE_STALL')
+        with pytest.raises(RuntimeError, match='timed out waiting for its producer'):
+            net.forward_ragged(M, R, N, erb_t, [n] * B)
+        out, loss = net.forward_ragged(M, R, N, erb_t, [n] * B)
+        ref_out, ref_loss = _net(golden_weights, NLMS).forward_ragged(M, R, N, erb_t, [n] * B)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref_out)
+    assert torch.equal(loss, ref_loss)
+
+
 def test_normaliser_lookahead_bit_exact(nlms_net, golden_erb):
     """aec_prepare_siglens / aec_process_prepared (Little_net.prepare_ragged ->
     forward_ragged(lookahead=token)): the normaliser pass of a batch queued on a
