@@ -195,6 +195,10 @@ __global__ __launch_bounds__(256) void norm_finalize_kernel(const double2* __res
 // The schedule is ordered so the 32 lanes of each mag gather hit 32 banks.
 // --------------------------------------------------------------------------
 
+// SIGPAR (few streams, the whole list in one round of waves): one (item, signal) task per wave
+// instead of an item's three signals in sequence, so a short call's latency is one transform, not
+// three; the same per-signal arithmetic (the same bits).
+template <bool SIGPAR>
 __global__ __launch_bounds__(256, 3) void analysis_kernel(AnalysisArgs p) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x;
@@ -235,28 +239,36 @@ __global__ __launch_bounds__(256, 3) void analysis_kernel(AnalysisArgs p) {
     // current one is transformed; the next item's descriptor one item ahead.
     const int NW = gridDim.x * 4;
     int64_t k = (int64_t)blockIdx.x * 4 + wave;
-    if (k >= p.nitems) return;
-    WorkItem it = p.items[k];
     float4 pf[kWavePf];
-    wave_prefetch(pf, p.sig[0] + (int64_t)it.b * p.ld, (int)it.n, it.wt, lane, al & 1);
+    if constexpr (SIGPAR) {
+        if (k >= p.nitems * p.nsig) return;
+    } else {
+        if (k >= p.nitems) return;
+    }
+    WorkItem it = p.items[SIGPAR ? k / p.nsig : k];
+    const int s0 = SIGPAR ? (int)(k % p.nsig) : 0;
+    // signal s's own length: its normaliser and zero padding (mic = it.n)
+    wave_prefetch(pf, p.sig[s0] + (int64_t)it.b * p.ld, s0 == 0 ? (int)it.n : p.slen[4 * it.b + s0], it.wt, lane,
+                  (al >> s0) & 1);
     for (;;) {
         const int64_t k2 = k + NW;
-        const WorkItem it2 = k2 < p.nitems ? p.items[k2] : it;
+        const WorkItem it2 = k2 < p.nitems && !SIGPAR ? p.items[k2] : it;
         const int64_t T = it.n / kHop + 1;
         const int64_t t = it.wt + gg;                                 // this group's frame
-        for (int s = 0; s < p.nsig; ++s) {
+        for (int s = s0; s < (SIGPAR ? s0 + 1 : p.nsig); ++s) {
             // keep the LDS table reads inside the loop (hoisting the loop-invariant
             // schedule / twiddle / window reads would pin ~100 VGPRs)
             asm volatile("" ::: "memory");
-            // signal s's own length: its normaliser and zero padding (mic = it.n)
             const int ns = s == 0 ? (int)it.n : p.slen[4 * it.b + s];
             const float cv = p.cvals ? p.cvals[it.b * 3 + s] : norm_scalar(p.mom, it.b, s, p.slen[4 * it.b + s]);
             wave_commit(wr, pf, cv, ns, it.wt, lane);
-            if (s + 1 < p.nsig)
+            if (SIGPAR) {
+            } else if (s + 1 < p.nsig) {
                 wave_prefetch(pf, p.sig[s + 1] + (int64_t)it.b * p.ld, p.slen[4 * it.b + s + 1], it.wt, lane,
                               (al >> (s + 1)) & 1);
-            else if (k2 < p.nitems)
+            } else if (k2 < p.nitems) {
                 wave_prefetch(pf, p.sig[0] + (int64_t)it2.b * p.ld, (int)it2.n, it2.wt, lane, al & 1);
+            }
             wave_fence();
             float2 v[16];
             load_frame(v, wr, sHann, gg, lb);
@@ -291,7 +303,7 @@ __global__ __launch_bounds__(256, 3) void analysis_kernel(AnalysisArgs p) {
             erb_project(scr, sSched, sComb, L, lb, sw,
                         t < T ? p.feats + ((int64_t)it.b * p.Tmax + t) * 96 + 32 * s : nullptr);
         }
-        if (k2 >= p.nitems) break;
+        if (SIGPAR || k2 >= p.nitems) break;      // SIGPAR: the host gives every task its own wave
         k = k2;
         it = it2;
     }
@@ -817,10 +829,17 @@ hipError_t launch_norm_finalize(const double2* mom, const int32_t* slen, float* 
 hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t st) {
     if (a.nitems <= 0) return hipSuccess;
     // persistent: at most kAnalysisBlocksPerCU blocks per CU, 4 waves (items) each
-    const int64_t want = (a.nitems + 3) / 4;
     const int64_t cap = (int64_t)a.num_cus * kAnalysisBlocksPerCU;
+    // few streams: one (item, signal) task per wave when the whole list fits one round of waves
+    const int64_t tasks = a.nitems * a.nsig;
+    if ((tasks + 3) / 4 <= cap) {
+        hipLaunchKernelGGL(analysis_kernel<true>, dim3((unsigned)((tasks + 3) / 4)), dim3(256),
+                           analysis_smem_bytes(a.sched_len), st, a);
+        return hipGetLastError();
+    }
+    const int64_t want = (a.nitems + 3) / 4;
     const unsigned grid = (unsigned)(want < cap ? want : cap);
-    hipLaunchKernelGGL(analysis_kernel, dim3(grid), dim3(256), analysis_smem_bytes(a.sched_len), st, a);
+    hipLaunchKernelGGL(analysis_kernel<false>, dim3(grid), dim3(256), analysis_smem_bytes(a.sched_len), st, a);
     return hipGetLastError();
 }
 

@@ -104,7 +104,9 @@ def test_ragged_batch_equals_batch_of_one(gpu_net, golden_erb):
 
 def test_batch_invariance_and_determinism(gpu_net, golden_erb):
     """Stream b's output does not depend on the other streams (bit-exact), and
-    repeated calls are bit-identical."""
+    repeated calls are bit-identical.  The 8-stream calls run the analysis as
+    one (item, signal) task per wave; the 72-stream call as persistent waves
+    walking items signal by signal (analysis_kernel<false>): the same bits."""
     from aec_amd import synth
     B, n = 8, 20000
     mic, ref, near = synth.batch(B, n, seed0=40)
@@ -117,9 +119,12 @@ def test_batch_invariance_and_determinism(gpu_net, golden_erb):
         perm = torch.tensor([3, 1, 7, 0, 2, 6, 5, 4], device=dev)
         o3, _ = gpu_net.forward_ragged(M[perm], R[perm], N[perm], erb_t, [n] * B)
         o4, _ = gpu_net.forward_ragged(M[2:3], R[2:3], N[2:3], erb_t, [n])
+        rep = lambda x: x.repeat(9, 1)                               # 72 x 20 items x 3 signals > one wave round
+        o5, _ = gpu_net.forward_ragged(rep(M), rep(R), rep(N), erb_t, [n] * 9 * B)
     assert torch.equal(o1, o2)
     assert torch.equal(o1[perm], o3)
     assert torch.equal(o1[2:3], o4)
+    assert torch.equal(o5, rep(o1))
 
 
 @pytest.mark.parametrize('n', [1000, 4097, 33333])
