@@ -231,7 +231,7 @@ def test_small_batch_split_path_bit_exact(golden_weights, golden_erb, monkeypatc
                 assert np.array_equal(f0[k][i, :n // 256 + 1], f1[k][i, :n // 256 + 1], equal_nan=True), (key, k, i)
 
 
-@pytest.mark.parametrize('B,n', [(5, 0), (1, 160000), (64, 160000)])
+@pytest.mark.parametrize('B,n', [(5, 0), (1, 160000), (64, 160000), (128, 48000)])
 def test_small_batch_pipeline_bit_exact(golden_weights, golden_erb, monkeypatch, B, n):
     """The pipelined split path (AEC_SMALLB_PIPE, default on): the NLMS
     recursion and mic_erb run in producer blocks of the GRU + synthesis launch,
@@ -240,8 +240,9 @@ def test_small_batch_pipeline_bit_exact(golden_weights, golden_erb, monkeypatch,
     est_erb and loss are bit-identical to the three-launch split path
     (AEC_SMALLB_PIPE=0) and the waveform to the per-stream K2n block
     (AEC_SMALLB=0): ragged lengths (n = 0: 33333, 4097, 255, 16000, 256), one
-    10 s stream (the batch-1 latency case) and 64 of them (128 blocks spread
-    over every XCD).  Repeated calls reuse the counters (a new epoch per call)."""
+    10 s stream (the batch-1 latency case), 64 of them (128 blocks spread
+    over every XCD) and 128 streams of 3 s (256 blocks: one per CU, the
+    path's limit).  Repeated calls reuse the counters (a new epoch per call)."""
     from aec_amd import synth
     if n == 0:
         lens = [33333, 4097, 255, 16000, 256]
