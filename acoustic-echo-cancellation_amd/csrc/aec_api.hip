@@ -719,13 +719,18 @@ static aec_status process_impl(aec_handle* h, uint64_t token, const float* mic, 
     // the NLMS split path's K2 takes the normaliser scalars straight from the moment partials (the
     // same expression as norm_finalize_kernel): one launch fewer on the latency-bound small batches
     const bool split = h->cfg.nlms_taps > 0 && B <= h->small_b && h->nlms_mode == 0;
-    const bool fold_norm = split && !ps;
+    // the bypass path (no NLMS) with up to half the CUs of streams: GRU + synthesis fused (one stream
+    // per block) over K2's mic rows instead of gru_kernel + synthesis_kernel re-deriving the mic
+    // spectrum (the same values, tested bit-exact)
+    const bool bypass_fused = h->cfg.nlms_taps == 0 && h->fused && h->gru_mode == 0 &&
+                              2 * (int64_t)B <= (int64_t)h->num_cus;
+    const bool fold_norm = (split || bypass_fused) && !ps;
     if (!ps) {
         HIP_TRY(h, launch_moments(mic, ref, near, ld, h->d_slen, h->d_mom, 0, B, nsig, st));
         if (!fold_norm) HIP_TRY(h, launch_norm_finalize(h->d_mom, h->d_slen, h->d_cvals, 0, B, nsig, st));
     }
-    if (split) {
-        // few streams: transforms frame-parallel (K2 + rows), recursion per stream, mic_erb frame-parallel
+    if (split || bypass_fused) {
+        // packed mic / ref rows of K2
         const size_t need = (size_t)B * Tmax * 512 + (size_t)B * 256;      // + one dummy row per stream
         if (need > h->rows_cap) {
             if (h->have_last) HIP_TRY(h, hipEventSynchronize(h->ev_last));
@@ -735,6 +740,9 @@ static aec_status process_impl(aec_handle* h, uint64_t token, const float* mic, 
             HIP_TRY(h, hipMalloc(&h->d_rows, need * sizeof(float2)));
             h->rows_cap = need;
         }
+    }
+    if (split) {
+        // few streams: transforms frame-parallel (K2 + rows), recursion per stream, mic_erb frame-parallel
         AnalysisArgs a{};
         a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
         a.ld = ld; a.items = h->d_items; a.nitems = h->nitems;
@@ -768,10 +776,11 @@ static aec_status process_impl(aec_handle* h, uint64_t token, const float* mic, 
         AnalysisArgs a{};
         a.sig[0] = mic; a.sig[1] = ref; a.sig[2] = near;
         a.ld = ld; a.items = h->d_items; a.nitems = h->nitems;
-        a.num_cus = h->num_cus; a.cvals = cvals; a.slen = h->d_slen;
+        a.num_cus = h->num_cus; a.cvals = fold_norm ? nullptr : cvals; a.mom = h->d_mom; a.slen = h->d_slen;
         a.tables = reinterpret_cast<const float*>(h->d_tab);
         a.sched = h->d_sched; a.sched_len = h->sched_len; a.nsig = nsig;
         a.feats = h->d_feats; a.Tmax = Tmax;
+        if (bypass_fused) a.rows = h->d_rows;
         mark(h, st);
         HIP_TRY(h, launch_analysis(a, st));
     }
@@ -791,7 +800,8 @@ static aec_status process_impl(aec_handle* h, uint64_t token, const float* mic, 
     y.tables = reinterpret_cast<const float*>(h->d_tab);
     y.bintab = h->d_bintab; y.est = h->d_est; y.Tmax = Tmax;
     y.out = out; y.ld_out = ld_out;
-    y.spec = h->cfg.nlms_taps > 0 ? h->d_spec : nullptr;
+    y.spec = h->cfg.nlms_taps > 0 ? h->d_spec : (bypass_fused ? h->d_rows : nullptr);
+    y.spec_stride = bypass_fused ? 512 : 256;
     y.fmode = h->fused_mode;
     if (pipe) {
         PipeArgs q{};

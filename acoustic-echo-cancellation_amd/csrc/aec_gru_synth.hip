@@ -654,7 +654,8 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
 #pragma unroll
         for (int z = 0; z < NS; ++z)
             if (s == z) nhop = nhops[z], bq = bs[z];
-        const float2* spec = y.spec + (int64_t)bq * y.Tmax * 256;
+        const int64_t sstride = y.spec_stride ? y.spec_stride : 256;
+        const float2* spec = y.spec + (int64_t)bq * y.Tmax * sstride;
         float2 xa[8] = {}, xb[8] = {}, x128 = {};
         auto load_rows = [&](int cc) {
             // E rows of chunk cc.  A frame past the last one (t > nhop) feeds no
@@ -662,7 +663,7 @@ __global__ __launch_bounds__(64 * (NS + kHelperWaves), 1) void gru_synth_kernel(
             // read any valid row: the index is clamped, the loads stay plain
             // global loads with no per-lane select.
             const int64_t t = min((int64_t)cc * TF + fs, nhop);
-            const float2* row = spec + t * 256;
+            const float2* row = spec + t * sstride;
 #pragma unroll
             for (int m = 0; m < 8; ++m) {
                 const int kk = lb + 16 * m;
@@ -794,7 +795,7 @@ hipError_t launch_gru_synth(const GruArgs& g, const SynthArgs& y, int B, hipStre
 hipError_t launch_gru_synth_pipe(const GruArgs& g, const SynthArgs& y, const PipeArgs& q, int B, hipStream_t st) {
     if (B <= 0) return hipSuccess;
     if (!q.rows || !q.spec || !q.feats || !q.sched || q.sched_len > 48 || !q.progress || !q.err || !y.spec ||
-        q.spin_limit <= 0)
+        q.spin_limit <= 0 || (y.spec_stride != 0 && y.spec_stride != 256))
         return hipErrorInvalidValue;
     static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(gru_synth_kernel<1, true>),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -98,6 +98,8 @@ struct SynthArgs {
     int fmode;               // fused kernel timing experiments only (AEC_FUSED_MODE; results invalid
                              // unless 0): bit0 skip the synthesis, bit1 skip the OLA, bit2 skip the E loads
     unsigned long long wmap; // A/B builds only: role wave of hardware wave i = (wmap >> 4 i) & 15 (0: identity)
+    int64_t spec_stride;     // gru_synth: float2 per frame of `spec` (0: 256, the E rows; 512: K2's packed
+                             // mic / ref rows, the bypass path's mic spectrum)
 };
 
 // Fused streaming step (aec_stream.hip): one 256-sample hop of B streams.

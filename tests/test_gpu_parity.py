@@ -211,3 +211,46 @@ def test_unequal_signal_lengths_vs_golden(gpu_net, golden_erb):
     with pytest.raises(RuntimeError, match='frame count'):
         h.process(m.data_ptr(), r.data_ptr(), nn_.data_ptr(), bad, B, L, o.data_ptr(), L, None,
                   torch.cuda.current_stream().cuda_stream)
+
+
+@pytest.mark.parametrize('lens', [[33333, 4097, 255, 16000, 256], [160000]])
+def test_bypass_fused_synthesis_bit_exact(golden_weights, golden_erb, monkeypatch, lens):
+    """The bypass path (no NLMS: the reference-parity drop-in) with up to half
+    the CUs of streams runs the GRU and the synthesis as one kernel over K2's
+    packed mic rows (gru_synth_kernel, one stream per block) instead of
+    gru_kernel + synthesis_kernel re-deriving the mic spectrum
+    (AEC_FUSED_SYNTH=0): the same values, so the waveform and est_erb are
+    bit-identical and the loss equal to summation order (<= 1e-6)."""
+    import aec_amd
+    from aec_amd import synth
+    from conftest import PARAM_KEYS
+    L = max(lens)
+    mic, ref, near = (np.zeros((len(lens), L), np.float32) for _ in range(3))
+    for i, n in enumerate(lens):
+        mic[i, :n], ref[i, :n], near[i, :n] = synth.scene(n, 1300 + i)
+    dev = 'cuda:0'
+    erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
+    M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
+    res = {}
+    for fused in ('0', '1'):
+        monkeypatch.setenv('AEC_FUSED_SYNTH', fused)              # read when the handle is created
+        net = aec_amd.Little_net(aec_amd.speech_conf, 32).eval()
+        sd = net.state_dict()
+        for k in PARAM_KEYS:
+            sd[k] = torch.from_numpy(golden_weights[k])
+        net.load_state_dict(sd, strict=True)
+        net = net.to(dev)
+        net.set_debug(True)
+        with torch.no_grad():
+            out, loss = net.forward_ragged(M, R, N, erb_t, lens)
+        est = net.debug_intermediate('est_erb', len(lens), L // 256 + 1)
+        torch.cuda.synchronize()
+        res[fused] = out.cpu().numpy(), loss.cpu().numpy(), est.cpu().numpy()
+    (o0, l0, e0), (o1, l1, e1) = res['0'], res['1']
+    assert np.array_equal(o0, o1)
+    for i, n in enumerate(lens):
+        assert np.array_equal(e0[i, :n // 256 + 1], e1[i, :n // 256 + 1]), i
+    np.testing.assert_allclose(l1, l0, rtol=1e-6)
+    if len(lens) == 1:
+        o, l = O.little_net_forward(mic[0], ref[0], near[0], golden_erb.astype(np.float32), golden_weights)
+        assert _rms(o1[0], o) <= WAVE_RMS_TOL

@@ -22,10 +22,11 @@ ap = argparse.ArgumentParser()
 ap.add_argument('--sizes', default='1,16,64')
 ap.add_argument('--reps', type=int, default=20)
 ap.add_argument('--seconds', type=float, default=10.0)
+ap.add_argument('--bypass', action='store_true', help='no FD-NLMS (the reference-parity drop-in path)')
 a = ap.parse_args()
 dev = torch.device('cuda', 0)
 w = dict(np.load(os.path.join(REPO, 'tests', 'golden', 'weights.npz')))
-net = aec_amd.Little_net(aec_amd.speech_conf, 32, nlms=aec_amd.nlms_conf).eval()
+net = aec_amd.Little_net(aec_amd.speech_conf, 32, nlms=None if a.bypass else aec_amd.nlms_conf).eval()
 sd = net.state_dict()
 for k in ['gru1.weight_ih_l0', 'gru1.weight_hh_l0', 'gru1.bias_ih_l0', 'gru1.bias_hh_l0',
           'linear1.weight', 'linear1.bias', 'linear2.weight', 'linear2.bias']:
@@ -47,6 +48,6 @@ for B in [int(x) for x in a.sizes.split(',')]:
             if i >= 3:
                 lat.append(time.perf_counter() - t0)
     ms = float(np.median(lat)) * 1e3
-    print(json.dumps(dict(B=B, env=env, ms_median=round(ms, 4), ms_min=round(min(lat) * 1e3, 4),
+    print(json.dumps(dict(B=B, bypass=a.bypass, env=env, ms_median=round(ms, 4), ms_min=round(min(lat) * 1e3, 4),
                           frames_per_s=round(B * (n // 256 + 1) / ms * 1e3, 1), rtf=round(ms / 1e3 / a.seconds, 8),
                           out_sum=float(out.double().sum()), loss=float(loss.double().sum()))), flush=True)
