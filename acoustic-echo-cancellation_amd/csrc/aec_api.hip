@@ -242,7 +242,8 @@ struct aec_handle {
     int gru_mode = 0;            // AEC_GRU_MODE (A/B builds: timing experiments; results invalid unless 0)
     int nlms_mode = 0;           // AEC_NLMS_MODE: bit 4 two-pass ref ERB (tested); bits 0-3 A/B builds only (skip work)
     int nlms_prio = 0;           // AEC_NLMS_PRIO (A/B builds): wave priorities mic|ref|nlms digits (0 fastest measured)
-    int nlms_erb = 1;            // AEC_NLMS_ERB (A/B builds): role running the mic_erb pass (1 ref, 2 nlms)
+    int nlms_erb = 0;            // AEC_NLMS_ERB (A/B builds): role running the mic_erb pass (0: the mic
+                                 // waves without a near signal, else the ref waves; 1 ref, 2 nlms)
     int fused = 1;               // AEC_FUSED_SYNTH: GRU + synthesis in one kernel (NLMS path)
     int fused_mode = 0;          // AEC_FUSED_MODE (A/B builds: timing experiments; results invalid unless 0)
     int small_b = -1;            // AEC_SMALLB: NLMS batches up to this many streams take the split path;

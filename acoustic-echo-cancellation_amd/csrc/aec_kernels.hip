@@ -436,9 +436,12 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
     const float mu = p.mu, beta = p.beta, delta = p.delta;
     // mic_erb of chunk c2 from its error rows (complete since the barriers of
     // tick c2 + 1); this group's frame 4 q + gg.  Run by the ref waves
-    // (erb_role 1) or by the nlms waves after their recursion (erb_role 2).
-    // 1: ref waves (merged with the ref ERB), 2: nlms waves
-    const int erb_role = p.erb_role == 2 ? 2 : 1;
+    // (erb_role 1, merged with the ref ERB), by the nlms waves after their
+    // recursion (erb_role 2, A/B only), or, without a near signal, by the mic
+    // waves (erb_role 0: their near transform is gone, so the pass leaves the
+    // ref waves and the two transform roles carry one transform and one ERB
+    // projection pass each)
+    const int erb_role = p.erb_role == 2 ? 2 : (p.erb_role == 0 && !have_near ? 0 : 1);
     auto mic_erb_pass = [&](int c2) {
         const int64_t t2 = (int64_t)c2 * kFPB + 4 * q + gg;
         float* er = sE + (c2 & 1) * kFPB * kNRow + (4 * q + gg) * kNRow;
@@ -556,6 +559,7 @@ __global__ __launch_bounds__(kNlmsWaves * 64, 1) void nlms_analysis_kernel(NlmsA
                                have_near ? al_near : al_mic, xa, xb, x128);
                 row_to_scr(scr, lb, xa, xb, x128);
             }
+            if (erb_role == 0 && c >= 2 && !(p.mode & 4)) mic_erb_pass(c - 2);
         } else {
             const bool erb2 = erb_role == 1 && c >= 2 && !(p.mode & 4);     // mic_erb of chunk c-2 due
             if (c < nch && !(p.mode & 8)) {

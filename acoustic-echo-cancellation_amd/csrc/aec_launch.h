@@ -61,7 +61,7 @@ struct NlmsArgs {
     int taps;
     float mu, beta, delta;
     int prio;                // wave priorities (AEC_NLMS_PRIO, decimal digits mic|ref|nlms, 0..3 each)
-    int erb_role;            // waves that run the mic_erb pass: 1 ref (AEC_NLMS_ERB=1), 2 nlms
+    int erb_role;            // waves that run the mic_erb pass: 0 mic if no near (else ref), 1 ref, 2 nlms
     int mode;                // timing experiments only (AEC_NLMS_MODE): bit0 skip recursion,
                              // bit1 skip near transform, bit2 skip mic ERB, bit3 skip mic/ref transforms;
                              // bit4 (valid results): the ref waves' two ERB projections in two passes

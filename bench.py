@@ -111,6 +111,8 @@ def parse():
     ap.add_argument('--no-c3', action='store_true', help='skip the BASELINE config 3 (DCCRN bf16) figure')
     ap.add_argument('--c3-steps', type=int, default=10, help='timed steps of the config 3 figure')
     ap.add_argument('--no-train', action='store_true', help='skip the training-step figure')
+    ap.add_argument('--no-near-leg', action='store_true',
+                    help='skip the near=None (no loss) timed leg reported beside the headline')
     ap.add_argument('--train-steps', type=int, default=10, help='timed steps of the training-step figure')
     return ap.parse_args()
 
@@ -896,16 +898,18 @@ def main():
 
     tokens = {}                                  # step index -> look-ahead token of its batch
 
-    def step():
+    def step(nr=near):
+        # nr: the near-end signal (the loss target); None = the deployment form (no clean near-end
+        # exists outside synthetic data; test.py:159 discards the loss): no near transform, no loss
         n_ = kstep[0]
         k = n_ % inflight
         kstep[0] += 1
         if side is not None:
             with torch.cuda.stream(side):
-                tokens[n_ + args.lookahead] = nets[(k + args.lookahead) % inflight].prepare_ragged(mic, ref, near,
+                tokens[n_ + args.lookahead] = nets[(k + args.lookahead) % inflight].prepare_ragged(mic, ref, nr,
                                                                                                   lens)
         with torch.cuda.stream(streams[k]):
-            return nets[k].forward_ragged(mic, ref, near, erb, lens, lookahead=tokens.pop(n_, None))
+            return nets[k].forward_ragged(mic, ref, nr, erb, lens, lookahead=tokens.pop(n_, None))
 
     with torch.no_grad():
         for _ in range(2):
@@ -944,6 +948,38 @@ def main():
             dist.barrier()
         el = time.perf_counter() - t0
         el = shard.max_over_ranks(el)              # all_reduce(MAX) of one scalar, outside the timed region
+        # the same pipelined step without the near-end signal (reported beside `value`, never as it):
+        # the enhanced waveform only, as the reference's inference entry point uses it (test.py:159
+        # keeps out_wav and discards the loss); the look-ahead queue is drained and refilled first,
+        # since a token is tied to the signals it was prepared for
+        no_near = None
+        if not args.no_near_leg:
+            torch.cuda.synchronize(dev)
+            tokens.clear()
+            kstep[0] = 0
+            if side is not None:
+                for j in range(args.lookahead):
+                    with torch.cuda.stream(side):
+                        tokens[j] = nets[j % inflight].prepare_ragged(mic, ref, None, lens)
+            for _ in range(warm_steps):
+                step(None)
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t2 = time.perf_counter()
+            for _ in range(args.steps):
+                step(None)
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            el2 = shard.max_over_ranks(time.perf_counter() - t2)
+            no_near = {'frames_per_s': round(world * B * T * args.steps / el2, 1),
+                       'ms_per_step': round(el2 / args.steps * 1e3, 4), 'steps': args.steps,
+                       'what': 'the same 256-stream pipelined step with near=None: mic / ref moments, no near-end '
+                               'transform, no loss (the enhanced waveform is bit-identical to the headline path, '
+                               'tests/test_gpu_nlms.py::test_no_near_waveform_bit_exact); not the headline, which '
+                               'runs the reference forward whole (ERB.py:252-334, loss included)'}
         # RTF at batch 1: one 10 s utterance, synchronous latency (median of 7)
         lat = []
         for _ in range(0 if args.no_rtf else 7):
@@ -1125,6 +1161,7 @@ def main():
                                   'alg_flops_per_frame': path_flops(args.pipeline),
                                   'hbm_frac': round(pipe_gbs / HBM_PEAK_GBS, 4),
                                   'fp32_frac': round(pipe_tfl / FP32_PEAK_TFLOPS, 4)},
+            'no_near': no_near,
             'erle': erle,
             'erle_bypass': erle_bypass,
             'cpu_baseline': cpu,

@@ -384,6 +384,40 @@ def test_normaliser_lookahead_bit_exact(nlms_net, golden_erb):
         torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize('B', [5, 140, 256])
+def test_no_near_waveform_bit_exact(nlms_net, golden_erb, B):
+    """near=None (the deployment form: no clean near-end signal, no loss;
+    test.py:159 keeps only out_wav): the K2n mic waves skip the near transform
+    and the normaliser pass covers mic / ref only.  The waveform must be
+    bit-identical to the call with near, on the pipelined split path (B = 5)
+    and the batch K2n path (B = 140, the bench's B = 256), with and without a
+    look-ahead normaliser token (bench.py's `no_near` leg)."""
+    from aec_amd import synth
+    dev = 'cuda:0'
+    erb_t = torch.tensor(golden_erb, dtype=torch.float32, device=dev)
+    rng = np.random.default_rng(B)
+    lens = [int(x) for x in rng.integers(256, 48000, size=B)]
+    lens[0] = 48000
+    L = max(lens)
+    mic, ref, near = (np.zeros((B, L), np.float32) for _ in range(3))
+    for i, n in enumerate(lens):
+        m, r, nn_ = synth.scene(n, 1300 + i)
+        mic[i, :n], ref[i, :n], near[i, :n] = m, r, nn_
+    M, R, N = (torch.tensor(a, device=dev) for a in (mic, ref, near))
+    side = torch.cuda.Stream()
+    with torch.no_grad():
+        o0, l0 = nlms_net.forward_ragged(M, R, N, erb_t, lens)
+        o1, l1 = nlms_net.forward_ragged(M, R, None, erb_t, lens)
+        assert l0 is not None and l1 is None
+        assert np.array_equal(o0.cpu().numpy(), o1.cpu().numpy())
+        with torch.cuda.stream(side):
+            tok = nlms_net.prepare_ragged(M, R, None, lens, producer=torch.cuda.current_stream())
+        o2, l2 = nlms_net.forward_ragged(M, R, None, erb_t, lens, lookahead=tok)
+        assert l2 is None
+        assert np.array_equal(o0.cpu().numpy(), o2.cpu().numpy())
+    torch.cuda.synchronize()
+
+
 def test_max_batch_4096_streams_matches_single_calls(nlms_net, golden_erb):
     """BASELINE C4/C5's 4,096-stream sweep point at 10 s: > 4 GiB spectrum and
     input buffers (64-bit row / spectrum offsets), ragged lengths.  Sampled
