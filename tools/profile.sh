@@ -16,12 +16,12 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-    python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu --no-c3 --no-train --no-rtf --no-sweep "$@" > "$OUT/trace_bench.log" 2>&1
+    python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu --no-c3 --no-train --no-rtf --no-sweep --no-near-leg "$@" > "$OUT/trace_bench.log" 2>&1
 echo "trace done"
 i=0
 for set in FETCH_SIZE WRITE_SIZE; do
     i=$((i+1))
     timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d "$OUT/pmc_$i" -o run -- \
-        python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu --no-c3 --no-train --no-rtf --no-sweep "$@" > "$OUT/pmc_$i.log" 2>&1
+        python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu --no-c3 --no-train --no-rtf --no-sweep --no-near-leg "$@" > "$OUT/pmc_$i.log" 2>&1
     echo "pmc $i done: $set"
 done

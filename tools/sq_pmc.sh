@@ -19,6 +19,6 @@ for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_W
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_WAVES GRBM_GUI_ACTIVE"; do
     i=$((i+1))
     timeout -s KILL 90 rocprofv3 --pmc $set --output-format csv -d "$OUT/pmc_$i" -o run -- \
-        python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu --no-c3 --no-rtf --no-train --no-sweep "$@" > "$OUT/pmc_$i.log" 2>&1
+        python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu --no-c3 --no-rtf --no-train --no-sweep --no-near-leg "$@" > "$OUT/pmc_$i.log" 2>&1
     echo "pmc $i done"
 done
