@@ -697,6 +697,13 @@ def run_c5_stream(dev, B=256, hops=200, dtype='fp8', world=1, with_cpu=False, sw
                rtf=round(dt / 0.016, 5), roofline=c5_roofline(conf, B, dt * 1e3, pmc),
                latency_ms_per_hop_b1=lat_b1['ms_per_hop_synchronous_median'] if lat_b1 else None,
                batch1=lat_b1, streams_sweep_frames_per_s_per_gpu=streams_sweep, erle=erle, cpu_baseline=None)
+    if lat_b1:
+        # what limits the hop: one stream's back-to-back hop against B streams' (a latency chain of 7
+        # launches when the two are about equal, not MFMA or HBM throughput)
+        r1 = lat_b1['ms_per_hop_back_to_back'] / (dt * 1e3)
+        res['roofline']['limiter'] = (f'latency: one stream\'s hop takes {r1:.2f} of {B} streams\' '
+                                      f'({lat_b1["ms_per_hop_back_to_back"]} vs {round(dt * 1e3, 4)} ms back to '
+                                      f'back), the 7-launch chain, not throughput')
     if with_cpu and world == 1:
         res['cpu_baseline'] = cpu_baseline_c5(cpu_seconds, net, conf, aec_amd.nlms_conf, B)
     del net
