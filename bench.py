@@ -907,7 +907,7 @@ def main():
 
     def step(nr=near):
         # nr: the near-end signal (the loss target); None = the deployment form (no clean near-end
-        # exists outside synthetic data; test.py:159 discards the loss): no near transform, no loss
+        # exists outside synthetic data; test.py:157 discards the loss): no near transform, no loss
         n_ = kstep[0]
         k = n_ % inflight
         kstep[0] += 1
@@ -956,7 +956,7 @@ def main():
         el = time.perf_counter() - t0
         el = shard.max_over_ranks(el)              # all_reduce(MAX) of one scalar, outside the timed region
         # the same pipelined step without the near-end signal (reported beside `value`, never as it):
-        # the enhanced waveform only, as the reference's inference entry point uses it (test.py:159
+        # the enhanced waveform only, as the reference's inference entry point uses it (test.py:157
         # keeps out_wav and discards the loss); the look-ahead queue is drained and refilled first,
         # since a token is tied to the signals it was prepared for
         no_near = None

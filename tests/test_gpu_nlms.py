@@ -387,7 +387,7 @@ def test_normaliser_lookahead_bit_exact(nlms_net, golden_erb):
 @pytest.mark.parametrize('B', [5, 140, 256])
 def test_no_near_waveform_bit_exact(nlms_net, golden_erb, B):
     """near=None (the deployment form: no clean near-end signal, no loss;
-    test.py:159 keeps only out_wav): the K2n mic waves skip the near transform
+    test.py:157 keeps only out_wav): the K2n mic waves skip the near transform
     and the normaliser pass covers mic / ref only.  The waveform must be
     bit-identical to the call with near, on the pipelined split path (B = 5)
     and the batch K2n path (B = 140, the bench's B = 256), with and without a
